@@ -1,0 +1,683 @@
+// gs_api.cpp — C ABI (include/gsplat.h): contexts, scenes and the per-frame pipeline.
+//
+// Frame (gs_render_device), all on one HIP stream:
+//   memset(tickets, histograms, counters) -> k_project -> [read n_vis, K] ->
+//   memset(look-back words) -> 4 x k_sort_pass (depth key, 8 bits each) -> k_bin ->
+//   1-2 x k_sort_pass (tile id) -> k_ranges -> k_composite
+// Reference call stack replaced: Renderer.animate/draw (src/renderer.ts:332-387, :301-330).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/gsplat.h"
+#include "gs_device.h"
+
+using namespace gs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct GsError : std::runtime_error {
+    int code;
+    GsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            throw GsError(e_ == hipErrorOutOfMemory ? GS_ERR_OOM : GS_ERR_HIP,           \
+                          std::string(#expr) + ": " + hipGetErrorString(e_));            \
+    } while (0)
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const GsError& e) {
+        return fail(e.code, e.what());
+    } catch (const std::bad_alloc&) {
+        return fail(GS_ERR_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(GS_ERR_INTERNAL, e.what());
+    } catch (...) {
+        return fail(GS_ERR_INTERNAL, "unknown exception");
+    }
+}
+
+template <class T>
+void dev_alloc(T*& p, size_t count) {
+    p = nullptr;
+    if (count == 0) count = 1;
+    HIPCHK(hipMalloc((void**)&p, count * sizeof(T)));
+}
+template <class T>
+void dev_free(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+inline uint64_t round_up(uint64_t a, uint64_t b) { return (a + b - 1) / b * b; }
+
+enum { EV_BEGIN, EV_PROJECT, EV_SORT, EV_BIN, EV_TSORT, EV_RANGES, EV_COMPOSITE, EV_COUNT };
+
+}  // namespace
+
+struct gs_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t* d_err = nullptr;
+    uint32_t* h_pinned = nullptr;  // [0..3] counters (2 x u64), [4] err
+    void* d_out = nullptr;
+    size_t d_out_bytes = 0;
+    hipEvent_t ev[EV_COUNT] = {};
+    bool timed = false;
+    hipStream_t timed_stream = nullptr;
+    gs_stats stats{};
+    std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
+};
+
+struct gs_scene {
+    gs_ctx* ctx = nullptr;
+    uint64_t n = 0;
+    int n_sh = 0;
+    float* planes = nullptr;
+    uint64_t stride = 0;
+    // depth sort ping-pong; keys0 (project output, N entries) aliases keysB
+    uint32_t *keysA = nullptr, *valsA = nullptr, *keysB = nullptr, *valsB = nullptr;
+    float4* rec = nullptr;
+    // zero-per-frame metadata block: tickets | depth hist | tile hist | counters
+    uint8_t* meta = nullptr;
+    size_t meta_bytes = 0;
+    uint32_t* tickets = nullptr;          // 16
+    uint32_t* hist_depth = nullptr;       // 8 x 4 x 256
+    uint32_t* hist_tile = nullptr;        // 8 x 2 x 256
+    unsigned long long* counters = nullptr;  // 2
+    uint32_t* status_depth = nullptr;     // 4 passes x sort_parts(N) x 256
+    unsigned long long* status_bin = nullptr;  // bin_parts(N)
+    // tile lists
+    uint64_t kcap = 0;
+    uint32_t *tkA = nullptr, *tvA = nullptr, *tkB = nullptr, *tvB = nullptr;
+    uint32_t* status_tile = nullptr;      // 2 passes x sort_parts(kcap) x 256
+    uint2* ranges = nullptr;
+    int ranges_cap = 0;
+    // last frame
+    uint64_t last_nvis = 0, last_k = 0;
+    bool have_frame = false;
+};
+
+static constexpr size_t kMetaTickets = 0, kMetaHistDepth = 64,
+                        kMetaHistTile = kMetaHistDepth + kHistShards * 1024 * 4,
+                        kMetaCounters = kMetaHistTile + kHistShards * 512 * 4,
+                        kMetaBytes = kMetaCounters + 64;
+
+static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
+    if (k <= s->kcap && s->tkA) return;
+    uint64_t cap = std::max<uint64_t>(k + k / 2, std::max<uint64_t>(1u << 20, s->kcap));
+    if (cap > 0xFFFFFFFFull) cap = std::max<uint64_t>(k, 0xFFFFFFFFull);
+    if (k > 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "more than 2^32 tile entries");
+    dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB); dev_free(s->status_tile);
+    dev_alloc(s->tkA, cap); dev_alloc(s->tvA, cap); dev_alloc(s->tkB, cap); dev_alloc(s->tvB, cap);
+    dev_alloc(s->status_tile, 2 * (size_t)sort_parts(cap) * 256);
+    s->kcap = cap;
+}
+
+static void ensure_ranges(gs_scene* s, int n_tiles) {
+    if (n_tiles <= s->ranges_cap && s->ranges) return;
+    dev_free(s->ranges);
+    dev_alloc(s->ranges, (size_t)n_tiles);
+    s->ranges_cap = n_tiles;
+}
+
+static void ensure_out(gs_ctx* c, size_t bytes) {
+    if (bytes <= c->d_out_bytes && c->d_out) return;
+    if (c->d_out) (void)hipFree(c->d_out);
+    c->d_out = nullptr;
+    HIPCHK(hipMalloc(&c->d_out, bytes));
+    c->d_out_bytes = bytes;
+}
+
+// (P*V) in the reference's evaluation order (src/simple_render.ts:228, WGSL mat4 product).
+static void mat4_mul_ref(const float* A, const float* B, float* R) {
+#pragma clang fp contract(off)
+    for (int j = 0; j < 4; ++j)
+        for (int i = 0; i < 4; ++i)
+            R[4 * j + i] = ((A[i] * B[4 * j + 0] + A[4 + i] * B[4 * j + 1]) + A[8 + i] * B[4 * j + 2]) +
+                           A[12 + i] * B[4 * j + 3];
+}
+
+static void strip_geometry(int H, int si, int sc, int& tr_begin, int& tr_end, int& rows_padded) {
+    const int TR = (H + kTile - 1) / kTile;
+    const int per = (TR + sc - 1) / sc;
+    tr_begin = std::min(si * per, TR);
+    tr_end = std::min((si + 1) * per, TR);
+    rows_padded = per * kTile;
+}
+
+static void check_device_error(gs_ctx* c) {
+    uint32_t e = 0;
+    HIPCHK(hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
+    if (e) {
+        HIPCHK(hipMemset(c->d_err, 0, 4));
+        char buf[128];
+        snprintf(buf, sizeof buf, "device protocol failure (err bits 0x%x)", e);
+        throw GsError(GS_ERR_DEVICE_FAULT, buf);
+    }
+}
+
+// The per-frame pipeline.  `out` is device memory of rows_padded*W (strip) or H*W pixels.
+static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o,
+                         void* out, hipStream_t st) {
+    int tr_begin, tr_end, rows_padded;
+    const int sc = std::max(1, o.strip_count);
+    strip_geometry(H, o.strip_index, sc, tr_begin, tr_end, rows_padded);
+    const int TX = (W + kTile - 1) / kTile;
+    const int n_tiles = TX * (tr_end - tr_begin);
+    const bool timed = o.timing != 0;
+    if (timed) HIPCHK(hipEventRecord(c->ev[EV_BEGIN], st));
+
+    HIPCHK(hipMemsetAsync(s->meta, 0, kMetaBytes, st));
+    HIPCHK(hipMemsetAsync(c->d_err, 0, 4, st));
+    ProjParams pp{};
+    pp.planes = s->planes;
+    pp.plane_stride = s->stride;
+    pp.n = (uint32_t)s->n;
+    pp.n_sh = s->n_sh;
+    std::memcpy(pp.V, uni + 0, 64);
+    mat4_mul_ref(uni + 16, uni + 0, pp.PV);
+    std::memcpy(pp.cam, uni + 32, 12);
+    pp.scale_mod = uni[39];
+    pp.P00 = uni[16];
+    pp.P11 = uni[21];
+    pp.W = W;
+    pp.H = H;
+    pp.tile_row_begin = tr_begin;
+    pp.tile_row_end = tr_end;
+    pp.tiles_x = TX;
+    pp.keys_out = s->keysB;
+    pp.rec = s->rec;
+    pp.hist = s->hist_depth;
+    pp.counters = s->counters;
+    const int grid = (int)std::min<uint64_t>(2048, std::max<uint64_t>(1, (s->n + kProjThreads - 1) / kProjThreads));
+    if (n_tiles > 0 && s->n > 0) launch_project(pp, grid, st);
+    if (timed) HIPCHK(hipEventRecord(c->ev[EV_PROJECT], st));
+
+    // n_vis and K size the rest of the frame
+    HIPCHK(hipMemcpyAsync(c->h_pinned, s->counters, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const unsigned long long* hc = (const unsigned long long*)c->h_pinned;
+    const uint64_t n_vis = (n_tiles > 0) ? hc[0] : 0, K = (n_tiles > 0) ? hc[1] : 0;
+    ensure_tile_capacity(s, K);
+    ensure_ranges(s, std::max(n_tiles, 1));
+
+    const uint32_t parts_n = sort_parts(s->n), parts_v = sort_parts(n_vis);
+    // look-back words: pass 0 over N, passes 1-3 over n_vis; bin over n_vis; tile passes over K
+    HIPCHK(hipMemsetAsync(s->status_depth, 0, (size_t)(parts_n + 3 * (size_t)parts_v) * 1024, st));
+    HIPCHK(hipMemsetAsync(s->status_bin, 0, (size_t)bin_parts(n_vis) * 8 + 8, st));
+    HIPCHK(hipMemsetAsync(s->status_tile, 0, (size_t)2 * sort_parts(K) * 1024 + 4, st));
+
+    if (n_vis > 0) {
+        // ---- depth sort: keysB(N, sentinel-filtered) -> A -> B -> A -> B
+        const uint32_t* kin[4] = {s->keysB, s->keysA, s->keysB, s->keysA};
+        const uint32_t* vin[4] = {nullptr, s->valsA, s->valsB, s->valsA};
+        uint32_t* kout[4] = {s->keysA, s->keysB, s->keysA, s->keysB};
+        uint32_t* vout[4] = {s->valsA, s->valsB, s->valsA, s->valsB};
+        size_t status_off = 0;
+        for (int ps = 0; ps < 4; ++ps) {
+            SortPass sp{};
+            sp.keys_in = kin[ps];
+            sp.vals_in = vin[ps];
+            sp.keys_out = kout[ps];
+            sp.vals_out = vout[ps];
+            sp.n = (uint32_t)(ps == 0 ? s->n : n_vis);
+            sp.shift = 8 * ps;
+            sp.mask = 255;
+            sp.filter_sentinel = ps == 0;
+            sp.hist = s->hist_depth + 256 * ps;
+            sp.hist_stride = 1024;
+            sp.status = s->status_depth + status_off;
+            sp.ticket = s->tickets + ps;
+            sp.err = c->d_err;
+            launch_sort_pass(sp, st);
+            status_off += (size_t)sort_parts(sp.n) * 256;
+        }
+        if (timed) HIPCHK(hipEventRecord(c->ev[EV_SORT], st));
+
+        // ---- binning in depth order
+        BinParams bp{};
+        bp.sorted_vals = s->valsB;
+        bp.rec = s->rec;
+        bp.n_vis = (uint32_t)n_vis;
+        bp.tile_row_begin = tr_begin;
+        bp.tiles_x = TX;
+        bp.capacity = s->kcap;
+        bp.tkeys = s->tkA;
+        bp.tvals = s->tvA;
+        bp.hist = s->hist_tile;
+        bp.status = s->status_bin;
+        bp.ticket = s->tickets + 4;
+        bp.err = c->d_err;
+        launch_bin(bp, st);
+        if (timed) HIPCHK(hipEventRecord(c->ev[EV_BIN], st));
+
+        // ---- stable sort of (tile, splat) by tile id
+        const int tile_passes = n_tiles > 256 ? 2 : 1;
+        uint32_t *tk_in = s->tkA, *tv_in = s->tvA, *tk_out = s->tkB, *tv_out = s->tvB;
+        for (int ps = 0; ps < tile_passes; ++ps) {
+            SortPass sp{};
+            sp.keys_in = tk_in;
+            sp.vals_in = tv_in;
+            sp.keys_out = tk_out;
+            sp.vals_out = tv_out;
+            sp.n = (uint32_t)K;
+            sp.shift = 8 * ps;
+            sp.mask = 255;
+            sp.filter_sentinel = 0;
+            sp.hist = s->hist_tile + 256 * ps;
+            sp.hist_stride = 512;
+            sp.status = s->status_tile + (size_t)ps * sort_parts(K) * 256;
+            sp.ticket = s->tickets + 5 + ps;
+            sp.err = c->d_err;
+            launch_sort_pass(sp, st);
+            std::swap(tk_in, tk_out);
+            std::swap(tv_in, tv_out);
+        }
+        if (timed) HIPCHK(hipEventRecord(c->ev[EV_TSORT], st));
+        HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)n_tiles * sizeof(uint2), st));
+        launch_ranges(tk_in, K, s->ranges, st);
+        if (timed) HIPCHK(hipEventRecord(c->ev[EV_RANGES], st));
+
+        CompositeParams cp{};
+        cp.ranges = s->ranges;
+        cp.tvals = tv_in;
+        cp.rec = s->rec;
+        cp.W = W;
+        cp.H = H;
+        cp.tiles_x = TX;
+        cp.tile_row_begin = tr_begin;
+        cp.row0 = sc > 1 ? tr_begin * kTile : 0;
+        cp.n_tiles = n_tiles;
+        cp.t_min = o.t_min;
+        cp.out = out;
+        cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
+        launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
+    } else {
+        if (timed) {
+            HIPCHK(hipEventRecord(c->ev[EV_SORT], st));
+            HIPCHK(hipEventRecord(c->ev[EV_BIN], st));
+            HIPCHK(hipEventRecord(c->ev[EV_TSORT], st));
+        }
+        HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)std::max(n_tiles, 1) * sizeof(uint2), st));
+        if (timed) HIPCHK(hipEventRecord(c->ev[EV_RANGES], st));
+        CompositeParams cp{};
+        cp.ranges = s->ranges;
+        cp.tvals = s->tvA;
+        cp.rec = s->rec;
+        cp.W = W;
+        cp.H = H;
+        cp.tiles_x = TX;
+        cp.tile_row_begin = tr_begin;
+        cp.row0 = sc > 1 ? tr_begin * kTile : 0;
+        cp.n_tiles = n_tiles;
+        cp.t_min = o.t_min;
+        cp.out = out;
+        cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
+        launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
+    }
+    HIPCHK(hipGetLastError());
+    if (timed) HIPCHK(hipEventRecord(c->ev[EV_COMPOSITE], st));
+    c->timed = timed;
+    c->timed_stream = st;
+    s->last_nvis = n_vis;
+    s->last_k = K;
+    s->have_frame = true;
+    c->stats.n = s->n;
+    c->stats.n_vis = n_vis;
+    c->stats.k_entries = K;
+    c->stats.tile_row_begin = tr_begin;
+    c->stats.tile_row_end = tr_end;
+    c->stats.tiles_x = TX;
+}
+
+static void validate_render_args(gs_ctx* c, gs_scene* s, const void* uni, int W, int H,
+                                 const gs_opts* o) {
+    if (!c || !s || !uni) throw GsError(GS_ERR_INVALID, "null ctx/scene/uniforms");
+    if (s->ctx != c) throw GsError(GS_ERR_INVALID, "scene belongs to another context");
+    if (W <= 0 || H <= 0 || W > 65535 * kTile || H > 65535 * kTile)
+        throw GsError(GS_ERR_INVALID, "bad image size");
+    if (o) {
+        if (o->strip_count < 1 || o->strip_index < 0 || o->strip_index >= o->strip_count)
+            throw GsError(GS_ERR_INVALID, "bad strip index/count");
+        if (o->accum != GS_ACCUM_FP32 && o->accum != GS_ACCUM_FP16_TARGET)
+            throw GsError(GS_ERR_INVALID, "bad accum mode");
+        if (o->out_format != GS_OUT_RGBA_F32 && o->out_format != GS_OUT_RGBA_F16)
+            throw GsError(GS_ERR_INVALID, "bad out_format");
+        if (!(o->t_min >= 0.0f && o->t_min < 1.0f)) throw GsError(GS_ERR_INVALID, "t_min must be in [0,1)");
+        if (o->ref_quirks) throw GsError(GS_ERR_UNSUPPORTED, "ref_quirks not built in this version");
+    }
+}
+
+static size_t out_bytes_for(int W, int H, const gs_opts& o) {
+    int tb, te, rows_padded;
+    strip_geometry(H, o.strip_index, std::max(1, o.strip_count), tb, te, rows_padded);
+    const size_t rows = o.strip_count > 1 ? (size_t)rows_padded : (size_t)H;
+    return rows * (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
+}
+
+extern "C" {
+
+int gs_abi_version(void) { return GS_ABI_VERSION; }
+const char* gs_last_error(void) { return g_last_error.c_str(); }
+
+int gs_device_count(int* out) {
+    return guarded([&] {
+        if (!out) throw GsError(GS_ERR_INVALID, "null out");
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        *out = n;
+        return GS_OK;
+    });
+}
+
+void gs_opts_default(gs_opts* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->struct_size = sizeof(gs_opts);
+    o->accum = GS_ACCUM_FP32;
+    o->out_format = GS_OUT_RGBA_F32;
+    o->t_min = 1e-4f;
+    o->strip_index = 0;
+    o->strip_count = 1;
+}
+
+int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
+    return guarded([&] {
+        if (!out) throw GsError(GS_ERR_INVALID, "null out");
+        *out = nullptr;
+        if (ndev != 1 && !(ndev == 0 && devices == nullptr))
+            throw GsError(GS_ERR_UNSUPPORTED, "one device per context (use one process per GPU)");
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+            throw GsError(GS_ERR_NO_DEVICE, "no HIP device available");
+        const int dev = devices ? devices[0] : 0;
+        if (dev < 0 || dev >= count) throw GsError(GS_ERR_INVALID, "device index out of range");
+        HIPCHK(hipSetDevice(dev));
+        gs_ctx* c = new gs_ctx();
+        c->device = dev;
+        try {
+            HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            dev_alloc(c->d_err, 4);
+            HIPCHK(hipMemset(c->d_err, 0, 4));
+            HIPCHK(hipHostMalloc((void**)&c->h_pinned, 64, hipHostMallocDefault));
+            for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+        } catch (...) {
+            gs_ctx_destroy(c);
+            throw;
+        }
+        *out = c;
+        return GS_OK;
+    });
+}
+
+void gs_ctx_destroy(gs_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    while (!c->scenes.empty()) gs_scene_free(c->scenes.back());
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->d_out) (void)hipFree(c->d_out);
+    dev_free(c->d_err);
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene** out) {
+    return guarded([&] {
+        if (!c || !out || (!aos && n)) throw GsError(GS_ERR_INVALID, "null argument");
+        *out = nullptr;
+        if (n_sh != 1 && n_sh != 4 && n_sh != 9 && n_sh != 16)
+            throw GsError(GS_ERR_UNSUPPORTED, "n_sh_coeffs must be 1, 4, 9 or 16");
+        if (n >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "scene larger than 2^32-1 Gaussians");
+        HIPCHK(hipSetDevice(c->device));
+        gs_scene* s = new gs_scene();
+        s->ctx = c;
+        s->n = n;
+        s->n_sh = n_sh;
+        try {
+            s->stride = round_up(std::max<uint64_t>(n, 1), 64);
+            dev_alloc(s->planes, (size_t)(11 + 3 * n_sh) * s->stride);
+            dev_alloc(s->keysA, n);
+            dev_alloc(s->valsA, n);
+            dev_alloc(s->keysB, n);
+            dev_alloc(s->valsB, n);
+            dev_alloc(s->rec, 4 * (size_t)std::max<uint64_t>(n, 1));
+            dev_alloc(s->meta, kMetaBytes);
+            s->tickets = (uint32_t*)(s->meta + kMetaTickets);
+            s->hist_depth = (uint32_t*)(s->meta + kMetaHistDepth);
+            s->hist_tile = (uint32_t*)(s->meta + kMetaHistTile);
+            s->counters = (unsigned long long*)(s->meta + kMetaCounters);
+            dev_alloc(s->status_depth, 4 * (size_t)sort_parts(n) * 256 + 256);
+            dev_alloc(s->status_bin, (size_t)bin_parts(n) + 1);
+            ensure_tile_capacity(s, 4 * n + (1u << 20));
+            // AoS -> SoA on device, in chunks of 4M records
+            const uint64_t rb = 64 + 16 * (uint64_t)n_sh;
+            const uint64_t chunk = std::min<uint64_t>(n, 1u << 22);
+            uint8_t* tmp = nullptr;
+            if (n) dev_alloc(tmp, chunk * rb);
+            for (uint64_t i0 = 0; i0 < n; i0 += chunk) {
+                const uint64_t m = std::min(chunk, n - i0);
+                HIPCHK(hipMemcpyAsync(tmp, (const uint8_t*)aos + i0 * rb, m * rb, hipMemcpyHostToDevice,
+                                      c->stream));
+                launch_transpose(tmp, m, n_sh, s->planes + i0, s->stride, c->stream);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipStreamSynchronize(c->stream));
+            }
+            dev_free(tmp);
+        } catch (...) {
+            gs_scene_free(s);
+            throw;
+        }
+        c->scenes.push_back(s);
+        *out = s;
+        return GS_OK;
+    });
+}
+
+void gs_scene_free(gs_scene* s) {
+    if (!s) return;
+    if (s->ctx) {
+        (void)hipSetDevice(s->ctx->device);
+        (void)hipStreamSynchronize(s->ctx->stream);
+        auto& v = s->ctx->scenes;
+        v.erase(std::remove(v.begin(), v.end(), s), v.end());
+    }
+    dev_free(s->planes);
+    dev_free(s->keysA); dev_free(s->valsA); dev_free(s->keysB); dev_free(s->valsB);
+    dev_free(s->rec);
+    dev_free(s->meta);
+    dev_free(s->status_depth);
+    dev_free(s->status_bin);
+    dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB);
+    dev_free(s->status_tile);
+    dev_free(s->ranges);
+    delete s;
+}
+
+uint64_t gs_scene_count(const gs_scene* s) { return s ? s->n : 0; }
+
+int gs_strip_rows(int H, int si, int sc, int* row0, int* rows_padded) {
+    return guarded([&] {
+        if (H <= 0 || sc < 1 || si < 0 || si >= sc || !row0 || !rows_padded)
+            throw GsError(GS_ERR_INVALID, "bad strip arguments");
+        int tb, te, rp;
+        strip_geometry(H, si, sc, tb, te, rp);
+        *row0 = tb * kTile;
+        *rows_padded = rp;
+        return GS_OK;
+    });
+}
+
+int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_opts* opts,
+                     void* out_dev, uint64_t out_bytes, void* stream) {
+    return guarded([&] {
+        validate_render_args(c, s, uni, W, H, opts);
+        gs_opts o;
+        gs_opts_default(&o);
+        if (opts) o = *opts;
+        if (!out_dev) throw GsError(GS_ERR_INVALID, "null output");
+        if (out_bytes < out_bytes_for(W, H, o)) throw GsError(GS_ERR_INVALID, "output buffer too small");
+        HIPCHK(hipSetDevice(c->device));
+        hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+        render_frame(c, s, (const float*)uni, W, H, o, out_dev, st);
+        return GS_OK;
+    });
+}
+
+int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_opts* opts, void* out_host) {
+    return guarded([&] {
+        validate_render_args(c, s, uni, W, H, opts);
+        gs_opts o;
+        gs_opts_default(&o);
+        if (opts) o = *opts;
+        HIPCHK(hipSetDevice(c->device));
+        const size_t bytes = out_bytes_for(W, H, o);
+        ensure_out(c, bytes);
+        render_frame(c, s, (const float*)uni, W, H, o, c->d_out, c->stream);
+        if (out_host) HIPCHK(hipMemcpyAsync(out_host, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        check_device_error(c);
+        return GS_OK;
+    });
+}
+
+int gs_sync(gs_ctx* c) {
+    return guarded([&] {
+        if (!c) throw GsError(GS_ERR_INVALID, "null ctx");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipDeviceSynchronize());
+        check_device_error(c);
+        return GS_OK;
+    });
+}
+
+int gs_timings(gs_ctx* c, gs_stats* out) {
+    return guarded([&] {
+        if (!c || !out) throw GsError(GS_ERR_INVALID, "null argument");
+        HIPCHK(hipSetDevice(c->device));
+        gs_stats st = c->stats;
+        st.ms_total = st.ms_project = st.ms_sort = st.ms_bin = st.ms_tile_sort = st.ms_ranges =
+            st.ms_composite = st.ms_other = 0.0f;
+        if (c->timed) {
+            HIPCHK(hipEventSynchronize(c->ev[EV_COMPOSITE]));
+            auto el = [&](int a, int b) {
+                float ms = 0;
+                HIPCHK(hipEventElapsedTime(&ms, c->ev[a], c->ev[b]));
+                return ms;
+            };
+            st.ms_total = el(EV_BEGIN, EV_COMPOSITE);
+            st.ms_project = el(EV_BEGIN, EV_PROJECT);
+            st.ms_sort = el(EV_PROJECT, EV_SORT);
+            st.ms_bin = el(EV_SORT, EV_BIN);
+            st.ms_tile_sort = el(EV_BIN, EV_TSORT);
+            st.ms_ranges = el(EV_TSORT, EV_RANGES);
+            st.ms_composite = el(EV_RANGES, EV_COMPOSITE);
+        }
+        *out = st;
+        return GS_OK;
+    });
+}
+
+int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit, int end_bit) {
+    return guarded([&] {
+        if (!c || (!keys && n) || (!vals && n)) throw GsError(GS_ERR_INVALID, "null argument");
+        if (begin_bit < 0 || end_bit > 32 || begin_bit >= end_bit) throw GsError(GS_ERR_INVALID, "bad bit range");
+        if (n >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "n too large");
+        if (n == 0) return GS_OK;
+        HIPCHK(hipSetDevice(c->device));
+        const int npass = (end_bit - begin_bit + 7) / 8;
+        uint32_t *kA, *vA, *kB, *vB, *hist, *status, *tick;
+        dev_alloc(kA, n); dev_alloc(vA, n); dev_alloc(kB, n); dev_alloc(vB, n);
+        dev_alloc(hist, (size_t)kHistShards * npass * 256);
+        dev_alloc(status, (size_t)npass * sort_parts(n) * 256);
+        dev_alloc(tick, 8);
+        hipStream_t st = c->stream;
+        HIPCHK(hipMemcpyAsync(kA, keys, n * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(vA, vals, n * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(hist, 0, (size_t)kHistShards * npass * 256 * 4, st));
+        HIPCHK(hipMemsetAsync(status, 0, (size_t)npass * sort_parts(n) * 1024, st));
+        HIPCHK(hipMemsetAsync(tick, 0, 32, st));
+        HIPCHK(hipMemsetAsync(c->d_err, 0, 4, st));
+        // histogram of each pass's digit, masked to the bit range
+        launch_hist_keys(kA, (uint32_t)n, begin_bit, end_bit, npass, hist, st);
+        uint32_t *ki = kA, *vi = vA, *ko = kB, *vo = vB;
+        for (int ps = 0; ps < npass; ++ps) {
+            SortPass sp{};
+            sp.keys_in = ki; sp.vals_in = vi; sp.keys_out = ko; sp.vals_out = vo;
+            sp.n = (uint32_t)n;
+            sp.shift = begin_bit + 8 * ps;
+            const int bits = std::min(8, end_bit - sp.shift);
+            sp.mask = (1u << bits) - 1u;
+            sp.filter_sentinel = 0;
+            sp.hist = hist + 256 * ps;
+            sp.hist_stride = npass * 256;
+            sp.status = status + (size_t)ps * sort_parts(n) * 256;
+            sp.ticket = tick + ps;
+            sp.err = c->d_err;
+            launch_sort_pass(sp, st);
+            std::swap(ki, ko);
+            std::swap(vi, vo);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(keys, ki, n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(vals, vi, n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        dev_free(kA); dev_free(vA); dev_free(kB); dev_free(vB); dev_free(hist); dev_free(status); dev_free(tick);
+        check_device_error(c);
+        return GS_OK;
+    });
+}
+
+int gs_debug_last_order(gs_ctx* c, gs_scene* s, uint32_t* out_keys, uint32_t* out_index, uint64_t cap,
+                        uint64_t* out_n) {
+    return guarded([&] {
+        if (!c || !s || !out_n) throw GsError(GS_ERR_INVALID, "null argument");
+        if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        *out_n = s->last_nvis;
+        const uint64_t m = std::min(cap, s->last_nvis);
+        if (m && out_keys) HIPCHK(hipMemcpy(out_keys, s->keysB, m * 4, hipMemcpyDeviceToHost));
+        if (m && out_index) HIPCHK(hipMemcpy(out_index, s->valsB, m * 4, hipMemcpyDeviceToHost));
+        return GS_OK;
+    });
+}
+
+int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
+    return guarded([&] {
+        if (!c || !s || !out16) throw GsError(GS_ERR_INVALID, "null argument");
+        if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        const uint64_t m = std::min(cap, s->n);
+        if (m) HIPCHK(hipMemcpy(out16, s->rec, m * 64, hipMemcpyDeviceToHost));
+        return GS_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,282 @@
+"""ctypes binding of libgsplat.so (include/gsplat.h) for tests and bench.py.
+
+The user-facing host of this renderer is the reference's own TypeScript surface
+(`GpuContext` / `Renderer`, ts/ + addon/); this module is the same C ABI seen from Python.
+There is no CPU fallback: importing works without a GPU (the library loads), but every render
+call needs a HIP device and fails loudly otherwise.
+"""
+import atexit
+import ctypes
+import os
+import sys
+import weakref
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libgsplat.so")
+
+GS_OK = 0
+GS_ACCUM_FP32, GS_ACCUM_FP16_TARGET = 0, 1
+GS_OUT_RGBA_F32, GS_OUT_RGBA_F16 = 0, 1
+
+# every symbol include/gsplat.h declares
+EXPORTED_SYMBOLS = (
+    "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy",
+    "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows",
+    "gs_render", "gs_render_device", "gs_timings", "gs_sync", "gs_present", "gs_look_at",
+    "gs_perspective", "gs_camera_position", "gs_pack_uniforms", "gs_synth_aos",
+    "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records",
+)
+
+
+class GsOpts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("accum", ctypes.c_int32),
+                ("out_format", ctypes.c_int32), ("t_min", ctypes.c_float),
+                ("ref_quirks", ctypes.c_int32), ("strip_index", ctypes.c_int32),
+                ("strip_count", ctypes.c_int32), ("timing", ctypes.c_int32)]
+
+
+class GsStats(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("n_vis", ctypes.c_uint64), ("k_entries", ctypes.c_uint64),
+                ("tile_row_begin", ctypes.c_int32), ("tile_row_end", ctypes.c_int32),
+                ("tiles_x", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+                ("ms_total", ctypes.c_float), ("ms_project", ctypes.c_float),
+                ("ms_sort", ctypes.c_float), ("ms_bin", ctypes.c_float),
+                ("ms_tile_sort", ctypes.c_float), ("ms_ranges", ctypes.c_float),
+                ("ms_composite", ctypes.c_float), ("ms_other", ctypes.c_float)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved0"}
+
+
+class GsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("gsplat error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+_LIVE = weakref.WeakSet()  # open contexts, closed (with their scenes) at interpreter exit
+
+
+@atexit.register
+def _close_all():
+    for c in list(_LIVE):
+        c.close()
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libgsplat.so not built (run `make -C gaussian-splatting-web_amd`): %s" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        P, U64, I, F, D = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_float, ctypes.c_double
+        L.gs_last_error.restype = ctypes.c_char_p
+        L.gs_ctx_create.argtypes = [P, I, ctypes.POINTER(P)]
+        L.gs_ctx_destroy.argtypes = [P]
+        L.gs_ctx_destroy.restype = None
+        L.gs_scene_upload.argtypes = [P, P, U64, I, ctypes.POINTER(P)]
+        L.gs_scene_free.argtypes = [P]
+        L.gs_scene_free.restype = None
+        L.gs_scene_count.argtypes = [P]
+        L.gs_scene_count.restype = U64
+        L.gs_opts_default.argtypes = [ctypes.POINTER(GsOpts)]
+        L.gs_opts_default.restype = None
+        L.gs_strip_rows.argtypes = [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]
+        L.gs_render.argtypes = [P, P, P, I, I, ctypes.POINTER(GsOpts), P]
+        L.gs_render_device.argtypes = [P, P, P, I, I, ctypes.POINTER(GsOpts), P, U64, P]
+        L.gs_timings.argtypes = [P, ctypes.POINTER(GsStats)]
+        L.gs_sync.argtypes = [P]
+        L.gs_present.argtypes = [P, I, I, P]
+        L.gs_look_at.argtypes = [P, P, P, P]
+        L.gs_perspective.argtypes = [D, D, D, D, P]
+        L.gs_camera_position.argtypes = [P, P]
+        L.gs_pack_uniforms.argtypes = [P, P, P, F, F, F, F, F, P]
+        L.gs_synth_aos.argtypes = [U64, U64, I, I, P]
+        L.gs_debug_sort_pairs.argtypes = [P, P, P, U64, I, I]
+        L.gs_debug_last_order.argtypes = [P, P, P, P, U64, ctypes.POINTER(U64)]
+        L.gs_debug_last_records.argtypes = [P, P, P, U64]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != GS_OK:
+        raise GsError(rc, lib().gs_last_error().decode(errors="replace"))
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------ camera / uniforms (host)
+def look_at(eye, target, up=(0.0, 1.0, 0.0)):
+    out = np.zeros(16, np.float32)
+    e, t, u = (np.ascontiguousarray(v, np.float64) for v in (eye, target, up))
+    _check(lib().gs_look_at(_ptr(e), _ptr(t), _ptr(u), _ptr(out)))
+    return out
+
+
+def perspective(fovy, aspect, z_near, z_far):
+    out = np.zeros(16, np.float32)
+    _check(lib().gs_perspective(float(fovy), float(aspect), float(z_near), float(z_far), _ptr(out)))
+    return out
+
+
+def camera_position(view):
+    v = np.ascontiguousarray(view, np.float32)
+    out = np.zeros(3, np.float32)
+    _check(lib().gs_camera_position(_ptr(v), _ptr(out)))
+    return out
+
+
+def pack_uniforms(view, proj, cam_pos=None, tan_half_fov=(0.0, 0.0), focal=(0.0, 0.0), scale_modifier=1.0):
+    v = np.ascontiguousarray(view, np.float32)
+    p = np.ascontiguousarray(proj, np.float32)
+    c = camera_position(v) if cam_pos is None else np.ascontiguousarray(cam_pos, np.float32)
+    out = np.zeros(40, np.float32)
+    _check(lib().gs_pack_uniforms(_ptr(v), _ptr(p), _ptr(c), float(tan_half_fov[0]), float(tan_half_fov[1]),
+                                  float(focal[0]), float(focal[1]), float(scale_modifier), _ptr(out)))
+    return out
+
+
+def bench_uniforms(W, H):
+    """SURVEY §8d synthetic-scene camera: lookAt([0,0,0],[0,0,-1],[0,1,0]), perspective(60deg,W/H,.03,1000)."""
+    view = look_at((0.0, 0.0, 0.0), (0.0, 0.0, -1.0))
+    proj = perspective(1.04719755, W / H, 0.03, 1000.0)
+    return pack_uniforms(view, proj, focal=(W, H))
+
+
+def synth_aos(n, seed, W=1920, H=1080):
+    """Seeded synthetic scene as reference AoS records (320 B each, SH degree 3)."""
+    out = np.empty(n * 80, np.float32)
+    _check(lib().gs_synth_aos(int(n), int(seed), int(W), int(H), _ptr(out)))
+    return out
+
+
+def present(rgba, W, H):
+    src = np.ascontiguousarray(rgba, np.float32).reshape(-1)
+    out = np.empty_like(src)
+    _check(lib().gs_present(_ptr(src), int(W), int(H), _ptr(out)))
+    return out.reshape(H, W, 4)
+
+
+def strip_rows(H, strip_index, strip_count):
+    r0, rp = ctypes.c_int(), ctypes.c_int()
+    _check(lib().gs_strip_rows(int(H), int(strip_index), int(strip_count), ctypes.byref(r0), ctypes.byref(rp)))
+    return r0.value, rp.value
+
+
+def device_count():
+    n = ctypes.c_int()
+    _check(lib().gs_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def make_opts(accum=GS_ACCUM_FP32, out_format=GS_OUT_RGBA_F32, t_min=1e-4, strip_index=0, strip_count=1,
+              timing=0, ref_quirks=0):
+    o = GsOpts()
+    lib().gs_opts_default(ctypes.byref(o))
+    o.accum, o.out_format, o.t_min = accum, out_format, t_min
+    o.strip_index, o.strip_count, o.timing, o.ref_quirks = strip_index, strip_count, timing, ref_quirks
+    return o
+
+
+# ------------------------------------------------------------------ context / scene / render
+class Context:
+    """GpuContext equivalent: one HIP device."""
+
+    def __init__(self, device=0):
+        self.handle = ctypes.c_void_p()
+        self.scenes = weakref.WeakSet()
+        dev = (ctypes.c_int * 1)(device)
+        _check(lib().gs_ctx_create(dev, 1, ctypes.byref(self.handle)))
+        _LIVE.add(self)
+
+    def close(self):
+        # scenes first: the C side frees attached scenes with the context anyway, but the
+        # Python objects must forget their handles before that happens
+        for sc in list(self.scenes):
+            sc.close()
+        if self.handle:
+            lib().gs_ctx_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        if not sys.is_finalizing():
+            self.close()
+
+    def sync(self):
+        _check(lib().gs_sync(self.handle))
+
+    def timings(self):
+        st = GsStats()
+        _check(lib().gs_timings(self.handle, ctypes.byref(st)))
+        return st.as_dict()
+
+    def sort_pairs(self, keys, vals, begin_bit=0, end_bit=32):
+        k = np.array(keys, np.uint32, copy=True)
+        v = np.array(vals, np.uint32, copy=True)
+        assert k.shape == v.shape
+        _check(lib().gs_debug_sort_pairs(self.handle, _ptr(k), _ptr(v), k.size, begin_bit, end_bit))
+        return k, v
+
+
+class Scene:
+    def __init__(self, ctx, aos, n, n_sh=16):
+        self.ctx = ctx
+        self.n = int(n)
+        buf = np.ascontiguousarray(np.frombuffer(aos, np.uint8) if not isinstance(aos, np.ndarray) else aos)
+        assert buf.nbytes == self.n * (64 + 16 * n_sh), (buf.nbytes, n, n_sh)
+        self.handle = ctypes.c_void_p()
+        _check(lib().gs_scene_upload(ctx.handle, _ptr(buf), self.n, int(n_sh), ctypes.byref(self.handle)))
+        ctx.scenes.add(self)
+
+    def close(self):
+        if self.handle and self.ctx.handle:
+            lib().gs_scene_free(self.handle)
+        self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        if not sys.is_finalizing():
+            self.close()
+
+    def render(self, uniforms, W, H, opts=None):
+        o = opts if opts is not None else make_opts()
+        rows = H if o.strip_count <= 1 else strip_rows(H, o.strip_index, o.strip_count)[1]
+        if o.out_format == GS_OUT_RGBA_F16:
+            out = np.empty((rows, W, 4), np.float16)
+        else:
+            out = np.empty((rows, W, 4), np.float32)
+        u = np.ascontiguousarray(uniforms, np.float32)
+        _check(lib().gs_render(self.ctx.handle, self.handle, _ptr(u), int(W), int(H), ctypes.byref(o), _ptr(out)))
+        return out
+
+    def render_device(self, uniforms, W, H, out_ptr, out_bytes, stream_ptr=None, opts=None):
+        o = opts if opts is not None else make_opts()
+        u = np.ascontiguousarray(uniforms, np.float32)
+        _check(lib().gs_render_device(self.ctx.handle, self.handle, _ptr(u), int(W), int(H), ctypes.byref(o),
+                                      ctypes.c_void_p(out_ptr), int(out_bytes),
+                                      ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def last_order(self):
+        n = ctypes.c_uint64()
+        _check(lib().gs_debug_last_order(self.ctx.handle, self.handle, None, None, 0, ctypes.byref(n)))
+        keys = np.empty(n.value, np.uint32)
+        idx = np.empty(n.value, np.uint32)
+        _check(lib().gs_debug_last_order(self.ctx.handle, self.handle, _ptr(keys), _ptr(idx), n.value,
+                                         ctypes.byref(n)))
+        return keys, idx
+
+    def last_records(self):
+        out = np.empty((self.n, 16), np.float32)
+        _check(lib().gs_debug_last_records(self.ctx.handle, self.handle, _ptr(out), self.n))
+        return out

@@ -1,0 +1,160 @@
+/* gsplat.h — C ABI of the MI355X Gaussian-splat forward renderer (libgsplat.so).
+ *
+ * Drop-in boundary for the WebGPU path of Lontoone/gaussian-splatting-web (reference @ 2024-12-20,
+ * paths relative to /root/reference).  The reference binds its GPU work through WebGPU objects
+ * owned by `GpuContext` and `Renderer`; this ABI is what the Node N-API addon
+ * (gaussian-splatting-web_amd/addon/gsplat_napi.cc) binds in their place:
+ *
+ *   gs_ctx_create / gs_ctx_destroy  <- GpuContext.create / GpuContext.destroy  (src/gpu_context.ts:12-32)
+ *                                      Renderer.requestContext                (src/renderer.ts:79-100)
+ *   gs_scene_upload / gs_scene_free <- Renderer ctor's pointDataBuffer upload (src/renderer.ts:139-146)
+ *                                      and destroyImpl's buffer destroys      (src/renderer.ts:281-292)
+ *   gs_render / gs_render_device    <- Renderer.draw: init-sort pass + radix sort + SimpleRender.draw
+ *                                      (src/renderer.ts:301-319, src/shaders.ts:42-73,
+ *                                       src/simple_render.ts:217-332, :169-200, :509-537)
+ *   gs_pack_uniforms                <- uniformLayout.pack in Renderer.animate  (src/renderer.ts:24-33, :349-384)
+ *   gs_look_at / gs_perspective /
+ *   gs_camera_position              <- wgpu-matrix lookAt/perspective/inverse+getTranslation as used by
+ *                                      src/camera.ts:101-138 (f32 storage semantics)
+ *   gs_present                      <- PostProcessRenderer.draw               (src/post_process_render.ts:54-77)
+ *
+ * Conventions: every function returns 0 on success and a negative gs_status on failure; no C++
+ * exception crosses the ABI; gs_last_error() returns a thread-local message for the last failure.
+ * One gs_ctx per host thread; calls on a ctx are serialised by the caller.
+ *
+ * Scene input = the reference's AoS record (PackedGaussians.gaussiansBuffer, src/ply.ts:249-257):
+ *   position f32x3 @0, scale f32x3 @16 (already |exp(s)|), rot f32x4 @32 (= (-x,-y,-z,w) of the
+ *   normalised PLY quaternion), opacityLogit f32 @48, sh[n_sh] f32x3 @64 + 16k; record size
+ *   64 + 16*n_sh bytes, n_sh in {1,4,9,16}.  The host buffer is borrowed for the call only.
+ * Uniforms = the reference's 160-byte block (view mat4 @0, proj mat4 @64, camPos vec3 @128,
+ *   tanHalfFovX/Y @140/144, focalX/Y @148/152, scaleModifier @156; matrices column-major).
+ * Output = W*H premultiplied RGBA in framebuffer row order (row 0 = top), i.e. the contents of
+ *   SimpleRender.framebuffer (src/simple_render.ts:499-505), as f32x4 (or f16x4) per pixel.
+ */
+#ifndef GSPLAT_H
+#define GSPLAT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+typedef struct gs_ctx gs_ctx;
+typedef struct gs_scene gs_scene;
+
+typedef enum gs_status {
+    GS_OK = 0,
+    GS_ERR_INVALID = -1,     /* bad argument */
+    GS_ERR_NO_DEVICE = -2,   /* no HIP device (GpuContext.create rejects) */
+    GS_ERR_HIP = -3,         /* HIP runtime error */
+    GS_ERR_OOM = -4,         /* device allocation failed */
+    GS_ERR_UNSUPPORTED = -5, /* e.g. SH coefficient count not in {1,4,9,16} */
+    GS_ERR_DEVICE_FAULT = -6,/* a kernel reported a protocol failure (bounded spin expired) */
+    GS_ERR_INTERNAL = -7
+} gs_status;
+
+typedef enum gs_accum {
+    GS_ACCUM_FP32 = 0,        /* fp32 accumulation (default) */
+    GS_ACCUM_FP16_TARGET = 1  /* round dst to fp16 after every blend, as the rgba16float target does */
+} gs_accum;
+
+typedef enum gs_out_format {
+    GS_OUT_RGBA_F32 = 0,
+    GS_OUT_RGBA_F16 = 1
+} gs_out_format;
+
+typedef struct gs_opts {
+    uint32_t struct_size; /* sizeof(gs_opts); set by gs_opts_default */
+    int32_t accum;        /* gs_accum */
+    int32_t out_format;   /* gs_out_format */
+    float t_min;          /* a pixel stops compositing once (1 - alpha) < t_min; 0 = never (default 1e-4) */
+    int32_t ref_quirks;   /* 1: reproduce the reference's init-sort grid truncation (src/renderer.ts:306):
+                             only trunc(max(N/8,8))*8 slots are keyed per frame, the rest keep the previous
+                             frame's sorted (key,value) (zero on the first frame).  State lives in the scene. */
+    int32_t strip_index;  /* row strip rendered by this call, 0 <= strip_index < strip_count */
+    int32_t strip_count;  /* number of equal row strips (16-px tile rows, see gs_strip_rows); 1 = whole image */
+    int32_t timing;       /* 1: record per-stage hipEvent timings (gs_timings) */
+} gs_opts;
+
+typedef struct gs_stats {
+    uint64_t n;           /* Gaussians in the scene */
+    uint64_t n_vis;       /* splats that reach the sort (visible in this strip) */
+    uint64_t k_entries;   /* (tile, splat) pairs binned */
+    int32_t tile_row_begin, tile_row_end;  /* tile rows rendered by the last call */
+    int32_t tiles_x, reserved0;
+    float ms_total;       /* stage times of the last timed gs_render* (0 if timing was off) */
+    float ms_project, ms_sort, ms_bin, ms_tile_sort, ms_ranges, ms_composite, ms_other;
+} gs_stats;
+
+/* ---- library / device ---------------------------------------------------------------------- */
+int gs_abi_version(void);
+const char* gs_last_error(void);
+int gs_device_count(int* out_count);
+
+/* GpuContext.create: rejects (GS_ERR_NO_DEVICE) when no HIP device exists.  ndev == 1 for now;
+ * `devices` may be NULL (device 0). */
+int gs_ctx_create(const int* devices, int ndev, gs_ctx** out_ctx);
+/* Also frees every scene still attached to the context (do not free those scenes afterwards). */
+void gs_ctx_destroy(gs_ctx* ctx);
+
+/* Copies the AoS scene once into device memory as SoA planes (AoS -> SoA transpose on device). */
+int gs_scene_upload(gs_ctx* ctx, const void* aos, uint64_t n, int n_sh_coeffs, gs_scene** out_scene);
+void gs_scene_free(gs_scene* scene);
+uint64_t gs_scene_count(const gs_scene* scene);
+
+void gs_opts_default(gs_opts* opts);
+
+/* Rows of image covered by strip `strip_index` of `strip_count`: tile rows
+ * [s*ceil(TR/G), min((s+1)*ceil(TR/G), TR)), TR = ceil(H/16).  *row0 = first image row,
+ * *rows_padded = ceil(TR/G)*16 (every strip's output buffer has this many rows, so an
+ * all-gather of the G strip buffers is the image followed by padding rows). */
+int gs_strip_rows(int H, int strip_index, int strip_count, int* row0, int* rows_padded);
+
+/* Render one frame.  out_host_or_null: W*H pixels (strip_count == 1) or rows_padded*W pixels
+ * (strip mode) of the chosen out_format, or NULL to keep the frame on the device.  Synchronous. */
+int gs_render(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int W, int H,
+              const gs_opts* opts, void* out_host_or_null);
+
+/* Same, writing into device memory `out_dev` (>= out_bytes) on `hip_stream` (NULL = the ctx's
+ * stream).  Returns when the work is enqueued; the caller synchronises the stream. */
+int gs_render_device(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int W, int H,
+                     const gs_opts* opts, void* out_dev, uint64_t out_bytes, void* hip_stream);
+
+int gs_timings(gs_ctx* ctx, gs_stats* out_stats);
+int gs_sync(gs_ctx* ctx);
+
+/* PostProcessRenderer (src/post_process_render.ts:54-77) on the host-visible image: y flip,
+ * a' = sat(1.5a), a' = a'^4 if a' < 0.99.  rgba_in/out: W*H f32x4 host buffers. */
+int gs_present(const float* rgba_in, int W, int H, float* rgba_out);
+
+/* ---- camera / uniforms (headless producer; wgpu-matrix 2.9.1 semantics, f32 storage) ------- */
+int gs_look_at(const double eye[3], const double target[3], const double up[3], float out_view[16]);
+int gs_perspective(double fovy_radians, double aspect, double z_near, double z_far, float out_proj[16]);
+int gs_camera_position(const float view[16], float out_pos[3]);
+int gs_pack_uniforms(const float view[16], const float proj[16], const float cam_pos[3],
+                     float tan_half_fov_x, float tan_half_fov_y, float focal_x, float focal_y,
+                     float scale_modifier, void* out160);
+
+/* ---- synthetic scenes (seeded splitmix64) -------------------------------------- */
+/* Writes n records of 320 bytes (SH degree 3) in the reference AoS layout. */
+int gs_synth_aos(uint64_t n, uint64_t seed, int W, int H, void* out_aos);
+
+/* ---- checks used by tests ------------------------------------------------------------------ */
+/* Stable ascending GPU radix sort of (key,value) on bits [begin_bit,end_bit): host in/out. */
+int gs_debug_sort_pairs(gs_ctx* ctx, uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit,
+                        int end_bit);
+/* Sorted depth keys and original Gaussian indices of the last frame (visible splats only). */
+int gs_debug_last_order(gs_ctx* ctx, gs_scene* scene, uint32_t* out_keys, uint32_t* out_index,
+                        uint64_t capacity, uint64_t* out_n);
+/* Projected record of every Gaussian in the last frame: 16 floats each
+ * (cx, cy, e1hat.x, e1hat.y, e2hat.x, e2hat.y, opacity, r, g, b, rect bits x2, key bits, 0,0,0);
+ * rows of culled Gaussians are undefined. */
+int gs_debug_last_records(gs_ctx* ctx, gs_scene* scene, float* out16, uint64_t capacity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSPLAT_H */

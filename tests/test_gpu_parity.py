@@ -1,0 +1,274 @@
+"""GPU parity tests: the HIP renderer (through the C ABI) against the CPU oracle.
+
+Tolerances:
+  * depth keys and the sorted draw order: bit-exact;
+  * projected floats: <= 1e-5 relative (colour/opacity) and <= 1e-3 px absolute (centre);
+  * image vs the fp32 oracle: MSE < 1e-8 and max-abs <= 1e-3 outside <= 0.01 % pixels
+    (pixels whose quad-edge / alpha-threshold test flips under last-ulp differences);
+  * image vs the fp16-target oracle: MSE < 1e-5 and >= 99.9 % pixels within 2e-2.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as orc
+from conftest import camera, load_scene
+
+pytestmark = pytest.mark.gpu
+
+gs = pytest.importorskip("gsplat_amd")
+
+SMALL_SCENES = ["simple", "pc_short", "m3splat"]
+SMALL_CAMS = ["app", "close", "behind"]
+
+
+def dump(name, **arrays):
+    """On failure, keep the arrays for offline diffing (GS_DUMP_DIR, e.g. gpurun_out/)."""
+    d = os.environ.get("GS_DUMP_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        np.savez_compressed(os.path.join(d, name + ".npz"), **arrays)
+
+
+def image_close_fp32(img, ref, frac_out=1e-4, tol=1e-3, name=None):
+    d = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    mse = float((d ** 2).mean())
+    bad = float((d.max(axis=-1) > tol).mean())
+    ok = mse < 1e-8 and bad <= frac_out
+    if not ok and name:
+        dump(name, img=img, ref=ref)
+    return mse, bad, ok
+
+
+def image_close_fp16(img, ref):
+    d = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    mse = float((d ** 2).mean())
+    good = float((d.max(axis=-1) <= 2e-2).mean())
+    return mse, good, mse < 1e-5 and good >= 0.999
+
+
+# ------------------------------------------------------------------------------- sort
+@pytest.mark.parametrize("n", [1, 7, 100, 4095, 4096, 4097, 65536 + 13, 1_000_003])
+def test_sort_pairs_exact(gpu_ctx, n):
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    keys[::3] = keys[0]  # many ties: stability matters
+    vals = np.arange(n, dtype=np.uint32)
+    k, v = gpu_ctx.sort_pairs(keys, vals)
+    order = np.argsort(keys, kind="stable")
+    assert np.array_equal(k, keys[order])
+    assert np.array_equal(v, vals[order])
+
+
+@pytest.mark.parametrize("bits", [(0, 8), (0, 13), (0, 16), (8, 24), (3, 30)])
+def test_sort_partial_bits(gpu_ctx, bits):
+    b0, b1 = bits
+    n = 300_001
+    rng = np.random.default_rng(b0 * 31 + b1)
+    keys = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    vals = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    k, v = gpu_ctx.sort_pairs(keys, vals, b0, b1)
+    digit = (keys >> np.uint32(b0)) & np.uint32((1 << (b1 - b0)) - 1) if b1 - b0 < 32 else keys
+    order = np.argsort(digit, kind="stable")
+    assert np.array_equal(k, keys[order])
+    assert np.array_equal(v, vals[order])
+
+
+def test_sort_matches_oracle(gpu_ctx):
+    rng = np.random.default_rng(5)
+    n = 200_000
+    keys = (rng.integers(0, 64, n) * 1000003).astype(np.uint32)
+    vals = rng.permutation(n).astype(np.uint32)
+    k, v = gpu_ctx.sort_pairs(keys, vals)
+    ko, vo = orc.stable_sort_pairs(keys, vals)
+    assert np.array_equal(k, ko) and np.array_equal(v, vo)
+
+
+# ------------------------------------------------------------------------------- projection + order
+@pytest.mark.parametrize("scene", SMALL_SCENES)
+@pytest.mark.parametrize("cam", SMALL_CAMS)
+def test_projection_and_order(gpu_ctx, scene, cam):
+    aos, n, nsh = load_scene(scene)
+    W, H = 256, 256
+    u, _ = camera(scene + "_" + cam, W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, nsh)
+    sc.render(u, W, H)
+    sp = orc.project(aos, n, nsh, u, W, H)
+    vis = sp["visible"] == 1
+    keys, idx = sc.last_order()
+    # visible set and draw order are bit-exact
+    ok_, ov_ = orc.stable_sort_pairs(sp["key"][vis], np.nonzero(vis)[0].astype(np.uint32))
+    assert np.array_equal(idx, ov_)
+    assert np.array_equal(keys, ok_)
+    rec = sc.last_records()[vis]
+    o = sp[vis]
+    np.testing.assert_allclose(rec[:, 0], o["c"][:, 0], atol=1e-3, rtol=1e-5)
+    np.testing.assert_allclose(rec[:, 1], o["c"][:, 1], atol=1e-3, rtol=1e-5)
+    np.testing.assert_allclose(rec[:, 6], o["op"], rtol=1e-5)
+    np.testing.assert_allclose(rec[:, 7:10], o["col"], rtol=1e-5, atol=1e-6)
+    e1n = (o["e1"] ** 2).sum(1, keepdims=True)
+    e2n = (o["e2"] ** 2).sum(1, keepdims=True)
+    g1, g2 = rec[:, 2:4].astype(np.float64), rec[:, 4:6].astype(np.float64)
+    r1, r2 = (o["e1"] / e1n).astype(np.float64), (o["e2"] / e2n).astype(np.float64)
+    # u^2+v^2 = d^T (e1^ e1^T + e2^ e2^T) d: rotation-invariant conic, tight tolerance
+    conic_g = g1[:, :, None] * g1[:, None, :] + g2[:, :, None] * g2[:, None, :]
+    conic_r = r1[:, :, None] * r1[:, None, :] + r2[:, :, None] * r2[:, None, :]
+    scale = np.abs(conic_r).reshape(len(r1), -1).max(1)[:, None, None]
+    assert np.all(np.abs(conic_g - conic_r) <= 2e-5 * scale)
+    # the axes themselves: the eigenvector direction is ill-conditioned when lambda1 ~ lambda2
+    np.testing.assert_allclose(g1, r1, rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(g2, r2, rtol=2e-3, atol=1e-5)
+    assert np.array_equal(rec[:, 12].view(np.uint32), o["key"])
+
+
+# ------------------------------------------------------------------------------- images
+@pytest.mark.parametrize("scene", SMALL_SCENES)
+@pytest.mark.parametrize("cam", SMALL_CAMS)
+@pytest.mark.parametrize("size", [(256, 256), (96, 64)])
+def test_image_small_fp32(gpu_ctx, scene, cam, size):
+    W, H = size
+    aos, n, nsh = load_scene(scene)
+    u, _ = camera(scene + "_" + cam, W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, nsh)
+    img = sc.render(u, W, H, gs.make_opts(t_min=1e-4))
+    ref, st = orc.render(aos, n, nsh, u, W, H, accum=0, t_min=1e-4)
+    mse, bad, ok = image_close_fp32(img, ref)
+    assert ok, (mse, bad)
+    assert gpu_ctx.timings()["n_vis"] == st["n_vis"]
+
+
+@pytest.mark.parametrize("scene", SMALL_SCENES)
+def test_image_small_fp16_target(gpu_ctx, scene):
+    W, H = 256, 256
+    aos, n, nsh = load_scene(scene)
+    u, _ = camera(scene + "_behind", W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, nsh)
+    img = sc.render(u, W, H, gs.make_opts(accum=gs.GS_ACCUM_FP16_TARGET, t_min=0.0))
+    ref, _ = orc.render(aos, n, nsh, u, W, H, accum=1, t_min=0.0)
+    mse, good, ok = image_close_fp16(img, ref)
+    assert ok, (mse, good)
+
+
+def test_image_no_early_stop(gpu_ctx):
+    W, H = 256, 256
+    aos, n, nsh = load_scene("pc_short")
+    u, _ = camera("pc_short_behind", W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, nsh)
+    img = sc.render(u, W, H, gs.make_opts(t_min=0.0))
+    ref, _ = orc.render(aos, n, nsh, u, W, H, accum=0, t_min=0.0)
+    assert image_close_fp32(img, ref)[2]
+
+
+def test_synthetic_1m_1080p(gpu_ctx):
+    """Config 3 (synthetic 1 M @ 1920x1080) against the full oracle."""
+    W, H = 1920, 1080
+    aos = gs.synth_aos(1_000_000, 1, W, H)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, 1_000_000, 16)
+    img = sc.render(u, W, H, gs.make_opts(timing=1))
+    st_gpu = gpu_ctx.timings()
+    ref, st = orc.render(aos.view(np.uint8), 1_000_000, 16, u, W, H, accum=0, t_min=1e-4)
+    assert st_gpu["n_vis"] == st["n_vis"]
+    assert st["k_tiles"] <= st_gpu["k_entries"] <= st["k_tiles"] * 1.02
+    mse, bad, ok = image_close_fp32(img, ref, name="synth1m")
+    assert ok, (mse, bad)
+    keys, idx = sc.last_order()
+    assert np.all(keys[1:] >= keys[:-1])
+
+
+def test_strips_match_full_image(gpu_ctx):
+    W, H = 1920, 1080
+    aos = gs.synth_aos(200_000, 3, W, H)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, 200_000, 16)
+    full = sc.render(u, W, H)
+    for G in (2, 3, 8):
+        parts = [sc.render(u, W, H, gs.make_opts(strip_index=g, strip_count=G)) for g in range(G)]
+        img = np.concatenate(parts, axis=0)[:H]
+        assert np.array_equal(img, full), G
+
+
+def test_deterministic(gpu_ctx):
+    W, H = 640, 480
+    aos = gs.synth_aos(300_000, 9, W, H)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, 300_000, 16)
+    a = sc.render(u, W, H)
+    b = sc.render(u, W, H)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_f16_output(gpu_ctx):
+    W, H = 320, 200
+    aos = gs.synth_aos(50_000, 4, W, H)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, 50_000, 16)
+    a = sc.render(u, W, H)
+    h = sc.render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16))
+    assert np.array_equal(a.astype(np.float16), h)
+
+
+# ------------------------------------------------------------------------------- edge cases
+def test_empty_scene(gpu_ctx):
+    sc = gs.Scene(gpu_ctx, np.zeros(0, np.uint8), 0, 16)
+    img = sc.render(gs.bench_uniforms(64, 48), 64, 48)
+    assert img.shape == (48, 64, 4) and not img.any()
+
+
+def test_all_culled(gpu_ctx):
+    W, H = 200, 100
+    aos = gs.synth_aos(10_000, 2, W, H)
+    view = gs.look_at((0.0, 0.0, 0.0), (0.0, 0.0, 1.0))  # looking away from every splat
+    u = gs.pack_uniforms(view, gs.perspective(1.04719755, W / H, 0.03, 1000.0))
+    sc = gs.Scene(gpu_ctx, aos, 10_000, 16)
+    img = sc.render(u, W, H)
+    assert not img.any()
+    assert gpu_ctx.timings()["n_vis"] == 0
+
+
+@pytest.mark.parametrize("size", [(1, 1), (17, 33), (16, 16), (1023, 7)])
+def test_odd_sizes(gpu_ctx, size):
+    W, H = size
+    aos = gs.synth_aos(20_000, 11, max(W, 2), max(H, 2))
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, 20_000, 16)
+    img = sc.render(u, W, H)
+    ref, _ = orc.render(aos.view(np.uint8), 20_000, 16, u, W, H)
+    r = image_close_fp32(img, ref, name="odd_%dx%d" % (W, H))
+    assert r[2], r
+
+
+def test_huge_splats(gpu_ctx):
+    """Splats clamped by the 4096-px cap (full-screen quads) and a Gaussian at the camera."""
+    W, H = 320, 240
+    n = 64
+    aos = gs.synth_aos(n, 21, W, H).reshape(n, 80)
+    aos[:, 4:7] = 0.5  # large scales
+    aos[0, 0:3] = (0.0, 0.0, -0.0301)  # just past the near plane
+    aos = aos.reshape(-1)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    img = sc.render(u, W, H)
+    ref, st = orc.render(aos.view(np.uint8), n, 16, u, W, H)
+    r = image_close_fp32(img, ref, name="huge_splats")
+    assert r[2], r
+
+
+@pytest.mark.parametrize("nsh", [1, 4, 9])
+def test_lower_sh_degrees(gpu_ctx, nsh):
+    W, H = 128, 96
+    n = 5000
+    full = gs.synth_aos(n, 13, W, H).reshape(n, 80)
+    rec = full[:, : 16 + 4 * nsh].copy().reshape(-1)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, rec, n, nsh)
+    img = sc.render(u, W, H)
+    ref, _ = orc.render(rec.view(np.uint8), n, nsh, u, W, H)
+    r = image_close_fp32(img, ref, name="sh%d" % nsh)
+    assert r[2], r
+
+
+def test_bad_arguments(gpu_ctx):
+    with pytest.raises(gs.GsError):
+        gs.Scene(gpu_ctx, np.zeros(112, np.uint8), 1, 3)  # n_sh=3 is not a record size the reference makes
