@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Msplats/s (and fps) at 1920x1080 on a 6.1 M-Gaussian scene, 1..8 MI355X.
+
+BASELINE.json metric "Msplats/s + frames/s at 1920x1080, 6 M Gaussians; 1/2/4/8 MI355X",
+configs[3] ("INRIA bicycle ~6 M at 1920x1080, 1->8 MI355X row-strip + RCCL all-gather").  The
+bicycle PLY is not in this image, so the workload is the seeded synthetic stand-in of SURVEY §8d
+(seed 6, N = 6,100,000, SH degree 3) — reported in `data`/`config`.
+
+A step = one frame: uniform upload -> project/key -> depth sort -> bin -> tile sort -> composite
+(-> all-gather of the row strips at N > 1).  The scene is uploaded before timing (inputs resident
+in HBM).  Launch:  python bench.py [--gpus 1 --steps 50 --warmup 5]
+                   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gaussian-splatting-web_amd"))
+
+import numpy as np  # noqa: E402
+
+import gsplat_amd as gs  # noqa: E402
+from gsplat_amd.strips import strip_geometry  # noqa: E402
+
+HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(stage, n, n_vis, k, W, H):
+    """Bytes a kernel must move per launch."""
+    if stage == "project":
+        # read pos+scale+rot+opacity (44 B) of every Gaussian and SH (192 B) of visible ones;
+        # write the depth key (4 B) of every Gaussian and the 64-B record of visible ones
+        return 48 * n + 256 * n_vis
+    if stage == "composite":
+        # read each (tile, splat) entry (4 B) and gather its 40-B record; write RGBA f32
+        return 44 * k + 16 * W * H
+    if stage == "sort":
+        # 4 passes x (read key+val 8 B, write 8 B) over n_vis; pass 0 reads N keys
+        return 4 * n + 4 * 16 * n_vis
+    raise KeyError(stage)
+
+
+def frame_bytes(n, n_vis, k, W, H):
+    """B = 236 N + 148 N_vis + 48 K + 16 W H."""
+    return 236 * n + 148 * n_vis + 48 * k + 16 * W * H
+
+
+def cpu_baseline(aos, n, W, H, u):
+    """The oracle (CPU restatement of the reference semantics) on the same frame, host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as orc
+    t0 = time.perf_counter()
+    _, st = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=1e-4)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt / 1e6, "unit": "Msplats/s", "cores": orc.num_threads(), "kind": "port",
+            "sample": "1 full frame of the same %d-Gaussian %dx%d workload (project, std::stable_sort, "
+                      "composite; %.1f s wall)" % (n, W, H, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=6_100_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--seed", type=int, default=6)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (args.gpus, args.gpus))
+    W, H, N = args.width, args.height, args.n
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    aos = gs.synth_aos(N, args.seed, W, H)
+    u = gs.bench_uniforms(W, H)
+    ctx = gs.Context(local_rank)
+    scene = gs.Scene(ctx, aos, N, 16)
+
+    row0, rows_padded, t0, t1 = strip_geometry(H, rank, world)
+    opts = gs.make_opts(strip_index=rank, strip_count=world, timing=1)
+    strip_bytes = rows_padded * W * 16
+    if world > 1:
+        import torch
+        stream = torch.cuda.current_stream()
+        strip = torch.empty((rows_padded, W, 4), dtype=torch.float32, device="cuda")
+        full = torch.empty((world * rows_padded, W, 4), dtype=torch.float32, device="cuda")
+        from gsplat_amd.strips import gather_strips
+
+        def frame():
+            scene.render_device(u, W, H, strip.data_ptr(), strip_bytes, stream.cuda_stream, opts)
+            gather_strips(strip, full)
+
+        def sync():
+            torch.cuda.synchronize()
+            dist.barrier()
+    else:
+        buf = gs.DeviceBuffer(H * W * 16)
+
+        def frame():
+            scene.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, opts)
+
+        def sync():
+            ctx.sync()
+
+    for _ in range(args.warmup):
+        frame()
+    sync()
+    ctx.timings_reset()
+    sync()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    sync()
+    elapsed = time.perf_counter() - t_start
+    st = ctx.timings()
+    if world > 1:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        tot = torch.tensor([st["n_vis"], st["k_entries"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        n_vis_all, k_all = (int(x) for x in tot.tolist())
+    else:
+        n_vis_all, k_all = st["n_vis"], st["k_entries"]
+
+    ms = elapsed / args.steps * 1e3
+    fps = args.steps / elapsed
+    value = N * args.steps / elapsed / 1e6
+
+    # roofline of the dominant kernel (this rank's per-launch event time, HIP events on the
+    # stream the kernel runs on; algorithmic bytes per launch of this rank)
+    stages = {"project": st["ms_project"], "composite": st["ms_composite"], "sort": st["ms_sort"]}
+    dom = max(stages, key=stages.get)
+    rows_here = max(0, min(t1 * 16, H) - row0)
+    a_bytes = algorithmic_bytes(dom, N, st["n_vis"], st["k_entries"], W, rows_here)
+    achieved = a_bytes / (stages[dom] * 1e-3) / 1e9
+    fb = frame_bytes(N, n_vis_all, k_all, W, H)
+
+    if rank == 0:
+        out = {
+            "metric": "Msplats/s at 1920x1080, 6.1 M Gaussians (synthetic bicycle stand-in)",
+            "value": round(value, 3),
+            "unit": "Msplats/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "fps": round(fps, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SURVEY §8d generator, splitmix64 seed %d; bicycle PLY absent)" % args.seed,
+            "config": {"workload": "configs[3]: %d Gaussians (SH deg 3) at %dx%d, lookAt([0,0,0],[0,0,-1]) "
+                                   "perspective(60deg,W/H,0.03,1000)" % (N, W, H),
+                       "n_gaussians": N, "width": W, "height": H,
+                       "parallelism": "row-strips x%d + all-gather" % world if world > 1 else "single GPU"},
+            "stages_ms": {k: round(st[k], 4) for k in ("ms_total", "ms_project", "ms_sort", "ms_bin",
+                                                          "ms_tile_sort", "ms_ranges", "ms_composite",
+                                                          "ms_other")},
+            "n_vis": n_vis_all,
+            "k_entries": k_all,
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": int(a_bytes)},
+            "frame_roofline": {"bytes": int(fb), "frac": round(fb / (ms * 1e-3) / (world * HBM_PEAK), 4),
+                               "compulsory_frac": round((236 * N + 16 * W * H) / (ms * 1e-3) / (world * HBM_PEAK), 4),
+                               "formula": "236N + 148N_vis + 48K + 16WH (SURVEY 8d)"},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(aos, N, W, H, u)
+        print(json.dumps(out), flush=True)
+
+    scene.close()
+    ctx.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -72,7 +72,14 @@ void dev_free(T*& p) {
 
 inline uint64_t round_up(uint64_t a, uint64_t b) { return (a + b - 1) / b * b; }
 
-enum { EV_BEGIN, EV_PROJECT, EV_SORT, EV_BIN, EV_TSORT, EV_RANGES, EV_COMPOSITE, EV_COUNT };
+// Per-frame timing events (opts.timing): kernels are bracketed directly.
+enum { EV_BEGIN, EV_PROJ0, EV_PROJ1, EV_SORT0, EV_SORT1, EV_BIN1, EV_TSORT1, EV_COMP0, EV_COMP1, EV_COUNT };
+enum { ST_TOTAL, ST_PROJECT, ST_SORT, ST_BIN, ST_TSORT, ST_RANGES, ST_COMPOSITE, ST_COUNT };
+
+struct FrameEvents {
+    hipEvent_t ev[EV_COUNT] = {};
+    bool pending = false;
+};
 
 }  // namespace
 
@@ -83,9 +90,10 @@ struct gs_ctx {
     uint32_t* h_pinned = nullptr;  // [0..3] counters (2 x u64), [4] err
     void* d_out = nullptr;
     size_t d_out_bytes = 0;
-    hipEvent_t ev[EV_COUNT] = {};
-    bool timed = false;
-    hipStream_t timed_stream = nullptr;
+    FrameEvents fe[2];          // ping-pong: frame t's events are read at frame t+1's mid-frame sync
+    int fe_cur = 0;
+    double acc_ms[ST_COUNT] = {};
+    uint32_t acc_frames = 0;
     gs_stats stats{};
     std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
 };
@@ -178,6 +186,25 @@ static void check_device_error(gs_ctx* c) {
     }
 }
 
+static void harvest(gs_ctx* c, FrameEvents& f) {
+    if (!f.pending) return;
+    HIPCHK(hipEventSynchronize(f.ev[EV_COMP1]));
+    auto el = [&](int a, int b) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, f.ev[a], f.ev[b]));
+        return (double)ms;
+    };
+    c->acc_ms[ST_TOTAL] += el(EV_BEGIN, EV_COMP1);
+    c->acc_ms[ST_PROJECT] += el(EV_PROJ0, EV_PROJ1);
+    c->acc_ms[ST_SORT] += el(EV_SORT0, EV_SORT1);
+    c->acc_ms[ST_BIN] += el(EV_SORT1, EV_BIN1);
+    c->acc_ms[ST_TSORT] += el(EV_BIN1, EV_TSORT1);
+    c->acc_ms[ST_RANGES] += el(EV_TSORT1, EV_COMP0);
+    c->acc_ms[ST_COMPOSITE] += el(EV_COMP0, EV_COMP1);
+    c->acc_frames++;
+    f.pending = false;
+}
+
 // The per-frame pipeline.  `out` is device memory of rows_padded*W (strip) or H*W pixels.
 static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o,
                          void* out, hipStream_t st) {
@@ -187,7 +214,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     const int TX = (W + kTile - 1) / kTile;
     const int n_tiles = TX * (tr_end - tr_begin);
     const bool timed = o.timing != 0;
-    if (timed) HIPCHK(hipEventRecord(c->ev[EV_BEGIN], st));
+    FrameEvents& fe = c->fe[c->fe_cur];
+    if (timed) {
+        harvest(c, fe);  // slot reuse: its previous frame completed long ago (or wait for it)
+        HIPCHK(hipEventRecord(fe.ev[EV_BEGIN], st));
+    }
 
     HIPCHK(hipMemsetAsync(s->meta, 0, kMetaBytes, st));
     HIPCHK(hipMemsetAsync(c->d_err, 0, 4, st));
@@ -212,12 +243,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.hist = s->hist_depth;
     pp.counters = s->counters;
     const int grid = (int)std::min<uint64_t>(2048, std::max<uint64_t>(1, (s->n + kProjThreads - 1) / kProjThreads));
+    if (timed) HIPCHK(hipEventRecord(fe.ev[EV_PROJ0], st));
     if (n_tiles > 0 && s->n > 0) launch_project(pp, grid, st);
-    if (timed) HIPCHK(hipEventRecord(c->ev[EV_PROJECT], st));
+    if (timed) HIPCHK(hipEventRecord(fe.ev[EV_PROJ1], st));
 
     // n_vis and K size the rest of the frame
     HIPCHK(hipMemcpyAsync(c->h_pinned, s->counters, 16, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    harvest(c, c->fe[c->fe_cur ^ 1]);  // previous frame's events are complete now
     const unsigned long long* hc = (const unsigned long long*)c->h_pinned;
     const uint64_t n_vis = (n_tiles > 0) ? hc[0] : 0, K = (n_tiles > 0) ? hc[1] : 0;
     ensure_tile_capacity(s, K);
@@ -228,6 +261,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     HIPCHK(hipMemsetAsync(s->status_depth, 0, (size_t)(parts_n + 3 * (size_t)parts_v) * 1024, st));
     HIPCHK(hipMemsetAsync(s->status_bin, 0, (size_t)bin_parts(n_vis) * 8 + 8, st));
     HIPCHK(hipMemsetAsync(s->status_tile, 0, (size_t)2 * sort_parts(K) * 1024 + 4, st));
+    if (timed) HIPCHK(hipEventRecord(fe.ev[EV_SORT0], st));
 
     if (n_vis > 0) {
         // ---- depth sort: keysB(N, sentinel-filtered) -> A -> B -> A -> B
@@ -254,7 +288,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             launch_sort_pass(sp, st);
             status_off += (size_t)sort_parts(sp.n) * 256;
         }
-        if (timed) HIPCHK(hipEventRecord(c->ev[EV_SORT], st));
+        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_SORT1], st));
 
         // ---- binning in depth order
         BinParams bp{};
@@ -271,7 +305,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.ticket = s->tickets + 4;
         bp.err = c->d_err;
         launch_bin(bp, st);
-        if (timed) HIPCHK(hipEventRecord(c->ev[EV_BIN], st));
+        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_BIN1], st));
 
         // ---- stable sort of (tile, splat) by tile id
         const int tile_passes = n_tiles > 256 ? 2 : 1;
@@ -295,10 +329,10 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             std::swap(tk_in, tk_out);
             std::swap(tv_in, tv_out);
         }
-        if (timed) HIPCHK(hipEventRecord(c->ev[EV_TSORT], st));
+        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_TSORT1], st));
         HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)n_tiles * sizeof(uint2), st));
         launch_ranges(tk_in, K, s->ranges, st);
-        if (timed) HIPCHK(hipEventRecord(c->ev[EV_RANGES], st));
+        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_COMP0], st));
 
         CompositeParams cp{};
         cp.ranges = s->ranges;
@@ -316,12 +350,12 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
     } else {
         if (timed) {
-            HIPCHK(hipEventRecord(c->ev[EV_SORT], st));
-            HIPCHK(hipEventRecord(c->ev[EV_BIN], st));
-            HIPCHK(hipEventRecord(c->ev[EV_TSORT], st));
+            HIPCHK(hipEventRecord(fe.ev[EV_SORT1], st));
+            HIPCHK(hipEventRecord(fe.ev[EV_BIN1], st));
+            HIPCHK(hipEventRecord(fe.ev[EV_TSORT1], st));
         }
         HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)std::max(n_tiles, 1) * sizeof(uint2), st));
-        if (timed) HIPCHK(hipEventRecord(c->ev[EV_RANGES], st));
+        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_COMP0], st));
         CompositeParams cp{};
         cp.ranges = s->ranges;
         cp.tvals = s->tvA;
@@ -338,9 +372,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
     }
     HIPCHK(hipGetLastError());
-    if (timed) HIPCHK(hipEventRecord(c->ev[EV_COMPOSITE], st));
-    c->timed = timed;
-    c->timed_stream = st;
+    if (timed) {
+        HIPCHK(hipEventRecord(fe.ev[EV_COMP1], st));
+        fe.pending = true;
+        c->fe_cur ^= 1;
+    }
     s->last_nvis = n_vis;
     s->last_k = K;
     s->have_frame = true;
@@ -422,7 +458,8 @@ int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
             dev_alloc(c->d_err, 4);
             HIPCHK(hipMemset(c->d_err, 0, 4));
             HIPCHK(hipHostMalloc((void**)&c->h_pinned, 64, hipHostMallocDefault));
-            for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+            for (auto& f : c->fe)
+                for (auto& e : f.ev) HIPCHK(hipEventCreate(&e));
         } catch (...) {
             gs_ctx_destroy(c);
             throw;
@@ -437,8 +474,9 @@ void gs_ctx_destroy(gs_ctx* c) {
     (void)hipSetDevice(c->device);
     while (!c->scenes.empty()) gs_scene_free(c->scenes.back());
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto& e : c->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto& f : c->fe)
+        for (auto& e : f.ev)
+            if (e) (void)hipEventDestroy(e);
     if (c->d_out) (void)hipFree(c->d_out);
     dev_free(c->d_err);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
@@ -580,25 +618,33 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
     return guarded([&] {
         if (!c || !out) throw GsError(GS_ERR_INVALID, "null argument");
         HIPCHK(hipSetDevice(c->device));
+        harvest(c, c->fe[c->fe_cur ^ 1]);
+        harvest(c, c->fe[c->fe_cur]);
         gs_stats st = c->stats;
-        st.ms_total = st.ms_project = st.ms_sort = st.ms_bin = st.ms_tile_sort = st.ms_ranges =
-            st.ms_composite = st.ms_other = 0.0f;
-        if (c->timed) {
-            HIPCHK(hipEventSynchronize(c->ev[EV_COMPOSITE]));
-            auto el = [&](int a, int b) {
-                float ms = 0;
-                HIPCHK(hipEventElapsedTime(&ms, c->ev[a], c->ev[b]));
-                return ms;
-            };
-            st.ms_total = el(EV_BEGIN, EV_COMPOSITE);
-            st.ms_project = el(EV_BEGIN, EV_PROJECT);
-            st.ms_sort = el(EV_PROJECT, EV_SORT);
-            st.ms_bin = el(EV_SORT, EV_BIN);
-            st.ms_tile_sort = el(EV_BIN, EV_TSORT);
-            st.ms_ranges = el(EV_TSORT, EV_RANGES);
-            st.ms_composite = el(EV_RANGES, EV_COMPOSITE);
-        }
+        st.frames = (int32_t)c->acc_frames;
+        const double k = c->acc_frames ? 1.0 / c->acc_frames : 0.0;
+        st.ms_total = (float)(c->acc_ms[ST_TOTAL] * k);
+        st.ms_project = (float)(c->acc_ms[ST_PROJECT] * k);
+        st.ms_sort = (float)(c->acc_ms[ST_SORT] * k);
+        st.ms_bin = (float)(c->acc_ms[ST_BIN] * k);
+        st.ms_tile_sort = (float)(c->acc_ms[ST_TSORT] * k);
+        st.ms_ranges = (float)(c->acc_ms[ST_RANGES] * k);
+        st.ms_composite = (float)(c->acc_ms[ST_COMPOSITE] * k);
+        st.ms_other = st.ms_total - (st.ms_project + st.ms_sort + st.ms_bin + st.ms_tile_sort +
+                                     st.ms_ranges + st.ms_composite);
         *out = st;
+        return GS_OK;
+    });
+}
+
+int gs_timings_reset(gs_ctx* c) {
+    return guarded([&] {
+        if (!c) throw GsError(GS_ERR_INVALID, "null ctx");
+        HIPCHK(hipSetDevice(c->device));
+        harvest(c, c->fe[0]);
+        harvest(c, c->fe[1]);
+        for (auto& v : c->acc_ms) v = 0.0;
+        c->acc_frames = 0;
         return GS_OK;
     });
 }

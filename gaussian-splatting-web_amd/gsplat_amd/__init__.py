@@ -24,7 +24,7 @@ GS_OUT_RGBA_F32, GS_OUT_RGBA_F16 = 0, 1
 EXPORTED_SYMBOLS = (
     "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy",
     "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows",
-    "gs_render", "gs_render_device", "gs_timings", "gs_sync", "gs_present", "gs_look_at",
+    "gs_render", "gs_render_device", "gs_timings", "gs_timings_reset", "gs_sync", "gs_present", "gs_look_at",
     "gs_perspective", "gs_camera_position", "gs_pack_uniforms", "gs_synth_aos",
     "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records",
 )
@@ -40,14 +40,14 @@ class GsOpts(ctypes.Structure):
 class GsStats(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("n_vis", ctypes.c_uint64), ("k_entries", ctypes.c_uint64),
                 ("tile_row_begin", ctypes.c_int32), ("tile_row_end", ctypes.c_int32),
-                ("tiles_x", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+                ("tiles_x", ctypes.c_int32), ("frames", ctypes.c_int32),
                 ("ms_total", ctypes.c_float), ("ms_project", ctypes.c_float),
                 ("ms_sort", ctypes.c_float), ("ms_bin", ctypes.c_float),
                 ("ms_tile_sort", ctypes.c_float), ("ms_ranges", ctypes.c_float),
                 ("ms_composite", ctypes.c_float), ("ms_other", ctypes.c_float)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved0"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class GsError(RuntimeError):
@@ -88,6 +88,7 @@ def lib():
         L.gs_render.argtypes = [P, P, P, I, I, ctypes.POINTER(GsOpts), P]
         L.gs_render_device.argtypes = [P, P, P, I, I, ctypes.POINTER(GsOpts), P, U64, P]
         L.gs_timings.argtypes = [P, ctypes.POINTER(GsStats)]
+        L.gs_timings_reset.argtypes = [P]
         L.gs_sync.argtypes = [P]
         L.gs_present.argtypes = [P, I, I, P]
         L.gs_look_at.argtypes = [P, P, P, P]
@@ -222,6 +223,9 @@ class Context:
         _check(lib().gs_timings(self.handle, ctypes.byref(st)))
         return st.as_dict()
 
+    def timings_reset(self):
+        _check(lib().gs_timings_reset(self.handle))
+
     def sort_pairs(self, keys, vals, begin_bit=0, end_bit=32):
         k = np.array(keys, np.uint32, copy=True)
         v = np.array(vals, np.uint32, copy=True)
@@ -280,3 +284,37 @@ class Scene:
         out = np.empty((self.n, 16), np.float32)
         _check(lib().gs_debug_last_records(self.ctx.handle, self.handle, _ptr(out), self.n))
         return out
+
+
+# ------------------------------------------------------------------ raw device memory (no torch)
+class DeviceBuffer:
+    """hipMalloc'd device memory for frames kept on the GPU (bench.py at N=1 needs no torch)."""
+    _hip = None
+
+    def __init__(self, nbytes):
+        if DeviceBuffer._hip is None:
+            h = ctypes.CDLL("libamdhip64.so")
+            h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+            h.hipFree.argtypes = [ctypes.c_void_p]
+            h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+            DeviceBuffer._hip = h
+        self.nbytes = int(nbytes)
+        self.ptr = ctypes.c_void_p()
+        rc = DeviceBuffer._hip.hipMalloc(ctypes.byref(self.ptr), self.nbytes)
+        if rc != 0:
+            raise GsError(-4, "hipMalloc(%d) failed: %d" % (self.nbytes, rc))
+
+    def to_host(self, out):
+        rc = DeviceBuffer._hip.hipMemcpy(_ptr(out), self.ptr, min(out.nbytes, self.nbytes), 2)
+        if rc != 0:
+            raise GsError(-3, "hipMemcpy D2H failed: %d" % rc)
+        return out
+
+    def free(self):
+        if self.ptr:
+            DeviceBuffer._hip.hipFree(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        if not sys.is_finalizing():
+            self.free()

@@ -84,9 +84,11 @@ typedef struct gs_stats {
     uint64_t n_vis;       /* splats that reach the sort (visible in this strip) */
     uint64_t k_entries;   /* (tile, splat) pairs binned */
     int32_t tile_row_begin, tile_row_end;  /* tile rows rendered by the last call */
-    int32_t tiles_x, reserved0;
-    float ms_total;       /* stage times of the last timed gs_render* (0 if timing was off) */
+    int32_t tiles_x;
+    int32_t frames;       /* timed frames averaged below (opts.timing = 1) since gs_timings_reset */
+    float ms_total;       /* mean HIP-event times per timed frame: whole frame and per stage; */
     float ms_project, ms_sort, ms_bin, ms_tile_sort, ms_ranges, ms_composite, ms_other;
+                          /* project / composite are single kernels, the others kernel groups */
 } gs_stats;
 
 /* ---- library / device ---------------------------------------------------------------------- */
@@ -124,6 +126,7 @@ int gs_render_device(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int 
                      const gs_opts* opts, void* out_dev, uint64_t out_bytes, void* hip_stream);
 
 int gs_timings(gs_ctx* ctx, gs_stats* out_stats);
+int gs_timings_reset(gs_ctx* ctx);
 int gs_sync(gs_ctx* ctx);
 
 /* PostProcessRenderer (src/post_process_render.ts:54-77) on the host-visible image: y flip,
