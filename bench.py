@@ -135,11 +135,11 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        tot = torch.tensor([st["n_vis"], st["k_entries"]], dtype=torch.float64, device="cuda")
+        tot = torch.tensor([st["n_vis"], st["k_total"], st["k_entries"]], dtype=torch.float64, device="cuda")
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        n_vis_all, k_all = (int(x) for x in tot.tolist())
+        n_vis_all, k_all, k_binned = (int(x) for x in tot.tolist())
     else:
-        n_vis_all, k_all = st["n_vis"], st["k_entries"]
+        n_vis_all, k_all, k_binned = st["n_vis"], st["k_total"], st["k_entries"]
 
     ms = elapsed / args.steps * 1e3
     fps = args.steps / elapsed
@@ -177,7 +177,9 @@ def main():
                                                           "ms_tile_sort", "ms_ranges", "ms_composite",
                                                           "ms_other")},
             "n_vis": n_vis_all,
-            "k_entries": k_all,
+            "k_total": k_all,
+            "k_binned": k_binned,
+            "chunk_fraction": round(st["chunk_fraction"], 4),
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": None,
                          "algorithmic_bytes_per_launch": int(a_bytes)},

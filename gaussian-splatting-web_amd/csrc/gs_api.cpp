@@ -1,16 +1,20 @@
 // gs_api.cpp — C ABI (include/gsplat.h): contexts, scenes and the per-frame pipeline.
 //
-// Frame (gs_render_device), all on one HIP stream:
-//   memset(tickets, histograms, counters) -> k_project -> [read n_vis, K] ->
-//   memset(look-back words) -> 4 x k_sort_pass (depth key, 8 bits each) -> k_bin ->
-//   1-2 x k_sort_pass (tile id) -> k_ranges -> k_composite
+// A frame (render_frame) is a fixed sequence of launches on one HIP stream with no host round
+// trip; data-dependent sizes live in FrameCtl on the device:
+//   memset(FrameCtl, histograms) -> k_project -> 4 radix passes (depth key; carries the Gaussian
+//   index and its packed tile rectangle) -> per chunk: bin (count/scan/emit) -> 1-2 radix passes
+//   (tile id) -> k_ranges -> k_composite
+// Chunk 0 = the front ceil(f * n_vis) depth ranks; chunk 1 = the rest, binned only into tiles
+// chunk 0 left unsaturated.  f adapts from earlier frames' statistics (read back asynchronously);
+// the image does not depend on f.
 // Reference call stack replaced: Renderer.animate/draw (src/renderer.ts:332-387, :301-330).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
-#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -72,8 +76,12 @@ void dev_free(T*& p) {
 
 inline uint64_t round_up(uint64_t a, uint64_t b) { return (a + b - 1) / b * b; }
 
-// Per-frame timing events (opts.timing): kernels are bracketed directly.
-enum { EV_BEGIN, EV_PROJ0, EV_PROJ1, EV_SORT0, EV_SORT1, EV_BIN1, EV_TSORT1, EV_COMP0, EV_COMP1, EV_COUNT };
+// Per-frame timing events (opts.timing): kernel groups are bracketed directly.
+enum {
+    EV_BEGIN, EV_PROJ0, EV_PROJ1, EV_SORT1,
+    EV_BIN_0, EV_TSORT_0, EV_RANGES_0, EV_COMP_0,
+    EV_BIN_1, EV_TSORT_1, EV_RANGES_1, EV_COMP_1, EV_COUNT
+};
 enum { ST_TOTAL, ST_PROJECT, ST_SORT, ST_BIN, ST_TSORT, ST_RANGES, ST_COMPOSITE, ST_COUNT };
 
 struct FrameEvents {
@@ -81,20 +89,21 @@ struct FrameEvents {
     bool pending = false;
 };
 
+constexpr float kChunkF0 = 0.35f;  // first chunk fraction before any statistics exist
+
 }  // namespace
 
 struct gs_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    uint32_t* d_err = nullptr;
-    uint32_t* h_pinned = nullptr;  // [0..3] counters (2 x u64), [4] err
     void* d_out = nullptr;
     size_t d_out_bytes = 0;
-    FrameEvents fe[2];          // ping-pong: frame t's events are read at frame t+1's mid-frame sync
+    FrameEvents fe[2];  // ping-pong: frame t's events are read once frame t+1 needs the slot
     int fe_cur = 0;
     double acc_ms[ST_COUNT] = {};
     uint32_t acc_frames = 0;
     gs_stats stats{};
+    gs_scene* last_scene = nullptr;
     std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
 };
 
@@ -104,50 +113,65 @@ struct gs_scene {
     int n_sh = 0;
     float* planes = nullptr;
     uint64_t stride = 0;
-    // depth sort ping-pong; keys0 (project output, N entries) aliases keysB
-    uint32_t *keysA = nullptr, *valsA = nullptr, *keysB = nullptr, *valsB = nullptr;
+    // depth sort ping-pong: keys, Gaussian index, packed tile rectangle; project writes keysB/auxB
+    uint32_t *keysA = nullptr, *valsA = nullptr, *auxA = nullptr;
+    uint32_t *keysB = nullptr, *valsB = nullptr, *auxB = nullptr;
     float4* rec = nullptr;
-    // zero-per-frame metadata block: tickets | depth hist | tile hist | counters
+    // zero-per-frame block: FrameCtl | depth hist | tile hist x 2 chunks
     uint8_t* meta = nullptr;
-    size_t meta_bytes = 0;
-    uint32_t* tickets = nullptr;          // 16
-    uint32_t* hist_depth = nullptr;       // 8 x 4 x 256
-    uint32_t* hist_tile = nullptr;        // 8 x 2 x 256
-    unsigned long long* counters = nullptr;  // 2
-    uint32_t* status_depth = nullptr;     // 4 passes x sort_parts(N) x 256
-    unsigned long long* status_bin = nullptr;  // bin_parts(N)
+    FrameCtl* ctl = nullptr;
+    uint32_t* hist_depth = nullptr;     // 8 x 4 x 256
+    uint32_t* hist_tile[2] = {};        // 8 x 2 x 256 per chunk
+    uint32_t* bin_part = nullptr;       // bin_parts(N) + 1
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tkA = nullptr, *tvA = nullptr, *tkB = nullptr, *tvB = nullptr;
-    uint32_t* status_tile = nullptr;      // 2 passes x sort_parts(kcap) x 256
+    uint32_t* radix_offsets = nullptr;  // 256 x sort_parts(max(N, kcap))
     uint2* ranges = nullptr;
-    int ranges_cap = 0;
-    // last frame
-    uint64_t last_nvis = 0, last_k = 0;
+    uint8_t* done = nullptr;
+    int tiles_cap = 0;
+    float4* state = nullptr;
+    uint64_t state_cap = 0;
+    // asynchronous frame statistics (chunk controller, capacity)
+    FrameCtl* h_ctl = nullptr;  // pinned, 2 slots
+    hipEvent_t stat_ev[2] = {};
+    bool stat_pending[2] = {};
+    int stat_cur = 0;
+    FrameCtl last{};            // latest harvested statistics
+    bool have_last = false;
+    float chunk_f = kChunkF0;
     bool have_frame = false;
 };
 
-static constexpr size_t kMetaTickets = 0, kMetaHistDepth = 64,
+static constexpr size_t kMetaCtl = 0, kMetaHistDepth = 256,
                         kMetaHistTile = kMetaHistDepth + kHistShards * 1024 * 4,
-                        kMetaCounters = kMetaHistTile + kHistShards * 512 * 4,
-                        kMetaBytes = kMetaCounters + 64;
+                        kMetaBytes = kMetaHistTile + 2 * kHistShards * 512 * 4;
+static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
 static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
     if (k <= s->kcap && s->tkA) return;
-    uint64_t cap = std::max<uint64_t>(k + k / 2, std::max<uint64_t>(1u << 20, s->kcap));
-    if (cap > 0xFFFFFFFFull) cap = std::max<uint64_t>(k, 0xFFFFFFFFull);
-    if (k > 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "more than 2^32 tile entries");
-    dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB); dev_free(s->status_tile);
+    if (k >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "more than 2^32 tile entries");
+    const uint64_t cap = std::min<uint64_t>(0xFFFFFFFEull, std::max<uint64_t>(k + k / 2, 1u << 20));
+    dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB); dev_free(s->radix_offsets);
     dev_alloc(s->tkA, cap); dev_alloc(s->tvA, cap); dev_alloc(s->tkB, cap); dev_alloc(s->tvB, cap);
-    dev_alloc(s->status_tile, 2 * (size_t)sort_parts(cap) * 256);
+    dev_alloc(s->radix_offsets, 256 * (size_t)sort_parts(std::max<uint64_t>(cap, s->n)));
     s->kcap = cap;
 }
 
-static void ensure_ranges(gs_scene* s, int n_tiles) {
-    if (n_tiles <= s->ranges_cap && s->ranges) return;
+static void ensure_tiles(gs_scene* s, int n_tiles) {
+    if (n_tiles <= s->tiles_cap && s->ranges) return;
     dev_free(s->ranges);
+    dev_free(s->done);
     dev_alloc(s->ranges, (size_t)n_tiles);
-    s->ranges_cap = n_tiles;
+    dev_alloc(s->done, (size_t)n_tiles);
+    s->tiles_cap = n_tiles;
+}
+
+static void ensure_state(gs_scene* s, uint64_t pixels) {
+    if (pixels <= s->state_cap && s->state) return;
+    dev_free(s->state);
+    dev_alloc(s->state, pixels);
+    s->state_cap = pixels;
 }
 
 static void ensure_out(gs_ctx* c, size_t bytes) {
@@ -175,34 +199,45 @@ static void strip_geometry(int H, int si, int sc, int& tr_begin, int& tr_end, in
     rows_padded = per * kTile;
 }
 
-static void check_device_error(gs_ctx* c) {
-    uint32_t e = 0;
-    HIPCHK(hipMemcpy(&e, c->d_err, 4, hipMemcpyDeviceToHost));
-    if (e) {
-        HIPCHK(hipMemset(c->d_err, 0, 4));
-        char buf[128];
-        snprintf(buf, sizeof buf, "device protocol failure (err bits 0x%x)", e);
-        throw GsError(GS_ERR_DEVICE_FAULT, buf);
-    }
-}
-
 static void harvest(gs_ctx* c, FrameEvents& f) {
     if (!f.pending) return;
-    HIPCHK(hipEventSynchronize(f.ev[EV_COMP1]));
+    HIPCHK(hipEventSynchronize(f.ev[EV_COMP_1]));
     auto el = [&](int a, int b) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, f.ev[a], f.ev[b]));
         return (double)ms;
     };
-    c->acc_ms[ST_TOTAL] += el(EV_BEGIN, EV_COMP1);
+    c->acc_ms[ST_TOTAL] += el(EV_BEGIN, EV_COMP_1);
     c->acc_ms[ST_PROJECT] += el(EV_PROJ0, EV_PROJ1);
-    c->acc_ms[ST_SORT] += el(EV_SORT0, EV_SORT1);
-    c->acc_ms[ST_BIN] += el(EV_SORT1, EV_BIN1);
-    c->acc_ms[ST_TSORT] += el(EV_BIN1, EV_TSORT1);
-    c->acc_ms[ST_RANGES] += el(EV_TSORT1, EV_COMP0);
-    c->acc_ms[ST_COMPOSITE] += el(EV_COMP0, EV_COMP1);
+    c->acc_ms[ST_SORT] += el(EV_PROJ1, EV_SORT1);
+    c->acc_ms[ST_BIN] += el(EV_SORT1, EV_BIN_0) + el(EV_COMP_0, EV_BIN_1);
+    c->acc_ms[ST_TSORT] += el(EV_BIN_0, EV_TSORT_0) + el(EV_BIN_1, EV_TSORT_1);
+    c->acc_ms[ST_RANGES] += el(EV_TSORT_0, EV_RANGES_0) + el(EV_TSORT_1, EV_RANGES_1);
+    c->acc_ms[ST_COMPOSITE] += el(EV_RANGES_0, EV_COMP_0) + el(EV_RANGES_1, EV_COMP_1);
     c->acc_frames++;
     f.pending = false;
+}
+
+// Latest frame statistics that have arrived on the host; `wait` blocks for the newest frame.
+static void collect_stats(gs_scene* s, bool wait) {
+    for (int k = 0; k < 2; ++k) {
+        const int slot = (s->stat_cur + k) & 1;  // older slot first
+        if (!s->stat_pending[slot]) continue;
+        if (wait) {
+            HIPCHK(hipEventSynchronize(s->stat_ev[slot]));
+        } else if (hipEventQuery(s->stat_ev[slot]) != hipSuccess) {
+            continue;
+        }
+        s->last = s->h_ctl[slot];
+        s->have_last = true;
+        s->stat_pending[slot] = false;
+        // chunk controller: keep chunk 1's entries a small fraction of chunk 0's
+        const double k0 = s->last.k_chunk[0], k1 = s->last.k_chunk[1];
+        if (s->last.not_done > 0 && k1 > 0.25 * std::max(k0, 1.0))
+            s->chunk_f = std::min(1.0f, s->chunk_f * 1.5f);
+        else if (k1 < 0.05 * k0)
+            s->chunk_f = std::max(1.0f / 64.0f, s->chunk_f * 0.9f);
+    }
 }
 
 // The per-frame pipeline.  `out` is device memory of rows_padded*W (strip) or H*W pixels.
@@ -213,19 +248,26 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     strip_geometry(H, o.strip_index, sc, tr_begin, tr_end, rows_padded);
     const int TX = (W + kTile - 1) / kTile;
     const int n_tiles = TX * (tr_end - tr_begin);
+    collect_stats(s, false);
+    if (s->have_last && s->last.k_total > s->kcap) ensure_tile_capacity(s, s->last.k_total);
+    ensure_tiles(s, std::max(n_tiles, 1));
+    const float f = o.chunk_fraction > 0.0f ? std::min(o.chunk_fraction, 1.0f) : s->chunk_f;
+    const bool two_chunks = f < 1.0f;
+    if (two_chunks) ensure_state(s, (uint64_t)W * H);
+
     const bool timed = o.timing != 0;
     FrameEvents& fe = c->fe[c->fe_cur];
-    if (timed) {
-        harvest(c, fe);  // slot reuse: its previous frame completed long ago (or wait for it)
-        HIPCHK(hipEventRecord(fe.ev[EV_BEGIN], st));
-    }
+    auto mark = [&](int e) {
+        if (timed) HIPCHK(hipEventRecord(fe.ev[e], st));
+    };
+    if (timed) harvest(c, fe);  // slot reuse: its frame completed long ago (or wait for it)
+    mark(EV_BEGIN);
 
     HIPCHK(hipMemsetAsync(s->meta, 0, kMetaBytes, st));
-    HIPCHK(hipMemsetAsync(c->d_err, 0, 4, st));
     ProjParams pp{};
     pp.planes = s->planes;
     pp.plane_stride = s->stride;
-    pp.n = (uint32_t)s->n;
+    pp.n = n_tiles > 0 ? (uint32_t)s->n : 0u;
     pp.n_sh = s->n_sh;
     std::memcpy(pp.V, uni + 0, 64);
     mat4_mul_ref(uni + 16, uni + 0, pp.PV);
@@ -239,76 +281,69 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.tile_row_end = tr_end;
     pp.tiles_x = TX;
     pp.keys_out = s->keysB;
+    pp.rect_out = s->auxB;
     pp.rec = s->rec;
     pp.hist = s->hist_depth;
-    pp.counters = s->counters;
-    const int grid = (int)std::min<uint64_t>(2048, std::max<uint64_t>(1, (s->n + kProjThreads - 1) / kProjThreads));
-    if (timed) HIPCHK(hipEventRecord(fe.ev[EV_PROJ0], st));
-    if (n_tiles > 0 && s->n > 0) launch_project(pp, grid, st);
-    if (timed) HIPCHK(hipEventRecord(fe.ev[EV_PROJ1], st));
+    pp.ctl = s->ctl;
+    mark(EV_PROJ0);
+    launch_project(pp, st);
+    mark(EV_PROJ1);
 
-    // n_vis and K size the rest of the frame
-    HIPCHK(hipMemcpyAsync(c->h_pinned, s->counters, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    harvest(c, c->fe[c->fe_cur ^ 1]);  // previous frame's events are complete now
-    const unsigned long long* hc = (const unsigned long long*)c->h_pinned;
-    const uint64_t n_vis = (n_tiles > 0) ? hc[0] : 0, K = (n_tiles > 0) ? hc[1] : 0;
-    ensure_tile_capacity(s, K);
-    ensure_ranges(s, std::max(n_tiles, 1));
+    // ---- depth sort: (keysB, index, auxB) over N, sentinels dropped -> A -> B -> A -> B
+    const uint32_t* kin[4] = {s->keysB, s->keysA, s->keysB, s->keysA};
+    const uint32_t* vin[4] = {nullptr, s->valsA, s->valsB, s->valsA};
+    const uint32_t* ain[4] = {s->auxB, s->auxA, s->auxB, s->auxA};
+    uint32_t* kout[4] = {s->keysA, s->keysB, s->keysA, s->keysB};
+    uint32_t* vout[4] = {s->valsA, s->valsB, s->valsA, s->valsB};
+    uint32_t* aout[4] = {s->auxA, s->auxB, s->auxA, s->auxB};
+    for (int ps = 0; ps < 4; ++ps) {
+        SortPass sp{};
+        sp.keys_in = kin[ps];
+        sp.vals_in = vin[ps];
+        sp.aux_in = ain[ps];
+        sp.keys_out = kout[ps];
+        sp.vals_out = vout[ps];
+        sp.aux_out = aout[ps];
+        sp.n = pp.n;
+        sp.n_dev = ps == 0 ? nullptr : &s->ctl->n_vis;
+        sp.parts_max = sort_parts(pp.n);
+        sp.shift = 8 * ps;
+        sp.mask = 255;
+        sp.filter_sentinel = ps == 0;
+        sp.hist = s->hist_depth + 256 * ps;
+        sp.hist_stride = 1024;
+        sp.offsets = s->radix_offsets;
+        launch_sort_pass(sp, st);
+    }
+    mark(EV_SORT1);
 
-    const uint32_t parts_n = sort_parts(s->n), parts_v = sort_parts(n_vis);
-    // look-back words: pass 0 over N, passes 1-3 over n_vis; bin over n_vis; tile passes over K
-    HIPCHK(hipMemsetAsync(s->status_depth, 0, (size_t)(parts_n + 3 * (size_t)parts_v) * 1024, st));
-    HIPCHK(hipMemsetAsync(s->status_bin, 0, (size_t)bin_parts(n_vis) * 8 + 8, st));
-    HIPCHK(hipMemsetAsync(s->status_tile, 0, (size_t)2 * sort_parts(K) * 1024 + 4, st));
-    if (timed) HIPCHK(hipEventRecord(fe.ev[EV_SORT0], st));
-
-    if (n_vis > 0) {
-        // ---- depth sort: keysB(N, sentinel-filtered) -> A -> B -> A -> B
-        const uint32_t* kin[4] = {s->keysB, s->keysA, s->keysB, s->keysA};
-        const uint32_t* vin[4] = {nullptr, s->valsA, s->valsB, s->valsA};
-        uint32_t* kout[4] = {s->keysA, s->keysB, s->keysA, s->keysB};
-        uint32_t* vout[4] = {s->valsA, s->valsB, s->valsA, s->valsB};
-        size_t status_off = 0;
-        for (int ps = 0; ps < 4; ++ps) {
-            SortPass sp{};
-            sp.keys_in = kin[ps];
-            sp.vals_in = vin[ps];
-            sp.keys_out = kout[ps];
-            sp.vals_out = vout[ps];
-            sp.n = (uint32_t)(ps == 0 ? s->n : n_vis);
-            sp.shift = 8 * ps;
-            sp.mask = 255;
-            sp.filter_sentinel = ps == 0;
-            sp.hist = s->hist_depth + 256 * ps;
-            sp.hist_stride = 1024;
-            sp.status = s->status_depth + status_off;
-            sp.ticket = s->tickets + ps;
-            sp.err = c->d_err;
-            launch_sort_pass(sp, st);
-            status_off += (size_t)sort_parts(sp.n) * 256;
+    // ---- chunks: bin -> tile-id sort -> ranges -> composite
+    const int tile_passes = n_tiles > 256 ? 2 : 1;
+    for (int chunk = 0; chunk < 2; ++chunk) {
+        const int eb = chunk == 0 ? EV_BIN_0 : EV_BIN_1;
+        if (chunk == 1 && !two_chunks) {
+            for (int e = 0; e < 4; ++e) mark(eb + e);
+            break;
         }
-        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_SORT1], st));
-
-        // ---- binning in depth order
         BinParams bp{};
         bp.sorted_vals = s->valsB;
+        bp.sorted_rect = s->auxB;
         bp.rec = s->rec;
-        bp.n_vis = (uint32_t)n_vis;
+        bp.done = s->done;
+        bp.ctl = s->ctl;
+        bp.chunk = chunk;
+        bp.chunk_f = f;
         bp.tile_row_begin = tr_begin;
         bp.tiles_x = TX;
-        bp.capacity = s->kcap;
+        bp.n_max = std::max<uint32_t>(pp.n, 1);
+        bp.capacity = (uint32_t)s->kcap;
+        bp.part_tot = s->bin_part;
         bp.tkeys = s->tkA;
         bp.tvals = s->tvA;
-        bp.hist = s->hist_tile;
-        bp.status = s->status_bin;
-        bp.ticket = s->tickets + 4;
-        bp.err = c->d_err;
+        bp.hist = s->hist_tile[chunk];
         launch_bin(bp, st);
-        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_BIN1], st));
+        mark(eb);
 
-        // ---- stable sort of (tile, splat) by tile id
-        const int tile_passes = n_tiles > 256 ? 2 : 1;
         uint32_t *tk_in = s->tkA, *tv_in = s->tvA, *tk_out = s->tkB, *tv_out = s->tvB;
         for (int ps = 0; ps < tile_passes; ++ps) {
             SortPass sp{};
@@ -316,23 +351,22 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.vals_in = tv_in;
             sp.keys_out = tk_out;
             sp.vals_out = tv_out;
-            sp.n = (uint32_t)K;
+            sp.n = (uint32_t)s->kcap;
+            sp.n_dev = &s->ctl->k_chunk[chunk];
+            sp.parts_max = sort_parts(s->kcap);
             sp.shift = 8 * ps;
             sp.mask = 255;
-            sp.filter_sentinel = 0;
-            sp.hist = s->hist_tile + 256 * ps;
+            sp.hist = s->hist_tile[chunk] + 256 * ps;
             sp.hist_stride = 512;
-            sp.status = s->status_tile + (size_t)ps * sort_parts(K) * 256;
-            sp.ticket = s->tickets + 5 + ps;
-            sp.err = c->d_err;
+            sp.offsets = s->radix_offsets;
             launch_sort_pass(sp, st);
             std::swap(tk_in, tk_out);
             std::swap(tv_in, tv_out);
         }
-        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_TSORT1], st));
-        HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)n_tiles * sizeof(uint2), st));
-        launch_ranges(tk_in, K, s->ranges, st);
-        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_COMP0], st));
+        mark(eb + 1);
+        HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)std::max(n_tiles, 1) * sizeof(uint2), st));
+        launch_ranges(tk_in, &s->ctl->k_chunk[chunk], (uint32_t)s->kcap, s->ranges, st);
+        mark(eb + 2);
 
         CompositeParams cp{};
         cp.ranges = s->ranges;
@@ -345,44 +379,33 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         cp.row0 = sc > 1 ? tr_begin * kTile : 0;
         cp.n_tiles = n_tiles;
         cp.t_min = o.t_min;
+        cp.mode = !two_chunks ? kCompSingle : (chunk == 0 ? kCompFirst : kCompSecond);
+        cp.state = s->state;
+        cp.done = s->done;
+        cp.ctl = s->ctl;
         cp.out = out;
         cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
         launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
-    } else {
-        if (timed) {
-            HIPCHK(hipEventRecord(fe.ev[EV_SORT1], st));
-            HIPCHK(hipEventRecord(fe.ev[EV_BIN1], st));
-            HIPCHK(hipEventRecord(fe.ev[EV_TSORT1], st));
-        }
-        HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)std::max(n_tiles, 1) * sizeof(uint2), st));
-        if (timed) HIPCHK(hipEventRecord(fe.ev[EV_COMP0], st));
-        CompositeParams cp{};
-        cp.ranges = s->ranges;
-        cp.tvals = s->tvA;
-        cp.rec = s->rec;
-        cp.W = W;
-        cp.H = H;
-        cp.tiles_x = TX;
-        cp.tile_row_begin = tr_begin;
-        cp.row0 = sc > 1 ? tr_begin * kTile : 0;
-        cp.n_tiles = n_tiles;
-        cp.t_min = o.t_min;
-        cp.out = out;
-        cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
-        launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
+        mark(eb + 3);
     }
     HIPCHK(hipGetLastError());
     if (timed) {
-        HIPCHK(hipEventRecord(fe.ev[EV_COMP1], st));
         fe.pending = true;
         c->fe_cur ^= 1;
     }
-    s->last_nvis = n_vis;
-    s->last_k = K;
+    // frame statistics back to the host, asynchronously
+    const int slot = s->stat_cur;
+    if (s->stat_pending[slot]) {  // two frames in flight: wait for the older one
+        HIPCHK(hipEventSynchronize(s->stat_ev[slot]));
+        collect_stats(s, false);
+    }
+    HIPCHK(hipMemcpyAsync(&s->h_ctl[slot], s->ctl, sizeof(FrameCtl), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(s->stat_ev[slot], st));
+    s->stat_pending[slot] = true;
+    s->stat_cur ^= 1;
     s->have_frame = true;
+    c->last_scene = s;
     c->stats.n = s->n;
-    c->stats.n_vis = n_vis;
-    c->stats.k_entries = K;
     c->stats.tile_row_begin = tr_begin;
     c->stats.tile_row_end = tr_end;
     c->stats.tiles_x = TX;
@@ -392,8 +415,7 @@ static void validate_render_args(gs_ctx* c, gs_scene* s, const void* uni, int W,
                                  const gs_opts* o) {
     if (!c || !s || !uni) throw GsError(GS_ERR_INVALID, "null ctx/scene/uniforms");
     if (s->ctx != c) throw GsError(GS_ERR_INVALID, "scene belongs to another context");
-    if (W <= 0 || H <= 0 || W > 65535 * kTile || H > 65535 * kTile)
-        throw GsError(GS_ERR_INVALID, "bad image size");
+    if (W <= 0 || H <= 0 || W > 65535 || H > 65535) throw GsError(GS_ERR_INVALID, "bad image size");
     if (o) {
         if (o->strip_count < 1 || o->strip_index < 0 || o->strip_index >= o->strip_count)
             throw GsError(GS_ERR_INVALID, "bad strip index/count");
@@ -402,6 +424,7 @@ static void validate_render_args(gs_ctx* c, gs_scene* s, const void* uni, int W,
         if (o->out_format != GS_OUT_RGBA_F32 && o->out_format != GS_OUT_RGBA_F16)
             throw GsError(GS_ERR_INVALID, "bad out_format");
         if (!(o->t_min >= 0.0f && o->t_min < 1.0f)) throw GsError(GS_ERR_INVALID, "t_min must be in [0,1)");
+        if (!(o->chunk_fraction >= 0.0f)) throw GsError(GS_ERR_INVALID, "chunk_fraction must be >= 0");
         if (o->ref_quirks) throw GsError(GS_ERR_UNSUPPORTED, "ref_quirks not built in this version");
     }
 }
@@ -411,6 +434,16 @@ static size_t out_bytes_for(int W, int H, const gs_opts& o) {
     strip_geometry(H, o.strip_index, std::max(1, o.strip_count), tb, te, rows_padded);
     const size_t rows = o.strip_count > 1 ? (size_t)rows_padded : (size_t)H;
     return rows * (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
+}
+
+// Frame errors surface here: every frame's FrameCtl comes back asynchronously.
+static void check_frame_errors(gs_scene* s) {
+    collect_stats(s, true);
+    if (s->have_last && (s->last.err & kErrOverflow)) {
+        s->last.err = 0;
+        ensure_tile_capacity(s, s->last.k_total);
+        throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded; capacity grown, render again");
+    }
 }
 
 extern "C" {
@@ -437,6 +470,7 @@ void gs_opts_default(gs_opts* o) {
     o->t_min = 1e-4f;
     o->strip_index = 0;
     o->strip_count = 1;
+    o->chunk_fraction = 0.0f;
 }
 
 int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
@@ -455,9 +489,6 @@ int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
         c->device = dev;
         try {
             HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-            dev_alloc(c->d_err, 4);
-            HIPCHK(hipMemset(c->d_err, 0, 4));
-            HIPCHK(hipHostMalloc((void**)&c->h_pinned, 64, hipHostMallocDefault));
             for (auto& f : c->fe)
                 for (auto& e : f.ev) HIPCHK(hipEventCreate(&e));
         } catch (...) {
@@ -478,8 +509,6 @@ void gs_ctx_destroy(gs_ctx* c) {
         for (auto& e : f.ev)
             if (e) (void)hipEventDestroy(e);
     if (c->d_out) (void)hipFree(c->d_out);
-    dev_free(c->d_err);
-    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -490,7 +519,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
         *out = nullptr;
         if (n_sh != 1 && n_sh != 4 && n_sh != 9 && n_sh != 16)
             throw GsError(GS_ERR_UNSUPPORTED, "n_sh_coeffs must be 1, 4, 9 or 16");
-        if (n >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "scene larger than 2^32-1 Gaussians");
+        if (n >= 0xFFFFFFF0ull) throw GsError(GS_ERR_UNSUPPORTED, "scene larger than 2^32-16 Gaussians");
         HIPCHK(hipSetDevice(c->device));
         gs_scene* s = new gs_scene();
         s->ctx = c;
@@ -499,18 +528,17 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
         try {
             s->stride = round_up(std::max<uint64_t>(n, 1), 64);
             dev_alloc(s->planes, (size_t)(11 + 3 * n_sh) * s->stride);
-            dev_alloc(s->keysA, n);
-            dev_alloc(s->valsA, n);
-            dev_alloc(s->keysB, n);
-            dev_alloc(s->valsB, n);
+            dev_alloc(s->keysA, n); dev_alloc(s->valsA, n); dev_alloc(s->auxA, n);
+            dev_alloc(s->keysB, n); dev_alloc(s->valsB, n); dev_alloc(s->auxB, n);
             dev_alloc(s->rec, 4 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->meta, kMetaBytes);
-            s->tickets = (uint32_t*)(s->meta + kMetaTickets);
+            s->ctl = (FrameCtl*)(s->meta + kMetaCtl);
             s->hist_depth = (uint32_t*)(s->meta + kMetaHistDepth);
-            s->hist_tile = (uint32_t*)(s->meta + kMetaHistTile);
-            s->counters = (unsigned long long*)(s->meta + kMetaCounters);
-            dev_alloc(s->status_depth, 4 * (size_t)sort_parts(n) * 256 + 256);
-            dev_alloc(s->status_bin, (size_t)bin_parts(n) + 1);
+            s->hist_tile[0] = (uint32_t*)(s->meta + kMetaHistTile);
+            s->hist_tile[1] = s->hist_tile[0] + kHistShards * 512;
+            dev_alloc(s->bin_part, (size_t)bin_parts(n) + 1);
+            HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hipHostMallocDefault));
+            for (auto& e : s->stat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             ensure_tile_capacity(s, 4 * n + (1u << 20));
             // AoS -> SoA on device, in chunks of 4M records
             const uint64_t rb = 64 + 16 * (uint64_t)n_sh;
@@ -543,16 +571,22 @@ void gs_scene_free(gs_scene* s) {
         (void)hipStreamSynchronize(s->ctx->stream);
         auto& v = s->ctx->scenes;
         v.erase(std::remove(v.begin(), v.end(), s), v.end());
+        if (s->ctx->last_scene == s) s->ctx->last_scene = nullptr;
     }
     dev_free(s->planes);
-    dev_free(s->keysA); dev_free(s->valsA); dev_free(s->keysB); dev_free(s->valsB);
+    dev_free(s->keysA); dev_free(s->valsA); dev_free(s->auxA);
+    dev_free(s->keysB); dev_free(s->valsB); dev_free(s->auxB);
     dev_free(s->rec);
     dev_free(s->meta);
-    dev_free(s->status_depth);
-    dev_free(s->status_bin);
+    dev_free(s->bin_part);
     dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB);
-    dev_free(s->status_tile);
+    dev_free(s->radix_offsets);
     dev_free(s->ranges);
+    dev_free(s->done);
+    dev_free(s->state);
+    for (auto& e : s->stat_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (s->h_ctl) (void)hipHostFree(s->h_ctl);
     delete s;
 }
 
@@ -580,6 +614,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
         if (!out_dev) throw GsError(GS_ERR_INVALID, "null output");
         if (out_bytes < out_bytes_for(W, H, o)) throw GsError(GS_ERR_INVALID, "output buffer too small");
         HIPCHK(hipSetDevice(c->device));
+        if (s->have_last && (s->last.err & kErrOverflow)) check_frame_errors(s);
         hipStream_t st = stream ? (hipStream_t)stream : c->stream;
         render_frame(c, s, (const float*)uni, W, H, o, out_dev, st);
         return GS_OK;
@@ -595,10 +630,16 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
         HIPCHK(hipSetDevice(c->device));
         const size_t bytes = out_bytes_for(W, H, o);
         ensure_out(c, bytes);
-        render_frame(c, s, (const float*)uni, W, H, o, c->d_out, c->stream);
-        if (out_host) HIPCHK(hipMemcpyAsync(out_host, c->d_out, bytes, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        check_device_error(c);
+        for (int attempt = 0;; ++attempt) {
+            render_frame(c, s, (const float*)uni, W, H, o, c->d_out, c->stream);
+            HIPCHK(hipStreamSynchronize(c->stream));
+            collect_stats(s, true);
+            if (!(s->last.err & kErrOverflow)) break;
+            s->last.err = 0;
+            if (attempt >= 2) throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded");
+            ensure_tile_capacity(s, s->last.k_total);  // grow and render the frame again
+        }
+        if (out_host) HIPCHK(hipMemcpy(out_host, c->d_out, bytes, hipMemcpyDeviceToHost));
         return GS_OK;
     });
 }
@@ -609,7 +650,7 @@ int gs_sync(gs_ctx* c) {
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipDeviceSynchronize());
-        check_device_error(c);
+        for (gs_scene* s : c->scenes) check_frame_errors(s);
         return GS_OK;
     });
 }
@@ -621,6 +662,15 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
         harvest(c, c->fe[c->fe_cur ^ 1]);
         harvest(c, c->fe[c->fe_cur]);
         gs_stats st = c->stats;
+        if (c->last_scene) {
+            collect_stats(c->last_scene, true);
+            const FrameCtl& l = c->last_scene->last;
+            st.n_vis = l.n_vis;
+            st.k_entries = (uint64_t)l.k_chunk[0] + l.k_chunk[1];
+            st.k_total = l.k_total;
+            st.tiles_unsaturated = l.not_done;
+            st.chunk_fraction = c->last_scene->chunk_f;
+        }
         st.frames = (int32_t)c->acc_frames;
         const double k = c->acc_frames ? 1.0 / c->acc_frames : 0.0;
         st.ms_total = (float)(c->acc_ms[ST_TOTAL] * k);
@@ -657,18 +707,14 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
         if (n == 0) return GS_OK;
         HIPCHK(hipSetDevice(c->device));
         const int npass = (end_bit - begin_bit + 7) / 8;
-        uint32_t *kA, *vA, *kB, *vB, *hist, *status, *tick;
+        uint32_t *kA, *vA, *kB, *vB, *hist, *offs;
         dev_alloc(kA, n); dev_alloc(vA, n); dev_alloc(kB, n); dev_alloc(vB, n);
         dev_alloc(hist, (size_t)kHistShards * npass * 256);
-        dev_alloc(status, (size_t)npass * sort_parts(n) * 256);
-        dev_alloc(tick, 8);
+        dev_alloc(offs, (size_t)256 * sort_parts(n));
         hipStream_t st = c->stream;
         HIPCHK(hipMemcpyAsync(kA, keys, n * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(vA, vals, n * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(hist, 0, (size_t)kHistShards * npass * 256 * 4, st));
-        HIPCHK(hipMemsetAsync(status, 0, (size_t)npass * sort_parts(n) * 1024, st));
-        HIPCHK(hipMemsetAsync(tick, 0, 32, st));
-        HIPCHK(hipMemsetAsync(c->d_err, 0, 4, st));
         // histogram of each pass's digit, masked to the bit range
         launch_hist_keys(kA, (uint32_t)n, begin_bit, end_bit, npass, hist, st);
         uint32_t *ki = kA, *vi = vA, *ko = kB, *vo = vB;
@@ -676,15 +722,13 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
             SortPass sp{};
             sp.keys_in = ki; sp.vals_in = vi; sp.keys_out = ko; sp.vals_out = vo;
             sp.n = (uint32_t)n;
+            sp.parts_max = sort_parts(n);
             sp.shift = begin_bit + 8 * ps;
             const int bits = std::min(8, end_bit - sp.shift);
             sp.mask = (1u << bits) - 1u;
-            sp.filter_sentinel = 0;
             sp.hist = hist + 256 * ps;
             sp.hist_stride = npass * 256;
-            sp.status = status + (size_t)ps * sort_parts(n) * 256;
-            sp.ticket = tick + ps;
-            sp.err = c->d_err;
+            sp.offsets = offs;
             launch_sort_pass(sp, st);
             std::swap(ki, ko);
             std::swap(vi, vo);
@@ -693,8 +737,7 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
         HIPCHK(hipMemcpyAsync(keys, ki, n * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(vals, vi, n * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        dev_free(kA); dev_free(vA); dev_free(kB); dev_free(vB); dev_free(hist); dev_free(status); dev_free(tick);
-        check_device_error(c);
+        dev_free(kA); dev_free(vA); dev_free(kB); dev_free(vB); dev_free(hist); dev_free(offs);
         return GS_OK;
     });
 }
@@ -706,8 +749,9 @@ int gs_debug_last_order(gs_ctx* c, gs_scene* s, uint32_t* out_keys, uint32_t* ou
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipStreamSynchronize(c->stream));
-        *out_n = s->last_nvis;
-        const uint64_t m = std::min(cap, s->last_nvis);
+        collect_stats(s, true);
+        *out_n = s->last.n_vis;
+        const uint64_t m = std::min<uint64_t>(cap, s->last.n_vis);
         if (m && out_keys) HIPCHK(hipMemcpy(out_keys, s->keysB, m * 4, hipMemcpyDeviceToHost));
         if (m && out_index) HIPCHK(hipMemcpy(out_index, s->valsB, m * 4, hipMemcpyDeviceToHost));
         return GS_OK;

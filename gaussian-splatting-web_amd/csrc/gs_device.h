@@ -1,4 +1,9 @@
-// gs_device.h — shared constants and kernel-launch entry points (host side of gs_kernels.hip).
+// gs_device.h — shared constants, the device-side frame control block, kernel parameter blocks
+// and launchers (host side of gs_kernels.hip).
+//
+// A frame is a fixed sequence of launches with no host round trip: every count that depends on
+// the data (visible splats, entries per chunk, unsaturated tiles) lives in FrameCtl on the device
+// and every kernel sizes its work from it (grid-stride loops over a worst-case grid).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -9,17 +14,33 @@ constexpr int kTile = 16;             // 16x16-pixel composite tile
 constexpr int kProjThreads = 256;
 constexpr int kSortThreads = 256;     // 4 waves
 constexpr int kSortIPT = 16;          // items per thread
-constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per Onesweep partition
+constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per radix partition
 constexpr int kBinThreads = 256;
 constexpr int kBinIPT = 8;
 constexpr int kBinTile = kBinThreads * kBinIPT;     // 2048 ranks per binning partition
 constexpr int kHistShards = 8;        // global histograms sharded by blockIdx % 8 (XCD group)
-constexpr int kRadixBins = 256;
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // key of a culled Gaussian (no visible splat has it)
 constexpr int kRecFloats = 16;        // 64-B projected record
+constexpr int kMaxGrid = 2048;        // persistent grids: 8 workgroups per CU
+constexpr uint32_t kMinChunk0 = 65536;  // smallest first chunk (depth ranks)
 
-// Device-side error word bits (ctx->d_err); a nonzero word fails the frame.
-constexpr uint32_t kErrSpinSort = 1u, kErrSpinBin = 2u, kErrOverflow = 4u;
+// Packed tile rectangle carried through the depth sort (32 bits): tx0[0:12) ty0[12:24)
+// (w-1)[24:28) (h-1)[28:32).  Rectangles wider or taller than 16 tiles use kRectLarge (the
+// binning reads the full rectangle from the record); kRectEmpty = visible but binds no tile.
+constexpr uint32_t kRectLarge = 0xFFFFFFFFu;
+constexpr uint32_t kRectEmpty = 0xFFFFFFFEu;
+
+// Device-side error bits (FrameCtl::err); a nonzero word fails the frame.
+constexpr uint32_t kErrOverflow = 1u;
+
+struct FrameCtl {                 // zeroed at the start of every frame
+    unsigned long long k_total;   // sum of tile counts over visible splats (project)
+    uint32_t n_vis;               // splats reaching the sort (project)
+    uint32_t k_chunk[2];          // (tile, splat) entries per chunk (binning scan)
+    uint32_t not_done;            // tiles still accepting splats after chunk 0
+    uint32_t err;
+    uint32_t pad[9];
+};
 
 struct ProjParams {
     const float* planes;      // SoA planes, plane p at planes + p * plane_stride
@@ -34,40 +55,49 @@ struct ProjParams {
     int W, H;
     int tile_row_begin, tile_row_end, tiles_x;
     uint32_t* keys_out;       // [n]: depth key or kSentinel
+    uint32_t* rect_out;       // [n]: packed tile rectangle
     float4* rec;              // [n][4]: projected records
     uint32_t* hist;           // [kHistShards][4][256] depth-key digit histograms (zeroed)
-    unsigned long long* counters;  // [0] = n_vis, [1] = K (sum of tile counts)
+    FrameCtl* ctl;
 };
 
 struct SortPass {
     const uint32_t* keys_in;
     const uint32_t* vals_in;  // nullptr: values are the element index (first depth pass)
+    const uint32_t* aux_in;   // optional second value array carried with the elements
     uint32_t* keys_out;
-    uint32_t* vals_out;       // may be nullptr? no: always written
-    uint32_t n;               // elements read
+    uint32_t* vals_out;
+    uint32_t* aux_out;
+    uint32_t n;               // element count, or an upper bound when n_dev is set
+    const uint32_t* n_dev;    // device-side element count (nullable)
+    uint32_t parts_max;       // sort_parts(upper bound): stride of `offsets`, grid bound
     int shift;
     uint32_t mask;            // digit mask (<= 255)
     int filter_sentinel;      // 1: drop keys == kSentinel (they carry no digit)
-    const uint32_t* hist;     // [kHistShards][npass][256] slice base for this pass, stride hist_stride
+    const uint32_t* hist;     // global digit histogram of this pass, kHistShards shards
     int hist_stride;          // elements between shards
-    uint32_t* status;         // [parts][256] look-back words (zeroed)
-    uint32_t* ticket;         // partition ticket counter (zeroed)
-    uint32_t* err;
+    uint32_t* offsets;        // [256][parts_max] scratch: partition counts, then offsets
 };
 
 struct BinParams {
     const uint32_t* sorted_vals;  // [n_vis] Gaussian index in depth order
-    const float4* rec;
-    uint32_t n_vis;
+    const uint32_t* sorted_rect;  // [n_vis] packed tile rectangle in depth order
+    const float4* rec;            // records (full rectangle of kRectLarge splats)
+    const uint8_t* done;          // chunk 1: per-tile "saturated after chunk 0"
+    FrameCtl* ctl;
+    int chunk;                    // 0 or 1
+    float chunk_f;                // chunk 0 = ceil(chunk_f * n_vis) depth ranks (>= kMinChunk0);
+                                  // >= 1: chunk 0 takes every rank
     int tile_row_begin, tiles_x;
-    uint64_t capacity;            // entry capacity of out arrays
+    uint32_t n_max;               // upper bound of n_vis (grid / scratch sizing)
+    uint32_t capacity;            // entry capacity of out arrays
+    uint32_t* part_tot;           // [bin_parts(n_max) + 1] scratch
     uint32_t* tkeys;              // out: strip-relative tile id
     uint32_t* tvals;              // out: Gaussian index
     uint32_t* hist;               // [kHistShards][2][256] tile-id digit histograms (zeroed)
-    unsigned long long* status;   // [parts] look-back words (zeroed)
-    uint32_t* ticket;
-    uint32_t* err;
 };
+
+enum CompositeMode { kCompSingle = 0, kCompFirst = 1, kCompSecond = 2 };
 
 struct CompositeParams {
     const uint2* ranges;          // [n_tiles] (begin, end) into tvals
@@ -76,6 +106,10 @@ struct CompositeParams {
     int W, H, tiles_x, tile_row_begin, row0;  // row0 = first image row of the output buffer
     int n_tiles;
     float t_min;
+    int mode;                     // CompositeMode
+    float4* state;                // per pixel (rgb, T or dst.a) of unsaturated tiles, image rows
+    uint8_t* done;                // per tile: 1 = saturated after chunk 0
+    FrameCtl* ctl;
     void* out;                    // rows_padded x W pixels
     int out_f16;
 };
@@ -83,15 +117,16 @@ struct CompositeParams {
 // launchers (gs_kernels.hip)
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, uint64_t stride,
                       hipStream_t s);
-void launch_project(const ProjParams& p, int grid, hipStream_t s);
+void launch_project(const ProjParams& p, hipStream_t s);
 void launch_hist_keys(const uint32_t* keys, uint32_t n, int begin_bit, int end_bit, int npass,
                       uint32_t* hist, hipStream_t s);
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);
-void launch_ranges(const uint32_t* tkeys, uint64_t k, uint2* ranges, hipStream_t s);
+void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
+                   hipStream_t s);
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);
 
-inline uint32_t sort_parts(uint64_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }
-inline uint32_t bin_parts(uint64_t n) { return (uint32_t)((n + kBinTile - 1) / kBinTile); }
+__host__ __device__ inline uint32_t sort_parts(uint64_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }
+__host__ __device__ inline uint32_t bin_parts(uint64_t n) { return (uint32_t)((n + kBinTile - 1) / kBinTile); }
 
 }  // namespace gs

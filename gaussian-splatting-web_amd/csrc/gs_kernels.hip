@@ -4,8 +4,8 @@
 //   k_project     per Gaussian: depth key (src/shaders.ts:36-68) + vs_points projection
 //                 (src/simple_render.ts:217-332) + SH colour (:26-66) + tile rectangle;
 //                 streaming, one pass over the SoA planes; fuses the radix histograms.
-//   k_sort_pass   one stable 8-bit LSD radix pass, Onesweep style (partition ticket +
-//                 decoupled look-back); replaces webgpu-radix-sort's 16 x 2-bit passes (RS:621-654).
+//   k_radix_*     one stable 8-bit LSD radix pass (upsweep / scan / downsweep); replaces
+//                 webgpu-radix-sort's 16 x 2-bit passes (RS:621-654).
 //   k_bin         per depth-sorted splat: (tile, splat) pairs emitted in depth order
 //                 (order-preserving exclusive scan with look-back, wave64 ballot ranks).
 //   k_ranges      per tile: [begin, end) of its list after the stable tile-id sort.
@@ -21,10 +21,7 @@
 namespace gs {
 namespace {
 
-constexpr uint32_t kFlagAgg = 1u << 30, kFlagInc = 2u << 30, kValMask = (1u << 30) - 1;
-constexpr unsigned long long kFlagAgg64 = 1ull << 62, kFlagInc64 = 2ull << 62,
-                             kValMask64 = (1ull << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr float kSqrtLog2e = 1.2011224087864498f;  // sqrt(log2(e))
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -60,19 +57,6 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp
     *total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
     __syncthreads();
     return base + incl - v;
-}
-
-__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_relaxed(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_relaxed64(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_relaxed64(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ============================================================================ k_transpose
@@ -276,7 +260,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
         }
         vis = vis && pixel_rect(f.cx, f.cy, qhx, qhy, p.W, row_lo, row_hi, qxl, qxh, qyl, qyh);
 
-        uint32_t key = kSentinel;
+        uint32_t key = kSentinel, prect = kRectEmpty;
         if (vis) {
             key = sortable_key(vz);
             // binning rectangle: quad box intersected with the alpha >= 1/255 disc box, widened by
@@ -287,12 +271,18 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
             hx = hx * 1.0001f + 0.02f;
             hy = hy * 1.0001f + 0.02f;
             float xl, xh, yl, yh;
-            uint32_t ntiles = 0, rx = 0, ry = 0;
+            uint32_t ntiles = 0, rx = 0, ry = 0, bbx = 0xFFFFu, bby = 0xFFFFu;  // empty box
             if (pixel_rect(f.cx, f.cy, hx, hy, p.W, row_lo, row_hi, xl, xh, yl, yh)) {
-                const int tx0 = (int)xl >> 4, tx1 = (int)xh >> 4, ty0 = (int)yl >> 4, ty1 = (int)yh >> 4;
-                ntiles = (uint32_t)((tx1 - tx0 + 1) * (ty1 - ty0 + 1));
-                rx = (uint32_t)tx0 | ((uint32_t)ty0 << 16);
-                ry = (uint32_t)tx1 | ((uint32_t)ty1 << 16);
+                bbx = (uint32_t)xl | ((uint32_t)xh << 16);
+                bby = (uint32_t)yl | ((uint32_t)yh << 16);
+                const uint32_t tx0 = (uint32_t)xl >> 4, tx1 = (uint32_t)xh >> 4,
+                               ty0 = (uint32_t)yl >> 4, ty1 = (uint32_t)yh >> 4;
+                ntiles = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+                rx = tx0 | (ty0 << 16);
+                ry = tx1 | (ty1 << 16);
+                prect = (tx1 - tx0 < 16 && ty1 - ty0 < 16)
+                            ? (tx0 | (ty0 << 12) | ((tx1 - tx0) << 24) | ((ty1 - ty0) << 28))
+                            : kRectLarge;
             }
             // colour (:321, dir = normalize(p - camPos))
             const float dx = x - p.cam[0], dy = y - p.cam[1], dz = z - p.cam[2];
@@ -301,12 +291,16 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
             const float cr = sh_channel(P, S, i, 0, p.n_sh, X, Y, Z);
             const float cg = sh_channel(P, S, i, 1, p.n_sh, X, Y, Z);
             const float cb = sh_channel(P, S, i, 2, p.n_sh, X, Y, Z);
-            const float n1 = f.e1x * f.e1x + f.e1y * f.e1y, n2 = f.e2x * f.e2x + f.e2y * f.e2y;
+            // composite record: u' = d.(e1/|e1|^2)*sqrt(log2 e), so u'^2+v'^2 = (u^2+v^2) log2 e and
+            // alpha = op * exp(-(u^2+v^2)) = exp2(log2(op) - (u'^2+v'^2))
+            const float k1 = kSqrtLog2e / (f.e1x * f.e1x + f.e1y * f.e1y);
+            const float k2 = kSqrtLog2e / (f.e2x * f.e2x + f.e2y * f.e2y);
             float4* r = p.rec + 4 * (uint64_t)i;
-            r[0] = make_float4(f.cx, f.cy, f.e1x / n1, f.e1y / n1);
-            r[1] = make_float4(f.e2x / n2, f.e2y / n2, op, cr);
-            r[2] = make_float4(cg, cb, __uint_as_float(rx), __uint_as_float(ry));
-            r[3] = make_float4(__uint_as_float(key), __uint_as_float(ntiles), 0.0f, 0.0f);
+            r[0] = make_float4(f.cx, f.cy, f.e1x * k1, f.e1y * k1);
+            r[1] = make_float4(f.e2x * k2, f.e2y * k2, log2f(op), cr);
+            r[2] = make_float4(cg, cb, __uint_as_float(bbx), __uint_as_float(bby));
+            r[3] = make_float4(__uint_as_float(key), __uint_as_float(ntiles), __uint_as_float(rx),
+                               __uint_as_float(ry));
             atomicAdd(&s_hist[0][key & 255], 1u);
             atomicAdd(&s_hist[1][(key >> 8) & 255], 1u);
             atomicAdd(&s_hist[2][(key >> 16) & 255], 1u);
@@ -315,6 +309,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
             my_k += ntiles;
         }
         p.keys_out[i] = key;
+        p.rect_out[i] = prect;
     }
     if (my_vis) {
         atomicAdd(&s_vis, my_vis);
@@ -327,8 +322,8 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
         if (c) atomicAdd(gh + t, c);
     }
     if (threadIdx.x == 0 && s_vis) {
-        atomicAdd(p.counters + 0, (unsigned long long)s_vis);
-        atomicAdd(p.counters + 1, s_k);
+        atomicAdd(&p.ctl->n_vis, s_vis);
+        atomicAdd(&p.ctl->k_total, s_k);
     }
 }
 
@@ -356,210 +351,341 @@ __global__ __launch_bounds__(256) void k_hist_keys(const uint32_t* __restrict__ 
     }
 }
 
-// ============================================================================ k_sort_pass
-// One stable LSD pass.  Partition = 4096 consecutive elements, owned by the workgroup that drew
-// its ticket (so every predecessor it waits on is already running).  Per partition:
-//   1. wave-ordered stable ranking: element order inside the partition is (wave, item, lane);
-//      peers with the same digit are found with 8 ballots, counts kept per wave in LDS;
-//   2. digit counts published as an aggregate, decoupled look-back for the exclusive prefix;
-//   3. scatter through an LDS staging area so global writes of one digit run are contiguous.
-__global__ __launch_bounds__(kSortThreads) void k_sort_pass(SortPass p) {
+// ============================================================================ radix pass
+// One stable LSD pass = three launches, no inter-workgroup waiting:
+//   k_radix_upsweep    per 4096-element partition: digit histogram -> counts[digit][part]
+//   k_radix_scan       per digit: offsets[digit][part] = base[digit] + sum of earlier partitions
+//   k_radix_downsweep  per partition: stable local ranks (wave ballots, element order inside the
+//                      partition = (wave, item, lane)), LDS staging, contiguous writes per digit run
+// This replaces webgpu-radix-sort's 16 x 2-bit passes (RS:621-654) with 8-bit digits.
+
+__device__ __forceinline__ uint32_t radix_n(const SortPass& p) { return p.n_dev ? *p.n_dev : p.n; }
+__device__ __forceinline__ bool radix_valid(const SortPass& p, uint32_t n, uint64_t idx, uint32_t key) {
+    return idx < n && !(p.filter_sentinel && key == kSentinel);
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(SortPass p) {
+    __shared__ uint32_t s_hist[4][256];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t n = radix_n(p), parts = sort_parts(n);
+    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+        for (int t = tid; t < 1024; t += kSortThreads) (&s_hist[0][0])[t] = 0;
+        __syncthreads();
+        const uint64_t wbase = (uint64_t)part * kSortTile + (uint64_t)w * (kSortIPT * 64);
+#pragma unroll 4
+        for (int it = 0; it < kSortIPT; ++it) {
+            const uint64_t idx = wbase + it * 64 + lane;
+            const uint32_t key = idx < n ? p.keys_in[idx] : kSentinel;
+            if (radix_valid(p, n, idx, key)) atomicAdd(&s_hist[w][(key >> p.shift) & p.mask], 1u);
+        }
+        __syncthreads();
+        const uint32_t c = s_hist[0][tid] + s_hist[1][tid] + s_hist[2][tid] + s_hist[3][tid];
+        p.offsets[(uint64_t)tid * p.parts_max + part] = c;  // digit-major
+        __syncthreads();
+    }
+}
+
+// Block d scans column d over partitions and adds the global digit base (exclusive scan of the
+// global histogram, which the producing kernel accumulated in kHistShards shards).
+__global__ __launch_bounds__(256) void k_radix_scan(SortPass p) {
+    __shared__ uint32_t s_tmp[8];
+    __shared__ uint32_t s_base;
+    const int d = blockIdx.x, tid = threadIdx.x;
+    const uint32_t parts = sort_parts(radix_n(p));
+    uint32_t tot = 0;
+    for (int sh = 0; sh < kHistShards; ++sh) tot += p.hist[sh * p.hist_stride + tid];
+    uint32_t gtotal;
+    const uint32_t gbase = block_excl_scan256(tot, s_tmp, &gtotal);
+    if (tid == d) s_base = gbase;
+    __syncthreads();
+    uint32_t* col = p.offsets + (uint64_t)d * p.parts_max;
+    const uint32_t per = (parts + 255) / 256;
+    const uint32_t b0 = min(parts, tid * per), b1 = min(parts, b0 + per);
+    uint32_t sum = 0;
+    for (uint32_t i = b0; i < b1; ++i) sum += col[i];
+    uint32_t total;
+    uint32_t run = s_base + block_excl_scan256(sum, s_tmp, &total);
+    for (uint32_t i = b0; i < b1; ++i) {
+        const uint32_t c = col[i];
+        col[i] = run;
+        run += c;
+    }
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
     __shared__ uint32_t s_wave_hist[4][256];
     __shared__ uint32_t s_digit_start[256];
     __shared__ uint32_t s_global[256];
     __shared__ uint32_t s_keys[kSortTile];
     __shared__ uint32_t s_vals[kSortTile];
+    __shared__ uint32_t s_aux[kSortTile];
     __shared__ uint32_t s_tmp[8];
-    __shared__ uint32_t s_part;
 
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    if (tid == 0) s_part = atomicAdd(p.ticket, 1u);
-    for (int t = tid; t < 1024; t += kSortThreads) (&s_wave_hist[0][0])[t] = 0;
-    // global digit base for this pass: exclusive scan over bins of the sharded histogram
-    uint32_t gcount = 0;
-    for (int sh = 0; sh < kHistShards; ++sh) gcount += p.hist[sh * p.hist_stride + tid];
-    uint32_t gtotal;
-    const uint32_t gbase = block_excl_scan256(gcount, s_tmp, &gtotal);  // has __syncthreads
-    const uint32_t part = s_part;
-    const uint64_t base = (uint64_t)part * kSortTile;
+    const uint32_t n = radix_n(p), parts = sort_parts(n);
+    const bool has_aux = p.aux_in != nullptr;
+    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+        for (int t = tid; t < 1024; t += kSortThreads) (&s_wave_hist[0][0])[t] = 0;
+        s_global[tid] = p.offsets[(uint64_t)tid * p.parts_max + part];
+        const uint64_t wbase = (uint64_t)part * kSortTile + (uint64_t)w * (kSortIPT * 64);
 
-    uint32_t keys[kSortIPT], vals[kSortIPT], rank[kSortIPT];
-    const uint64_t wbase = base + (uint64_t)w * (kSortIPT * 64);
+        uint32_t keys[kSortIPT], vals[kSortIPT], aux[kSortIPT], rank[kSortIPT];
 #pragma unroll
-    for (int it = 0; it < kSortIPT; ++it) {
-        const uint64_t idx = wbase + it * 64 + lane;
-        const bool in = idx < p.n;
-        keys[it] = in ? p.keys_in[idx] : kSentinel;
-        vals[it] = in ? (p.vals_in ? p.vals_in[idx] : (uint32_t)idx) : 0u;
-        // valid marker folded into rank's top bit until ranked
-        const bool valid = in && !(p.filter_sentinel && keys[it] == kSentinel);
-        rank[it] = valid ? 0u : 0x80000000u;
-    }
-#pragma unroll
-    for (int it = 0; it < kSortIPT; ++it) {
-        const bool valid = (rank[it] & 0x80000000u) == 0u;
-        const uint32_t digit = (keys[it] >> p.shift) & p.mask;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (digit >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
+        for (int it = 0; it < kSortIPT; ++it) {
+            const uint64_t idx = wbase + it * 64 + lane;
+            const bool in = idx < n;
+            keys[it] = in ? p.keys_in[idx] : kSentinel;
+            vals[it] = in ? (p.vals_in ? p.vals_in[idx] : (uint32_t)idx) : 0u;
+            aux[it] = (in && has_aux) ? p.aux_in[idx] : 0u;
+            rank[it] = radix_valid(p, n, idx, keys[it]) ? 0u : 0x80000000u;  // top bit: unsorted
         }
-        if (valid) {
-            const uint32_t lower = __popcll(peers & lanemask_lt());
-            const uint32_t prev = s_wave_hist[w][digit];
-            rank[it] = prev + lower;
-            if (lower + 1 == (uint32_t)__popcll(peers)) s_wave_hist[w][digit] = prev + lower + 1;
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-
-    // per digit (thread = digit): wave offsets, partition count, publish, look-back
-    const int d = tid;
-    const uint32_t c0 = s_wave_hist[0][d], c1 = s_wave_hist[1][d], c2 = s_wave_hist[2][d],
-                   c3 = s_wave_hist[3][d];
-    const uint32_t cnt = c0 + c1 + c2 + c3;
-    uint32_t* st = p.status + (uint64_t)part * 256;
-    st_relaxed(st + d, (part == 0 ? kFlagInc : kFlagAgg) | cnt);
-    uint32_t excl = 0;
-    if (part > 0) {
-        int64_t q = (int64_t)part - 1;
-        uint32_t spins = 0;
-        while (q >= 0) {
-            const uint32_t s = ld_relaxed(p.status + (uint64_t)q * 256 + d);
-            const uint32_t flag = s & ~kValMask;
-            if (flag == 0u) {
-                if (++spins > kSpinLimit) { atomicOr(p.err, kErrSpinSort); break; }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            excl += s & kValMask;
-            if (flag == kFlagInc) break;
-            --q;
-        }
-        st_relaxed(st + d, kFlagInc | (excl + cnt));
-    }
-    uint32_t tile_total;
-    const uint32_t dstart = block_excl_scan256(cnt, s_tmp, &tile_total);  // has __syncthreads
-    s_digit_start[d] = dstart;
-    s_global[d] = gbase + excl;
-    s_wave_hist[0][d] = 0;
-    s_wave_hist[1][d] = c0;
-    s_wave_hist[2][d] = c0 + c1;
-    s_wave_hist[3][d] = c0 + c1 + c2;
-    __syncthreads();
-
+        __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kSortIPT; ++it) {
-        if ((rank[it] & 0x80000000u) == 0u) {
+        for (int it = 0; it < kSortIPT; ++it) {
+            const bool valid = (rank[it] & 0x80000000u) == 0u;
             const uint32_t digit = (keys[it] >> p.shift) & p.mask;
-            const uint32_t pos = s_digit_start[digit] + s_wave_hist[w][digit] + rank[it];
-            s_keys[pos] = keys[it];
-            s_vals[pos] = vals[it];
+            uint64_t peers = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const bool bit = (digit >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                peers &= bit ? bb : ~bb;
+            }
+            if (valid) {
+                const uint32_t lower = __popcll(peers & lanemask_lt());
+                const uint32_t prev = s_wave_hist[w][digit];
+                rank[it] = prev + lower;
+                if (lower + 1 == (uint32_t)__popcll(peers)) s_wave_hist[w][digit] = prev + lower + 1;
+            }
+            __builtin_amdgcn_wave_barrier();
         }
-    }
-    __syncthreads();
-    for (uint32_t q = tid; q < tile_total; q += kSortThreads) {
-        const uint32_t k = s_keys[q];
-        const uint32_t digit = (k >> p.shift) & p.mask;
-        const uint32_t dest = s_global[digit] + (q - s_digit_start[digit]);
-        p.keys_out[dest] = k;
-        p.vals_out[dest] = s_vals[q];
+        __syncthreads();
+
+        const int d = tid;
+        const uint32_t c0 = s_wave_hist[0][d], c1 = s_wave_hist[1][d], c2 = s_wave_hist[2][d],
+                       c3 = s_wave_hist[3][d];
+        uint32_t tile_total;
+        const uint32_t dstart = block_excl_scan256(c0 + c1 + c2 + c3, s_tmp, &tile_total);
+        s_digit_start[d] = dstart;
+        s_wave_hist[0][d] = 0;
+        s_wave_hist[1][d] = c0;
+        s_wave_hist[2][d] = c0 + c1;
+        s_wave_hist[3][d] = c0 + c1 + c2;
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kSortIPT; ++it) {
+            if ((rank[it] & 0x80000000u) == 0u) {
+                const uint32_t digit = (keys[it] >> p.shift) & p.mask;
+                const uint32_t pos = s_digit_start[digit] + s_wave_hist[w][digit] + rank[it];
+                s_keys[pos] = keys[it];
+                s_vals[pos] = vals[it];
+                if (has_aux) s_aux[pos] = aux[it];
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = tid; q < tile_total; q += kSortThreads) {
+            const uint32_t k = s_keys[q];
+            const uint32_t digit = (k >> p.shift) & p.mask;
+            const uint32_t dest = s_global[digit] + (q - s_digit_start[digit]);
+            p.keys_out[dest] = k;
+            p.vals_out[dest] = s_vals[q];
+            if (has_aux) p.aux_out[dest] = s_aux[q];
+        }
+        __syncthreads();
     }
 }
 
-// ============================================================================ k_bin
-__global__ __launch_bounds__(kBinThreads) void k_bin(BinParams p) {
-    __shared__ uint32_t s_off[kBinTile + 1];
-    __shared__ uint32_t s_j[kBinTile];
-    __shared__ uint2 s_rect[kBinTile];
-    __shared__ uint32_t s_hist[2][256];
-    __shared__ uint32_t s_tmp[8];
-    __shared__ uint32_t s_part;
-    __shared__ unsigned long long s_base;
-
-    const int tid = threadIdx.x;
-    if (tid == 0) s_part = atomicAdd(p.ticket, 1u);
-    s_hist[0][tid] = 0;
-    s_hist[1][tid] = 0;
-    __syncthreads();
-    const uint32_t part = s_part;
-    const uint64_t base = (uint64_t)part * kBinTile;
-    const uint32_t nitems = (uint32_t)min((uint64_t)kBinTile, (uint64_t)p.n_vis - base);
-
-    uint32_t cnt[kBinIPT];
-    uint32_t tsum = 0;
-#pragma unroll
-    for (int k = 0; k < kBinIPT; ++k) {
-        const uint32_t li = tid * kBinIPT + k;
-        cnt[k] = 0;
-        if (li < nitems) {
-            const uint32_t j = p.sorted_vals[base + li];
-            const float4 c = p.rec[4 * (uint64_t)j + 2];
-            const uint32_t rx = __float_as_uint(c.z), ry = __float_as_uint(c.w);
-            cnt[k] = __float_as_uint(p.rec[4 * (uint64_t)j + 3].y);  // 0: no pixel reaches 1/255
-            s_j[li] = j;
-            s_rect[li] = make_uint2(rx, ry);
-        }
-        tsum += cnt[k];
+// ============================================================================ binning
+// Chunk c covers depth ranks [r0, r1): chunk 0 = the first ceil(f * n_vis) ranks, chunk 1 = the
+// rest, binned only into tiles that were not saturated by chunk 0 (empty when all are).
+// Three launches per chunk, no inter-workgroup waiting: per-partition entry counts, one scan,
+// then the emission in depth order (cooperative, coalesced) plus the tile-id digit histograms.
+__device__ __forceinline__ void chunk_range(const BinParams& p, uint32_t& r0, uint32_t& r1) {
+    const uint32_t n = p.ctl->n_vis;
+    const uint32_t c0 = p.chunk_f >= 1.0f
+                            ? n
+                            : min(n, max(kMinChunk0, (uint32_t)ceilf(p.chunk_f * (float)n)));
+    if (p.chunk == 0) {
+        r0 = 0;
+        r1 = c0;
+    } else {
+        r0 = c0;
+        r1 = p.ctl->not_done ? n : c0;
     }
-    uint32_t total;
-    uint32_t run = block_excl_scan256(tsum, s_tmp, &total);
+}
+
+struct TileRect {
+    uint32_t x0, y0, x1, y1;  // inclusive, absolute tile coordinates
+};
+
+__device__ __forceinline__ bool rect_unpack(const BinParams& p, uint32_t pr, uint32_t j, TileRect& r) {
+    if (pr == kRectEmpty) return false;
+    if (pr == kRectLarge) {
+        const float4 m = p.rec[4 * (uint64_t)j + 3];
+        const uint32_t rx = __float_as_uint(m.z), ry = __float_as_uint(m.w);
+        r = {rx & 0xffffu, rx >> 16, ry & 0xffffu, ry >> 16};
+    } else {
+        r.x0 = pr & 0xfffu;
+        r.y0 = (pr >> 12) & 0xfffu;
+        r.x1 = r.x0 + ((pr >> 24) & 15u);
+        r.y1 = r.y0 + (pr >> 28);
+    }
+    return true;
+}
+
+__device__ __forceinline__ uint32_t tile_id(const BinParams& p, uint32_t tx, uint32_t ty) {
+    return (ty - (uint32_t)p.tile_row_begin) * (uint32_t)p.tiles_x + tx;
+}
+
+// entries of one splat in this chunk (chunk 1: only unsaturated tiles)
+__device__ __forceinline__ uint32_t rect_count(const BinParams& p, const TileRect& r) {
+    if (p.chunk == 0) return (r.x1 - r.x0 + 1) * (r.y1 - r.y0 + 1);
+    uint32_t c = 0;
+    for (uint32_t ty = r.y0; ty <= r.y1; ++ty)
+        for (uint32_t tx = r.x0; tx <= r.x1; ++tx) c += p.done[tile_id(p, tx, ty)] ? 0u : 1u;
+    return c;
+}
+
+__global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
+    __shared__ uint32_t s_tmp[8];
+    uint32_t r0, r1;
+    chunk_range(p, r0, r1);
+    const uint32_t parts = bin_parts(r1 - r0);
+    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+        uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < kBinIPT; ++k) {
-        s_off[tid * kBinIPT + k] = run;
-        run += cnt[k];
+        for (int k = 0; k < kBinIPT; ++k) {
+            const uint32_t r = r0 + part * kBinTile + threadIdx.x * kBinIPT + k;
+            if (r < r1) {
+                TileRect tr;
+                if (rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) sum += rect_count(p, tr);
+            }
+        }
+        uint32_t total;
+        block_excl_scan256(sum, s_tmp, &total);
+        if (threadIdx.x == 0) p.part_tot[part] = total;
+    }
+}
+
+// single workgroup: exclusive scan of the partition totals (in place), entry count, capacity
+__global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
+    __shared__ uint32_t s_w[16];
+    uint32_t r0, r1;
+    chunk_range(p, r0, r1);
+    const uint32_t parts = bin_parts(r1 - r0);
+    const uint32_t tid = threadIdx.x, per = (parts + 1023) / 1024;
+    const uint32_t b0 = min(parts, tid * per), b1 = min(parts, b0 + per);
+    unsigned long long sum = 0;
+    for (uint32_t i = b0; i < b1; ++i) sum += p.part_tot[i];
+    // 64-bit inclusive wave scan, then across the 16 waves
+    unsigned long long incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long t = __shfl_up(incl, d, 64);
+        if ((int)lane_id() >= d) incl += t;
+    }
+    __shared__ unsigned long long s_wsum[16];
+    if (lane_id() == 63) s_wsum[tid >> 6] = incl;
+    __syncthreads();
+    unsigned long long base = 0, total = 0;
+    for (uint32_t i = 0; i < 16; ++i) {
+        if (i < (tid >> 6)) base += s_wsum[i];
+        total += s_wsum[i];
+    }
+    unsigned long long run = base + incl - sum;
+    for (uint32_t i = b0; i < b1; ++i) {
+        const uint32_t c = p.part_tot[i];
+        p.part_tot[i] = (uint32_t)min(run, (unsigned long long)p.capacity);
+        run += c;
     }
     if (tid == 0) {
-        unsigned long long* st = p.status + part;
-        st_relaxed64(st, (part == 0 ? kFlagInc64 : kFlagAgg64) | (unsigned long long)total);
-        unsigned long long excl = 0;
-        if (part > 0) {
-            int64_t q = (int64_t)part - 1;
-            uint32_t spins = 0;
-            while (q >= 0) {
-                const unsigned long long s = ld_relaxed64(p.status + q);
-                const unsigned long long flag = s & ~kValMask64;
-                if (flag == 0ull) {
-                    if (++spins > kSpinLimit) { atomicOr(p.err, kErrSpinBin); break; }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += s & kValMask64;
-                if (flag == kFlagInc64) break;
-                --q;
+        p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
+        if (total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
+    }
+    (void)s_w;
+}
+
+__global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
+    __shared__ uint32_t s_off[kBinTile + 1];
+    __shared__ uint32_t s_j[kBinTile];
+    __shared__ TileRect s_rect[kBinTile];
+    __shared__ uint32_t s_hist[2][256];
+    __shared__ uint32_t s_tmp[8];
+    const int tid = threadIdx.x;
+    uint32_t r0, r1;
+    chunk_range(p, r0, r1);
+    const uint32_t parts = bin_parts(r1 - r0);
+    s_hist[0][tid] = 0;
+    s_hist[1][tid] = 0;
+    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+        const uint32_t base_r = r0 + part * kBinTile;
+        const uint32_t nitems = min((uint32_t)kBinTile, r1 - base_r);
+        uint32_t cnt[kBinIPT];
+        uint32_t tsum = 0;
+#pragma unroll
+        for (int k = 0; k < kBinIPT; ++k) {
+            const uint32_t li = tid * kBinIPT + k;
+            cnt[k] = 0;
+            if (li < nitems) {
+                const uint32_t j = p.sorted_vals[base_r + li];
+                TileRect tr;
+                if (rect_unpack(p, p.sorted_rect[base_r + li], j, tr)) cnt[k] = rect_count(p, tr);
+                s_j[li] = j;
+                s_rect[li] = tr;
             }
-            st_relaxed64(st, kFlagInc64 | (excl + total));
+            tsum += cnt[k];
         }
-        s_base = excl;
-    }
-    __syncthreads();
-    const unsigned long long obase = s_base;
-    if (obase + total > p.capacity) {
-        if (tid == 0) atomicOr(p.err, kErrOverflow);
-        return;
-    }
-    // cooperative, coalesced emission of this partition's entries (depth order preserved)
-    for (uint32_t e = tid; e < total; e += kBinThreads) {
-        int lo = 0, hi = (int)nitems - 1;
-        while (lo < hi) {  // largest s with s_off[s] <= e
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_off[mid] <= e) lo = mid; else hi = mid - 1;
+        uint32_t total;
+        uint32_t run = block_excl_scan256(tsum, s_tmp, &total);
+#pragma unroll
+        for (int k = 0; k < kBinIPT; ++k) {
+            s_off[tid * kBinIPT + k] = run;
+            run += cnt[k];
         }
-        const uint2 rc = s_rect[lo];
-        const uint32_t k = e - s_off[lo];
-        const uint32_t w = (rc.y & 0xffffu) - (rc.x & 0xffffu) + 1u;
-        const uint32_t tx = (rc.x & 0xffffu) + k % w;
-        const uint32_t ty = (rc.x >> 16) + k / w;
-        const uint32_t tile = (ty - (uint32_t)p.tile_row_begin) * (uint32_t)p.tiles_x + tx;
-        p.tkeys[obase + e] = tile;
-        p.tvals[obase + e] = s_j[lo];
-        atomicAdd(&s_hist[0][tile & 255], 1u);
-        atomicAdd(&s_hist[1][(tile >> 8) & 255], 1u);
+        __syncthreads();
+        const uint32_t obase = p.part_tot[part];
+        if (p.chunk == 0) {
+            // cooperative, coalesced emission (depth order preserved within every tile)
+            for (uint32_t e = tid; e < total; e += kBinThreads) {
+                if (obase + e >= p.capacity) break;
+                int lo = 0, hi = (int)nitems - 1;
+                while (lo < hi) {  // largest s with s_off[s] <= e
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_off[mid] <= e) lo = mid; else hi = mid - 1;
+                }
+                const TileRect tr = s_rect[lo];
+                const uint32_t k = e - s_off[lo];
+                const uint32_t w = tr.x1 - tr.x0 + 1;
+                const uint32_t tile = tile_id(p, tr.x0 + k % w, tr.y0 + k / w);
+                p.tkeys[obase + e] = tile;
+                p.tvals[obase + e] = s_j[lo];
+                atomicAdd(&s_hist[0][tile & 255], 1u);
+                atomicAdd(&s_hist[1][(tile >> 8) & 255], 1u);
+            }
+        } else {
+            // chunk 1 (few unsaturated tiles): every splat walks its own rectangle
+#pragma unroll
+            for (int k = 0; k < kBinIPT; ++k) {
+                const uint32_t li = tid * kBinIPT + k;
+                if (li >= nitems || cnt[k] == 0) continue;
+                const TileRect tr = s_rect[li];
+                uint32_t o = obase + s_off[li];
+                for (uint32_t ty = tr.y0; ty <= tr.y1; ++ty)
+                    for (uint32_t tx = tr.x0; tx <= tr.x1; ++tx) {
+                        const uint32_t tile = tile_id(p, tx, ty);
+                        if (p.done[tile]) continue;
+                        if (o < p.capacity) {
+                            p.tkeys[o] = tile;
+                            p.tvals[o] = s_j[li];
+                            atomicAdd(&s_hist[0][tile & 255], 1u);
+                            atomicAdd(&s_hist[1][(tile >> 8) & 255], 1u);
+                        }
+                        ++o;
+                    }
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
     uint32_t* gh = p.hist + (blockIdx.x % kHistShards) * 512;
     for (int t = tid; t < 512; t += kBinThreads) {
         const uint32_t c = (&s_hist[0][0])[t];
@@ -568,79 +694,146 @@ __global__ __launch_bounds__(kBinThreads) void k_bin(BinParams p) {
 }
 
 // ============================================================================ k_ranges
-__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tkeys, uint64_t k,
+__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tkeys,
+                                                const uint32_t* __restrict__ k_dev,
                                                 uint2* __restrict__ ranges) {
-    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < k;
-         q += (uint64_t)gridDim.x * 256) {
+    const uint32_t k = *k_dev;
+    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < k; q += gridDim.x * 256) {
         const uint32_t t = tkeys[q];
-        if (q == 0 || tkeys[q - 1] != t) ranges[t].x = (uint32_t)q;
-        if (q == k - 1 || tkeys[q + 1] != t) ranges[t].y = (uint32_t)(q + 1);
+        if (q == 0 || tkeys[q - 1] != t) ranges[t].x = q;
+        if (q == k - 1 || tkeys[q + 1] != t) ranges[t].y = q + 1;
     }
 }
 
 // ============================================================================ k_composite
-// One workgroup per 16x16 tile, one pixel per thread.  Splats of the tile's list (depth order)
-// are staged 256 at a time in LDS; every pixel evaluates fs_main's alpha at its centre and
-// blends front to back with the reference's blend state:
-//   dst.rgb = (col*alpha)*(1-dst.a) + dst.rgb ; dst.a = alpha*(1-dst.a) + dst.a
-// A pixel is done once dst.a == 1 (nothing can change it) or 1-dst.a < t_min; the workgroup
-// leaves as soon as every pixel is done.
+// Workgroup = one 16x16 tile; wave w owns the 8x8 quarter (w&1, w>>1), lane = one pixel.
+// The tile's depth-ordered list is consumed in batches of 256 splats: every thread gathers one
+// 48-B record into registers (next batch issued before the current one is blended) and parks it
+// in a double-buffered LDS stage; each wave then walks the batch on its own, skips splats whose
+// pixel box misses its quarter, and stops blending once its 64 pixels are saturated.  Per pixel,
+// fs_main's alpha = saturate(op * exp(-dot(uv,uv))), discarded below 1/255 and outside
+// |u|,|v| <= 2, is blended front to back with the reference's blend state
+// (src/simple_render.ts:169-200, :455-471):
+//   FP32        transmittance form: C += col * alpha * T, T *= 1 - alpha; no splat is accepted
+//               once T < t_min;
+//   FP16_TARGET dst = src * (1 - dst.a) + dst rounded to fp16 after every blend (rgba16float).
+// Chunked frames: mode kCompFirst marks saturated tiles done (and writes them out) and parks the
+// per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
 template <bool FP16_TARGET>
 __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
-    __shared__ float4 s_a[256];
-    __shared__ float4 s_b[256];
-    __shared__ float2 s_c[256];
+    __shared__ float4 sA[2][256];  // cx, cy, a, b
+    __shared__ float4 sB[2][256];  // c, d, log2(op), r
+    __shared__ float2 sC[2][256];  // g, b
+    __shared__ uint2 sD[2][256];   // pixel box
     const int tid = threadIdx.x;
     const int tile = blockIdx.x;
+    if (p.mode == kCompSecond && p.done[tile]) return;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
-    const int px = tx * kTile + (tid & 15), py = ty * kTile + (tid >> 4);
+    const int bx0 = tx * kTile + (w & 1) * 8, by0 = ty * kTile + (w >> 1) * 8;
+    const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
     const bool inside = px < p.W && py < p.H;
     const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
     const uint2 range = p.ranges[tile];
-    float cr = 0.0f, cg = 0.0f, cb = 0.0f, ca = 0.0f;
-    bool done = !inside;
-    for (uint32_t b0 = range.x; b0 < range.y; b0 += 256) {
-        const uint32_t e = b0 + tid;
+    const float4* __restrict__ rec = p.rec;
+    const uint32_t* __restrict__ tvals = p.tvals;
+    const float L = 2.0f * kSqrtLog2e, amin = 1.0f / 255.0f, t_min = p.t_min;
+    const uint64_t pix = (uint64_t)py * p.W + px;  // image-row index (state buffer)
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    float T = 1.0f;   // FP32: transmittance
+    float ca = 0.0f;  // FP16_TARGET: dst.a
+    if (p.mode == kCompSecond && inside) {
+        const float4 st = p.state[pix];
+        cr = st.x;
+        cg = st.y;
+        cb = st.z;
+        if (FP16_TARGET) ca = st.w; else T = st.w;
+    }
+    bool live = inside && (FP16_TARGET ? ca < 1.0f : T >= t_min);
+    bool wave_live = __any(live);
+
+    const uint32_t n = range.y - range.x;
+    const uint32_t nb = (n + 255) / 256;
+    float4 ga, gb, gc;
+    auto gather = [&](uint32_t batch) {
+        const uint32_t e = range.x + batch * 256 + tid;
         if (e < range.y) {
-            const uint32_t j = p.tvals[e];
-            const float4* r = p.rec + 4 * (uint64_t)j;
-            s_a[tid] = r[0];
-            s_b[tid] = r[1];
-            const float4 c = r[2];
-            s_c[tid] = make_float2(c.x, c.y);
+            const float4* r = rec + 4 * (uint64_t)tvals[e];
+            ga = r[0];
+            gb = r[1];
+            gc = r[2];
         }
-        __syncthreads();
-        const int cnt = (int)min(256u, range.y - b0);
-        if (!done) {
+    };
+    auto park = [&](int buf) {
+        sA[buf][tid] = ga;
+        sB[buf][tid] = gb;
+        sC[buf][tid] = make_float2(gc.x, gc.y);
+        sD[buf][tid] = make_uint2(__float_as_uint(gc.z), __float_as_uint(gc.w));
+    };
+    if (nb > 0) {
+        gather(0);
+        park(0);
+    }
+    __syncthreads();
+    for (uint32_t b = 0; b < nb; ++b) {
+        const int cur = b & 1;
+        if (b + 1 < nb) gather(b + 1);  // in flight while this batch is blended
+        if (wave_live) {
+            const int cnt = (int)min(256u, n - b * 256);
             for (int k = 0; k < cnt; ++k) {
-                const float4 A = s_a[k];
+                const uint2 bb = sD[cur][k];
+                if ((int)(bb.x & 0xffffu) > bx0 + 7 || (int)(bb.x >> 16) < bx0 ||
+                    (int)(bb.y & 0xffffu) > by0 + 7 || (int)(bb.y >> 16) < by0)
+                    continue;  // the splat misses this quarter (wave-uniform)
+                const float4 A = sA[cur][k];
+                const float4 B = sB[cur][k];
                 const float dx = fx - A.x, dy = fy - A.y;
                 const float u = dx * A.z + dy * A.w;
-                const float4 B = s_b[k];
                 const float v = dx * B.x + dy * B.y;
-                if (fabsf(u) <= 2.0f && fabsf(v) <= 2.0f) {
-                    const float alpha = fminf(__expf(-(u * u + v * v)) * B.z, 1.0f);
-                    if (alpha >= 1.0f / 255.0f) {
-                        const float2 C = s_c[k];
+                const float q = u * u + v * v;
+                const float alpha = __builtin_amdgcn_exp2f(B.z - q);
+                const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && alpha >= amin;
+                const float2 C = sC[cur][k];
+                if (FP16_TARGET) {
+                    if (hit) {
                         const float om = 1.0f - ca;
-                        cr = (B.w * alpha) * om + cr;
-                        cg = (C.x * alpha) * om + cg;
-                        cb = (C.y * alpha) * om + cb;
-                        ca = alpha * om + ca;
-                        if (FP16_TARGET) {
-                            cr = (float)(_Float16)cr;
-                            cg = (float)(_Float16)cg;
-                            cb = (float)(_Float16)cb;
-                            ca = (float)(_Float16)ca;
-                        }
-                        if (ca >= 1.0f || 1.0f - ca < p.t_min) { done = true; break; }
+                        cr = (float)(_Float16)((B.w * alpha) * om + cr);
+                        cg = (float)(_Float16)((C.x * alpha) * om + cg);
+                        cb = (float)(_Float16)((C.y * alpha) * om + cb);
+                        ca = (float)(_Float16)(alpha * om + ca);
+                        live = ca < 1.0f;  // dst.a == 1: later blends add exactly zero
                     }
+                } else {
+                    const float s = hit ? alpha * T : 0.0f;
+                    cr = B.w * s + cr;
+                    cg = C.x * s + cg;
+                    cb = C.y * s + cb;
+                    T = T - s;
+                    live = live && T >= t_min;
+                }
+                if (!__any(live)) {
+                    wave_live = false;
+                    break;
                 }
             }
         }
-        if (__syncthreads_count(!done) == 0) break;
+        if (b + 1 < nb) park(cur ^ 1);
+        if (__syncthreads_count(wave_live) == 0) break;
+    }
+    if (p.mode == kCompFirst) {
+        const bool tile_done = __syncthreads_count(live) == 0;
+        if (!tile_done) {  // park the pixels for chunk 1
+            if (inside) p.state[pix] = make_float4(cr, cg, cb, FP16_TARGET ? ca : T);
+            if (tid == 0) {
+                p.done[tile] = 0;
+                atomicAdd(&p.ctl->not_done, 1u);
+            }
+            return;
+        }
+        if (tid == 0) p.done[tile] = 1;
     }
     if (inside) {
+        if (!FP16_TARGET) ca = 1.0f - T;
         const uint64_t o = (uint64_t)(py - p.row0) * p.W + px;
         if (p.out_f16) {
             typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -661,7 +854,9 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, u
     hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, aos, n, n_sh,
                        planes, stride);
 }
-void launch_project(const ProjParams& p, int grid, hipStream_t s) {
+void launch_project(const ProjParams& p, hipStream_t s) {
+    const unsigned grid = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>(kMaxGrid, (p.n + kProjThreads - 1) / kProjThreads));
     hipLaunchKernelGGL(k_project, dim3(grid), dim3(kProjThreads), 0, s, p);
 }
 void launch_hist_keys(const uint32_t* keys, uint32_t n, int begin_bit, int end_bit, int npass,
@@ -671,19 +866,22 @@ void launch_hist_keys(const uint32_t* keys, uint32_t n, int begin_bit, int end_b
                        hist);
 }
 void launch_sort_pass(const SortPass& p, hipStream_t s) {
-    const uint32_t parts = sort_parts(p.n);
-    if (!parts) return;
-    hipLaunchKernelGGL(k_sort_pass, dim3(parts), dim3(kSortThreads), 0, s, p);
+    if (!p.parts_max) return;
+    const unsigned grid = std::min<uint32_t>(p.parts_max, kMaxGrid);
+    hipLaunchKernelGGL(k_radix_upsweep, dim3(grid), dim3(kSortThreads), 0, s, p);
+    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_radix_downsweep, dim3(grid), dim3(kSortThreads), 0, s, p);
 }
 void launch_bin(const BinParams& p, hipStream_t s) {
-    const uint32_t parts = bin_parts(p.n_vis);
-    if (!parts) return;
-    hipLaunchKernelGGL(k_bin, dim3(parts), dim3(kBinThreads), 0, s, p);
+    const unsigned grid = std::max<uint32_t>(1, std::min<uint32_t>(bin_parts(p.n_max), kMaxGrid));
+    hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(kBinThreads), 0, s, p);
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);
 }
-void launch_ranges(const uint32_t* tkeys, uint64_t k, uint2* ranges, hipStream_t s) {
-    if (!k) return;
-    const unsigned grid = (unsigned)std::min<uint64_t>(8192, (k + 255) / 256);
-    hipLaunchKernelGGL(k_ranges, dim3(grid), dim3(256), 0, s, tkeys, k, ranges);
+void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
+                   hipStream_t s) {
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (k_max + 255) / 256));
+    hipLaunchKernelGGL(k_ranges, dim3(grid), dim3(256), 0, s, tkeys, k_dev, ranges);
 }
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;

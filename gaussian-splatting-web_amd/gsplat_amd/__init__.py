@@ -34,11 +34,14 @@ class GsOpts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("accum", ctypes.c_int32),
                 ("out_format", ctypes.c_int32), ("t_min", ctypes.c_float),
                 ("ref_quirks", ctypes.c_int32), ("strip_index", ctypes.c_int32),
-                ("strip_count", ctypes.c_int32), ("timing", ctypes.c_int32)]
+                ("strip_count", ctypes.c_int32), ("timing", ctypes.c_int32),
+                ("chunk_fraction", ctypes.c_float)]
 
 
 class GsStats(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("n_vis", ctypes.c_uint64), ("k_entries", ctypes.c_uint64),
+                ("k_total", ctypes.c_uint64), ("tiles_unsaturated", ctypes.c_uint32),
+                ("chunk_fraction", ctypes.c_float),
                 ("tile_row_begin", ctypes.c_int32), ("tile_row_end", ctypes.c_int32),
                 ("tiles_x", ctypes.c_int32), ("frames", ctypes.c_int32),
                 ("ms_total", ctypes.c_float), ("ms_project", ctypes.c_float),
@@ -177,11 +180,12 @@ def device_count():
 
 
 def make_opts(accum=GS_ACCUM_FP32, out_format=GS_OUT_RGBA_F32, t_min=1e-4, strip_index=0, strip_count=1,
-              timing=0, ref_quirks=0):
+              timing=0, ref_quirks=0, chunk_fraction=0.0):
     o = GsOpts()
     lib().gs_opts_default(ctypes.byref(o))
     o.accum, o.out_format, o.t_min = accum, out_format, t_min
     o.strip_index, o.strip_count, o.timing, o.ref_quirks = strip_index, strip_count, timing, ref_quirks
+    o.chunk_fraction = chunk_fraction
     return o
 
 

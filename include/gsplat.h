@@ -77,12 +77,17 @@ typedef struct gs_opts {
     int32_t strip_index;  /* row strip rendered by this call, 0 <= strip_index < strip_count */
     int32_t strip_count;  /* number of equal row strips (16-px tile rows, see gs_strip_rows); 1 = whole image */
     int32_t timing;       /* 1: record per-stage hipEvent timings (gs_timings) */
+    float chunk_fraction; /* depth ranks composited before unsaturated tiles are re-binned: 0 = adaptive,
+                             >= 1 = one pass over every rank.  The image does not depend on it. */
 } gs_opts;
 
 typedef struct gs_stats {
     uint64_t n;           /* Gaussians in the scene */
     uint64_t n_vis;       /* splats that reach the sort (visible in this strip) */
-    uint64_t k_entries;   /* (tile, splat) pairs binned */
+    uint64_t k_entries;   /* (tile, splat) pairs binned (both chunks) */
+    uint64_t k_total;     /* pairs a single-chunk frame would bin (sum of tile counts, SURVEY's K) */
+    uint32_t tiles_unsaturated;  /* tiles chunk 0 left unsaturated */
+    float chunk_fraction; /* adaptive first-chunk fraction after the last frame */
     int32_t tile_row_begin, tile_row_end;  /* tile rows rendered by the last call */
     int32_t tiles_x;
     int32_t frames;       /* timed frames averaged below (opts.timing = 1) since gs_timings_reset */
@@ -152,9 +157,10 @@ int gs_debug_sort_pairs(gs_ctx* ctx, uint32_t* keys, uint32_t* vals, uint64_t n,
 /* Sorted depth keys and original Gaussian indices of the last frame (visible splats only). */
 int gs_debug_last_order(gs_ctx* ctx, gs_scene* scene, uint32_t* out_keys, uint32_t* out_index,
                         uint64_t capacity, uint64_t* out_n);
-/* Projected record of every Gaussian in the last frame: 16 floats each
- * (cx, cy, e1hat.x, e1hat.y, e2hat.x, e2hat.y, opacity, r, g, b, rect bits x2, key bits, 0,0,0);
- * rows of culled Gaussians are undefined. */
+/* Projected record of every Gaussian in the last frame, 16 floats each: centre cx, cy (pixels);
+ * quad axes e1/|e1|^2 and e2/|e2|^2 scaled by sqrt(log2 e) (2 floats each); log2(opacity);
+ * colour r, g, b; pixel box [x0|x1<<16, y0|y1<<16]; depth key; tile count; tile box (u32 bits).
+ * Rows of culled Gaussians are undefined. */
 int gs_debug_last_records(gs_ctx* ctx, gs_scene* scene, float* out16, uint64_t capacity);
 
 #ifdef __cplusplus

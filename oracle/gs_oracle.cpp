@@ -460,3 +460,60 @@ int or_num_threads(void) {
 }
 
 }  // extern "C"
+
+extern "C" {
+// Diagnostics for the tile compositor: per 16x16 tile, the list length (splats whose K-rectangle
+// touches the tile) and the number of list entries consumed before all of the tile's pixels stop
+// accepting splats (T < t_min), plus how many (8x8 quarter, entry) pairs overlap the splat box.
+int or_tile_stats(const or_splat* sp, const uint32_t* order, uint64_t n_order, int W, int H,
+                  float t_min, uint32_t* out_len, uint32_t* out_used, uint64_t* out_quarter_pairs) {
+    const int TX = (W + 15) / 16, TY = (H + 15) / 16;
+    std::vector<std::vector<uint32_t>> lists((size_t)TX * TY);
+    for (uint64_t o = 0; o < n_order; ++o) {
+        const or_splat& s = sp[order[o]];
+        if (!s.visible) continue;
+        for (int ty = s.rect[1] / 16; ty <= s.rect[3] / 16; ++ty)
+            for (int tx = s.rect[0] / 16; tx <= s.rect[2] / 16; ++tx) lists[(size_t)ty * TX + tx].push_back(order[o]);
+    }
+    uint64_t qp = 0;
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : qp)
+    for (int t = 0; t < TX * TY; ++t) {
+        const int tx = t % TX, ty = t / TX;
+        float T[256];
+        for (int i = 0; i < 256; ++i) {
+            const int px = tx * 16 + (i & 15), py = ty * 16 + (i >> 4);
+            T[i] = (px < W && py < H) ? 1.0f : 0.0f;
+        }
+        uint32_t used = 0;
+        for (uint32_t k = 0; k < lists[t].size(); ++k) {
+            bool any = false;
+            for (int i = 0; i < 256; ++i) any |= T[i] >= t_min && T[i] > 0.0f;
+            if (!any) break;
+            used = k + 1;
+            const or_splat& s = sp[lists[t][k]];
+            for (int qy = 0; qy < 2; ++qy)
+                for (int qx = 0; qx < 2; ++qx) {
+                    const int x0 = tx * 16 + qx * 8, y0 = ty * 16 + qy * 8;
+                    if (s.rect[0] <= x0 + 7 && s.rect[2] >= x0 && s.rect[1] <= y0 + 7 && s.rect[3] >= y0) ++qp;
+                }
+            const float e1n = s.e1[0] * s.e1[0] + s.e1[1] * s.e1[1];
+            const float e2n = s.e2[0] * s.e2[0] + s.e2[1] * s.e2[1];
+            for (int i = 0; i < 256; ++i) {
+                if (!(T[i] >= t_min && T[i] > 0.0f)) continue;
+                const int px = tx * 16 + (i & 15), py = ty * 16 + (i >> 4);
+                if (px < s.rect[0] || px > s.rect[2] || py < s.rect[1] || py > s.rect[3]) continue;
+                const float dx = ((float)px + 0.5f) - s.c[0], dy = ((float)py + 0.5f) - s.c[1];
+                const float uu = (dx * s.e1[0] + dy * s.e1[1]) / e1n, vv = (dx * s.e2[0] + dy * s.e2[1]) / e2n;
+                if (!(std::fabs(uu) <= 2.0f && std::fabs(vv) <= 2.0f)) continue;
+                const float a = saturate(std::exp(-(uu * uu + vv * vv)) * s.op);
+                if (a < 1.0f / 255.0f) continue;
+                T[i] *= 1.0f - a;
+            }
+        }
+        out_len[t] = (uint32_t)lists[t].size();
+        out_used[t] = used;
+    }
+    if (out_quarter_pairs) *out_quarter_pairs = qp;
+    return 0;
+}
+}
