@@ -117,11 +117,11 @@ struct gs_scene {
     uint32_t *keysA = nullptr, *valsA = nullptr, *auxA = nullptr;
     uint32_t *keysB = nullptr, *valsB = nullptr, *auxB = nullptr;
     float4* rec = nullptr;
-    // zero-per-frame block: FrameCtl | depth hist | tile hist x 2 chunks
+    // zero-per-frame block: FrameCtl | digit histograms of the 4 depth passes and of the
+    // 2 tile passes of each chunk (kHistShards x 256 words each)
     uint8_t* meta = nullptr;
     FrameCtl* ctl = nullptr;
-    uint32_t* hist_depth = nullptr;     // 8 x 4 x 256
-    uint32_t* hist_tile[2] = {};        // 8 x 2 x 256 per chunk
+    uint32_t* hist = nullptr;
     uint32_t* bin_part = nullptr;       // bin_parts(N) + 1
     // tile lists
     uint64_t kcap = 0;
@@ -143,9 +143,8 @@ struct gs_scene {
     bool have_frame = false;
 };
 
-static constexpr size_t kMetaCtl = 0, kMetaHistDepth = 256,
-                        kMetaHistTile = kMetaHistDepth + kHistShards * 1024 * 4,
-                        kMetaBytes = kMetaHistTile + 2 * kHistShards * 512 * 4;
+static constexpr size_t kHistWords = kHistShards * 256;
+static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 8 * kHistWords * 4;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
 static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
@@ -283,7 +282,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.keys_out = s->keysB;
     pp.rect_out = s->auxB;
     pp.rec = s->rec;
-    pp.hist = s->hist_depth;
     pp.ctl = s->ctl;
     mark(EV_PROJ0);
     launch_project(pp, st);
@@ -310,8 +308,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         sp.shift = 8 * ps;
         sp.mask = 255;
         sp.filter_sentinel = ps == 0;
-        sp.hist = s->hist_depth + 256 * ps;
-        sp.hist_stride = 1024;
+        sp.hist = s->hist + ps * kHistWords;
         sp.offsets = s->radix_offsets;
         launch_sort_pass(sp, st);
     }
@@ -340,7 +337,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.part_tot = s->bin_part;
         bp.tkeys = s->tkA;
         bp.tvals = s->tvA;
-        bp.hist = s->hist_tile[chunk];
         launch_bin(bp, st);
         mark(eb);
 
@@ -356,8 +352,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.parts_max = sort_parts(s->kcap);
             sp.shift = 8 * ps;
             sp.mask = 255;
-            sp.hist = s->hist_tile[chunk] + 256 * ps;
-            sp.hist_stride = 512;
+            sp.hist = s->hist + (4 + 2 * chunk + ps) * kHistWords;
             sp.offsets = s->radix_offsets;
             launch_sort_pass(sp, st);
             std::swap(tk_in, tk_out);
@@ -490,7 +485,7 @@ int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
         try {
             HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             for (auto& f : c->fe)
-                for (auto& e : f.ev) HIPCHK(hipEventCreate(&e));
+                for (auto& e : f.ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         } catch (...) {
             gs_ctx_destroy(c);
             throw;
@@ -533,9 +528,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->rec, 4 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->meta, kMetaBytes);
             s->ctl = (FrameCtl*)(s->meta + kMetaCtl);
-            s->hist_depth = (uint32_t*)(s->meta + kMetaHistDepth);
-            s->hist_tile[0] = (uint32_t*)(s->meta + kMetaHistTile);
-            s->hist_tile[1] = s->hist_tile[0] + kHistShards * 512;
+            s->hist = (uint32_t*)(s->meta + kMetaHist);
             dev_alloc(s->bin_part, (size_t)bin_parts(n) + 1);
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hipHostMallocDefault));
             for (auto& e : s->stat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -709,14 +702,12 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
         const int npass = (end_bit - begin_bit + 7) / 8;
         uint32_t *kA, *vA, *kB, *vB, *hist, *offs;
         dev_alloc(kA, n); dev_alloc(vA, n); dev_alloc(kB, n); dev_alloc(vB, n);
-        dev_alloc(hist, (size_t)kHistShards * npass * 256);
+        dev_alloc(hist, (size_t)npass * kHistWords);
         dev_alloc(offs, (size_t)256 * sort_parts(n));
         hipStream_t st = c->stream;
         HIPCHK(hipMemcpyAsync(kA, keys, n * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(vA, vals, n * 4, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemsetAsync(hist, 0, (size_t)kHistShards * npass * 256 * 4, st));
-        // histogram of each pass's digit, masked to the bit range
-        launch_hist_keys(kA, (uint32_t)n, begin_bit, end_bit, npass, hist, st);
+        HIPCHK(hipMemsetAsync(hist, 0, (size_t)npass * kHistWords * 4, st));
         uint32_t *ki = kA, *vi = vA, *ko = kB, *vo = vB;
         for (int ps = 0; ps < npass; ++ps) {
             SortPass sp{};
@@ -726,8 +717,7 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
             sp.shift = begin_bit + 8 * ps;
             const int bits = std::min(8, end_bit - sp.shift);
             sp.mask = (1u << bits) - 1u;
-            sp.hist = hist + 256 * ps;
-            sp.hist_stride = npass * 256;
+            sp.hist = hist + ps * kHistWords;
             sp.offsets = offs;
             launch_sort_pass(sp, st);
             std::swap(ki, ko);

@@ -57,7 +57,6 @@ struct ProjParams {
     uint32_t* keys_out;       // [n]: depth key or kSentinel
     uint32_t* rect_out;       // [n]: packed tile rectangle
     float4* rec;              // [n][4]: projected records
-    uint32_t* hist;           // [kHistShards][4][256] depth-key digit histograms (zeroed)
     FrameCtl* ctl;
 };
 
@@ -74,8 +73,8 @@ struct SortPass {
     int shift;
     uint32_t mask;            // digit mask (<= 255)
     int filter_sentinel;      // 1: drop keys == kSentinel (they carry no digit)
-    const uint32_t* hist;     // global digit histogram of this pass, kHistShards shards
-    int hist_stride;          // elements between shards
+    uint32_t* hist;           // [kHistShards][256] digit histogram of this pass (zeroed; the
+                              // upsweep accumulates it, the scan turns it into digit bases)
     uint32_t* offsets;        // [256][parts_max] scratch: partition counts, then offsets
 };
 
@@ -94,7 +93,6 @@ struct BinParams {
     uint32_t* part_tot;           // [bin_parts(n_max) + 1] scratch
     uint32_t* tkeys;              // out: strip-relative tile id
     uint32_t* tvals;              // out: Gaussian index
-    uint32_t* hist;               // [kHistShards][2][256] tile-id digit histograms (zeroed)
 };
 
 enum CompositeMode { kCompSingle = 0, kCompFirst = 1, kCompSecond = 2 };
@@ -118,8 +116,6 @@ struct CompositeParams {
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, uint64_t stride,
                       hipStream_t s);
 void launch_project(const ProjParams& p, hipStream_t s);
-void launch_hist_keys(const uint32_t* keys, uint32_t n, int begin_bit, int end_bit, int npass,
-                      uint32_t* hist, hipStream_t s);
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,

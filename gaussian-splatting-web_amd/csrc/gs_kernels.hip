@@ -213,10 +213,8 @@ __device__ __forceinline__ bool pixel_rect(float cx, float cy, float hx, float h
 }
 
 __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
-    __shared__ uint32_t s_hist[4][256];
     __shared__ unsigned long long s_k;
     __shared__ uint32_t s_vis;
-    for (int t = threadIdx.x; t < 1024; t += kProjThreads) (&s_hist[0][0])[t] = 0;
     if (threadIdx.x == 0) { s_k = 0; s_vis = 0; }
     __syncthreads();
 
@@ -301,10 +299,6 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
             r[2] = make_float4(cg, cb, __uint_as_float(bbx), __uint_as_float(bby));
             r[3] = make_float4(__uint_as_float(key), __uint_as_float(ntiles), __uint_as_float(rx),
                                __uint_as_float(ry));
-            atomicAdd(&s_hist[0][key & 255], 1u);
-            atomicAdd(&s_hist[1][(key >> 8) & 255], 1u);
-            atomicAdd(&s_hist[2][(key >> 16) & 255], 1u);
-            atomicAdd(&s_hist[3][key >> 24], 1u);
             ++my_vis;
             my_k += ntiles;
         }
@@ -316,38 +310,9 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
         atomicAdd(&s_k, my_k);
     }
     __syncthreads();
-    uint32_t* gh = p.hist + (blockIdx.x % kHistShards) * 1024;
-    for (int t = threadIdx.x; t < 1024; t += kProjThreads) {
-        const uint32_t c = (&s_hist[0][0])[t];
-        if (c) atomicAdd(gh + t, c);
-    }
     if (threadIdx.x == 0 && s_vis) {
         atomicAdd(&p.ctl->n_vis, s_vis);
         atomicAdd(&p.ctl->k_total, s_k);
-    }
-}
-
-// ============================================================================ histograms
-// Digit histograms of an arbitrary key array (used by the standalone sort entry point).
-__global__ __launch_bounds__(256) void k_hist_keys(const uint32_t* __restrict__ keys, uint32_t n,
-                                                   int begin_bit, int end_bit, int npass,
-                                                   uint32_t* hist) {
-    __shared__ uint32_t s_hist[4][256];
-    for (int t = threadIdx.x; t < 1024; t += 256) (&s_hist[0][0])[t] = 0;
-    __syncthreads();
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        const uint32_t k = keys[i];
-        for (int ps = 0; ps < npass; ++ps) {
-            const int sh = begin_bit + 8 * ps;
-            const uint32_t mask = (1u << min(8, end_bit - sh)) - 1u;
-            atomicAdd(&s_hist[ps][(k >> sh) & mask], 1u);
-        }
-    }
-    __syncthreads();
-    uint32_t* gh = hist + (blockIdx.x % kHistShards) * (npass * 256);
-    for (int t = threadIdx.x; t < npass * 256; t += 256) {
-        const uint32_t c = (&s_hist[0][0])[t];
-        if (c) atomicAdd(gh + t, c);
     }
 }
 
@@ -368,6 +333,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(SortPass p) {
     __shared__ uint32_t s_hist[4][256];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t n = radix_n(p), parts = sort_parts(n);
+    uint32_t total = 0;  // this workgroup's count of digit `tid` over all its partitions
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         for (int t = tid; t < 1024; t += kSortThreads) (&s_hist[0][0])[t] = 0;
         __syncthreads();
@@ -381,8 +347,11 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(SortPass p) {
         __syncthreads();
         const uint32_t c = s_hist[0][tid] + s_hist[1][tid] + s_hist[2][tid] + s_hist[3][tid];
         p.offsets[(uint64_t)tid * p.parts_max + part] = c;  // digit-major
+        total += c;
         __syncthreads();
     }
+    // global digit histogram of this pass (kHistShards shards, zeroed with the frame)
+    if (total) atomicAdd(&p.hist[(blockIdx.x % kHistShards) * 256 + tid], total);
 }
 
 // Block d scans column d over partitions and adds the global digit base (exclusive scan of the
@@ -393,7 +362,7 @@ __global__ __launch_bounds__(256) void k_radix_scan(SortPass p) {
     const int d = blockIdx.x, tid = threadIdx.x;
     const uint32_t parts = sort_parts(radix_n(p));
     uint32_t tot = 0;
-    for (int sh = 0; sh < kHistShards; ++sh) tot += p.hist[sh * p.hist_stride + tid];
+    for (int sh = 0; sh < kHistShards; ++sh) tot += p.hist[sh * 256 + tid];
     uint32_t gtotal;
     const uint32_t gbase = block_excl_scan256(tot, s_tmp, &gtotal);
     if (tid == d) s_base = gbase;
@@ -609,14 +578,11 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_off[kBinTile + 1];
     __shared__ uint32_t s_j[kBinTile];
     __shared__ TileRect s_rect[kBinTile];
-    __shared__ uint32_t s_hist[2][256];
     __shared__ uint32_t s_tmp[8];
     const int tid = threadIdx.x;
     uint32_t r0, r1;
     chunk_range(p, r0, r1);
     const uint32_t parts = bin_parts(r1 - r0);
-    s_hist[0][tid] = 0;
-    s_hist[1][tid] = 0;
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         const uint32_t base_r = r0 + part * kBinTile;
         const uint32_t nitems = min((uint32_t)kBinTile, r1 - base_r);
@@ -659,8 +625,6 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
                 const uint32_t tile = tile_id(p, tr.x0 + k % w, tr.y0 + k / w);
                 p.tkeys[obase + e] = tile;
                 p.tvals[obase + e] = s_j[lo];
-                atomicAdd(&s_hist[0][tile & 255], 1u);
-                atomicAdd(&s_hist[1][(tile >> 8) & 255], 1u);
             }
         } else {
             // chunk 1 (few unsaturated tiles): every splat walks its own rectangle
@@ -677,19 +641,12 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
                         if (o < p.capacity) {
                             p.tkeys[o] = tile;
                             p.tvals[o] = s_j[li];
-                            atomicAdd(&s_hist[0][tile & 255], 1u);
-                            atomicAdd(&s_hist[1][(tile >> 8) & 255], 1u);
                         }
                         ++o;
                     }
             }
         }
         __syncthreads();
-    }
-    uint32_t* gh = p.hist + (blockIdx.x % kHistShards) * 512;
-    for (int t = tid; t < 512; t += kBinThreads) {
-        const uint32_t c = (&s_hist[0][0])[t];
-        if (c) atomicAdd(gh + t, c);
     }
 }
 
@@ -858,12 +815,6 @@ void launch_project(const ProjParams& p, hipStream_t s) {
     const unsigned grid = (unsigned)std::max<uint64_t>(
         1, std::min<uint64_t>(kMaxGrid, (p.n + kProjThreads - 1) / kProjThreads));
     hipLaunchKernelGGL(k_project, dim3(grid), dim3(kProjThreads), 0, s, p);
-}
-void launch_hist_keys(const uint32_t* keys, uint32_t n, int begin_bit, int end_bit, int npass,
-                      uint32_t* hist, hipStream_t s) {
-    const unsigned grid = (unsigned)std::min<uint64_t>(1024, (n + 255) / 256 + 1);
-    hipLaunchKernelGGL(k_hist_keys, dim3(grid), dim3(256), 0, s, keys, n, begin_bit, end_bit, npass,
-                       hist);
 }
 void launch_sort_pass(const SortPass& p, hipStream_t s) {
     if (!p.parts_max) return;
