@@ -180,6 +180,7 @@ def main():
             "k_total": k_all,
             "k_binned": k_binned,
             "chunk_fraction": round(st["chunk_fraction"], 4),
+            "tiles_unsaturated": st["tiles_unsaturated"],
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": None,
                          "algorithmic_bytes_per_launch": int(a_bytes)},

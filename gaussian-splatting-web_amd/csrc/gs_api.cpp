@@ -111,24 +111,32 @@ struct gs_scene {
     gs_ctx* ctx = nullptr;
     uint64_t n = 0;
     int n_sh = 0;
-    float* planes = nullptr;
+    float* planes = nullptr;            // 11 geometry planes
     uint64_t stride = 0;
+    float4* shade = nullptr;            // shading blocks
     // depth sort ping-pong: keys, Gaussian index, packed tile rectangle; project writes keysB/auxB
     uint32_t *keysA = nullptr, *valsA = nullptr, *auxA = nullptr;
     uint32_t *keysB = nullptr, *valsB = nullptr, *auxB = nullptr;
-    float4* rec = nullptr;
+    float4* rec = nullptr;              // projected records, 4 float4 per Gaussian
+    float4* crec = nullptr;             // composite records, 3 float4 per slot
     // zero-per-frame block: FrameCtl | digit histograms of the 4 depth passes and of the
     // 2 tile passes of each chunk (kHistShards x 256 words each)
     uint8_t* meta = nullptr;
     FrameCtl* ctl = nullptr;
     uint32_t* hist = nullptr;
     uint32_t* bin_part = nullptr;       // bin_parts(N) + 1
+    uint32_t* shade_list = nullptr;     // N: splats whose colour the frame evaluates
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tkA = nullptr, *tvA = nullptr, *tkB = nullptr, *tvB = nullptr;
     uint32_t* radix_offsets = nullptr;  // 256 x sort_parts(max(N, kcap))
     uint2* ranges = nullptr;
     uint8_t* done = nullptr;
+    uint32_t* sat = nullptr;            // (strip rows + 1) x (tiles_x + 1), then the bitmask
+    size_t sat_cap = 0;
+    uint4* wide_items = nullptr;        // wide-splat queue (per chunk, reused)
+    uint32_t* wide_unit = nullptr;
+    uint32_t wide_cap = 0, wide_unit_cap = 0;
     int tiles_cap = 0;
     float4* state = nullptr;
     uint64_t state_cap = 0;
@@ -164,6 +172,28 @@ static void ensure_tiles(gs_scene* s, int n_tiles) {
     dev_alloc(s->ranges, (size_t)n_tiles);
     dev_alloc(s->done, (size_t)n_tiles);
     s->tiles_cap = n_tiles;
+}
+
+static void ensure_sat(gs_scene* s, size_t words) {
+    if (words <= s->sat_cap && s->sat) return;
+    dev_free(s->sat);
+    dev_alloc(s->sat, words);
+    s->sat_cap = words;
+}
+
+// Wide-splat queue: items <= entries / kWideTiles; one unit per tile row.  Overflowing splats
+// are emitted by the binning itself (slower, still exact).
+static void ensure_wide(gs_scene* s, int strip_rows) {
+    (void)strip_rows;
+    const uint32_t items = (uint32_t)std::min<uint64_t>(1u << 20, s->kcap / kWideTiles + 1024);
+    const uint32_t units = (uint32_t)std::min<uint64_t>(1u << 30, s->kcap / 8 + 4096);
+    if (s->wide_items && items <= s->wide_cap && units <= s->wide_unit_cap) return;
+    dev_free(s->wide_items);
+    dev_free(s->wide_unit);
+    dev_alloc(s->wide_items, items);
+    dev_alloc(s->wide_unit, units);
+    s->wide_cap = items;
+    s->wide_unit_cap = units;
 }
 
 static void ensure_state(gs_scene* s, uint64_t pixels) {
@@ -252,7 +282,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     ensure_tiles(s, std::max(n_tiles, 1));
     const float f = o.chunk_fraction > 0.0f ? std::min(o.chunk_fraction, 1.0f) : s->chunk_f;
     const bool two_chunks = f < 1.0f;
-    if (two_chunks) ensure_state(s, (uint64_t)W * H);
+    if (two_chunks) {
+        ensure_state(s, (uint64_t)W * H);
+        ensure_sat(s, (size_t)(tr_end - tr_begin + 1) * (TX + 1) + 2 + (size_t)(tr_end - tr_begin) * ((TX + 63) / 64) * 2);
+    }
+    ensure_wide(s, tr_end - tr_begin);
 
     const bool timed = o.timing != 0;
     FrameEvents& fe = c->fe[c->fe_cur];
@@ -267,10 +301,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.planes = s->planes;
     pp.plane_stride = s->stride;
     pp.n = n_tiles > 0 ? (uint32_t)s->n : 0u;
-    pp.n_sh = s->n_sh;
     std::memcpy(pp.V, uni + 0, 64);
     mat4_mul_ref(uni + 16, uni + 0, pp.PV);
-    std::memcpy(pp.cam, uni + 32, 12);
     pp.scale_mod = uni[39];
     pp.P00 = uni[16];
     pp.P11 = uni[21];
@@ -326,6 +358,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.sorted_vals = s->valsB;
         bp.sorted_rect = s->auxB;
         bp.rec = s->rec;
+        bp.crec = s->crec;
+        bp.shade = s->shade;
+        bp.shade_q = shade_quads(s->n_sh);
+        bp.n_sh = s->n_sh;
+        std::memcpy(bp.cam, uni + 32, 12);
         bp.done = s->done;
         bp.ctl = s->ctl;
         bp.chunk = chunk;
@@ -335,8 +372,21 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.n_max = std::max<uint32_t>(pp.n, 1);
         bp.capacity = (uint32_t)s->kcap;
         bp.part_tot = s->bin_part;
+        bp.part_stride = bin_parts(s->n) + 1;
         bp.tkeys = s->tkA;
         bp.tvals = s->tvA;
+        bp.sat = s->sat;
+        const size_t sat_words = (size_t)(tr_end - tr_begin + 1) * (TX + 1);
+        bp.mask = (const unsigned long long*)(s->sat + ((sat_words + 1) & ~(size_t)1));
+        bp.mask_words = (TX + 63) / 64;
+        bp.rows = tr_end - tr_begin;
+        bp.shade_list = s->shade_list;
+        bp.wide_items = s->wide_items;
+        bp.wide_cap = s->wide_cap;
+        bp.wide_unit = s->wide_unit;
+        bp.wide_unit_cap = s->wide_unit_cap;
+        if (chunk == 1)
+            launch_sat(s->done, TX, tr_end - tr_begin, s->sat, (unsigned long long*)bp.mask, st);
         launch_bin(bp, st);
         mark(eb);
 
@@ -366,7 +416,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         CompositeParams cp{};
         cp.ranges = s->ranges;
         cp.tvals = tv_in;
-        cp.rec = s->rec;
+        cp.rec = s->crec;
         cp.W = W;
         cp.H = H;
         cp.tiles_x = TX;
@@ -522,14 +572,17 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
         s->n_sh = n_sh;
         try {
             s->stride = round_up(std::max<uint64_t>(n, 1), 64);
-            dev_alloc(s->planes, (size_t)(11 + 3 * n_sh) * s->stride);
+            dev_alloc(s->planes, (size_t)11 * s->stride);
+            dev_alloc(s->shade, (size_t)shade_quads(n_sh) * std::max<uint64_t>(n, 1));
             dev_alloc(s->keysA, n); dev_alloc(s->valsA, n); dev_alloc(s->auxA, n);
             dev_alloc(s->keysB, n); dev_alloc(s->valsB, n); dev_alloc(s->auxB, n);
             dev_alloc(s->rec, 4 * (size_t)std::max<uint64_t>(n, 1));
+            dev_alloc(s->crec, 3 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->meta, kMetaBytes);
             s->ctl = (FrameCtl*)(s->meta + kMetaCtl);
             s->hist = (uint32_t*)(s->meta + kMetaHist);
-            dev_alloc(s->bin_part, (size_t)bin_parts(n) + 1);
+            dev_alloc(s->bin_part, 2 * ((size_t)bin_parts(n) + 1));
+            dev_alloc(s->shade_list, (size_t)n);
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hipHostMallocDefault));
             for (auto& e : s->stat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             ensure_tile_capacity(s, 4 * n + (1u << 20));
@@ -542,7 +595,8 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 const uint64_t m = std::min(chunk, n - i0);
                 HIPCHK(hipMemcpyAsync(tmp, (const uint8_t*)aos + i0 * rb, m * rb, hipMemcpyHostToDevice,
                                       c->stream));
-                launch_transpose(tmp, m, n_sh, s->planes + i0, s->stride, c->stream);
+                launch_transpose(tmp, m, n_sh, s->planes + i0, s->stride, s->shade + i0 * shade_quads(n_sh),
+                                 c->stream);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipStreamSynchronize(c->stream));
             }
@@ -567,15 +621,21 @@ void gs_scene_free(gs_scene* s) {
         if (s->ctx->last_scene == s) s->ctx->last_scene = nullptr;
     }
     dev_free(s->planes);
+    dev_free(s->shade);
     dev_free(s->keysA); dev_free(s->valsA); dev_free(s->auxA);
     dev_free(s->keysB); dev_free(s->valsB); dev_free(s->auxB);
     dev_free(s->rec);
+    dev_free(s->crec);
     dev_free(s->meta);
     dev_free(s->bin_part);
+    dev_free(s->shade_list);
     dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB);
     dev_free(s->radix_offsets);
     dev_free(s->ranges);
     dev_free(s->done);
+    dev_free(s->sat);
+    dev_free(s->wide_items);
+    dev_free(s->wide_unit);
     dev_free(s->state);
     for (auto& e : s->stat_ev)
         if (e) (void)hipEventDestroy(e);
@@ -662,6 +722,10 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
             st.k_entries = (uint64_t)l.k_chunk[0] + l.k_chunk[1];
             st.k_total = l.k_total;
             st.tiles_unsaturated = l.not_done;
+            st.k_chunk0 = l.k_chunk[0];
+            st.k_chunk1 = l.k_chunk[1];
+            st.wide_chunk0 = l.wide_n[0];
+            st.wide_chunk1 = l.wide_n[1];
             st.chunk_fraction = c->last_scene->chunk_f;
         }
         st.frames = (int32_t)c->acc_frames;
@@ -756,6 +820,17 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
         HIPCHK(hipStreamSynchronize(c->stream));
         const uint64_t m = std::min(cap, s->n);
         if (m) HIPCHK(hipMemcpy(out16, s->rec, m * 64, hipMemcpyDeviceToHost));
+        // colour words [8, 12): from the composite record of each binned splat
+        collect_stats(s, true);
+        const uint64_t slots = (uint64_t)s->last.shade_n[0] + s->last.shade_n[1];
+        if (slots) {
+            std::vector<uint32_t> js(slots);
+            std::vector<float> cr(slots * 12);
+            HIPCHK(hipMemcpy(js.data(), s->shade_list, slots * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(cr.data(), s->crec, slots * 48, hipMemcpyDeviceToHost));
+            for (uint64_t g = 0; g < slots; ++g)
+                if (js[g] < m) std::memcpy(out16 + 16 * (uint64_t)js[g] + 8, &cr[12 * g + 8], 16);
+        }
         return GS_OK;
     });
 }

@@ -16,13 +16,16 @@ constexpr int kSortThreads = 256;     // 4 waves
 constexpr int kSortIPT = 16;          // items per thread
 constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per radix partition
 constexpr int kBinThreads = 256;
-constexpr int kBinIPT = 8;
-constexpr int kBinTile = kBinThreads * kBinIPT;     // 2048 ranks per binning partition
+constexpr int kBinIPT = 2;
+constexpr int kBinTile = kBinThreads * kBinIPT;     // 512 ranks per binning partition
 constexpr int kHistShards = 8;        // global histograms sharded by blockIdx % 8 (XCD group)
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // key of a culled Gaussian (no visible splat has it)
 constexpr int kRecFloats = 16;        // 64-B projected record
 constexpr int kMaxGrid = 2048;        // persistent grids: 8 workgroups per CU
 constexpr uint32_t kMinChunk0 = 65536;  // smallest first chunk (depth ranks)
+constexpr uint32_t kWideTiles = 32;     // splats binding >= this many tiles are emitted row-wise
+constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
+constexpr int kMaskLdsWords = 2048;     // unsaturated-tile bitmask cached in LDS up to this size
 
 // Packed tile rectangle carried through the depth sort (32 bits): tx0[0:12) ty0[12:24)
 // (w-1)[24:28) (h-1)[28:32).  Rectangles wider or taller than 16 tiles use kRectLarge (the
@@ -39,17 +42,32 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t k_chunk[2];          // (tile, splat) entries per chunk (binning scan)
     uint32_t not_done;            // tiles still accepting splats after chunk 0
     uint32_t err;
-    uint32_t pad[9];
+    uint32_t wide_n[2];           // wide splats queued per chunk (binning)
+    uint32_t wide_rows[2];        // their tile rows (work units of k_bin_wide)
+    uint32_t shade_n[2];          // splats queued for colour per chunk (binning)
+    uint32_t pad[3];
 };
 
+// Scene layout in HBM: 11 SoA geometry planes (0-2 position, 3-5 log-free scale, 6-9 rotation,
+// 10 opacity logit; plane p at planes + p * plane_stride) streamed by k_project, and one AoS
+// shading block per Gaussian [x, y, z, sh[k][c] at 3 + 3k + c] padded to shade_q float4s
+// (208 B at SH degree 3), gathered by the binning for the splats that receive tile entries.
+__host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
+
+// Projected record, 4 float4 per Gaussian (at its original index, written by k_project):
+//   [0] cx, cy, e1x', e1y'      centre (pixels); quad axes e/|e|^2 * sqrt(log2 e)
+//   [1] e2x', e2y', log2(op), pixel box x (x0 | x1 << 16, u32 bits)
+//   [2] (unused)
+//   [3] depth key, tile count, pixel box x, pixel box y (u32 bits)
+// Composite record, 3 float4 per binned splat at its slot g (depth-rank order of the splats
+// that received entries; written by k_shade; the tile lists hold g):
+//   [0] = record [0], [1] = record [1], [2] r, g, b, pixel box y
 struct ProjParams {
-    const float* planes;      // SoA planes, plane p at planes + p * plane_stride
+    const float* planes;
     uint64_t plane_stride;
     uint32_t n;
-    int n_sh;
     float V[16];              // view, column-major
     float PV[16];             // proj * view (host-computed in the reference's order)
-    float cam[3];
     float scale_mod;
     float P00, P11;
     int W, H;
@@ -81,7 +99,12 @@ struct SortPass {
 struct BinParams {
     const uint32_t* sorted_vals;  // [n_vis] Gaussian index in depth order
     const uint32_t* sorted_rect;  // [n_vis] packed tile rectangle in depth order
-    const float4* rec;            // records (full rectangle of kRectLarge splats)
+    const float4* rec;            // records (rectangles of kRectLarge splats; k_shade input)
+    float4* crec;                 // out: composite records, 3 float4 per slot
+    const float4* shade;          // shading blocks (shade_q float4 per Gaussian)
+    uint32_t shade_q;
+    int n_sh;
+    float cam[3];
     const uint8_t* done;          // chunk 1: per-tile "saturated after chunk 0"
     FrameCtl* ctl;
     int chunk;                    // 0 or 1
@@ -90,17 +113,32 @@ struct BinParams {
     int tile_row_begin, tiles_x;
     uint32_t n_max;               // upper bound of n_vis (grid / scratch sizing)
     uint32_t capacity;            // entry capacity of out arrays
-    uint32_t* part_tot;           // [bin_parts(n_max) + 1] scratch
+    uint32_t* part_tot;           // [2][part_stride] scratch: entries, then splats with entries
+    uint32_t part_stride;         // >= bin_parts(n_max)
     uint32_t* tkeys;              // out: strip-relative tile id
     uint32_t* tvals;              // out: Gaussian index
+    // chunk 1: summed-area table of unsaturated tiles, (rows + 1) x (tiles_x + 1),
+    // sat[y][x] = unsaturated tiles in strip rows < y and columns < x; and the same set as a
+    // bitmask, mask_words 64-bit words per strip row (bit x of row y = tile (x, y) unsaturated)
+    const uint32_t* sat;
+    const unsigned long long* mask;
+    int mask_words;
+    int rows;                     // tile rows of the strip
+    uint32_t* shade_list;         // [n] Gaussian index of each composite slot g
+    // wide splats: item = (Gaussian index, output offset, x0 | x1 << 16, y0 | y1 << 16); one
+    // work unit per tile row, unit word = item << 12 | row offset (~0u: no item)
+    uint4* wide_items;
+    uint32_t wide_cap;
+    uint32_t* wide_unit;
+    uint32_t wide_unit_cap;
 };
 
 enum CompositeMode { kCompSingle = 0, kCompFirst = 1, kCompSecond = 2 };
 
 struct CompositeParams {
     const uint2* ranges;          // [n_tiles] (begin, end) into tvals
-    const uint32_t* tvals;
-    const float4* rec;
+    const uint32_t* tvals;        // composite slots
+    const float4* rec;            // composite records (3 float4 per slot)
     int W, H, tiles_x, tile_row_begin, row0;  // row0 = first image row of the output buffer
     int n_tiles;
     float t_min;
@@ -114,10 +152,12 @@ struct CompositeParams {
 
 // launchers (gs_kernels.hip)
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, uint64_t stride,
-                      hipStream_t s);
+                      float4* shade, hipStream_t s);
 void launch_project(const ProjParams& p, hipStream_t s);
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);
+void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
+                hipStream_t s);
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
                    hipStream_t s);
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);

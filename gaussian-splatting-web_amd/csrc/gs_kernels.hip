@@ -2,12 +2,12 @@
 //
 //   k_transpose   scene upload: reference AoS record (src/ply.ts:249-257) -> SoA planes
 //   k_project     per Gaussian: depth key (src/shaders.ts:36-68) + vs_points projection
-//                 (src/simple_render.ts:217-332) + SH colour (:26-66) + tile rectangle;
-//                 streaming, one pass over the SoA planes; fuses the radix histograms.
+//                 (src/simple_render.ts:217-332) + tile rectangle; one streaming pass over the
+//                 geometry planes (colour is deferred to the binning).
 //   k_radix_*     one stable 8-bit LSD radix pass (upsweep / scan / downsweep); replaces
 //                 webgpu-radix-sort's 16 x 2-bit passes (RS:621-654).
-//   k_bin         per depth-sorted splat: (tile, splat) pairs emitted in depth order
-//                 (order-preserving exclusive scan with look-back, wave64 ballot ranks).
+//   k_bin         per depth-sorted splat: (tile, splat) pairs emitted in depth order (count,
+//                 scan, emit); SH colour (:26-66) of every splat that receives an entry.
 //   k_ranges      per tile: [begin, end) of its list after the stable tile-id sort.
 //   k_composite   16x16 tile workgroup: front-to-back "under" blending of fs_main's alpha
 //                 (src/simple_render.ts:169-200, blend state :455-471), splat batches staged in LDS.
@@ -62,11 +62,11 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp
 // ============================================================================ k_transpose
 __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ aos, uint64_t n,
                                                    int n_sh, float* __restrict__ planes,
-                                                   uint64_t stride) {
+                                                   uint64_t stride, float4* __restrict__ shade) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float* r = (const float*)(aos + i * (uint64_t)(64 + 16 * n_sh));
-    // planes: 0-2 pos, 3-5 scale, 6-9 rot, 10 opacity logit, 11.. sh[k][c] at 11 + 3k + c
+    // src/ply.ts:249-257 record: pos[0:3] | scale[4:7] | rot[8:12] | opacity[12] | sh[k] at 16+4k
     planes[0 * stride + i] = r[0];
     planes[1 * stride + i] = r[1];
     planes[2 * stride + i] = r[2];
@@ -78,36 +78,25 @@ __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ a
     planes[8 * stride + i] = r[10];
     planes[9 * stride + i] = r[11];
     planes[10 * stride + i] = r[12];
-    for (int k = 0; k < n_sh; ++k)
-        for (int c = 0; c < 3; ++c) planes[(uint64_t)(11 + 3 * k + c) * stride + i] = r[16 + 4 * k + c];
+    const uint32_t q = shade_quads(n_sh);
+    float v[4 * 13];
+#pragma unroll
+    for (int t = 0; t < 4 * 13; ++t) v[t] = 0.0f;
+    v[0] = r[0];
+    v[1] = r[1];
+    v[2] = r[2];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < n_sh)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) v[3 + 3 * k + c] = r[16 + 4 * k + c];
+    float4* o = shade + i * q;
+#pragma unroll
+    for (uint32_t t = 0; t < 13; ++t)
+        if (t < q) o[t] = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
 }
 
 // ============================================================================ k_project
-// SH evaluation, src/simple_render.ts:26-66, one colour channel; coefficients beyond the
-// record's degree are absent (treated as 0; the reference draw shader assumes 16).
-__device__ __forceinline__ float sh_channel(const float* __restrict__ planes, uint64_t S, uint32_t i,
-                                            int c, int n_sh, float x, float y, float z) {
-    auto C = [&](int k) { return planes[(uint64_t)(11 + 3 * k + c) * S + i]; };
-    const float SH_C0 = 0.28209479177387814f, SH_C1 = 0.4886025119029199f;
-    float result = SH_C0 * C(0);
-    if (n_sh > 1) result = result + SH_C1 * (-y * C(1) + z * C(2) - x * C(3));
-    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
-    if (n_sh > 4)
-        result = result + 1.0925484305920792f * xy * C(4) + -1.0925484305920792f * yz * C(5) +
-                 0.31539156525252005f * (2.0f * zz - xx - yy) * C(6) +
-                 -1.0925484305920792f * xz * C(7) + 0.5462742152960396f * (xx - yy) * C(8);
-    if (n_sh > 9)
-        result = result + -0.5900435899266435f * y * (3.0f * xx - yy) * C(9) +
-                 2.890611442640554f * xy * z * C(10) +
-                 -0.4570457994644658f * y * (4.0f * zz - xx - yy) * C(11) +
-                 0.3731763325901154f * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * C(12) +
-                 -0.4570457994644658f * x * (4.0f * zz - xx - yy) * C(13) +
-                 1.445305721320277f * z * (xx - yy) * C(14) +
-                 -0.5900435899266435f * x * (xx - 3.0f * yy) * C(15);
-    result = result + 0.5f;
-    return fmaxf(result, 0.0f);
-}
-
 // ---- WGSL-order projection.  Everything that decides visibility, the depth key or the
 // splat footprint is evaluated in the reference's order with contraction off, so it is
 // bit-identical to the oracle restatement (oracle/gs_oracle.cpp project_one).
@@ -269,36 +258,26 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
             hx = hx * 1.0001f + 0.02f;
             hy = hy * 1.0001f + 0.02f;
             float xl, xh, yl, yh;
-            uint32_t ntiles = 0, rx = 0, ry = 0, bbx = 0xFFFFu, bby = 0xFFFFu;  // empty box
+            uint32_t ntiles = 0, bbx = 0xFFFFu, bby = 0xFFFFu;  // empty box
             if (pixel_rect(f.cx, f.cy, hx, hy, p.W, row_lo, row_hi, xl, xh, yl, yh)) {
                 bbx = (uint32_t)xl | ((uint32_t)xh << 16);
                 bby = (uint32_t)yl | ((uint32_t)yh << 16);
                 const uint32_t tx0 = (uint32_t)xl >> 4, tx1 = (uint32_t)xh >> 4,
                                ty0 = (uint32_t)yl >> 4, ty1 = (uint32_t)yh >> 4;
                 ntiles = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
-                rx = tx0 | (ty0 << 16);
-                ry = tx1 | (ty1 << 16);
                 prect = (tx1 - tx0 < 16 && ty1 - ty0 < 16)
                             ? (tx0 | (ty0 << 12) | ((tx1 - tx0) << 24) | ((ty1 - ty0) << 28))
                             : kRectLarge;
             }
-            // colour (:321, dir = normalize(p - camPos))
-            const float dx = x - p.cam[0], dy = y - p.cam[1], dz = z - p.cam[2];
-            const float dl = sqrtf(dx * dx + dy * dy + dz * dz);
-            const float X = dx / dl, Y = dy / dl, Z = dz / dl;
-            const float cr = sh_channel(P, S, i, 0, p.n_sh, X, Y, Z);
-            const float cg = sh_channel(P, S, i, 1, p.n_sh, X, Y, Z);
-            const float cb = sh_channel(P, S, i, 2, p.n_sh, X, Y, Z);
-            // composite record: u' = d.(e1/|e1|^2)*sqrt(log2 e), so u'^2+v'^2 = (u^2+v^2) log2 e and
+            // composite record (colour: k_bin_emit, only for splats that receive tile entries): u' = d.(e1/|e1|^2)*sqrt(log2 e), so u'^2+v'^2 = (u^2+v^2) log2 e and
             // alpha = op * exp(-(u^2+v^2)) = exp2(log2(op) - (u'^2+v'^2))
             const float k1 = kSqrtLog2e / (f.e1x * f.e1x + f.e1y * f.e1y);
             const float k2 = kSqrtLog2e / (f.e2x * f.e2x + f.e2y * f.e2y);
             float4* r = p.rec + 4 * (uint64_t)i;
             r[0] = make_float4(f.cx, f.cy, f.e1x * k1, f.e1y * k1);
-            r[1] = make_float4(f.e2x * k2, f.e2y * k2, log2f(op), cr);
-            r[2] = make_float4(cg, cb, __uint_as_float(bbx), __uint_as_float(bby));
-            r[3] = make_float4(__uint_as_float(key), __uint_as_float(ntiles), __uint_as_float(rx),
-                               __uint_as_float(ry));
+            r[1] = make_float4(f.e2x * k2, f.e2y * k2, log2f(op), __uint_as_float(bbx));
+            r[3] = make_float4(__uint_as_float(key), __uint_as_float(ntiles), __uint_as_float(bbx),
+                               __uint_as_float(bby));
             ++my_vis;
             my_k += ntiles;
         }
@@ -467,8 +446,9 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
 // ============================================================================ binning
 // Chunk c covers depth ranks [r0, r1): chunk 0 = the first ceil(f * n_vis) ranks, chunk 1 = the
 // rest, binned only into tiles that were not saturated by chunk 0 (empty when all are).
-// Three launches per chunk, no inter-workgroup waiting: per-partition entry counts, one scan,
-// then the emission in depth order (cooperative, coalesced) plus the tile-id digit histograms.
+// Launches per chunk, no inter-workgroup waiting: per-partition entry counts, one scan, the
+// emission in depth order, then the row-wise emission of wide splats.  Entry positions come from
+// the scan alone, so whichever kernel writes an entry, every tile's list stays in depth order.
 __device__ __forceinline__ void chunk_range(const BinParams& p, uint32_t& r0, uint32_t& r1) {
     const uint32_t n = p.ctl->n_vis;
     const uint32_t c0 = p.chunk_f >= 1.0f
@@ -489,10 +469,10 @@ struct TileRect {
 
 __device__ __forceinline__ bool rect_unpack(const BinParams& p, uint32_t pr, uint32_t j, TileRect& r) {
     if (pr == kRectEmpty) return false;
-    if (pr == kRectLarge) {
+    if (pr == kRectLarge) {  // tile box from the pixel box in the record
         const float4 m = p.rec[4 * (uint64_t)j + 3];
-        const uint32_t rx = __float_as_uint(m.z), ry = __float_as_uint(m.w);
-        r = {rx & 0xffffu, rx >> 16, ry & 0xffffu, ry >> 16};
+        const uint32_t bx = __float_as_uint(m.z), by = __float_as_uint(m.w);
+        r = {(bx & 0xffffu) >> 4, (by & 0xffffu) >> 4, bx >> 20, by >> 20};
     } else {
         r.x0 = pr & 0xfffu;
         r.y0 = (pr >> 12) & 0xfffu;
@@ -506,54 +486,96 @@ __device__ __forceinline__ uint32_t tile_id(const BinParams& p, uint32_t tx, uin
     return (ty - (uint32_t)p.tile_row_begin) * (uint32_t)p.tiles_x + tx;
 }
 
-// entries of one splat in this chunk (chunk 1: only unsaturated tiles)
-__device__ __forceinline__ uint32_t rect_count(const BinParams& p, const TileRect& r) {
-    if (p.chunk == 0) return (r.x1 - r.x0 + 1) * (r.y1 - r.y0 + 1);
+// unsaturated tiles in columns [x0, x1], absolute tile rows [y0, y1] (chunk 1)
+__device__ __forceinline__ uint32_t sat_count(const BinParams& p, uint32_t x0, uint32_t x1, uint32_t y0,
+                                              uint32_t y1) {
+    const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
+    const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
+    const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
+    return (b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]);
+}
+
+// bits [x0, x0 + w) of a bitmask row (w <= 32), bit i = column x0 + i
+__device__ __forceinline__ uint32_t mask_bits(const unsigned long long* row, int words, uint32_t x0, uint32_t w) {
+    const uint32_t wi = x0 >> 6, sh = x0 & 63;
+    unsigned long long v = row[wi] >> sh;
+    if (sh && (int)wi + 1 < words) v |= row[wi + 1] << (64 - sh);
+    return (uint32_t)v & (w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u));
+}
+
+// Block-wide view of the chunk-1 bitmask: LDS copy when it fits.
+__device__ __forceinline__ const unsigned long long* stage_mask(const BinParams& p, unsigned long long* lds) {
+    const int words = p.mask_words * p.rows;
+    if (p.chunk == 0) return nullptr;
+    if (words > kMaskLdsWords) return p.mask;
+    for (int q = threadIdx.x; q < words; q += blockDim.x) lds[q] = p.mask[q];
+    __syncthreads();
+    return lds;
+}
+
+__device__ __forceinline__ bool rect_wide(const TileRect& r) {
+    return (r.x1 - r.x0 + 1) * (r.y1 - r.y0 + 1) >= kWideTiles;
+}
+
+// Entries of one splat in this chunk: every tile of its rectangle (chunk 0) or the unsaturated
+// ones (chunk 1: bitmask rows when narrow, the summed-area table when wide).
+__device__ __forceinline__ uint32_t rect_count(const BinParams& p, const unsigned long long* m,
+                                               const TileRect& r) {
+    const uint32_t w = r.x1 - r.x0 + 1;
+    if (p.chunk == 0) return w * (r.y1 - r.y0 + 1);
+    if (rect_wide(r)) return sat_count(p, r.x0, r.x1, r.y0, r.y1);
     uint32_t c = 0;
     for (uint32_t ty = r.y0; ty <= r.y1; ++ty)
-        for (uint32_t tx = r.x0; tx <= r.x1; ++tx) c += p.done[tile_id(p, tx, ty)] ? 0u : 1u;
+        c += __popc(mask_bits(m + (uint64_t)(ty - p.tile_row_begin) * p.mask_words, p.mask_words, r.x0, w));
     return c;
 }
 
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     __shared__ uint32_t s_tmp[8];
+    __shared__ unsigned long long s_mask[kMaskLdsWords];
     uint32_t r0, r1;
     chunk_range(p, r0, r1);
     const uint32_t parts = bin_parts(r1 - r0);
+    if (blockIdx.x >= parts) return;
+    const unsigned long long* m = stage_mask(p, s_mask);
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        uint32_t sum = 0;
+        uint32_t sum = 0, nsh = 0;
 #pragma unroll
         for (int k = 0; k < kBinIPT; ++k) {
-            const uint32_t r = r0 + part * kBinTile + threadIdx.x * kBinIPT + k;
+            const uint32_t r = r0 + part * kBinTile + k * kBinThreads + threadIdx.x;
             if (r < r1) {
                 TileRect tr;
-                if (rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) sum += rect_count(p, tr);
+                if (rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) {
+                    const uint32_t c = rect_count(p, m, tr);
+                    sum += c;
+                    nsh += c ? 1u : 0u;
+                }
             }
         }
-        uint32_t total;
+        uint32_t total, total_sh;
         block_excl_scan256(sum, s_tmp, &total);
-        if (threadIdx.x == 0) p.part_tot[part] = total;
+        block_excl_scan256(nsh, s_tmp, &total_sh);
+        if (threadIdx.x == 0) {
+            p.part_tot[part] = total;
+            p.part_tot[p.part_stride + part] = total_sh;
+        }
     }
 }
 
-// single workgroup: exclusive scan of the partition totals (in place), entry count, capacity
-__global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
-    __shared__ uint32_t s_w[16];
-    uint32_t r0, r1;
-    chunk_range(p, r0, r1);
-    const uint32_t parts = bin_parts(r1 - r0);
+// Exclusive scan of `parts` 32-bit counts in place (one 1024-thread workgroup), clamped to
+// `clamp`; returns the 64-bit total to every thread.
+__device__ unsigned long long scan_parts(uint32_t* a, uint32_t parts, uint32_t clamp,
+                                         unsigned long long* s_wsum) {
     const uint32_t tid = threadIdx.x, per = (parts + 1023) / 1024;
     const uint32_t b0 = min(parts, tid * per), b1 = min(parts, b0 + per);
     unsigned long long sum = 0;
-    for (uint32_t i = b0; i < b1; ++i) sum += p.part_tot[i];
-    // 64-bit inclusive wave scan, then across the 16 waves
+    for (uint32_t i = b0; i < b1; ++i) sum += a[i];
     unsigned long long incl = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const unsigned long long t = __shfl_up(incl, d, 64);
         if ((int)lane_id() >= d) incl += t;
     }
-    __shared__ unsigned long long s_wsum[16];
     if (lane_id() == 63) s_wsum[tid >> 6] = incl;
     __syncthreads();
     unsigned long long base = 0, total = 0;
@@ -561,93 +583,318 @@ __global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
         if (i < (tid >> 6)) base += s_wsum[i];
         total += s_wsum[i];
     }
+    __syncthreads();
     unsigned long long run = base + incl - sum;
     for (uint32_t i = b0; i < b1; ++i) {
-        const uint32_t c = p.part_tot[i];
-        p.part_tot[i] = (uint32_t)min(run, (unsigned long long)p.capacity);
+        const uint32_t c = a[i];
+        a[i] = (uint32_t)min(run, (unsigned long long)clamp);
         run += c;
     }
-    if (tid == 0) {
-        p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
-        if (total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
-    }
-    (void)s_w;
+    return total;
 }
 
+// single workgroup: partition bases of the entries (capacity-clamped, overflow flagged) and of
+// the colour queue
+__global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
+    __shared__ unsigned long long s_wsum[16];
+    uint32_t r0, r1;
+    chunk_range(p, r0, r1);
+    const uint32_t parts = bin_parts(r1 - r0);
+    const unsigned long long total = scan_parts(p.part_tot, parts, p.capacity, s_wsum);
+    const unsigned long long nsh = scan_parts(p.part_tot + p.part_stride, parts, 0xFFFFFFFFu, s_wsum);
+    if (threadIdx.x == 0) {
+        p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
+        p.ctl->shade_n[p.chunk] = (uint32_t)nsh;
+        if (total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
+    }
+}
+
+// Queue a wide splat (composite slot g) for k_bin_wide; false when the queue is full (the caller
+// emits it itself).
+__device__ bool wide_push(const BinParams& p, uint32_t j, uint32_t out, const TileRect& r) {
+    const uint32_t h = r.y1 - r.y0 + 1;
+    const uint32_t slot = atomicAdd(&p.ctl->wide_n[p.chunk], 1u);
+    const uint32_t u0 = atomicAdd(&p.ctl->wide_rows[p.chunk], h);
+    const bool ok = slot < p.wide_cap && slot < (1u << 20) && (uint64_t)u0 + h <= p.wide_unit_cap;
+    for (uint32_t t = 0; t < h && u0 + t < p.wide_unit_cap; ++t)
+        p.wide_unit[u0 + t] = ok ? (slot << 12 | t) : 0xFFFFFFFFu;
+    if (ok) p.wide_items[slot] = make_uint4(j, out, r.x0 | (r.x1 << 16), r.y0 | (r.y1 << 16));
+    return ok;
+}
+
+// Entries [k0, k1) of a splat emitted here (local positions o + k) into the LDS stage at o + k - R0.
+__device__ __forceinline__ void stage_narrow(const BinParams& p, const unsigned long long* m, const TileRect& tr,
+                                             uint32_t o, uint32_t k0, uint32_t k1, uint32_t R0,
+                                             uint32_t* s_key) {
+    const uint32_t w = tr.x1 - tr.x0 + 1;
+    if (p.chunk == 0) {
+        for (uint32_t k = k0; k < k1; ++k) s_key[o + k - R0] = tile_id(p, tr.x0 + k % w, tr.y0 + k / w);
+        return;
+    }
+    uint32_t k = 0;
+    for (uint32_t ty = tr.y0; ty <= tr.y1 && k < k1; ++ty) {
+        const uint32_t t0 = tile_id(p, tr.x0, ty);
+        if (w > 32) {  // a wide splat the queue could not take
+            for (uint32_t x = 0; x < w && k < k1; ++x) {
+                if (p.done[t0 + x]) continue;
+                if (k >= k0) s_key[o + k - R0] = t0 + x;
+                ++k;
+            }
+            continue;
+        }
+        uint32_t bits = mask_bits(m + (uint64_t)(ty - p.tile_row_begin) * p.mask_words, p.mask_words, tr.x0, w);
+        while (bits && k < k1) {
+            const uint32_t x = __ffs(bits) - 1;
+            bits &= bits - 1;
+            if (k >= k0) s_key[o + k - R0] = t0 + x;
+            ++k;
+        }
+    }
+}
+
+constexpr uint32_t kEmitStage = 2048;  // entries staged in LDS per round
+
+// Per depth rank: colour (when it has entries), then its entries at the scanned output position.
+// Narrow splats' entries are staged in LDS and written out coalesced, round by round; the
+// positions of wide splats are left for k_bin_wide (queued here, written after this kernel).
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
-    __shared__ uint32_t s_off[kBinTile + 1];
-    __shared__ uint32_t s_j[kBinTile];
-    __shared__ TileRect s_rect[kBinTile];
     __shared__ uint32_t s_tmp[8];
+    __shared__ unsigned long long s_mask[kMaskLdsWords];
+    __shared__ uint32_t s_key[kEmitStage];
+    __shared__ uint32_t s_val[kEmitStage];
     const int tid = threadIdx.x;
     uint32_t r0, r1;
     chunk_range(p, r0, r1);
     const uint32_t parts = bin_parts(r1 - r0);
+    if (blockIdx.x >= parts) return;
+    const unsigned long long* m = stage_mask(p, s_mask);
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         const uint32_t base_r = r0 + part * kBinTile;
-        const uint32_t nitems = min((uint32_t)kBinTile, r1 - base_r);
-        uint32_t cnt[kBinIPT];
-        uint32_t tsum = 0;
+        uint32_t cnt[kBinIPT], j[kBinIPT];
+        bool narrow[kBinIPT];
+        TileRect tr[kBinIPT];
 #pragma unroll
         for (int k = 0; k < kBinIPT; ++k) {
-            const uint32_t li = tid * kBinIPT + k;
+            const uint32_t r = base_r + k * kBinThreads + tid;
             cnt[k] = 0;
-            if (li < nitems) {
-                const uint32_t j = p.sorted_vals[base_r + li];
-                TileRect tr;
-                if (rect_unpack(p, p.sorted_rect[base_r + li], j, tr)) cnt[k] = rect_count(p, tr);
-                s_j[li] = j;
-                s_rect[li] = tr;
+            if (r < r1) {
+                j[k] = p.sorted_vals[r];
+                if (rect_unpack(p, p.sorted_rect[r], j[k], tr[k])) cnt[k] = rect_count(p, m, tr[k]);
             }
-            tsum += cnt[k];
         }
-        uint32_t total;
-        uint32_t run = block_excl_scan256(tsum, s_tmp, &total);
+        // local output offsets: ranks in order (k, tid) within the partition, as in k_bin_count
+        uint32_t o[kBinIPT];
+        uint32_t total, T = 0;
 #pragma unroll
         for (int k = 0; k < kBinIPT; ++k) {
-            s_off[tid * kBinIPT + k] = run;
-            run += cnt[k];
+            o[k] = block_excl_scan256(cnt[k], s_tmp, &total) + T;
+            T += total;
         }
-        __syncthreads();
         const uint32_t obase = p.part_tot[part];
-        if (p.chunk == 0) {
-            // cooperative, coalesced emission (depth order preserved within every tile)
-            for (uint32_t e = tid; e < total; e += kBinThreads) {
-                if (obase + e >= p.capacity) break;
-                int lo = 0, hi = (int)nitems - 1;
-                while (lo < hi) {  // largest s with s_off[s] <= e
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (s_off[mid] <= e) lo = mid; else hi = mid - 1;
-                }
-                const TileRect tr = s_rect[lo];
-                const uint32_t k = e - s_off[lo];
-                const uint32_t w = tr.x1 - tr.x0 + 1;
-                const uint32_t tile = tile_id(p, tr.x0 + k % w, tr.y0 + k / w);
-                p.tkeys[obase + e] = tile;
-                p.tvals[obase + e] = s_j[lo];
-            }
-        } else {
-            // chunk 1 (few unsaturated tiles): every splat walks its own rectangle
+        uint32_t sb = p.part_tot[p.part_stride + part] + (p.chunk ? p.ctl->shade_n[0] : 0u);
+        uint32_t g[kBinIPT];
+#pragma unroll
+        for (int k = 0; k < kBinIPT; ++k) {
+            // every splat with entries gets a composite slot (rank order); lists carry the slot
+            uint32_t nsh;
+            const uint32_t so = block_excl_scan256(cnt[k] ? 1u : 0u, s_tmp, &nsh);
+            g[k] = sb + so;
+            if (cnt[k]) p.shade_list[g[k]] = j[k];
+            sb += nsh;
+            narrow[k] = cnt[k] != 0;
+            if (cnt[k] && rect_wide(tr[k]) && wide_push(p, g[k], obase + o[k], tr[k])) narrow[k] = false;
+        }
+        for (uint32_t R0 = 0; R0 < T; R0 += kEmitStage) {
+            const uint32_t R1 = min(T, R0 + kEmitStage);
 #pragma unroll
             for (int k = 0; k < kBinIPT; ++k) {
-                const uint32_t li = tid * kBinIPT + k;
-                if (li >= nitems || cnt[k] == 0) continue;
-                const TileRect tr = s_rect[li];
-                uint32_t o = obase + s_off[li];
-                for (uint32_t ty = tr.y0; ty <= tr.y1; ++ty)
-                    for (uint32_t tx = tr.x0; tx <= tr.x1; ++tx) {
-                        const uint32_t tile = tile_id(p, tx, ty);
-                        if (p.done[tile]) continue;
-                        if (o < p.capacity) {
-                            p.tkeys[o] = tile;
-                            p.tvals[o] = s_j[li];
-                        }
-                        ++o;
-                    }
+                if (!narrow[k] || o[k] >= R1 || o[k] + cnt[k] <= R0) continue;
+                const uint32_t k0 = R0 > o[k] ? R0 - o[k] : 0u, k1 = min(cnt[k], R1 - o[k]);
+                stage_narrow(p, m, tr[k], o[k], k0, k1, R0, s_key);
+                for (uint32_t q = k0; q < k1; ++q) s_val[o[k] + q - R0] = g[k];
+            }
+            __syncthreads();
+            // coalesced copy; slots of queued wide splats carry stale LDS words and are rewritten
+            // by k_bin_wide
+            for (uint32_t q = R0 + tid; q < R1; q += kBinThreads) {
+                const uint32_t oe = obase + q;
+                if (oe < p.capacity) {
+                    p.tkeys[oe] = s_key[q - R0];
+                    p.tvals[oe] = s_val[q - R0];
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Composite records of this chunk's slots: colour (src/simple_render.ts:26-66, :321-322:
+// dir = normalize(p - camPos), SH to degree 3, + 0.5, max(., 0)) plus the footprint words of the
+// projected record, written densely at the slot.  16 lanes per splat: lanes 0-12 load the
+// shading block (one coalesced 208-B read), lanes 13-15 the record words; each lane evaluates
+// its own coefficients' terms and the group sums them with xor shuffles.
+__global__ __launch_bounds__(256) void k_shade(BinParams p) {
+    const uint32_t g0 = p.chunk ? p.ctl->shade_n[0] : 0u;
+    const uint32_t n = p.ctl->shade_n[p.chunk];
+    const uint32_t lane = lane_id(), l = lane & 15;
+    const uint32_t nq = p.shade_q, ncoef = 3 * (uint32_t)p.n_sh;
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+    for (uint32_t base = wave * 4; base < n; base += nwaves * 4) {  // wave-uniform: shuffles below
+        const uint32_t gi = base + (lane >> 4);
+        const bool active = gi < n;
+        const uint32_t slot = g0 + gi;
+        const uint32_t j = active ? p.shade_list[slot] : 0u;
+        float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (active) {
+            if (l < nq) q = p.shade[(uint64_t)j * nq + l];
+            else if (l >= 13) q = p.rec[4 * (uint64_t)j + (l == 15 ? 3 : l - 13)];
+        }
+        const uint32_t gl = lane & ~15u;
+        const float px = __shfl(q.x, gl, 64), py = __shfl(q.y, gl, 64), pz = __shfl(q.z, gl, 64);
+        const float dx = px - p.cam[0], dy = py - p.cam[1], dz = pz - p.cam[2];
+        const float dl = sqrtf(dx * dx + dy * dy + dz * dz);
+        const float x = dx / dl, y = dy / dl, z = dz / dl;
+        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
+        float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
+        const float v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t i = 4 * l + t;  // float index in the block: 3 + 3k + c
+            if (l >= 13 || i < 3 || i >= 3 + ncoef) continue;
+            const uint32_t k = (i - 3) / 3, c = (i - 3) % 3;
+            float b;
+            switch (k) {
+                case 0: b = 0.28209479177387814f; break;
+                case 1: b = 0.4886025119029199f * -y; break;
+                case 2: b = 0.4886025119029199f * z; break;
+                case 3: b = 0.4886025119029199f * -x; break;
+                case 4: b = 1.0925484305920792f * xy; break;
+                case 5: b = -1.0925484305920792f * yz; break;
+                case 6: b = 0.31539156525252005f * (2.0f * zz - xx - yy); break;
+                case 7: b = -1.0925484305920792f * xz; break;
+                case 8: b = 0.5462742152960396f * (xx - yy); break;
+                case 9: b = -0.5900435899266435f * y * (3.0f * xx - yy); break;
+                case 10: b = 2.890611442640554f * xy * z; break;
+                case 11: b = -0.4570457994644658f * y * (4.0f * zz - xx - yy); break;
+                case 12: b = 0.3731763325901154f * z * (2.0f * zz - 3.0f * xx - 3.0f * yy); break;
+                case 13: b = -0.4570457994644658f * x * (4.0f * zz - xx - yy); break;
+                case 14: b = 1.445305721320277f * z * (xx - yy); break;
+                default: b = -0.5900435899266435f * x * (xx - 3.0f * yy); break;
+            }
+            const float bv = b * v[t];
+            acc0 += c == 0 ? bv : 0.0f;
+            acc1 += c == 1 ? bv : 0.0f;
+            acc2 += c == 2 ? bv : 0.0f;
+        }
+#pragma unroll
+        for (int d = 8; d >= 1; d >>= 1) {
+            acc0 += __shfl_xor(acc0, d, 64);
+            acc1 += __shfl_xor(acc1, d, 64);
+            acc2 += __shfl_xor(acc2, d, 64);
+        }
+        const float by = __shfl(q.w, gl + 15, 64);  // record word [3].w = pixel box y
+        if (active) {
+            float4* o = p.crec + 3 * (uint64_t)slot;
+            if (l == 13 || l == 14) o[l - 13] = q;
+            if (l == 0)
+                o[2] = make_float4(fmaxf(acc0 + 0.5f, 0.0f), fmaxf(acc1 + 0.5f, 0.0f), fmaxf(acc2 + 0.5f, 0.0f), by);
+        }
+    }
+}
+
+// Tile rows of wide splats, one row per work unit: each wave prefetches 64 units lane-parallel
+// (unit word, item, chunk-1 row count and prefix), then writes them one by one across its lanes.
+__global__ __launch_bounds__(kBinThreads) void k_bin_wide(BinParams p) {
+    __shared__ unsigned long long s_mask[kMaskLdsWords];
+    const uint32_t units = min(p.ctl->wide_rows[p.chunk], p.wide_unit_cap);
+    if (blockIdx.x * (kBinThreads / 64) * 64 >= units) return;
+    const unsigned long long* m = stage_mask(p, s_mask);
+    const uint32_t lane = lane_id();
+    const uint32_t wave = blockIdx.x * (kBinThreads / 64) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (kBinThreads / 64);
+    for (uint32_t u0 = wave * 64; u0 < units; u0 += nwaves * 64) {
+        const uint32_t u = u0 + lane;
+        uint32_t code = 0xFFFFFFFFu;
+        uint4 it = make_uint4(0, 0, 0, 0);
+        uint32_t rowcnt = 0, pre = 0;
+        if (u < units) code = p.wide_unit[u];
+        if (code != 0xFFFFFFFFu) {
+            it = p.wide_items[code >> 12];
+            const uint32_t x0 = it.z & 0xffffu, x1 = it.z >> 16, y0 = it.w & 0xffffu;
+            const uint32_t row = y0 + (code & 4095u);
+            if (p.chunk == 0) {
+                rowcnt = x1 - x0 + 1;
+                pre = (code & 4095u) * rowcnt;
+            } else {
+                rowcnt = sat_count(p, x0, x1, row, row);
+                pre = row > y0 ? sat_count(p, x0, x1, y0, row - 1) : 0u;
             }
         }
-        __syncthreads();
+        uint64_t todo = __ballot(rowcnt != 0);
+        while (todo) {
+            const int src = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            const uint32_t c = __shfl(code, src, 64);
+            const uint32_t gj = __shfl(it.x, src, 64), go = __shfl(it.y, src, 64) + __shfl(pre, src, 64);
+            const uint32_t gz = __shfl(it.z, src, 64), gw = __shfl(it.w, src, 64);
+            const uint32_t x0 = gz & 0xffffu, x1 = gz >> 16, row = (gw & 0xffffu) + (c & 4095u);
+            const uint32_t w = x1 - x0 + 1, t0 = tile_id(p, x0, row);
+            uint32_t o = go;
+            for (uint32_t xs = 0; xs < w; xs += 64) {
+                const uint32_t x = xs + lane;
+                bool f = x < w;
+                if (p.chunk == 1 && f) {
+                    const unsigned long long* mr = m + (uint64_t)(row - p.tile_row_begin) * p.mask_words;
+                    f = (mr[(x0 + x) >> 6] >> ((x0 + x) & 63)) & 1ull;
+                }
+                const uint64_t b = __ballot(f);
+                const uint32_t e = o + __popcll(b & lanemask_lt());
+                if (f && e < p.capacity) {
+                    p.tkeys[e] = t0 + x;
+                    p.tvals[e] = gj;
+                }
+                o += __popcll(b);
+            }
+        }
     }
+}
+
+// Summed-area table and bitmask of the tiles chunk 0 left unsaturated (done == 0): one
+// workgroup; row prefixes by waves, then column prefixes by threads, in LDS when the table fits.
+__global__ __launch_bounds__(1024) void k_sat(const uint8_t* __restrict__ done, int tiles_x, int rows,
+                                              uint32_t* __restrict__ sat,
+                                              unsigned long long* __restrict__ mask) {
+    __shared__ uint32_t s_sat[kSatMaxWords];
+    const uint32_t sw = (uint32_t)tiles_x + 1, words = sw * (uint32_t)(rows + 1);
+    const int mw = (tiles_x + 63) / 64;
+    uint32_t* t = words <= (uint32_t)kSatMaxWords ? s_sat : sat;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    for (uint32_t x = tid; x < sw; x += 1024) t[x] = 0;
+    for (int r = w; r < rows; r += 16) {
+        uint32_t* row = t + (uint64_t)(r + 1) * sw;
+        uint32_t run = 0;
+        if (lane == 0) row[0] = 0;
+        for (int x0 = 0; x0 < tiles_x; x0 += 64) {
+            const int x = x0 + lane;
+            const uint32_t v = (x < tiles_x && !done[(uint64_t)r * tiles_x + x]) ? 1u : 0u;
+            const uint64_t b = __ballot(v);
+            if (lane == 0) mask[(uint64_t)r * mw + (x0 >> 6)] = b;
+            const uint32_t incl = run + __popcll(b & ((lanemask_lt() << 1) | 1ull));
+            if (x < tiles_x) row[x + 1] = incl;
+            run += __popcll(b);
+        }
+    }
+    __syncthreads();
+    for (uint32_t x = tid; x < sw; x += 1024) {
+        uint32_t acc = 0;
+        for (int r = 1; r <= rows; ++r) {
+            acc += t[(uint64_t)r * sw + x];
+            t[(uint64_t)r * sw + x] = acc;
+        }
+    }
+    __syncthreads();
+    if (t == s_sat)
+        for (uint32_t q = tid; q < words; q += 1024) sat[q] = s_sat[q];
 }
 
 // ============================================================================ k_ranges
@@ -665,11 +912,13 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tke
 // ============================================================================ k_composite
 // Workgroup = one 16x16 tile; wave w owns the 8x8 quarter (w&1, w>>1), lane = one pixel.
 // The tile's depth-ordered list is consumed in batches of 256 splats: every thread gathers one
-// 48-B record into registers (next batch issued before the current one is blended) and parks it
-// in a double-buffered LDS stage; each wave then walks the batch on its own, skips splats whose
-// pixel box misses its quarter, and stops blending once its 64 pixels are saturated.  Per pixel,
-// fs_main's alpha = saturate(op * exp(-dot(uv,uv))), discarded below 1/255 and outside
-// |u|,|v| <= 2, is blended front to back with the reference's blend state
+// 48-B composite record into registers (the next batch is issued before the current one is
+// blended), parks it in a double-buffered LDS stage and marks which quarters its pixel box
+// touches; each wave compacts those marks with ballots into per-quarter index lists (one
+// 64-entry segment per producing wave, so batch order is kept without another barrier).  Each
+// wave then walks only its own quarter's list and stops once its 64 pixels are saturated.
+// Per pixel, fs_main's alpha = saturate(op * exp(-dot(uv,uv))), discarded below 1/255 and
+// outside |u|,|v| <= 2, is blended front to back with the reference's blend state
 // (src/simple_render.ts:169-200, :455-471):
 //   FP32        transmittance form: C += col * alpha * T, T *= 1 - alpha; no splat is accepted
 //               once T < t_min;
@@ -678,17 +927,18 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tke
 // per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
 template <bool FP16_TARGET>
 __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
-    __shared__ float4 sA[2][256];  // cx, cy, a, b
-    __shared__ float4 sB[2][256];  // c, d, log2(op), r
-    __shared__ float2 sC[2][256];  // g, b
-    __shared__ uint2 sD[2][256];   // pixel box
+    __shared__ float4 sA[2][256];       // cx, cy, a, b
+    __shared__ float4 sB[2][256];       // c, d, log2(op), pixel box x
+    __shared__ float4 sC[2][256];       // r, g, b, pixel box y
+    __shared__ uint8_t sL[2][4][256];   // per quarter: batch indices, segment = producing wave
+    __shared__ uint32_t sN[2][4][4];    // per quarter, per producing wave: list length
     const int tid = threadIdx.x;
     const int tile = blockIdx.x;
     if (p.mode == kCompSecond && p.done[tile]) return;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
-    const int bx0 = tx * kTile + (w & 1) * 8, by0 = ty * kTile + (w >> 1) * 8;
-    const int px = bx0 + (lane & 7), py = by0 + (lane >> 3);
+    const int tx0 = tx * kTile, ty0 = ty * kTile;
+    const int px = tx0 + (w & 1) * 8 + (lane & 7), py = ty0 + (w >> 1) * 8 + (lane >> 3);
     const bool inside = px < p.W && py < p.H;
     const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
     const uint2 range = p.ranges[tile];
@@ -712,10 +962,12 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
     const uint32_t n = range.y - range.x;
     const uint32_t nb = (n + 255) / 256;
     float4 ga, gb, gc;
+    bool gv = false;
     auto gather = [&](uint32_t batch) {
         const uint32_t e = range.x + batch * 256 + tid;
-        if (e < range.y) {
-            const float4* r = rec + 4 * (uint64_t)tvals[e];
+        gv = e < range.y;
+        if (gv) {
+            const float4* r = rec + 3 * (uint64_t)tvals[e];
             ga = r[0];
             gb = r[1];
             gc = r[2];
@@ -724,8 +976,45 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
     auto park = [&](int buf) {
         sA[buf][tid] = ga;
         sB[buf][tid] = gb;
-        sC[buf][tid] = make_float2(gc.x, gc.y);
-        sD[buf][tid] = make_uint2(__float_as_uint(gc.z), __float_as_uint(gc.w));
+        sC[buf][tid] = gc;
+        const uint32_t bx = __float_as_uint(gb.w), by = __float_as_uint(gc.w);
+        const int x0 = (int)(bx & 0xffffu), x1 = (int)(bx >> 16), y0 = (int)(by & 0xffffu), y1 = (int)(by >> 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int qx = tx0 + (q & 1) * 8, qy = ty0 + (q >> 1) * 8;
+            const bool hit = gv && x0 <= qx + 7 && x1 >= qx && y0 <= qy + 7 && y1 >= qy;
+            const uint64_t b = __ballot(hit);
+            if (hit) sL[buf][q][w * 64 + __popcll(b & lanemask_lt())] = (uint8_t)tid;
+            if (lane == 0) sN[buf][q][w] = (uint32_t)__popcll(b);
+        }
+    };
+    auto blend = [&](int k, int cur) {
+        const float4 A = sA[cur][k];
+        const float4 B = sB[cur][k];
+        const float4 C = sC[cur][k];
+        const float dx = fx - A.x, dy = fy - A.y;
+        const float u = dx * A.z + dy * A.w;
+        const float v = dx * B.x + dy * B.y;
+        const float qd = u * u + v * v;
+        const float alpha = __builtin_amdgcn_exp2f(B.z - qd);
+        const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && alpha >= amin;
+        if (FP16_TARGET) {
+            if (hit) {
+                const float om = 1.0f - ca;
+                cr = (float)(_Float16)((C.x * alpha) * om + cr);
+                cg = (float)(_Float16)((C.y * alpha) * om + cg);
+                cb = (float)(_Float16)((C.z * alpha) * om + cb);
+                ca = (float)(_Float16)(alpha * om + ca);
+                live = ca < 1.0f;  // dst.a == 1: later blends add exactly zero
+            }
+        } else {
+            const float s = hit ? alpha * T : 0.0f;
+            cr = C.x * s + cr;
+            cg = C.y * s + cg;
+            cb = C.z * s + cb;
+            T = T - s;
+            live = live && T >= t_min;
+        }
     };
     if (nb > 0) {
         gather(0);
@@ -736,41 +1025,22 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
         const int cur = b & 1;
         if (b + 1 < nb) gather(b + 1);  // in flight while this batch is blended
         if (wave_live) {
-            const int cnt = (int)min(256u, n - b * 256);
-            for (int k = 0; k < cnt; ++k) {
-                const uint2 bb = sD[cur][k];
-                if ((int)(bb.x & 0xffffu) > bx0 + 7 || (int)(bb.x >> 16) < bx0 ||
-                    (int)(bb.y & 0xffffu) > by0 + 7 || (int)(bb.y >> 16) < by0)
-                    continue;  // the splat misses this quarter (wave-uniform)
-                const float4 A = sA[cur][k];
-                const float4 B = sB[cur][k];
-                const float dx = fx - A.x, dy = fy - A.y;
-                const float u = dx * A.z + dy * A.w;
-                const float v = dx * B.x + dy * B.y;
-                const float q = u * u + v * v;
-                const float alpha = __builtin_amdgcn_exp2f(B.z - q);
-                const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && alpha >= amin;
-                const float2 C = sC[cur][k];
-                if (FP16_TARGET) {
-                    if (hit) {
-                        const float om = 1.0f - ca;
-                        cr = (float)(_Float16)((B.w * alpha) * om + cr);
-                        cg = (float)(_Float16)((C.x * alpha) * om + cg);
-                        cb = (float)(_Float16)((C.y * alpha) * om + cb);
-                        ca = (float)(_Float16)(alpha * om + ca);
-                        live = ca < 1.0f;  // dst.a == 1: later blends add exactly zero
+            for (int seg = 0; seg < 4 && wave_live; ++seg) {
+                const int cnt = (int)sN[cur][w][seg];
+                const uint8_t* list = &sL[cur][w][seg * 64];
+                int k = 0;
+                for (; k + 1 < cnt; k += 2) {
+                    const int i0 = list[k], i1 = list[k + 1];
+                    blend(i0, cur);
+                    blend(i1, cur);
+                    if (!__any(live)) {
+                        wave_live = false;
+                        break;
                     }
-                } else {
-                    const float s = hit ? alpha * T : 0.0f;
-                    cr = B.w * s + cr;
-                    cg = C.x * s + cg;
-                    cb = C.y * s + cb;
-                    T = T - s;
-                    live = live && T >= t_min;
                 }
-                if (!__any(live)) {
-                    wave_live = false;
-                    break;
+                if (wave_live && k < cnt) {
+                    blend(list[k], cur);
+                    if (!__any(live)) wave_live = false;
                 }
             }
         }
@@ -806,10 +1076,10 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
 
 // ============================================================================ launchers
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, uint64_t stride,
-                      hipStream_t s) {
+                      float4* shade, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, aos, n, n_sh,
-                       planes, stride);
+                       planes, stride, shade);
 }
 void launch_project(const ProjParams& p, hipStream_t s) {
     const unsigned grid = (unsigned)std::max<uint64_t>(
@@ -828,6 +1098,12 @@ void launch_bin(const BinParams& p, hipStream_t s) {
     hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(kBinThreads), 0, s, p);
     hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, p);
     hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);
+    hipLaunchKernelGGL(k_bin_wide, dim3(kMaxGrid), dim3(kBinThreads), 0, s, p);
+    hipLaunchKernelGGL(k_shade, dim3(kMaxGrid), dim3(256), 0, s, p);
+}
+void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
+                hipStream_t s) {
+    hipLaunchKernelGGL(k_sat, dim3(1), dim3(1024), 0, s, done, tiles_x, rows, sat, mask);
 }
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
                    hipStream_t s) {

@@ -47,7 +47,9 @@ class GsStats(ctypes.Structure):
                 ("ms_total", ctypes.c_float), ("ms_project", ctypes.c_float),
                 ("ms_sort", ctypes.c_float), ("ms_bin", ctypes.c_float),
                 ("ms_tile_sort", ctypes.c_float), ("ms_ranges", ctypes.c_float),
-                ("ms_composite", ctypes.c_float), ("ms_other", ctypes.c_float)]
+                ("ms_composite", ctypes.c_float), ("ms_other", ctypes.c_float),
+                ("k_chunk0", ctypes.c_uint32), ("k_chunk1", ctypes.c_uint32),
+                ("wide_chunk0", ctypes.c_uint32), ("wide_chunk1", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
