@@ -125,7 +125,7 @@ struct gs_scene {
     FrameCtl* ctl = nullptr;
     uint32_t* hist = nullptr;
     uint32_t* bin_part = nullptr;       // bin_parts(N) + 1
-    uint32_t* shade_list = nullptr;     // N: splats whose colour the frame evaluates
+    uint32_t* shade_list = nullptr;     // N: Gaussian index of each composite slot
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tkA = nullptr, *tvA = nullptr, *tkB = nullptr, *tvB = nullptr;
@@ -148,6 +148,7 @@ struct gs_scene {
     FrameCtl last{};            // latest harvested statistics
     bool have_last = false;
     float chunk_f = kChunkF0;
+    int last_tiles = 0;                 // tiles of the last frame's strip
     bool have_frame = false;
 };
 
@@ -260,12 +261,28 @@ static void collect_stats(gs_scene* s, bool wait) {
         s->last = s->h_ctl[slot];
         s->have_last = true;
         s->stat_pending[slot] = false;
-        // chunk controller: keep chunk 1's entries a small fraction of chunk 0's
-        const double k0 = s->last.k_chunk[0], k1 = s->last.k_chunk[1];
-        if (s->last.not_done > 0 && k1 > 0.25 * std::max(k0, 1.0))
-            s->chunk_f = std::min(1.0f, s->chunk_f * 1.5f);
-        else if (k1 < 0.05 * k0)
-            s->chunk_f = std::max(1.0f / 64.0f, s->chunk_f * 0.9f);
+        // chunk controller: chunk 0 should reach the depth rank at which the tiles saturate
+        // (from the composite: the last slot any tile needed; chunk-0 slots are the depth
+        // ranks with entries, so slot / slots0 * c0 estimates the rank), with a margin for
+        // camera motion; rises at once, decays slowly.  Mostly unsaturated frames use one chunk.
+        const FrameCtl& l = s->last;
+        const double tiles = std::max(1.0, (double)s->last_tiles);
+        uint32_t sat_slot = 0, sat_tiles = 0;
+        for (int k = 0; k < kHistShards; ++k) {
+            sat_slot = std::max(sat_slot, l.sat_slot[k]);
+            sat_tiles += l.sat_tiles[k];
+        }
+        float target = 1.0f;
+        if (l.n_vis > 0 && sat_tiles >= 0.5 * tiles) {
+            double rank;
+            if (sat_slot < l.shade_n[0])
+                rank = ((double)sat_slot + 1.0) / std::max(1.0, (double)l.shade_n[0]) * l.c0;
+            else  // a tile saturated in chunk 1: somewhere past c0
+                rank = (double)l.c0 * 1.5;
+            target = (float)std::min(1.0, 1.15 * rank / (double)l.n_vis);
+        }
+        target = std::max(target, 1.0f / 64.0f);
+        s->chunk_f = target >= s->chunk_f ? target : std::max(target, s->chunk_f * 0.95f);
     }
 }
 
@@ -280,6 +297,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     collect_stats(s, false);
     if (s->have_last && s->last.k_total > s->kcap) ensure_tile_capacity(s, s->last.k_total);
     ensure_tiles(s, std::max(n_tiles, 1));
+    s->last_tiles = n_tiles;
     const float f = o.chunk_fraction > 0.0f ? std::min(o.chunk_fraction, 1.0f) : s->chunk_f;
     const bool two_chunks = f < 1.0f;
     if (two_chunks) {

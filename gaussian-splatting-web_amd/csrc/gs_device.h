@@ -45,7 +45,10 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t wide_n[2];           // wide splats queued per chunk (binning)
     uint32_t wide_rows[2];        // their tile rows (work units of k_bin_wide)
     uint32_t shade_n[2];          // splats queued for colour per chunk (binning)
-    uint32_t pad[3];
+    uint32_t c0;                  // depth ranks in chunk 0
+    uint32_t pad0;
+    uint32_t sat_slot[kHistShards];   // per shard: max composite slot at which a tile saturated
+    uint32_t sat_tiles[kHistShards];  // per shard: tiles saturated by the end of the frame
 };
 
 // Scene layout in HBM: 11 SoA geometry planes (0-2 position, 3-5 log-free scale, 6-9 rotation,

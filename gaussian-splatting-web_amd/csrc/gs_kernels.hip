@@ -605,6 +605,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
     if (threadIdx.x == 0) {
         p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
         p.ctl->shade_n[p.chunk] = (uint32_t)nsh;
+        if (p.chunk == 0) p.ctl->c0 = r1;
         if (total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
     }
 }
@@ -928,10 +929,11 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tke
 template <bool FP16_TARGET>
 __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
     __shared__ float4 sA[2][256];       // cx, cy, a, b
-    __shared__ float4 sB[2][256];       // c, d, log2(op), pixel box x
-    __shared__ float4 sC[2][256];       // r, g, b, pixel box y
+    __shared__ float4 sB[2][256];       // c, d, log2(op), composite slot (bits)
+    __shared__ float4 sC[2][256];       // r, g, b, (pixel box y)
     __shared__ uint8_t sL[2][4][256];   // per quarter: batch indices, segment = producing wave
     __shared__ uint32_t sN[2][4][4];    // per quarter, per producing wave: list length
+    __shared__ uint32_t s_sat;          // slot that saturated the last wave
     const int tid = threadIdx.x;
     const int tile = blockIdx.x;
     if (p.mode == kCompSecond && p.done[tile]) return;
@@ -962,12 +964,14 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
     const uint32_t n = range.y - range.x;
     const uint32_t nb = (n + 255) / 256;
     float4 ga, gb, gc;
+    uint32_t gs_ = 0;
     bool gv = false;
     auto gather = [&](uint32_t batch) {
         const uint32_t e = range.x + batch * 256 + tid;
         gv = e < range.y;
         if (gv) {
-            const float4* r = rec + 3 * (uint64_t)tvals[e];
+            gs_ = tvals[e];
+            const float4* r = rec + 3 * (uint64_t)gs_;
             ga = r[0];
             gb = r[1];
             gc = r[2];
@@ -975,7 +979,7 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
     };
     auto park = [&](int buf) {
         sA[buf][tid] = ga;
-        sB[buf][tid] = gb;
+        sB[buf][tid] = make_float4(gb.x, gb.y, gb.z, __uint_as_float(gs_));  // box x: used below only
         sC[buf][tid] = gc;
         const uint32_t bx = __float_as_uint(gb.w), by = __float_as_uint(gc.w);
         const int x0 = (int)(bx & 0xffffu), x1 = (int)(bx >> 16), y0 = (int)(by & 0xffffu), y1 = (int)(by >> 16);
@@ -1016,6 +1020,7 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
             live = live && T >= t_min;
         }
     };
+    if (tid == 0) s_sat = 0;
     if (nb > 0) {
         gather(0);
         park(0);
@@ -1035,20 +1040,28 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
                     blend(i1, cur);
                     if (!__any(live)) {
                         wave_live = false;
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sB[cur][i1].w));
                         break;
                     }
                 }
                 if (wave_live && k < cnt) {
                     blend(list[k], cur);
-                    if (!__any(live)) wave_live = false;
+                    if (!__any(live)) {
+                        wave_live = false;
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sB[cur][list[k]].w));
+                    }
                 }
             }
         }
         if (b + 1 < nb) park(cur ^ 1);
         if (__syncthreads_count(wave_live) == 0) break;
     }
+    const bool tile_done = __syncthreads_count(live) == 0;
+    if (tile_done && tid == 0 && n > 0) {  // saturation statistics for the chunk controller
+        atomicAdd(&p.ctl->sat_tiles[tile % kHistShards], 1u);
+        atomicMax(&p.ctl->sat_slot[tile % kHistShards], s_sat);
+    }
     if (p.mode == kCompFirst) {
-        const bool tile_done = __syncthreads_count(live) == 0;
         if (!tile_done) {  // park the pixels for chunk 1
             if (inside) p.state[pix] = make_float4(cr, cg, cb, FP16_TARGET ? ca : T);
             if (tid == 0) {
