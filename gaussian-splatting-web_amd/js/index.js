@@ -1,0 +1,240 @@
+'use strict';
+// Node host mirror of the reference's TypeScript surface (src/gpu_context.ts, src/renderer.ts,
+// src/camera.ts), driving the MI355X renderer through the N-API addon (../lib/gsplat_napi.node).
+// Same names, argument meaning and error behaviour as the reference:
+//   * GpuContext.create() / Renderer.requestContext() reject with a STRING when no device exists
+//     (src/gpu_context.ts:12-26, src/renderer.ts:79-100);
+//   * new Renderer(canvas, camera, gaussians, context, fpsCounter) throws Error when the surface is
+//     missing (src/renderer.ts:119-122), copies the AoS scene once (:139-146) and starts the frame
+//     loop with requestAnimationFrame(() => this.animate(true)) (:278);
+//   * animate(forceDraw?) packs the 160-B uniform block from camera.getCamera() and draws only when
+//     the camera is dirty or forced (:332-387); draw(cb) renders and schedules cb (:301-330);
+//   * destroy() resolves after the next frame (:103-107, :281-292); resize() reallocates the
+//     W x H state (:293-299).
+// Headless conventions (SURVEY §8b): canvas = {width, height, present?, onFrame?}; after every
+// frame renderer.framebuffer (and canvas.framebuffer) holds SimpleRender.framebuffer's contents
+// (W*H premultiplied RGBA float32, row 0 = top) and, with canvas.present, canvas.image holds the
+// PostProcessRenderer output; fpsCounter = {innerText, style}; requestAnimationFrame = setImmediate
+// unless the host provides one.
+const path = require('path');
+
+let native = null;
+function addon() {
+    if (native === null) {
+        const p = process.env.GSPLAT_NAPI || path.join(__dirname, '..', 'lib', 'gsplat_napi.node');
+        native = require(p);  // throws if the addon was not built: there is no other backend
+    }
+    return native;
+}
+
+const raf = (cb) => (typeof requestAnimationFrame === 'function' ? requestAnimationFrame(cb) : setImmediate(cb));
+const now = () => Number(process.hrtime.bigint()) / 1e6;
+const FOV = 1.04719755;  // 60 degrees (src/camera.ts:4)
+
+const GS_ACCUM_FP32 = 0, GS_ACCUM_FP16_TARGET = 1, GS_OUT_RGBA_F32 = 0, GS_OUT_RGBA_F16 = 1;
+
+// ---------------------------------------------------------------------------- GpuContext
+class GpuContext {
+    constructor(gpu, adapter, device) {
+        this.gpu = gpu;          // {api: 'hip'}
+        this.adapter = adapter;  // {deviceIndex, deviceCount}
+        this.device = device;    // native context handle (gs_ctx*)
+    }
+
+    static async create(deviceIndex = 0) {
+        let n = 0;
+        try {
+            n = addon().deviceCount();
+        } catch (e) {
+            return Promise.reject('gsplat addon not available: ' + e.message);
+        }
+        if (n <= 0) return Promise.reject('No HIP device available (gs_device_count = 0)');
+        try {
+            const device = addon().ctxCreate(deviceIndex);
+            return new GpuContext({api: 'hip'}, {deviceIndex, deviceCount: n}, device);
+        } catch (e) {
+            return Promise.reject(String(e.message));
+        }
+    }
+
+    destroy() {
+        if (this.device) addon().ctxDestroy(this.device);
+        this.adapter = null;
+        this.device = null;
+    }
+}
+
+// ---------------------------------------------------------------------------- scene input
+// The reference's PackedGaussians (src/ply.ts:249-257): AoS records of 64 + 16 * nShCoeffs bytes.
+class PackedGaussians {
+    constructor(gaussiansBuffer, numGaussians, nShCoeffs = 16) {
+        this.gaussiansBuffer = gaussiansBuffer instanceof ArrayBuffer ? gaussiansBuffer : gaussiansBuffer.buffer;
+        this.numGaussians = numGaussians;
+        this.nShCoeffs = nShCoeffs;
+        this.gaussianArrayLayout = {size: numGaussians * (64 + 16 * nShCoeffs)};
+        this.sceneMin = null;
+        this.sceneMax = null;
+    }
+}
+
+// ---------------------------------------------------------------------------- cameras
+// Camera fields as src/camera.ts:56-138 (matrices Float32Array(16), column-major).
+class Camera {
+    constructor(height, width, viewMatrix, perspective, focalX, focalY, scaleModifier) {
+        this.height = height;
+        this.width = width;
+        this.viewMatrix = viewMatrix;
+        this.perspective = perspective;
+        this.focalX = focalX;
+        this.focalY = focalY;
+        this.scaleModifier = scaleModifier;
+    }
+
+    // Camera.default (src/camera.ts:101-111) for a canvas of width x height
+    static default(width, height) {
+        return new Camera(height, width, addon().lookAt([0, 0, -5], [0, 0, 0], [0, 1, 0]),
+                          addon().perspective(FOV, width / height, 0.03, 1000), width, height, 1);
+    }
+
+    static lookAt(eye, target, width, height, fovy = FOV, near = 0.03, far = 1000) {
+        return new Camera(height, width, addon().lookAt(eye, target, [0, 1, 0]),
+                          addon().perspective(fovy, width / height, near, far), width, height, 1);
+    }
+
+    // translation of inverse(view) (src/camera.ts:135-138)
+    getPosition() {
+        return addon().cameraPosition(this.viewMatrix);
+    }
+}
+
+// InteractiveCamera's contract as used by Renderer.animate: isDirty() / getCamera().
+class HeadlessCamera {
+    constructor(camera) {
+        this.camera = camera;
+        this.dirty = true;
+    }
+
+    setNewCamera(camera) {
+        this.camera = camera;
+        this.dirty = true;
+    }
+
+    setDirty() {
+        this.dirty = true;
+    }
+
+    isDirty() {
+        return this.dirty;
+    }
+
+    getCamera() {
+        this.dirty = false;
+        return this.camera;
+    }
+}
+
+// ---------------------------------------------------------------------------- Renderer
+class Renderer {
+    static async requestContext(gaussians, deviceIndex = 0) {
+        if (!gaussians || !gaussians.gaussiansBuffer) return Promise.reject('requestContext: no gaussians');
+        return GpuContext.create(deviceIndex);
+    }
+
+    // destroy the renderer; resolves when it's done (after the next frame)
+    async destroy() {
+        return new Promise((resolve) => {
+            this.destroyCallback = resolve;
+        });
+    }
+
+    constructor(canvas, interactiveCamera, gaussians, context, fpsCounter, options = {}) {
+        if (!canvas || !(canvas.width > 0) || !(canvas.height > 0)) {
+            throw new Error('Render surface not found! (canvas needs width and height)');
+        }
+        if (!context || !context.device) throw new Error('GpuContext is not initialised');
+        this.canvas = canvas;
+        this.interactiveCamera = interactiveCamera;
+        this.context = context;
+        this.fpsCounter = fpsCounter || {innerText: '', style: {}};
+        this.lastDraw = now();
+        this.numGaussians = gaussians.numGaussians;
+        this.destroyCallback = null;
+        this.opts = Object.assign({accum: GS_ACCUM_FP32, outFormat: GS_OUT_RGBA_F32, tMin: 1e-4}, options);
+        this.frames = 0;
+        // the AoS record buffer is borrowed for this call only (copied into HBM as SoA)
+        this.scene = addon().sceneUpload(context.device, gaussians.gaussiansBuffer, gaussians.numGaussians,
+                                         gaussians.nShCoeffs);
+        this.resize();
+        raf(() => this.animate(true));
+    }
+
+    destroyImpl() {
+        if (this.destroyCallback === null) throw new Error('destroyImpl called without destroyCallback set!');
+        if (this.scene && this.context.device) addon().sceneFree(this.scene);
+        this.scene = null;
+        this.context.destroy();
+        this.destroyCallback();
+    }
+
+    // reallocate the W x H-dependent state (src/renderer.ts:293-299)
+    resize() {
+        this.width = this.canvas.width;
+        this.height = this.canvas.height;
+        const px = this.width * this.height * 4;
+        this.framebuffer = this.opts.outFormat === GS_OUT_RGBA_F16 ? new Uint16Array(px) : new Float32Array(px);
+        this.image = this.canvas.present ? new Float32Array(px) : null;
+    }
+
+    // render one frame (depth keys + sort + tile composite), then schedule nextFrameCallback
+    draw(nextFrameCallback) {
+        if (this.canvas.width !== this.width || this.canvas.height !== this.height) this.resize();
+        addon().renderAsync(this.context.device, this.scene, this.uniforms, this.width, this.height, this.opts,
+                            this.framebuffer).then(() => {
+            this.frames++;
+            this.canvas.framebuffer = this.framebuffer;
+            if (this.image) {
+                addon().present(this.framebuffer, this.width, this.height, this.image);
+                this.canvas.image = this.image;
+            }
+            if (typeof this.canvas.onFrame === 'function') this.canvas.onFrame(this);
+            raf(nextFrameCallback);
+        }, (err) => {
+            this.lastError = err;
+            if (typeof this.canvas.onError === 'function') this.canvas.onError(err);
+            raf(nextFrameCallback);
+        });
+    }
+
+    animate(forceDraw) {
+        const t = now();
+        const fps = 1000 / (t - this.lastDraw);
+        this.lastDraw = t;
+        this.fpsCounter.innerText = 'FPS: ' + fps.toFixed(2);
+        if (this.fpsCounter.style) this.fpsCounter.style.display = 'block';
+
+        if (this.destroyCallback !== null) {
+            this.destroyImpl();
+            return;
+        }
+        if (!this.interactiveCamera.isDirty() && !forceDraw) {
+            raf(() => this.animate());
+            return;
+        }
+        const camera = this.interactiveCamera.getCamera();
+        const position = camera.getPosition();
+        const tanHalfFovX = 0.5 * this.canvas.width / camera.focalX;
+        const tanHalfFovY = 0.5 * this.canvas.height / camera.focalY;
+        this.uniforms = addon().packUniforms(camera.viewMatrix, camera.perspective, position, tanHalfFovX, tanHalfFovY,
+                                             camera.focalX, camera.focalY, camera.scaleModifier);
+        this.draw(() => this.animate());
+    }
+
+    timings() {
+        return addon().timings(this.context.device);
+    }
+}
+
+module.exports = {
+    GpuContext, Renderer, PackedGaussians, Camera, HeadlessCamera, addon,
+    GS_ACCUM_FP32, GS_ACCUM_FP16_TARGET, GS_OUT_RGBA_F32, GS_OUT_RGBA_F16,
+};

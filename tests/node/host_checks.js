@@ -1,0 +1,65 @@
+'use strict';
+// CPU-side checks of the Node host (no GPU needed): addon exports, the reference's rejection
+// behaviour without a device, and the camera / uniform producer against the wgpu-matrix fixtures.
+// Usage: node host_checks.js <cameras.json>   -> prints one JSON object
+const fs = require('fs');
+const path = require('path');
+const gs = require(path.join(__dirname, '..', '..', 'gaussian-splatting-web_amd', 'js'));
+
+async function main() {
+    const out = {};
+    const a = gs.addon();
+    out.exports = Object.keys(a).sort();
+    out.abi = a.abiVersion();
+    out.deviceCount = a.deviceCount();
+    // GpuContext.create / Renderer.requestContext reject with a string when there is no device
+    if (out.deviceCount === 0) {
+        try {
+            await gs.GpuContext.create();
+            out.createRejected = false;
+        } catch (e) {
+            out.createRejected = typeof e === 'string' ? 'string' : typeof e;
+        }
+        try {
+            await gs.Renderer.requestContext(new gs.PackedGaussians(new ArrayBuffer(320), 1, 16));
+            out.requestRejected = false;
+        } catch (e) {
+            out.requestRejected = typeof e === 'string' ? 'string' : typeof e;
+        }
+    }
+    // the Renderer constructor throws Error without a surface
+    try {
+        new gs.Renderer(null, null, null, null, null);
+        out.ctorThrows = false;
+    } catch (e) {
+        out.ctorThrows = e instanceof Error;
+    }
+    // render arguments are validated before any device work
+    try {
+        a.render(null, null, new ArrayBuffer(160), 4, 4, {}, null);
+        out.badHandle = 'accepted';
+    } catch (e) {
+        out.badHandle = e.code;
+    }
+    // camera producer: bit patterns of view/proj/camPos for every lookat fixture
+    const cams = JSON.parse(fs.readFileSync(process.argv[2], 'utf8'));
+    out.cams = [];
+    for (const c of cams) {
+        if (c.kind !== 'lookat') continue;
+        const cam = gs.Camera.lookAt(c.eye, c.target, c.W, c.H);
+        const bits = (f) => Array.from(new Uint32Array(Float32Array.from(f).buffer));
+        out.cams.push({name: c.name, W: c.W, H: c.H, view: bits(cam.viewMatrix), proj: bits(cam.perspective),
+                       campos: bits(cam.getPosition())});
+    }
+    // uniform block packing (src/renderer.ts:24-33) of the first camera
+    const c0 = gs.Camera.lookAt(cams[0].eye, cams[0].target, cams[0].W, cams[0].H);
+    const u = a.packUniforms(c0.viewMatrix, c0.perspective, c0.getPosition(), 0.5, 0.25, 100, 200, 1);
+    out.uniforms = Array.from(new Uint32Array(u));
+    out.strip = a.stripRows(1080, 3, 8);
+    console.log(JSON.stringify(out));
+}
+
+main().catch((e) => {
+    console.error(e);
+    process.exit(1);
+});

@@ -1,0 +1,77 @@
+"""The Node host (N-API addon + JS mirror of the reference's GpuContext/Renderer surface).
+
+CPU: addon exports, string rejection without a device, camera/uniform producer bit-exact against
+the wgpu-matrix fixtures.  GPU: the reference's frame loop (create -> Renderer -> animate/draw ->
+destroy) driven from node renders the same image as the C ABI and matches the oracle."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, camera, load_scene
+
+NODE = shutil.which("node")
+ADDON = os.path.join(ROOT, "gaussian-splatting-web_amd", "lib", "gsplat_napi.node")
+pytestmark = pytest.mark.skipif(not NODE or not os.path.exists(ADDON), reason="node or the addon is absent")
+
+EXPORTS = sorted(["abiVersion", "lastError", "deviceCount", "ctxCreate", "ctxDestroy", "sceneUpload", "sceneFree",
+                  "render", "renderAsync", "timings", "timingsReset", "sync", "present", "lookAt", "perspective",
+                  "cameraPosition", "packUniforms", "stripRows"])
+
+
+def run_node(*args, timeout=120):
+    r = subprocess.run([NODE] + list(args), capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_node_host_cpu():
+    out = run_node(os.path.join(ROOT, "tests", "node", "host_checks.js"), os.path.join(GOLDEN, "cameras.json"))
+    assert out["exports"] == EXPORTS
+    assert out["abi"] == 1
+    if out["deviceCount"] == 0:
+        assert out["createRejected"] == "string" and out["requestRejected"] == "string"
+    assert out["ctorThrows"] is True
+    assert out["badHandle"] == -1
+    cams = {(c["name"], c["W"], c["H"]): c for c in json.load(open(os.path.join(GOLDEN, "cameras.json")))}
+    assert len(out["cams"]) > 10
+    for c in out["cams"]:
+        ref = cams[(c["name"], c["W"], c["H"])]
+        assert c["view"] == ref["view"] and c["proj"] == ref["proj"] and c["campos"] == ref["campos"], c["name"]
+    u = np.array(out["uniforms"], np.uint32).view(np.float32)
+    ref = cams[(out["cams"][0]["name"], out["cams"][0]["W"], out["cams"][0]["H"])]
+    assert np.array_equal(u[0:16].view(np.uint32), np.array(ref["view"], np.uint32))
+    assert np.array_equal(u[35:40], np.array([0.5, 0.25, 100, 200, 1], np.float32))
+    assert out["strip"] == {"row0": 3 * 9 * 16, "rowsPadded": 9 * 16}
+
+
+@pytest.mark.gpu
+def test_node_frame_loop_gpu(tmp_path):
+    import gsplat_amd as gs
+    import oracle_py as orc
+    W, H = 256, 256
+    aos, n, nsh = load_scene("pc_short")
+    u, _ = camera("pc_short_app", W, H)
+    (tmp_path / "scene.bin").write_bytes(aos.tobytes())
+    (tmp_path / "uni.bin").write_bytes(u.tobytes())
+    out = run_node(os.path.join(ROOT, "tests", "node", "render_frames.js"), str(tmp_path / "scene.bin"), str(n),
+                   str(nsh), str(tmp_path / "uni.bin"), str(W), str(H), str(tmp_path / "img.f32"), "3")
+    assert out["frames"] == 3 and out["destroyed"] is True
+    img = np.fromfile(tmp_path / "img.f32", np.float32).reshape(H, W, 4)
+    # same image as the C ABI path, close to the oracle
+    ctx = gs.Context(0)
+    sc = gs.Scene(ctx, aos, n, nsh)
+    direct = sc.render(u, W, H)
+    dd = np.abs(img - direct)
+    assert np.array_equal(img, direct), (float(dd.max()), int((dd > 0).sum()), float(np.abs(img).sum()),
+                                         float(np.abs(direct).sum()), np.argwhere(dd > 0)[:5].tolist())
+    ref, _ = orc.render(aos, n, nsh, u, W, H, accum=0, t_min=1e-4)
+    d = np.abs(img.astype(np.float64) - ref)
+    assert float((d ** 2).mean()) < 1e-8
+    pres = np.fromfile(str(tmp_path / "img.f32") + ".present", np.float32).reshape(H, W, 4)
+    assert np.array_equal(pres, gs.present(direct, W, H))
+    sc.close()
+    ctx.close()
