@@ -32,16 +32,37 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 def algorithmic_bytes(stage, n, n_vis, k, W, H):
     """Bytes a kernel must move per launch."""
     if stage == "project":
-        # read pos+scale+rot+opacity (44 B) of every Gaussian and SH (192 B) of visible ones;
-        # write the depth key (4 B) of every Gaussian and the 64-B record of visible ones
-        return 48 * n + 256 * n_vis
+        # read the 11 geometry planes (44 B) and write key + packed tile rect (8 B) of every
+        # Gaussian; write the 48-B projected record of every visible one
+        return 52 * n + 48 * n_vis
     if stage == "composite":
-        # read each (tile, splat) entry (4 B) and gather its 40-B record; write RGBA f32
-        return 44 * k + 16 * W * H
+        # per (tile, splat) entry: the 4-B slot and the 48-B composite record; RGBA f32 out
+        return 52 * k + 16 * W * H
     if stage == "sort":
-        # 4 passes x (read key+val 8 B, write 8 B) over n_vis; pass 0 reads N keys
-        return 4 * n + 4 * 16 * n_vis
+        # 4 LSD passes: upsweep reads the key (4 B), downsweep reads key+index+rect and writes
+        # them (24 B); pass 0 runs over all N keys
+        return 28 * n + 3 * 28 * n_vis
     raise KeyError(stage)
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per frame of `kernel` from the committed PMC profile of this bench command
+    (profiles/<round>_pmc.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE, summed over the kernel's
+    launches in a frame); None when no profile is committed."""
+    names = {"composite": "k_composite<false>", "project": "k_project", "sort": "k_radix_"}
+    prof = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc.json")) \
+        if os.path.isdir(os.path.join(ROOT, "profiles")) else []
+    if not prof:
+        return None, None
+    d = json.load(open(os.path.join(ROOT, "profiles", prof[-1])))
+    tot = 0.0
+    for lab, e in d.items():
+        if lab.startswith(names[kernel]) and "traffic_bytes" in e:
+            if kernel == "sort" and not any(lab.startswith("k_radix_%s#%d" % (k, i)) for k in
+                                            ("upsweep", "scan", "downsweep") for i in range(4)):
+                continue  # depth passes only
+            tot += e["traffic_bytes"]
+    return (tot if tot else None), prof[-1]
 
 
 def frame_bytes(n, n_vis, k, W, H):
@@ -152,6 +173,7 @@ def main():
     rows_here = max(0, min(t1 * 16, H) - row0)
     a_bytes = algorithmic_bytes(dom, N, st["n_vis"], st["k_entries"], W, rows_here)
     achieved = a_bytes / (stages[dom] * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dom)
     fb = frame_bytes(N, n_vis_all, k_all, W, H)
 
     if rank == 0:
@@ -182,8 +204,11 @@ def main():
             "chunk_fraction": round(st["chunk_fraction"], 4),
             "tiles_unsaturated": st["tiles_unsaturated"],
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": None,
-                         "algorithmic_bytes_per_launch": int(a_bytes)},
+                         "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4),
+                         "traffic": int(traffic) if traffic else None,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": int(a_bytes),
+                         "per": "frame (the kernel's launches in one frame, HIP events on the render stream)"},
             "frame_roofline": {"bytes": int(fb), "frac": round(fb / (ms * 1e-3) / (world * HBM_PEAK), 4),
                                "compulsory_frac": round((236 * N + 16 * W * H) / (ms * 1e-3) / (world * HBM_PEAK), 4),
                                "formula": "236N + 148N_vis + 48K + 16WH (SURVEY 8d)"},
