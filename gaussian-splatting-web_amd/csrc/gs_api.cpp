@@ -78,9 +78,9 @@ inline uint64_t round_up(uint64_t a, uint64_t b) { return (a + b - 1) / b * b; }
 
 // Per-frame timing events (opts.timing): kernel groups are bracketed directly.
 enum {
-    EV_BEGIN, EV_PROJ0, EV_PROJ1, EV_SORT1,
-    EV_BIN_0, EV_TSORT_0, EV_RANGES_0, EV_COMP_0,
-    EV_BIN_1, EV_TSORT_1, EV_RANGES_1, EV_COMP_1, EV_COUNT
+    EV_BEGIN, EV_PROJ0, EV_PROJ1,
+    EV_DSORT_0, EV_BIN_0, EV_TSORT_0, EV_RANGES_0, EV_COMP_0,
+    EV_DSORT_1, EV_BIN_1, EV_TSORT_1, EV_RANGES_1, EV_COMP_1, EV_END, EV_COUNT
 };
 enum { ST_TOTAL, ST_PROJECT, ST_SORT, ST_BIN, ST_TSORT, ST_RANGES, ST_COMPOSITE, ST_COUNT };
 
@@ -89,7 +89,28 @@ struct FrameEvents {
     bool pending = false;
 };
 
-constexpr float kChunkF0 = 0.35f;  // first chunk fraction before any statistics exist
+constexpr uint32_t kNoSplit = 0xFFFFFFFFu;  // chunk threshold: every visible splat in chunk 0
+
+// Depth keys <-> the float they encode (src/shaders.ts:36-40; monotone in distance along the
+// view axis for both camera conventions).
+float key_to_float(uint32_t k) {
+    const uint32_t fu = (k & 0x80000000u) ? (k ^ 0x80000000u) : (k ^ 0x80000001u);
+    float f;
+    std::memcpy(&f, &fu, 4);
+    return f;
+}
+uint32_t float_to_key(float f) {
+    uint32_t fu;
+    std::memcpy(&fu, &f, 4);
+    return fu ^ ((fu >> 31) ? 0x80000001u : 0x80000000u);
+}
+// Threshold just past key k with its depth scaled by `factor` (> 1: farther).
+uint32_t scaled_threshold(uint32_t k, float factor) {
+    const float v = key_to_float(k) * factor;
+    if (!std::isfinite(v)) return kNoSplit;
+    const uint32_t t = float_to_key(v);
+    return t >= kNoSplit - 1 ? kNoSplit : t + 1;
+}
 
 }  // namespace
 
@@ -114,13 +135,14 @@ struct gs_scene {
     float* planes = nullptr;            // 11 geometry planes
     uint64_t stride = 0;
     float4* shade = nullptr;            // shading blocks
-    // depth sort ping-pong: keys, Gaussian index, packed tile rectangle; project writes keysB/auxB
+    // k_project output (depth key, packed tile rect per Gaussian), then the depth sort ping-pong
+    uint32_t *keysP = nullptr, *rectP = nullptr;
     uint32_t *keysA = nullptr, *valsA = nullptr, *auxA = nullptr;
     uint32_t *keysB = nullptr, *valsB = nullptr, *auxB = nullptr;
     float4* rec = nullptr;              // projected records, 4 float4 per Gaussian
     float4* crec = nullptr;             // composite records, 3 float4 per slot
-    // zero-per-frame block: FrameCtl | digit histograms of the 4 depth passes and of the
-    // 2 tile passes of each chunk (kHistShards x 256 words each)
+    // zero-per-frame block: FrameCtl | digit histograms of the 4 depth + 2 tile passes of each
+    // chunk (kHistShards x 256 words each)
     uint8_t* meta = nullptr;
     FrameCtl* ctl = nullptr;
     uint32_t* hist = nullptr;
@@ -147,13 +169,15 @@ struct gs_scene {
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
     bool have_last = false;
-    float chunk_f = kChunkF0;
+    uint32_t chunk_T = kNoSplit;        // adaptive chunk threshold for the next frame
+    uint32_t full_quant[8] = {};        // quantile keys of the last frame sorted in one chunk
+    bool have_quant = false;
     int last_tiles = 0;                 // tiles of the last frame's strip
     bool have_frame = false;
 };
 
 static constexpr size_t kHistWords = kHistShards * 256;
-static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 8 * kHistWords * 4;
+static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 12 * kHistWords * 4;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
 static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
@@ -231,16 +255,16 @@ static void strip_geometry(int H, int si, int sc, int& tr_begin, int& tr_end, in
 
 static void harvest(gs_ctx* c, FrameEvents& f) {
     if (!f.pending) return;
-    HIPCHK(hipEventSynchronize(f.ev[EV_COMP_1]));
+    HIPCHK(hipEventSynchronize(f.ev[EV_END]));
     auto el = [&](int a, int b) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, f.ev[a], f.ev[b]));
         return (double)ms;
     };
-    c->acc_ms[ST_TOTAL] += el(EV_BEGIN, EV_COMP_1);
+    c->acc_ms[ST_TOTAL] += el(EV_BEGIN, EV_END);
     c->acc_ms[ST_PROJECT] += el(EV_PROJ0, EV_PROJ1);
-    c->acc_ms[ST_SORT] += el(EV_PROJ1, EV_SORT1);
-    c->acc_ms[ST_BIN] += el(EV_SORT1, EV_BIN_0) + el(EV_COMP_0, EV_BIN_1);
+    c->acc_ms[ST_SORT] += el(EV_PROJ1, EV_DSORT_0) + el(EV_COMP_0, EV_DSORT_1);
+    c->acc_ms[ST_BIN] += el(EV_DSORT_0, EV_BIN_0) + el(EV_DSORT_1, EV_BIN_1);
     c->acc_ms[ST_TSORT] += el(EV_BIN_0, EV_TSORT_0) + el(EV_BIN_1, EV_TSORT_1);
     c->acc_ms[ST_RANGES] += el(EV_TSORT_0, EV_RANGES_0) + el(EV_TSORT_1, EV_RANGES_1);
     c->acc_ms[ST_COMPOSITE] += el(EV_RANGES_0, EV_COMP_0) + el(EV_RANGES_1, EV_COMP_1);
@@ -261,28 +285,23 @@ static void collect_stats(gs_scene* s, bool wait) {
         s->last = s->h_ctl[slot];
         s->have_last = true;
         s->stat_pending[slot] = false;
-        // chunk controller: chunk 0 should reach the depth rank at which the tiles saturate
-        // (from the composite: the last slot any tile needed; chunk-0 slots are the depth
-        // ranks with entries, so slot / slots0 * c0 estimates the rank), with a margin for
-        // camera motion; rises at once, decays slowly.  Mostly unsaturated frames use one chunk.
+        // chunk controller: chunk 0 = the splats nearer than 1.15x the depth at which the last
+        // tile saturated (measured by the composite), rising at once, decaying slowly (3 % of
+        // depth per frame); frames where most tiles never saturate use one chunk
         const FrameCtl& l = s->last;
-        const double tiles = std::max(1.0, (double)s->last_tiles);
-        uint32_t sat_slot = 0, sat_tiles = 0;
-        for (int k = 0; k < kHistShards; ++k) {
-            sat_slot = std::max(sat_slot, l.sat_slot[k]);
-            sat_tiles += l.sat_tiles[k];
+        if (l.n_vis > 0 && l.n_chunk[0] == l.n_vis) {  // one-chunk frame: quantiles of every rank
+            std::memcpy(s->full_quant, l.quant_key, sizeof(s->full_quant));
+            s->have_quant = true;
         }
-        float target = 1.0f;
-        if (l.n_vis > 0 && sat_tiles >= 0.5 * tiles) {
-            double rank;
-            if (sat_slot < l.shade_n[0])
-                rank = ((double)sat_slot + 1.0) / std::max(1.0, (double)l.shade_n[0]) * l.c0;
-            else  // a tile saturated in chunk 1: somewhere past c0
-                rank = (double)l.c0 * 1.5;
-            target = (float)std::min(1.0, 1.15 * rank / (double)l.n_vis);
-        }
-        target = std::max(target, 1.0f / 64.0f);
-        s->chunk_f = target >= s->chunk_f ? target : std::max(target, s->chunk_f * 0.95f);
+        uint32_t sat_tiles = 0;
+        for (int k = 0; k < kHistShards; ++k) sat_tiles += l.sat_tiles[k];
+        uint32_t target = kNoSplit;
+        if (l.n_vis > 0 && l.sat_key != 0 && sat_tiles >= 0.5 * std::max(1, s->last_tiles))
+            target = scaled_threshold(l.sat_key, 1.15f);
+        if (target >= s->chunk_T || s->chunk_T == kNoSplit)
+            s->chunk_T = target;
+        else
+            s->chunk_T = std::max(target, scaled_threshold(s->chunk_T, 0.97f));
     }
 }
 
@@ -298,8 +317,18 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     if (s->have_last && s->last.k_total > s->kcap) ensure_tile_capacity(s, s->last.k_total);
     ensure_tiles(s, std::max(n_tiles, 1));
     s->last_tiles = n_tiles;
-    const float f = o.chunk_fraction > 0.0f ? std::min(o.chunk_fraction, 1.0f) : s->chunk_f;
-    const bool two_chunks = f < 1.0f;
+    // chunk threshold: adaptive, one chunk (chunk_fraction >= 1), or a fixed split for tests and
+    // diagnostics (chunk_fraction in (0,1): the depth key at quantile 2^-t <= chunk_fraction of
+    // the last one-chunk frame; one chunk until such a frame exists)
+    uint32_t T = s->chunk_T;
+    if (o.chunk_fraction >= 1.0f) {
+        T = kNoSplit;
+    } else if (o.chunk_fraction > 0.0f) {
+        const int t = std::min(7, std::max(0, (int)std::ceil(-std::log2((double)o.chunk_fraction))));
+        T = s->have_quant ? s->full_quant[t] + 1u : kNoSplit;
+        if (T == 0) T = kNoSplit;
+    }
+    const bool two_chunks = T != kNoSplit;
     if (two_chunks) {
         ensure_state(s, (uint64_t)W * H);
         ensure_sat(s, (size_t)(tr_end - tr_begin + 1) * (TX + 1) + 2 + (size_t)(tr_end - tr_begin) * ((TX + 63) / 64) * 2);
@@ -329,52 +358,62 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.tile_row_begin = tr_begin;
     pp.tile_row_end = tr_end;
     pp.tiles_x = TX;
-    pp.keys_out = s->keysB;
-    pp.rect_out = s->auxB;
+    pp.keys_out = s->keysP;
+    pp.rect_out = s->rectP;
     pp.rec = s->rec;
     pp.ctl = s->ctl;
     mark(EV_PROJ0);
     launch_project(pp, st);
     mark(EV_PROJ1);
 
-    // ---- depth sort: (keysB, index, auxB) over N, sentinels dropped -> A -> B -> A -> B
-    const uint32_t* kin[4] = {s->keysB, s->keysA, s->keysB, s->keysA};
-    const uint32_t* vin[4] = {nullptr, s->valsA, s->valsB, s->valsA};
-    const uint32_t* ain[4] = {s->auxB, s->auxA, s->auxB, s->auxA};
-    uint32_t* kout[4] = {s->keysA, s->keysB, s->keysA, s->keysB};
-    uint32_t* vout[4] = {s->valsA, s->valsB, s->valsA, s->valsB};
-    uint32_t* aout[4] = {s->auxA, s->auxB, s->auxA, s->auxB};
-    for (int ps = 0; ps < 4; ++ps) {
-        SortPass sp{};
-        sp.keys_in = kin[ps];
-        sp.vals_in = vin[ps];
-        sp.aux_in = ain[ps];
-        sp.keys_out = kout[ps];
-        sp.vals_out = vout[ps];
-        sp.aux_out = aout[ps];
-        sp.n = pp.n;
-        sp.n_dev = ps == 0 ? nullptr : &s->ctl->n_vis;
-        sp.parts_max = sort_parts(pp.n);
-        sp.shift = 8 * ps;
-        sp.mask = 255;
-        sp.filter_sentinel = ps == 0;
-        sp.hist = s->hist + ps * kHistWords;
-        sp.offsets = s->radix_offsets;
-        launch_sort_pass(sp, st);
-    }
-    mark(EV_SORT1);
-
-    // ---- chunks: bin -> tile-id sort -> ranges -> composite
+    // ---- per chunk: depth sort of the chunk's splats -> bin -> tile-id sort -> ranges -> composite
     const int tile_passes = n_tiles > 256 ? 2 : 1;
+    const size_t sat_words = (size_t)(tr_end - tr_begin + 1) * (TX + 1);
+    unsigned long long* unsat_mask = (unsigned long long*)(s->sat + ((sat_words + 1) & ~(size_t)1));
     for (int chunk = 0; chunk < 2; ++chunk) {
-        const int eb = chunk == 0 ? EV_BIN_0 : EV_BIN_1;
+        const int eb = chunk == 0 ? EV_DSORT_0 : EV_DSORT_1;
         if (chunk == 1 && !two_chunks) {
-            for (int e = 0; e < 4; ++e) mark(eb + e);
+            for (int e = 0; e < 5; ++e) mark(eb + e);
             break;
         }
+        if (chunk == 1) launch_sat(s->done, TX, tr_end - tr_begin, s->sat, unsat_mask, s->ctl, st);
+        // (keysP, index, rectP) over N; pass 0 keeps this chunk's splats -> A -> B -> A -> B
+        const uint32_t* kin[4] = {s->keysP, s->keysA, s->keysB, s->keysA};
+        const uint32_t* vin[4] = {nullptr, s->valsA, s->valsB, s->valsA};
+        const uint32_t* ain[4] = {s->rectP, s->auxA, s->auxB, s->auxA};
+        uint32_t* kout[4] = {s->keysA, s->keysB, s->keysA, s->keysB};
+        uint32_t* vout[4] = {s->valsA, s->valsB, s->valsA, s->valsB};
+        uint32_t* aout[4] = {s->auxA, s->auxB, s->auxA, s->auxB};
+        for (int ps = 0; ps < 4; ++ps) {
+            SortPass sp{};
+            sp.keys_in = kin[ps];
+            sp.vals_in = vin[ps];
+            sp.aux_in = ain[ps];
+            sp.keys_out = kout[ps];
+            sp.vals_out = vout[ps];
+            sp.aux_out = aout[ps];
+            sp.n = pp.n;
+            sp.n_dev = ps == 0 ? nullptr : &s->ctl->n_chunk[chunk];
+            sp.gate = chunk == 1 ? &s->ctl->not_done : nullptr;  // chunk 1: only with unsaturated tiles
+            sp.parts_max = sort_parts(pp.n);
+            sp.shift = 8 * ps;
+            sp.mask = 255;
+            sp.filter = ps > 0 ? kFiltNone : (chunk == 0 ? kFiltBelow : kFiltTail);
+            sp.thresh = T;
+            sp.count_out = ps == 0 ? &s->ctl->n_chunk[chunk] : nullptr;
+            sp.rec = s->rec;
+            sp.sat = s->sat;
+            sp.tiles_x = TX;
+            sp.tile_row_begin = tr_begin;
+            sp.hist = s->hist + (6 * chunk + ps) * kHistWords;
+            sp.offsets = s->radix_offsets;
+            launch_sort_pass(sp, st);
+        }
+        mark(eb);
         BinParams bp{};
         bp.sorted_vals = s->valsB;
         bp.sorted_rect = s->auxB;
+        bp.sorted_keys = s->keysB;
         bp.rec = s->rec;
         bp.crec = s->crec;
         bp.shade = s->shade;
@@ -384,7 +423,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.done = s->done;
         bp.ctl = s->ctl;
         bp.chunk = chunk;
-        bp.chunk_f = f;
         bp.tile_row_begin = tr_begin;
         bp.tiles_x = TX;
         bp.n_max = std::max<uint32_t>(pp.n, 1);
@@ -394,8 +432,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.tkeys = s->tkA;
         bp.tvals = s->tvA;
         bp.sat = s->sat;
-        const size_t sat_words = (size_t)(tr_end - tr_begin + 1) * (TX + 1);
-        bp.mask = (const unsigned long long*)(s->sat + ((sat_words + 1) & ~(size_t)1));
+        bp.mask = unsat_mask;
         bp.mask_words = (TX + 63) / 64;
         bp.rows = tr_end - tr_begin;
         bp.shade_list = s->shade_list;
@@ -403,10 +440,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.wide_cap = s->wide_cap;
         bp.wide_unit = s->wide_unit;
         bp.wide_unit_cap = s->wide_unit_cap;
-        if (chunk == 1)
-            launch_sat(s->done, TX, tr_end - tr_begin, s->sat, (unsigned long long*)bp.mask, st);
         launch_bin(bp, st);
-        mark(eb);
+        mark(eb + 1);
 
         uint32_t *tk_in = s->tkA, *tv_in = s->tvA, *tk_out = s->tkB, *tv_out = s->tvB;
         for (int ps = 0; ps < tile_passes; ++ps) {
@@ -420,16 +455,16 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.parts_max = sort_parts(s->kcap);
             sp.shift = 8 * ps;
             sp.mask = 255;
-            sp.hist = s->hist + (4 + 2 * chunk + ps) * kHistWords;
+            sp.hist = s->hist + (6 * chunk + 4 + ps) * kHistWords;
             sp.offsets = s->radix_offsets;
             launch_sort_pass(sp, st);
             std::swap(tk_in, tk_out);
             std::swap(tv_in, tv_out);
         }
-        mark(eb + 1);
+        mark(eb + 2);
         HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)std::max(n_tiles, 1) * sizeof(uint2), st));
         launch_ranges(tk_in, &s->ctl->k_chunk[chunk], (uint32_t)s->kcap, s->ranges, st);
-        mark(eb + 2);
+        mark(eb + 3);
 
         CompositeParams cp{};
         cp.ranges = s->ranges;
@@ -449,8 +484,10 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         cp.out = out;
         cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
         launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
-        mark(eb + 3);
+        mark(eb + 4);
     }
+    launch_frame_stats(s->ctl, s->shade_list, s->rec, st);
+    mark(EV_END);
     HIPCHK(hipGetLastError());
     if (timed) {
         fe.pending = true;
@@ -592,6 +629,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             s->stride = round_up(std::max<uint64_t>(n, 1), 64);
             dev_alloc(s->planes, (size_t)11 * s->stride);
             dev_alloc(s->shade, (size_t)shade_quads(n_sh) * std::max<uint64_t>(n, 1));
+            dev_alloc(s->keysP, n); dev_alloc(s->rectP, n);
             dev_alloc(s->keysA, n); dev_alloc(s->valsA, n); dev_alloc(s->auxA, n);
             dev_alloc(s->keysB, n); dev_alloc(s->valsB, n); dev_alloc(s->auxB, n);
             dev_alloc(s->rec, 4 * (size_t)std::max<uint64_t>(n, 1));
@@ -640,6 +678,7 @@ void gs_scene_free(gs_scene* s) {
     }
     dev_free(s->planes);
     dev_free(s->shade);
+    dev_free(s->keysP); dev_free(s->rectP);
     dev_free(s->keysA); dev_free(s->valsA); dev_free(s->auxA);
     dev_free(s->keysB); dev_free(s->valsB); dev_free(s->auxB);
     dev_free(s->rec);
@@ -744,7 +783,7 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
             st.k_chunk1 = l.k_chunk[1];
             st.wide_chunk0 = l.wide_n[0];
             st.wide_chunk1 = l.wide_n[1];
-            st.chunk_fraction = c->last_scene->chunk_f;
+            st.chunk_fraction = l.n_vis ? (float)l.n_chunk[0] / (float)l.n_vis : 0.0f;
         }
         st.frames = (int32_t)c->acc_frames;
         const double k = c->acc_frames ? 1.0 / c->acc_frames : 0.0;

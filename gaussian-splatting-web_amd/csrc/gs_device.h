@@ -22,7 +22,6 @@ constexpr int kHistShards = 8;        // global histograms sharded by blockIdx %
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // key of a culled Gaussian (no visible splat has it)
 constexpr int kRecFloats = 16;        // 64-B projected record
 constexpr int kMaxGrid = 2048;        // persistent grids: 8 workgroups per CU
-constexpr uint32_t kMinChunk0 = 65536;  // smallest first chunk (depth ranks)
 constexpr uint32_t kWideTiles = 32;     // splats binding >= this many tiles are emitted row-wise
 constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
 constexpr int kMaskLdsWords = 2048;     // unsaturated-tile bitmask cached in LDS up to this size
@@ -38,15 +37,17 @@ constexpr uint32_t kErrOverflow = 1u;
 
 struct FrameCtl {                 // zeroed at the start of every frame
     unsigned long long k_total;   // sum of tile counts over visible splats (project)
-    uint32_t n_vis;               // splats reaching the sort (project)
+    uint32_t n_vis;               // visible splats (project)
     uint32_t k_chunk[2];          // (tile, splat) entries per chunk (binning scan)
     uint32_t not_done;            // tiles still accepting splats after chunk 0
     uint32_t err;
     uint32_t wide_n[2];           // wide splats queued per chunk (binning)
     uint32_t wide_rows[2];        // their tile rows (work units of k_bin_wide)
     uint32_t shade_n[2];          // splats queued for colour per chunk (binning)
-    uint32_t c0;                  // depth ranks in chunk 0
-    uint32_t pad0;
+    uint32_t n_chunk[2];          // depth-sorted splats per chunk (count of radix pass 0)
+    uint32_t sat_key;             // depth key of the farthest splat a tile saturated at
+    uint32_t sat_slot_max;        // (k_frame_stats)
+    uint32_t quant_key[8];        // key at rank ceil(n_chunk[0] / 2^t) - 1 of chunk 0, t = 0..7
     uint32_t sat_slot[kHistShards];   // per shard: max composite slot at which a tile saturated
     uint32_t sat_tiles[kHistShards];  // per shard: tiles saturated by the end of the frame
 };
@@ -54,7 +55,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
 // Scene layout in HBM: 11 SoA geometry planes (0-2 position, 3-5 log-free scale, 6-9 rotation,
 // 10 opacity logit; plane p at planes + p * plane_stride) streamed by k_project, and one AoS
 // shading block per Gaussian [x, y, z, sh[k][c] at 3 + 3k + c] padded to shade_q float4s
-// (208 B at SH degree 3), gathered by the binning for the splats that receive tile entries.
+// (208 B at SH degree 3), gathered by k_shade for the splats that receive tile entries.
 __host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
 
 // Projected record, 4 float4 per Gaussian (at its original index, written by k_project):
@@ -81,6 +82,14 @@ struct ProjParams {
     FrameCtl* ctl;
 };
 
+// Element filter of a radix pass (the first pass of a depth chunk decides chunk membership).
+enum RadixFilter {
+    kFiltNone = 0,
+    kFiltSentinel = 1,  // drop culled Gaussians (key == kSentinel)
+    kFiltBelow = 2,     // chunk 0: key < thresh
+    kFiltTail = 3       // chunk 1: thresh <= key < kSentinel and the rect touches an unsaturated tile
+};
+
 struct SortPass {
     const uint32_t* keys_in;
     const uint32_t* vals_in;  // nullptr: values are the element index (first depth pass)
@@ -90,10 +99,17 @@ struct SortPass {
     uint32_t* aux_out;
     uint32_t n;               // element count, or an upper bound when n_dev is set
     const uint32_t* n_dev;    // device-side element count (nullable)
+    const uint32_t* gate;     // optional: the pass is empty when *gate == 0
     uint32_t parts_max;       // sort_parts(upper bound): stride of `offsets`, grid bound
     int shift;
     uint32_t mask;            // digit mask (<= 255)
-    int filter_sentinel;      // 1: drop keys == kSentinel (they carry no digit)
+    int filter;               // RadixFilter
+    uint32_t thresh;          // chunk threshold key (kFiltBelow / kFiltTail)
+    uint32_t* count_out;      // optional: number of elements kept (written by the scan)
+    // kFiltTail: the element's tile rect is aux; wide rects from rec; unsaturated-tile SAT
+    const float4* rec;
+    const uint32_t* sat;
+    int tiles_x, tile_row_begin;
     uint32_t* hist;           // [kHistShards][256] digit histogram of this pass (zeroed; the
                               // upsweep accumulates it, the scan turns it into digit bases)
     uint32_t* offsets;        // [256][parts_max] scratch: partition counts, then offsets
@@ -111,8 +127,7 @@ struct BinParams {
     const uint8_t* done;          // chunk 1: per-tile "saturated after chunk 0"
     FrameCtl* ctl;
     int chunk;                    // 0 or 1
-    float chunk_f;                // chunk 0 = ceil(chunk_f * n_vis) depth ranks (>= kMinChunk0);
-                                  // >= 1: chunk 0 takes every rank
+    const uint32_t* sorted_keys;  // [n_chunk] depth keys in order (chunk 0: quantile keys)
     int tile_row_begin, tiles_x;
     uint32_t n_max;               // upper bound of n_vis (grid / scratch sizing)
     uint32_t capacity;            // entry capacity of out arrays
@@ -159,8 +174,9 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, u
 void launch_project(const ProjParams& p, hipStream_t s);
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);
+void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, const float4* rec, hipStream_t s);
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
-                hipStream_t s);
+                const FrameCtl* ctl, hipStream_t s);
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
                    hipStream_t s);
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);

@@ -303,9 +303,37 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
 //                      partition = (wave, item, lane)), LDS staging, contiguous writes per digit run
 // This replaces webgpu-radix-sort's 16 x 2-bit passes (RS:621-654) with 8-bit digits.
 
-__device__ __forceinline__ uint32_t radix_n(const SortPass& p) { return p.n_dev ? *p.n_dev : p.n; }
-__device__ __forceinline__ bool radix_valid(const SortPass& p, uint32_t n, uint64_t idx, uint32_t key) {
-    return idx < n && !(p.filter_sentinel && key == kSentinel);
+__device__ __forceinline__ uint32_t radix_n(const SortPass& p) {
+    if (p.gate && *p.gate == 0) return 0;
+    return p.n_dev ? *p.n_dev : p.n;
+}
+// kFiltTail: does the element's tile rect (aux; wide rects from the record of Gaussian j) touch
+// a tile chunk 0 left unsaturated?  Summed-area table lookups (L2-resident).
+__device__ __forceinline__ bool tail_overlaps(const SortPass& p, uint32_t pr, uint32_t j) {
+    if (pr == kRectEmpty) return false;
+    uint32_t x0, y0, x1, y1;
+    if (pr == kRectLarge) {
+        const float4 m = p.rec[4 * (uint64_t)j + 3];
+        const uint32_t bx = __float_as_uint(m.z), by = __float_as_uint(m.w);
+        x0 = (bx & 0xffffu) >> 4; y0 = (by & 0xffffu) >> 4; x1 = bx >> 20; y1 = by >> 20;
+    } else {
+        x0 = pr & 0xfffu; y0 = (pr >> 12) & 0xfffu;
+        x1 = x0 + ((pr >> 24) & 15u); y1 = y0 + (pr >> 28);
+    }
+    const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
+    const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
+    const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
+    return (b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]) != 0u;
+}
+
+__device__ __forceinline__ bool radix_valid(const SortPass& p, uint32_t n, uint64_t idx, uint32_t key, uint32_t aux) {
+    if (idx >= n) return false;
+    switch (p.filter) {
+        case kFiltNone: return true;
+        case kFiltSentinel: return key != kSentinel;
+        case kFiltBelow: return key < p.thresh;
+        default: return key >= p.thresh && key != kSentinel && tail_overlaps(p, aux, (uint32_t)idx);
+    }
 }
 
 __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(SortPass p) {
@@ -321,7 +349,8 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(SortPass p) {
         for (int it = 0; it < kSortIPT; ++it) {
             const uint64_t idx = wbase + it * 64 + lane;
             const uint32_t key = idx < n ? p.keys_in[idx] : kSentinel;
-            if (radix_valid(p, n, idx, key)) atomicAdd(&s_hist[w][(key >> p.shift) & p.mask], 1u);
+            const uint32_t aux = (p.filter == kFiltTail && idx < n) ? p.aux_in[idx] : 0u;
+            if (radix_valid(p, n, idx, key, aux)) atomicAdd(&s_hist[w][(key >> p.shift) & p.mask], 1u);
         }
         __syncthreads();
         const uint32_t c = s_hist[0][tid] + s_hist[1][tid] + s_hist[2][tid] + s_hist[3][tid];
@@ -345,6 +374,7 @@ __global__ __launch_bounds__(256) void k_radix_scan(SortPass p) {
     uint32_t gtotal;
     const uint32_t gbase = block_excl_scan256(tot, s_tmp, &gtotal);
     if (tid == d) s_base = gbase;
+    if (d == 0 && tid == 0 && p.count_out) *p.count_out = gtotal;  // elements kept by this pass
     __syncthreads();
     uint32_t* col = p.offsets + (uint64_t)d * p.parts_max;
     const uint32_t per = (parts + 255) / 256;
@@ -385,14 +415,47 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
             keys[it] = in ? p.keys_in[idx] : kSentinel;
             vals[it] = in ? (p.vals_in ? p.vals_in[idx] : (uint32_t)idx) : 0u;
             aux[it] = (in && has_aux) ? p.aux_in[idx] : 0u;
-            rank[it] = radix_valid(p, n, idx, keys[it]) ? 0u : 0x80000000u;  // top bit: unsorted
+            rank[it] = radix_valid(p, n, idx, keys[it], aux[it]) ? 0u : 0x80000000u;  // top bit: unsorted
         }
         __syncthreads();
+        if (p.filter != kFiltNone) {
+            // filtered pass: compact each wave's kept elements, in order, into the front rows of its
+            // slice of the stage (order within the partition is unchanged), so ranking only visits
+            // rows that hold kept elements
+            uint32_t* wk = s_keys + w * (kSortIPT * 64);
+            uint32_t* wv = s_vals + w * (kSortIPT * 64);
+            uint32_t* wa = s_aux + w * (kSortIPT * 64);
+            uint32_t m = 0;
+#pragma unroll
+            for (int it = 0; it < kSortIPT; ++it) {
+                const bool valid = (rank[it] & 0x80000000u) == 0u;
+                const uint64_t b = __ballot(valid);
+                if (valid) {
+                    const uint32_t q = m + __popcll(b & lanemask_lt());
+                    wk[q] = keys[it];
+                    wv[q] = vals[it];
+                    if (has_aux) wa[q] = aux[it];
+                }
+                m += __popcll(b);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < kSortIPT; ++it) {
+                const uint32_t q = it * 64 + lane;
+                const bool valid = q < m;
+                keys[it] = valid ? wk[q] : kSentinel;
+                vals[it] = valid ? wv[q] : 0u;
+                aux[it] = (valid && has_aux) ? wa[q] : 0u;
+                rank[it] = valid ? 0u : 0x80000000u;
+            }
+            __syncthreads();
+        }
 #pragma unroll
         for (int it = 0; it < kSortIPT; ++it) {
             const bool valid = (rank[it] & 0x80000000u) == 0u;
             const uint32_t digit = (keys[it] >> p.shift) & p.mask;
             uint64_t peers = __ballot(valid);
+            if (peers == 0) continue;  // wave-uniform: no kept element in this row
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
                 const bool bit = (digit >> b) & 1u;
@@ -444,23 +507,15 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
 }
 
 // ============================================================================ binning
-// Chunk c covers depth ranks [r0, r1): chunk 0 = the first ceil(f * n_vis) ranks, chunk 1 = the
-// rest, binned only into tiles that were not saturated by chunk 0 (empty when all are).
+// Chunk c is the depth-sorted array of its splats: chunk 0 = visible splats with key < T, chunk 1
+// = those with key >= T whose rect touches a tile chunk 0 left unsaturated (binned into those
+// tiles only).  Concatenated, the two stable sorts are the full stable order.
 // Launches per chunk, no inter-workgroup waiting: per-partition entry counts, one scan, the
 // emission in depth order, then the row-wise emission of wide splats.  Entry positions come from
 // the scan alone, so whichever kernel writes an entry, every tile's list stays in depth order.
 __device__ __forceinline__ void chunk_range(const BinParams& p, uint32_t& r0, uint32_t& r1) {
-    const uint32_t n = p.ctl->n_vis;
-    const uint32_t c0 = p.chunk_f >= 1.0f
-                            ? n
-                            : min(n, max(kMinChunk0, (uint32_t)ceilf(p.chunk_f * (float)n)));
-    if (p.chunk == 0) {
-        r0 = 0;
-        r1 = c0;
-    } else {
-        r0 = c0;
-        r1 = p.ctl->not_done ? n : c0;
-    }
+    r0 = 0;
+    r1 = p.ctl->n_chunk[p.chunk];
 }
 
 struct TileRect {
@@ -605,9 +660,12 @@ __global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
     if (threadIdx.x == 0) {
         p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
         p.ctl->shade_n[p.chunk] = (uint32_t)nsh;
-        if (p.chunk == 0) p.ctl->c0 = r1;
-        if (total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
     }
+    if (p.chunk == 0 && threadIdx.x < 8 && r1 > 0) {  // quantile keys (fixed-fraction chunking)
+        const uint32_t q = (r1 + (1u << threadIdx.x) - 1) >> threadIdx.x;
+        p.ctl->quant_key[threadIdx.x] = p.sorted_keys[q - 1];
+    }
+    if (threadIdx.x == 0 && total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
 }
 
 // Queue a wide splat (composite slot g) for k_bin_wide; false when the queue is full (the caller
@@ -860,12 +918,26 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_wide(BinParams p) {
     }
 }
 
+// End of frame: the depth key of the farthest splat any tile saturated at (chunk controller).
+__global__ __launch_bounds__(64) void k_frame_stats(FrameCtl* ctl, const uint32_t* shade_list,
+                                                    const float4* rec) {
+    if (threadIdx.x != 0) return;
+    uint32_t slot = 0, tiles = 0;
+    for (int k = 0; k < kHistShards; ++k) {
+        slot = max(slot, ctl->sat_slot[k]);
+        tiles += ctl->sat_tiles[k];
+    }
+    ctl->sat_slot_max = slot;
+    ctl->sat_key = tiles ? __float_as_uint(rec[4 * (uint64_t)shade_list[slot] + 3].x) : 0u;
+}
+
 // Summed-area table and bitmask of the tiles chunk 0 left unsaturated (done == 0): one
 // workgroup; row prefixes by waves, then column prefixes by threads, in LDS when the table fits.
 __global__ __launch_bounds__(1024) void k_sat(const uint8_t* __restrict__ done, int tiles_x, int rows,
                                               uint32_t* __restrict__ sat,
-                                              unsigned long long* __restrict__ mask) {
+                                              unsigned long long* __restrict__ mask, const FrameCtl* ctl) {
     __shared__ uint32_t s_sat[kSatMaxWords];
+    if (ctl->not_done == 0) return;  // every tile saturated: chunk 1 is empty and never reads it
     const uint32_t sw = (uint32_t)tiles_x + 1, words = sw * (uint32_t)(rows + 1);
     const int mw = (tiles_x + 63) / 64;
     uint32_t* t = words <= (uint32_t)kSatMaxWords ? s_sat : sat;
@@ -996,14 +1068,18 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
         const float4 A = sA[cur][k];
         const float4 B = sB[cur][k];
         const float4 C = sC[cur][k];
+        // every rounding is spelled out (explicit fma or contraction off), so each inlined copy of
+        // this blend rounds identically and the image cannot depend on where batches split
         const float dx = fx - A.x, dy = fy - A.y;
-        const float u = dx * A.z + dy * A.w;
-        const float v = dx * B.x + dy * B.y;
-        const float qd = u * u + v * v;
+        const float u = __builtin_fmaf(dx, A.z, dy * A.w);
+        const float v = __builtin_fmaf(dx, B.x, dy * B.y);
+        const float qd = __builtin_fmaf(u, u, v * v);
         const float alpha = __builtin_amdgcn_exp2f(B.z - qd);
         const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && alpha >= amin;
         if (FP16_TARGET) {
             if (hit) {
+#pragma clang fp contract(off)
+                // the blend unit: src * (1 - dst.a) + dst, stored as fp16 (as the oracle does it)
                 const float om = 1.0f - ca;
                 cr = (float)(_Float16)((C.x * alpha) * om + cr);
                 cg = (float)(_Float16)((C.y * alpha) * om + cg);
@@ -1013,9 +1089,9 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
             }
         } else {
             const float s = hit ? alpha * T : 0.0f;
-            cr = C.x * s + cr;
-            cg = C.y * s + cg;
-            cb = C.z * s + cb;
+            cr = __builtin_fmaf(C.x, s, cr);
+            cg = __builtin_fmaf(C.y, s, cg);
+            cb = __builtin_fmaf(C.z, s, cb);
             T = T - s;
             live = live && T >= t_min;
         }
@@ -1114,9 +1190,12 @@ void launch_bin(const BinParams& p, hipStream_t s) {
     hipLaunchKernelGGL(k_bin_wide, dim3(kMaxGrid), dim3(kBinThreads), 0, s, p);
     hipLaunchKernelGGL(k_shade, dim3(kMaxGrid), dim3(256), 0, s, p);
 }
+void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, const float4* rec, hipStream_t s) {
+    hipLaunchKernelGGL(k_frame_stats, dim3(1), dim3(64), 0, s, ctl, shade_list, rec);
+}
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
-                hipStream_t s) {
-    hipLaunchKernelGGL(k_sat, dim3(1), dim3(1024), 0, s, done, tiles_x, rows, sat, mask);
+                const FrameCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(k_sat, dim3(1), dim3(1024), 0, s, done, tiles_x, rows, sat, mask, ctl);
 }
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
                    hipStream_t s) {

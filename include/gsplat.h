@@ -77,8 +77,10 @@ typedef struct gs_opts {
     int32_t strip_index;  /* row strip rendered by this call, 0 <= strip_index < strip_count */
     int32_t strip_count;  /* number of equal row strips (16-px tile rows, see gs_strip_rows); 1 = whole image */
     int32_t timing;       /* 1: record per-stage hipEvent timings (gs_timings) */
-    float chunk_fraction; /* depth ranks composited before unsaturated tiles are re-binned: 0 = adaptive,
-                             >= 1 = one pass over every rank.  The image does not depend on it. */
+    float chunk_fraction; /* depth split between the two chunks (the image never depends on it):
+                             0 = adaptive (from the depth at which tiles saturated last frame),
+                             >= 1 = one chunk, (0,1) = fixed split at the depth-rank quantile
+                             2^-t <= chunk_fraction of the last one-chunk frame (tests/diagnostics) */
 } gs_opts;
 
 typedef struct gs_stats {
@@ -87,7 +89,7 @@ typedef struct gs_stats {
     uint64_t k_entries;   /* (tile, splat) pairs binned (both chunks) */
     uint64_t k_total;     /* pairs a single-chunk frame would bin (sum of tile counts, SURVEY's K) */
     uint32_t tiles_unsaturated;  /* tiles chunk 0 left unsaturated */
-    float chunk_fraction; /* adaptive first-chunk fraction after the last frame */
+    float chunk_fraction; /* fraction of the visible splats sorted in chunk 0 (last frame) */
     int32_t tile_row_begin, tile_row_end;  /* tile rows rendered by the last call */
     int32_t tiles_x;
     int32_t frames;       /* timed frames averaged below (opts.timing = 1) since gs_timings_reset */
