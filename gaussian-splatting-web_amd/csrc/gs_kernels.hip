@@ -983,63 +983,74 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tke
 }
 
 // ============================================================================ k_composite
-// Workgroup = one 16x16 tile; wave w owns the 8x8 quarter (w&1, w>>1), lane = one pixel.
-// The tile's depth-ordered list is consumed in batches of 256 splats: every thread gathers one
+// Workgroup = one 16x16 tile, 2 waves; wave h owns the 8-wide column half h, and each lane owns
+// two pixels of one column, 8 rows apart (rows r and r + 8), so every per-splat cost (LDS reads,
+// x terms, loop control) is shared by two pixels and the y-dependent math runs as packed float2.
+// The tile's depth-ordered list is consumed in batches of 128 splats: every thread gathers one
 // 48-B composite record into registers (the next batch is issued before the current one is
-// blended), parks it in a double-buffered LDS stage and marks which quarters its pixel box
-// touches; each wave compacts those marks with ballots into per-quarter index lists (one
-// 64-entry segment per producing wave, so batch order is kept without another barrier).  Each
-// wave then walks only its own quarter's list and stops once its 64 pixels are saturated.
-// Per pixel, fs_main's alpha = saturate(op * exp(-dot(uv,uv))), discarded below 1/255 and
-// outside |u|,|v| <= 2, is blended front to back with the reference's blend state
-// (src/simple_render.ts:169-200, :455-471):
+// blended), parks it in a double-buffered LDS stage and marks which halves its pixel box
+// touches; ballots compact the marks into per-half index lists (one 64-entry segment per
+// producing wave, so batch order is kept without another barrier).  Each wave walks only its
+// half's list and stops once its 128 pixels are saturated.  Per pixel, fs_main's
+// alpha = saturate(op * exp(-dot(uv,uv))), discarded below 1/255 and outside |u|,|v| <= 2, is
+// blended front to back with the reference's blend state (src/simple_render.ts:169-200, :455-471):
 //   FP32        transmittance form: C += col * alpha * T, T *= 1 - alpha; no splat is accepted
 //               once T < t_min;
 //   FP16_TARGET dst = src * (1 - dst.a) + dst rounded to fp16 after every blend (rgba16float).
 // Chunked frames: mode kCompFirst marks saturated tiles done (and writes them out) and parks the
 // per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
+constexpr int kCompBatch = 128;
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 template <bool FP16_TARGET>
-__global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
-    __shared__ float4 sA[2][256];       // cx, cy, a, b
-    __shared__ float4 sB[2][256];       // c, d, log2(op), composite slot (bits)
-    __shared__ float4 sC[2][256];       // r, g, b, (pixel box y)
-    __shared__ uint8_t sL[2][4][256];   // per quarter: batch indices, segment = producing wave
-    __shared__ uint32_t sN[2][4][4];    // per quarter, per producing wave: list length
-    __shared__ uint32_t s_sat;          // slot that saturated the last wave
+__global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
+    __shared__ float4 sA[2][kCompBatch];       // cx, cy, a, b
+    __shared__ float4 sB[2][kCompBatch];       // c, d, log2(op), composite slot (bits)
+    __shared__ float4 sC[2][kCompBatch];       // r, g, b, (pixel box y)
+    __shared__ uint8_t sL[2][2][kCompBatch];   // per half: batch indices, segment = producing wave
+    __shared__ uint32_t sN[2][2][2];           // per half, per producing wave: list length
+    __shared__ uint32_t s_sat;                 // slot that saturated the last wave
     const int tid = threadIdx.x;
     const int tile = blockIdx.x;
     if (p.mode == kCompSecond && p.done[tile]) return;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int h = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
     const int tx0 = tx * kTile, ty0 = ty * kTile;
-    const int px = tx0 + (w & 1) * 8 + (lane & 7), py = ty0 + (w >> 1) * 8 + (lane >> 3);
-    const bool inside = px < p.W && py < p.H;
-    const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+    const int px = tx0 + h * 8 + (lane & 7), py = ty0 + (lane >> 3);  // pixels (px, py), (px, py + 8)
+    const bool in0 = px < p.W && py < p.H, in1 = px < p.W && py + 8 < p.H;
+    const float fx = (float)px + 0.5f;
+    const f2 fy = {(float)py + 0.5f, (float)py + 8.5f};
     const uint2 range = p.ranges[tile];
     const float4* __restrict__ rec = p.rec;
     const uint32_t* __restrict__ tvals = p.tvals;
     const float L = 2.0f * kSqrtLog2e, amin = 1.0f / 255.0f, t_min = p.t_min;
-    const uint64_t pix = (uint64_t)py * p.W + px;  // image-row index (state buffer)
-    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    float T = 1.0f;   // FP32: transmittance
-    float ca = 0.0f;  // FP16_TARGET: dst.a
-    if (p.mode == kCompSecond && inside) {
-        const float4 st = p.state[pix];
-        cr = st.x;
-        cg = st.y;
-        cb = st.z;
-        if (FP16_TARGET) ca = st.w; else T = st.w;
+    const uint64_t pix0 = (uint64_t)py * p.W + px, pix1 = pix0 + 8 * (uint64_t)p.W;  // state index
+    f2 cr = {0.0f, 0.0f}, cg = {0.0f, 0.0f}, cb = {0.0f, 0.0f};
+    f2 T = {1.0f, 1.0f};   // FP32: transmittance
+    f2 ca = {0.0f, 0.0f};  // FP16_TARGET: dst.a
+    if (p.mode == kCompSecond) {
+        if (in0) {
+            const float4 st = p.state[pix0];
+            cr.x = st.x; cg.x = st.y; cb.x = st.z;
+            if (FP16_TARGET) ca.x = st.w; else T.x = st.w;
+        }
+        if (in1) {
+            const float4 st = p.state[pix1];
+            cr.y = st.x; cg.y = st.y; cb.y = st.z;
+            if (FP16_TARGET) ca.y = st.w; else T.y = st.w;
+        }
     }
-    bool live = inside && (FP16_TARGET ? ca < 1.0f : T >= t_min);
-    bool wave_live = __any(live);
+    bool live0 = in0 && (FP16_TARGET ? ca.x < 1.0f : T.x >= t_min);
+    bool live1 = in1 && (FP16_TARGET ? ca.y < 1.0f : T.y >= t_min);
+    bool wave_live = __any(live0 || live1);
 
     const uint32_t n = range.y - range.x;
-    const uint32_t nb = (n + 255) / 256;
+    const uint32_t nb = (n + kCompBatch - 1) / kCompBatch;
     float4 ga, gb, gc;
     uint32_t gs_ = 0;
     bool gv = false;
     auto gather = [&](uint32_t batch) {
-        const uint32_t e = range.x + batch * 256 + tid;
+        const uint32_t e = range.x + batch * kCompBatch + tid;
         gv = e < range.y;
         if (gv) {
             gs_ = tvals[e];
@@ -1053,15 +1064,15 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
         sA[buf][tid] = ga;
         sB[buf][tid] = make_float4(gb.x, gb.y, gb.z, __uint_as_float(gs_));  // box x: used below only
         sC[buf][tid] = gc;
-        const uint32_t bx = __float_as_uint(gb.w), by = __float_as_uint(gc.w);
-        const int x0 = (int)(bx & 0xffffu), x1 = (int)(bx >> 16), y0 = (int)(by & 0xffffu), y1 = (int)(by >> 16);
+        const uint32_t bx = __float_as_uint(gb.w);
+        const int x0 = (int)(bx & 0xffffu), x1 = (int)(bx >> 16);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int qx = tx0 + (q & 1) * 8, qy = ty0 + (q >> 1) * 8;
-            const bool hit = gv && x0 <= qx + 7 && x1 >= qx && y0 <= qy + 7 && y1 >= qy;
+        for (int q = 0; q < 2; ++q) {
+            const int qx = tx0 + q * 8;
+            const bool hit = gv && x0 <= qx + 7 && x1 >= qx;
             const uint64_t b = __ballot(hit);
-            if (hit) sL[buf][q][w * 64 + __popcll(b & lanemask_lt())] = (uint8_t)tid;
-            if (lane == 0) sN[buf][q][w] = (uint32_t)__popcll(b);
+            if (hit) sL[buf][q][h * 64 + __popcll(b & lanemask_lt())] = (uint8_t)tid;
+            if (lane == 0) sN[buf][q][h] = (uint32_t)__popcll(b);
         }
     };
     auto blend = [&](int k, int cur) {
@@ -1070,30 +1081,42 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
         const float4 C = sC[cur][k];
         // every rounding is spelled out (explicit fma or contraction off), so each inlined copy of
         // this blend rounds identically and the image cannot depend on where batches split
-        const float dx = fx - A.x, dy = fy - A.y;
-        const float u = __builtin_fmaf(dx, A.z, dy * A.w);
-        const float v = __builtin_fmaf(dx, B.x, dy * B.y);
-        const float qd = __builtin_fmaf(u, u, v * v);
-        const float alpha = __builtin_amdgcn_exp2f(B.z - qd);
-        const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && alpha >= amin;
+        const float dx = fx - A.x;
+        const f2 dy = fy - A.y;
+        const f2 u = __builtin_elementwise_fma(dy, (f2)A.w, (f2)(dx * A.z));
+        const f2 v = __builtin_elementwise_fma(dy, (f2)B.y, (f2)(dx * B.x));
+        const f2 qd = __builtin_elementwise_fma(u, u, v * v);
+        const f2 e = (f2)B.z - qd;
+        const float a0 = __builtin_amdgcn_exp2f(e.x), a1 = __builtin_amdgcn_exp2f(e.y);
+        const bool hit0 = live0 && fmaxf(fabsf(u.x), fabsf(v.x)) <= L && a0 >= amin;
+        const bool hit1 = live1 && fmaxf(fabsf(u.y), fabsf(v.y)) <= L && a1 >= amin;
         if (FP16_TARGET) {
-            if (hit) {
 #pragma clang fp contract(off)
-                // the blend unit: src * (1 - dst.a) + dst, stored as fp16 (as the oracle does it)
-                const float om = 1.0f - ca;
-                cr = (float)(_Float16)((C.x * alpha) * om + cr);
-                cg = (float)(_Float16)((C.y * alpha) * om + cg);
-                cb = (float)(_Float16)((C.z * alpha) * om + cb);
-                ca = (float)(_Float16)(alpha * om + ca);
-                live = ca < 1.0f;  // dst.a == 1: later blends add exactly zero
+            // the blend unit: src * (1 - dst.a) + dst, stored as fp16 (as the oracle does it)
+            if (hit0) {
+                const float om = 1.0f - ca.x;
+                cr.x = (float)(_Float16)((C.x * a0) * om + cr.x);
+                cg.x = (float)(_Float16)((C.y * a0) * om + cg.x);
+                cb.x = (float)(_Float16)((C.z * a0) * om + cb.x);
+                ca.x = (float)(_Float16)(a0 * om + ca.x);
+                live0 = ca.x < 1.0f;  // dst.a == 1: later blends add exactly zero
+            }
+            if (hit1) {
+                const float om = 1.0f - ca.y;
+                cr.y = (float)(_Float16)((C.x * a1) * om + cr.y);
+                cg.y = (float)(_Float16)((C.y * a1) * om + cg.y);
+                cb.y = (float)(_Float16)((C.z * a1) * om + cb.y);
+                ca.y = (float)(_Float16)(a1 * om + ca.y);
+                live1 = ca.y < 1.0f;
             }
         } else {
-            const float s = hit ? alpha * T : 0.0f;
-            cr = __builtin_fmaf(C.x, s, cr);
-            cg = __builtin_fmaf(C.y, s, cg);
-            cb = __builtin_fmaf(C.z, s, cb);
-            T = T - s;
-            live = live && T >= t_min;
+            const f2 s2 = {hit0 ? a0 * T.x : 0.0f, hit1 ? a1 * T.y : 0.0f};
+            cr = __builtin_elementwise_fma((f2)C.x, s2, cr);
+            cg = __builtin_elementwise_fma((f2)C.y, s2, cg);
+            cb = __builtin_elementwise_fma((f2)C.z, s2, cb);
+            T = T - s2;
+            live0 = live0 && T.x >= t_min;
+            live1 = live1 && T.y >= t_min;
         }
     };
     if (tid == 0) s_sat = 0;
@@ -1106,15 +1129,15 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
         const int cur = b & 1;
         if (b + 1 < nb) gather(b + 1);  // in flight while this batch is blended
         if (wave_live) {
-            for (int seg = 0; seg < 4 && wave_live; ++seg) {
-                const int cnt = (int)sN[cur][w][seg];
-                const uint8_t* list = &sL[cur][w][seg * 64];
+            for (int seg = 0; seg < 2 && wave_live; ++seg) {
+                const int cnt = (int)sN[cur][h][seg];
+                const uint8_t* list = &sL[cur][h][seg * 64];
                 int k = 0;
                 for (; k + 1 < cnt; k += 2) {
                     const int i0 = list[k], i1 = list[k + 1];
                     blend(i0, cur);
                     blend(i1, cur);
-                    if (!__any(live)) {
+                    if (!__any(live0 || live1)) {
                         wave_live = false;
                         if (lane == 0) atomicMax(&s_sat, __float_as_uint(sB[cur][i1].w));
                         break;
@@ -1122,7 +1145,7 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
                 }
                 if (wave_live && k < cnt) {
                     blend(list[k], cur);
-                    if (!__any(live)) {
+                    if (!__any(live0 || live1)) {
                         wave_live = false;
                         if (lane == 0) atomicMax(&s_sat, __float_as_uint(sB[cur][list[k]].w));
                     }
@@ -1132,14 +1155,15 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
         if (b + 1 < nb) park(cur ^ 1);
         if (__syncthreads_count(wave_live) == 0) break;
     }
-    const bool tile_done = __syncthreads_count(live) == 0;
+    const bool tile_done = __syncthreads_count(live0 || live1) == 0;
     if (tile_done && tid == 0 && n > 0) {  // saturation statistics for the chunk controller
         atomicAdd(&p.ctl->sat_tiles[tile % kHistShards], 1u);
         atomicMax(&p.ctl->sat_slot[tile % kHistShards], s_sat);
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {  // park the pixels for chunk 1
-            if (inside) p.state[pix] = make_float4(cr, cg, cb, FP16_TARGET ? ca : T);
+            if (in0) p.state[pix0] = make_float4(cr.x, cg.x, cb.x, FP16_TARGET ? ca.x : T.x);
+            if (in1) p.state[pix1] = make_float4(cr.y, cg.y, cb.y, FP16_TARGET ? ca.y : T.y);
             if (tid == 0) {
                 p.done[tile] = 0;
                 atomicAdd(&p.ctl->not_done, 1u);
@@ -1148,16 +1172,15 @@ __global__ __launch_bounds__(256) void k_composite(CompositeParams p) {
         }
         if (tid == 0) p.done[tile] = 1;
     }
-    if (inside) {
-        if (!FP16_TARGET) ca = 1.0f - T;
-        const uint64_t o = (uint64_t)(py - p.row0) * p.W + px;
-        if (p.out_f16) {
-            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-            h4 h = {(_Float16)cr, (_Float16)cg, (_Float16)cb, (_Float16)ca};
-            ((h4*)p.out)[o] = h;
-        } else {
-            ((float4*)p.out)[o] = make_float4(cr, cg, cb, ca);
-        }
+    if (!FP16_TARGET) ca = (f2)1.0f - T;
+    const uint64_t o0 = (uint64_t)(py - p.row0) * p.W + px, o1 = o0 + 8 * (uint64_t)p.W;
+    if (p.out_f16) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        if (in0) ((h4*)p.out)[o0] = h4{(_Float16)cr.x, (_Float16)cg.x, (_Float16)cb.x, (_Float16)ca.x};
+        if (in1) ((h4*)p.out)[o1] = h4{(_Float16)cr.y, (_Float16)cg.y, (_Float16)cb.y, (_Float16)ca.y};
+    } else {
+        if (in0) ((float4*)p.out)[o0] = make_float4(cr.x, cg.x, cb.x, ca.x);
+        if (in1) ((float4*)p.out)[o1] = make_float4(cr.y, cg.y, cb.y, ca.y);
     }
 }
 
@@ -1205,9 +1228,9 @@ void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max,
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;
     if (accum_fp16)
-        hipLaunchKernelGGL(k_composite<true>, dim3(p.n_tiles), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(k_composite<true>, dim3(p.n_tiles), dim3(128), 0, s, p);
     else
-        hipLaunchKernelGGL(k_composite<false>, dim3(p.n_tiles), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(k_composite<false>, dim3(p.n_tiles), dim3(128), 0, s, p);
 }
 
 }  // namespace gs
