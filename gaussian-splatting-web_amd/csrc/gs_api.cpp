@@ -134,12 +134,13 @@ struct gs_scene {
     int n_sh = 0;
     float* planes = nullptr;            // 11 geometry planes
     uint64_t stride = 0;
-    float4* shade = nullptr;            // shading blocks
+    float4* shade = nullptr;            // shading blocks (shade_stride float4 per Gaussian)
+    float4* r01 = nullptr;              // projected records (see gs_device.h)
+    float4* r2 = nullptr;
     // k_project output (depth key, packed tile rect per Gaussian), then the depth sort ping-pong
     uint32_t *keysP = nullptr, *rectP = nullptr;
     uint32_t *keysA = nullptr, *valsA = nullptr, *auxA = nullptr;
     uint32_t *keysB = nullptr, *valsB = nullptr, *auxB = nullptr;
-    float4* rec = nullptr;              // projected records, 4 float4 per Gaussian
     float4* crec = nullptr;             // composite records, 3 float4 per slot
     // zero-per-frame block: FrameCtl | digit histograms of the 4 depth + 2 tile passes of each
     // chunk (kHistShards x 256 words each)
@@ -179,6 +180,8 @@ struct gs_scene {
 static constexpr size_t kHistWords = kHistShards * 256;
 static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 12 * kHistWords * 4;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
+
+static Records records(gs_scene* s) { return Records{s->r01, s->r2}; }
 
 static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
     if (k <= s->kcap && s->tkA) return;
@@ -360,7 +363,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.tiles_x = TX;
     pp.keys_out = s->keysP;
     pp.rect_out = s->rectP;
-    pp.rec = s->rec;
+    pp.rec = records(s);
     pp.ctl = s->ctl;
     mark(EV_PROJ0);
     launch_project(pp, st);
@@ -401,7 +404,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.filter = ps > 0 ? kFiltNone : (chunk == 0 ? kFiltBelow : kFiltTail);
             sp.thresh = T;
             sp.count_out = ps == 0 ? &s->ctl->n_chunk[chunk] : nullptr;
-            sp.rec = s->rec;
+            sp.rec = records(s);
             sp.sat = s->sat;
             sp.tiles_x = TX;
             sp.tile_row_begin = tr_begin;
@@ -414,10 +417,10 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.sorted_vals = s->valsB;
         bp.sorted_rect = s->auxB;
         bp.sorted_keys = s->keysB;
-        bp.rec = s->rec;
-        bp.crec = s->crec;
+        bp.rec = records(s);
         bp.shade = s->shade;
-        bp.shade_q = shade_quads(s->n_sh);
+        bp.shade_stride = shade_stride(s->n_sh);
+        bp.crec = s->crec;
         bp.n_sh = s->n_sh;
         std::memcpy(bp.cam, uni + 32, 12);
         bp.done = s->done;
@@ -441,6 +444,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.wide_unit = s->wide_unit;
         bp.wide_unit_cap = s->wide_unit_cap;
         launch_bin(bp, st);
+        // colour in the same stream: overlapping k_shade with the tile-id sort on a second stream
+        // was measured slower (both are memory-bound and contend)
+        launch_shade(bp, st);
         mark(eb + 1);
 
         uint32_t *tk_in = s->tkA, *tv_in = s->tvA, *tk_out = s->tkB, *tv_out = s->tvB;
@@ -486,7 +492,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
         mark(eb + 4);
     }
-    launch_frame_stats(s->ctl, s->shade_list, s->rec, st);
+    launch_frame_stats(s->ctl, s->shade_list, records(s), st);
     mark(EV_END);
     HIPCHK(hipGetLastError());
     if (timed) {
@@ -628,11 +634,12 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
         try {
             s->stride = round_up(std::max<uint64_t>(n, 1), 64);
             dev_alloc(s->planes, (size_t)11 * s->stride);
-            dev_alloc(s->shade, (size_t)shade_quads(n_sh) * std::max<uint64_t>(n, 1));
+            dev_alloc(s->shade, (size_t)shade_stride(n_sh) * std::max<uint64_t>(n, 1));
+            dev_alloc(s->r01, 2 * (size_t)std::max<uint64_t>(n, 1));
+            dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->keysP, n); dev_alloc(s->rectP, n);
             dev_alloc(s->keysA, n); dev_alloc(s->valsA, n); dev_alloc(s->auxA, n);
             dev_alloc(s->keysB, n); dev_alloc(s->valsB, n); dev_alloc(s->auxB, n);
-            dev_alloc(s->rec, 4 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->crec, 3 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->meta, kMetaBytes);
             s->ctl = (FrameCtl*)(s->meta + kMetaCtl);
@@ -651,7 +658,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 const uint64_t m = std::min(chunk, n - i0);
                 HIPCHK(hipMemcpyAsync(tmp, (const uint8_t*)aos + i0 * rb, m * rb, hipMemcpyHostToDevice,
                                       c->stream));
-                launch_transpose(tmp, m, n_sh, s->planes + i0, s->stride, s->shade + i0 * shade_quads(n_sh),
+                launch_transpose(tmp, m, n_sh, s->planes + i0, s->stride, s->shade + i0 * shade_stride(n_sh),
                                  c->stream);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipStreamSynchronize(c->stream));
@@ -678,10 +685,11 @@ void gs_scene_free(gs_scene* s) {
     }
     dev_free(s->planes);
     dev_free(s->shade);
+    dev_free(s->r01);
+    dev_free(s->r2);
     dev_free(s->keysP); dev_free(s->rectP);
     dev_free(s->keysA); dev_free(s->valsA); dev_free(s->auxA);
     dev_free(s->keysB); dev_free(s->valsB); dev_free(s->auxB);
-    dev_free(s->rec);
     dev_free(s->crec);
     dev_free(s->meta);
     dev_free(s->bin_part);
@@ -876,7 +884,16 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipStreamSynchronize(c->stream));
         const uint64_t m = std::min(cap, s->n);
-        if (m) HIPCHK(hipMemcpy(out16, s->rec, m * 64, hipMemcpyDeviceToHost));
+        if (m) {  // r01 -> words [0, 8); r2 -> words [12, 16); colour below
+            std::vector<float> a((size_t)m * 8), b((size_t)m * 4);
+            HIPCHK(hipMemcpy(a.data(), s->r01, a.size() * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(b.data(), s->r2, b.size() * 4, hipMemcpyDeviceToHost));
+            for (uint64_t j = 0; j < m; ++j) {
+                std::memcpy(out16 + 16 * j, &a[8 * j], 32);
+                std::memset(out16 + 16 * j + 8, 0, 16);
+                std::memcpy(out16 + 16 * j + 12, &b[4 * j], 16);
+            }
+        }
         // colour words [8, 12): from the composite record of each binned splat
         collect_stats(s, true);
         const uint64_t slots = (uint64_t)s->last.shade_n[0] + s->last.shade_n[1];

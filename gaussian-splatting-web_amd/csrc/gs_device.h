@@ -53,19 +53,27 @@ struct FrameCtl {                 // zeroed at the start of every frame
 };
 
 // Scene layout in HBM: 11 SoA geometry planes (0-2 position, 3-5 log-free scale, 6-9 rotation,
-// 10 opacity logit; plane p at planes + p * plane_stride) streamed by k_project, and one AoS
-// shading block per Gaussian [x, y, z, sh[k][c] at 3 + 3k + c] padded to shade_q float4s
-// (208 B at SH degree 3), gathered by k_shade for the splats that receive tile entries.
-__host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
-
-// Projected record, 4 float4 per Gaussian (at its original index, written by k_project):
-//   [0] cx, cy, e1x', e1y'      centre (pixels); quad axes e/|e|^2 * sqrt(log2 e)
-//   [1] e2x', e2y', log2(op), pixel box x (x0 | x1 << 16, u32 bits)
-//   [2] (unused)
-//   [3] depth key, tile count, pixel box x, pixel box y (u32 bits)
+// 10 opacity logit; plane p at planes + p * plane_stride) streamed by k_project, and one
+// shading block per Gaussian [x, y, z, sh[k][c] at 3 + 3k + c] of shade_stride float4 (a power
+// of two, so a block never straddles more 128-B lines than it must; 256 B at SH degree 3).
+// The frame's projected record of Gaussian j (k_project, dense arrays indexed by j):
+//   r01[2j]     cx, cy, e1x', e1y'      centre (pixels); quad axes e/|e|^2 * sqrt(log2 e)
+//   r01[2j+1]   e2x', e2y', log2(op), pixel box x (x0 | x1 << 16, u32 bits)
+//   r2[j]       depth key, tile count, pixel box x, pixel box y (u32 bits)
 // Composite record, 3 float4 per binned splat at its slot g (depth-rank order of the splats
 // that received entries; written by k_shade; the tile lists hold g):
-//   [0] = record [0], [1] = record [1], [2] r, g, b, pixel box y
+//   [0] = r01[2j], [1] = r01[2j+1], [2] r, g, b, 0
+__host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
+__host__ __device__ inline uint32_t shade_stride(int n_sh) {
+    const uint32_t q = shade_quads(n_sh);
+    return q <= 2 ? 2 : q <= 4 ? 4 : q <= 8 ? 8 : 16;
+}
+
+struct Records {
+    float4* r01;
+    float4* r2;
+};
+
 struct ProjParams {
     const float* planes;
     uint64_t plane_stride;
@@ -78,7 +86,7 @@ struct ProjParams {
     int tile_row_begin, tile_row_end, tiles_x;
     uint32_t* keys_out;       // [n]: depth key or kSentinel
     uint32_t* rect_out;       // [n]: packed tile rectangle
-    float4* rec;              // [n][4]: projected records
+    Records rec;              // out: the projected record of every visible Gaussian
     FrameCtl* ctl;
 };
 
@@ -106,8 +114,8 @@ struct SortPass {
     int filter;               // RadixFilter
     uint32_t thresh;          // chunk threshold key (kFiltBelow / kFiltTail)
     uint32_t* count_out;      // optional: number of elements kept (written by the scan)
-    // kFiltTail: the element's tile rect is aux; wide rects from rec; unsaturated-tile SAT
-    const float4* rec;
+    // kFiltTail: the element's tile rect is aux; wide rects from the record; unsaturated-tile SAT
+    Records rec;
     const uint32_t* sat;
     int tiles_x, tile_row_begin;
     uint32_t* hist;           // [kHistShards][256] digit histogram of this pass (zeroed; the
@@ -118,10 +126,10 @@ struct SortPass {
 struct BinParams {
     const uint32_t* sorted_vals;  // [n_vis] Gaussian index in depth order
     const uint32_t* sorted_rect;  // [n_vis] packed tile rectangle in depth order
-    const float4* rec;            // records (rectangles of kRectLarge splats; k_shade input)
+    Records rec;                  // projected records (k_shade input, wide rects)
+    const float4* shade;          // shading blocks
+    uint32_t shade_stride;        // float4 per block
     float4* crec;                 // out: composite records, 3 float4 per slot
-    const float4* shade;          // shading blocks (shade_q float4 per Gaussian)
-    uint32_t shade_q;
     int n_sh;
     float cam[3];
     const uint8_t* done;          // chunk 1: per-tile "saturated after chunk 0"
@@ -173,8 +181,9 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, u
                       float4* shade, hipStream_t s);
 void launch_project(const ProjParams& p, hipStream_t s);
 void launch_sort_pass(const SortPass& p, hipStream_t s);
-void launch_bin(const BinParams& p, hipStream_t s);
-void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, const float4* rec, hipStream_t s);
+void launch_bin(const BinParams& p, hipStream_t s);    // count, scan, emit, wide rows
+void launch_shade(const BinParams& p, hipStream_t s);  // composite records of the chunk's slots
+void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, Records rec, hipStream_t s);
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s);
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ a
         if (k < n_sh)
 #pragma unroll
             for (int c = 0; c < 3; ++c) v[3 + 3 * k + c] = r[16 + 4 * k + c];
-    float4* o = shade + i * q;
+    float4* o = shade + i * shade_stride(n_sh);
 #pragma unroll
     for (uint32_t t = 0; t < 13; ++t)
         if (t < q) o[t] = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
@@ -273,11 +273,11 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
             // alpha = op * exp(-(u^2+v^2)) = exp2(log2(op) - (u'^2+v'^2))
             const float k1 = kSqrtLog2e / (f.e1x * f.e1x + f.e1y * f.e1y);
             const float k2 = kSqrtLog2e / (f.e2x * f.e2x + f.e2y * f.e2y);
-            float4* r = p.rec + 4 * (uint64_t)i;
+            float4* r = p.rec.r01 + 2 * (uint64_t)i;
             r[0] = make_float4(f.cx, f.cy, f.e1x * k1, f.e1y * k1);
             r[1] = make_float4(f.e2x * k2, f.e2y * k2, log2f(op), __uint_as_float(bbx));
-            r[3] = make_float4(__uint_as_float(key), __uint_as_float(ntiles), __uint_as_float(bbx),
-                               __uint_as_float(bby));
+            p.rec.r2[i] = make_float4(__uint_as_float(key), __uint_as_float(ntiles), __uint_as_float(bbx),
+                                      __uint_as_float(bby));
             ++my_vis;
             my_k += ntiles;
         }
@@ -313,7 +313,7 @@ __device__ __forceinline__ bool tail_overlaps(const SortPass& p, uint32_t pr, ui
     if (pr == kRectEmpty) return false;
     uint32_t x0, y0, x1, y1;
     if (pr == kRectLarge) {
-        const float4 m = p.rec[4 * (uint64_t)j + 3];
+        const float4 m = p.rec.r2[j];
         const uint32_t bx = __float_as_uint(m.z), by = __float_as_uint(m.w);
         x0 = (bx & 0xffffu) >> 4; y0 = (by & 0xffffu) >> 4; x1 = bx >> 20; y1 = by >> 20;
     } else {
@@ -525,7 +525,7 @@ struct TileRect {
 __device__ __forceinline__ bool rect_unpack(const BinParams& p, uint32_t pr, uint32_t j, TileRect& r) {
     if (pr == kRectEmpty) return false;
     if (pr == kRectLarge) {  // tile box from the pixel box in the record
-        const float4 m = p.rec[4 * (uint64_t)j + 3];
+        const float4 m = p.rec.r2[j];
         const uint32_t bx = __float_as_uint(m.z), by = __float_as_uint(m.w);
         r = {(bx & 0xffffu) >> 4, (by & 0xffffu) >> 4, bx >> 20, by >> 20};
     } else {
@@ -789,14 +789,14 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
 
 // Composite records of this chunk's slots: colour (src/simple_render.ts:26-66, :321-322:
 // dir = normalize(p - camPos), SH to degree 3, + 0.5, max(., 0)) plus the footprint words of the
-// projected record, written densely at the slot.  16 lanes per splat: lanes 0-12 load the
-// shading block (one coalesced 208-B read), lanes 13-15 the record words; each lane evaluates
-// its own coefficients' terms and the group sums them with xor shuffles.
+// projected record, written densely at the slot.  16 lanes per splat: lanes 0-12 read the
+// line-aligned shading block (one coalesced load), lanes 14-15 the 32-B record quads; each lane
+// evaluates its own coefficients' terms and the group sums them with xor shuffles.
 __global__ __launch_bounds__(256) void k_shade(BinParams p) {
     const uint32_t g0 = p.chunk ? p.ctl->shade_n[0] : 0u;
     const uint32_t n = p.ctl->shade_n[p.chunk];
     const uint32_t lane = lane_id(), l = lane & 15;
-    const uint32_t nq = p.shade_q, ncoef = 3 * (uint32_t)p.n_sh;
+    const uint32_t nq = shade_quads(p.n_sh), ncoef = 3 * (uint32_t)p.n_sh;
     const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
     for (uint32_t base = wave * 4; base < n; base += nwaves * 4) {  // wave-uniform: shuffles below
         const uint32_t gi = base + (lane >> 4);
@@ -804,9 +804,9 @@ __global__ __launch_bounds__(256) void k_shade(BinParams p) {
         const uint32_t slot = g0 + gi;
         const uint32_t j = active ? p.shade_list[slot] : 0u;
         float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (active) {
-            if (l < nq) q = p.shade[(uint64_t)j * nq + l];
-            else if (l >= 13) q = p.rec[4 * (uint64_t)j + (l == 15 ? 3 : l - 13)];
+        if (active) {  // lanes 0..nq-1: the shading block; lanes 14, 15: record quads r01
+            if (l < nq) q = p.shade[(uint64_t)j * p.shade_stride + l];
+            else if (l >= 14) q = p.rec.r01[2 * (uint64_t)j + (l - 14)];
         }
         const uint32_t gl = lane & ~15u;
         const float px = __shfl(q.x, gl, 64), py = __shfl(q.y, gl, 64), pz = __shfl(q.z, gl, 64);
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(256) void k_shade(BinParams p) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const uint32_t i = 4 * l + t;  // float index in the block: 3 + 3k + c
-            if (l >= 13 || i < 3 || i >= 3 + ncoef) continue;
+            if (l >= nq || i < 3 || i >= 3 + ncoef) continue;
             const uint32_t k = (i - 3) / 3, c = (i - 3) % 3;
             float b;
             switch (k) {
@@ -851,12 +851,11 @@ __global__ __launch_bounds__(256) void k_shade(BinParams p) {
             acc1 += __shfl_xor(acc1, d, 64);
             acc2 += __shfl_xor(acc2, d, 64);
         }
-        const float by = __shfl(q.w, gl + 15, 64);  // record word [3].w = pixel box y
         if (active) {
             float4* o = p.crec + 3 * (uint64_t)slot;
-            if (l == 13 || l == 14) o[l - 13] = q;
+            if (l >= 14) o[l - 14] = q;
             if (l == 0)
-                o[2] = make_float4(fmaxf(acc0 + 0.5f, 0.0f), fmaxf(acc1 + 0.5f, 0.0f), fmaxf(acc2 + 0.5f, 0.0f), by);
+                o[2] = make_float4(fmaxf(acc0 + 0.5f, 0.0f), fmaxf(acc1 + 0.5f, 0.0f), fmaxf(acc2 + 0.5f, 0.0f), 0.0f);
         }
     }
 }
@@ -920,7 +919,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_wide(BinParams p) {
 
 // End of frame: the depth key of the farthest splat any tile saturated at (chunk controller).
 __global__ __launch_bounds__(64) void k_frame_stats(FrameCtl* ctl, const uint32_t* shade_list,
-                                                    const float4* rec) {
+                                                    Records rec) {
     if (threadIdx.x != 0) return;
     uint32_t slot = 0, tiles = 0;
     for (int k = 0; k < kHistShards; ++k) {
@@ -928,7 +927,7 @@ __global__ __launch_bounds__(64) void k_frame_stats(FrameCtl* ctl, const uint32_
         tiles += ctl->sat_tiles[k];
     }
     ctl->sat_slot_max = slot;
-    ctl->sat_key = tiles ? __float_as_uint(rec[4 * (uint64_t)shade_list[slot] + 3].x) : 0u;
+    ctl->sat_key = tiles ? __float_as_uint(rec.r2[shade_list[slot]].x) : 0u;
 }
 
 // Summed-area table and bitmask of the tiles chunk 0 left unsaturated (done == 0): one
@@ -1006,7 +1005,7 @@ template <bool FP16_TARGET>
 __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     __shared__ float4 sA[2][kCompBatch];       // cx, cy, a, b
     __shared__ float4 sB[2][kCompBatch];       // c, d, log2(op), composite slot (bits)
-    __shared__ float4 sC[2][kCompBatch];       // r, g, b, (pixel box y)
+    __shared__ float4 sC[2][kCompBatch];       // r, g, b, -
     __shared__ uint8_t sL[2][2][kCompBatch];   // per half: batch indices, segment = producing wave
     __shared__ uint32_t sN[2][2][2];           // per half, per producing wave: list length
     __shared__ uint32_t s_sat;                 // slot that saturated the last wave
@@ -1211,9 +1210,11 @@ void launch_bin(const BinParams& p, hipStream_t s) {
     hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, p);
     hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);
     hipLaunchKernelGGL(k_bin_wide, dim3(kMaxGrid), dim3(kBinThreads), 0, s, p);
+}
+void launch_shade(const BinParams& p, hipStream_t s) {
     hipLaunchKernelGGL(k_shade, dim3(kMaxGrid), dim3(256), 0, s, p);
 }
-void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, const float4* rec, hipStream_t s) {
+void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, Records rec, hipStream_t s) {
     hipLaunchKernelGGL(k_frame_stats, dim3(1), dim3(64), 0, s, ctl, shade_list, rec);
 }
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,

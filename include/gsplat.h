@@ -163,10 +163,9 @@ int gs_debug_last_order(gs_ctx* ctx, gs_scene* scene, uint32_t* out_keys, uint32
                         uint64_t capacity, uint64_t* out_n);
 /* Projected record of every Gaussian in the last frame, 16 floats each: centre cx, cy (pixels);
  * quad axes e1/|e1|^2 and e2/|e2|^2 scaled by sqrt(log2 e) (2 floats each); log2(opacity);
- * pixel box x [x0|x1<<16] (u32 bits); colour r, g, b; pixel box y [y0|y1<<16]; depth key; tile
- * count; pixel box x, y again.  The colour is evaluated only for splats that received a tile
- * entry (tile count > 0 and inside the chunks binned this frame); rows of culled Gaussians and
- * the colour of unbinned splats are undefined. */
+ * pixel box x [x0|x1<<16] (u32 bits); colour r, g, b; 0; depth key; tile count; pixel box x, y
+ * (u32 bits).  The colour is evaluated only for splats that received a tile entry this frame;
+ * rows of culled Gaussians and the colour of unbinned splats are undefined. */
 int gs_debug_last_records(gs_ctx* ctx, gs_scene* scene, float* out16, uint64_t capacity);
 
 #ifdef __cplusplus
