@@ -166,6 +166,8 @@ struct gs_scene {
     // asynchronous frame statistics (chunk controller, capacity)
     FrameCtl* h_ctl = nullptr;  // pinned, 2 slots
     hipEvent_t stat_ev[2] = {};
+    uint32_t* h_not_done = nullptr;  // pinned: chunk 0's unsaturated-tile count, read mid-frame
+    hipEvent_t mid_ev = nullptr;
     bool stat_pending[2] = {};
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
@@ -375,7 +377,15 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     unsigned long long* unsat_mask = (unsigned long long*)(s->sat + ((sat_words + 1) & ~(size_t)1));
     for (int chunk = 0; chunk < 2; ++chunk) {
         const int eb = chunk == 0 ? EV_DSORT_0 : EV_DSORT_1;
-        if (chunk == 1 && !two_chunks) {
+        if (chunk == 1 && two_chunks) {
+            // chunk 1 only when chunk 0 left a tile unsaturated: read that count back (4 B, pinned)
+            // and decide here.  Enqueued but empty, chunk 1's ~26 launches cost ~0.13 ms of GPU
+            // time; this costs one short wait for chunk 0 (host run-ahead is lost for it).
+            HIPCHK(hipMemcpyAsync(s->h_not_done, &s->ctl->not_done, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipEventRecord(s->mid_ev, st));
+            HIPCHK(hipEventSynchronize(s->mid_ev));
+        }
+        if (chunk == 1 && (!two_chunks || *s->h_not_done == 0)) {
             for (int e = 0; e < 5; ++e) mark(eb + e);
             break;
         }
@@ -647,6 +657,8 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->bin_part, 2 * ((size_t)bin_parts(n) + 1));
             dev_alloc(s->shade_list, (size_t)n);
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hipHostMallocDefault));
+            HIPCHK(hipHostMalloc((void**)&s->h_not_done, 64, hipHostMallocDefault));
+            HIPCHK(hipEventCreateWithFlags(&s->mid_ev, hipEventDisableTiming));
             for (auto& e : s->stat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             ensure_tile_capacity(s, 4 * n + (1u << 20));
             // AoS -> SoA on device, in chunks of 4M records
@@ -705,6 +717,8 @@ void gs_scene_free(gs_scene* s) {
     for (auto& e : s->stat_ev)
         if (e) (void)hipEventDestroy(e);
     if (s->h_ctl) (void)hipHostFree(s->h_ctl);
+    if (s->h_not_done) (void)hipHostFree(s->h_not_done);
+    if (s->mid_ev) (void)hipEventDestroy(s->mid_ev);
     delete s;
 }
 
