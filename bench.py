@@ -102,8 +102,9 @@ def main():
             sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (args.gpus, args.gpus))
     W, H, N = args.width, args.height, args.n
 
+    launched = "WORLD_SIZE" in os.environ  # torch.distributed.run: the RCCL path, even at N = 1
     dist = None
-    if world > 1:
+    if launched:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
@@ -117,7 +118,7 @@ def main():
     row0, rows_padded, t0, t1 = strip_geometry(H, rank, world)
     opts = gs.make_opts(strip_index=rank, strip_count=world, timing=1)
     strip_bytes = rows_padded * W * 16
-    if world > 1:
+    if launched:
         import torch
         stream = torch.cuda.current_stream()
         strip = torch.empty((rows_padded, W, 4), dtype=torch.float32, device="cuda")
@@ -151,7 +152,7 @@ def main():
     sync()
     elapsed = time.perf_counter() - t_start
     st = ctx.timings()
-    if world > 1:
+    if launched:
         import torch
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

@@ -74,7 +74,6 @@ void dev_free(T*& p) {
     p = nullptr;
 }
 
-inline uint64_t round_up(uint64_t a, uint64_t b) { return (a + b - 1) / b * b; }
 
 // Per-frame timing events (opts.timing): kernel groups are bracketed directly.
 enum {
@@ -132,9 +131,9 @@ struct gs_scene {
     gs_ctx* ctx = nullptr;
     uint64_t n = 0;
     int n_sh = 0;
-    float* planes = nullptr;            // 11 geometry planes
-    uint64_t stride = 0;
+    float4* geo = nullptr;              // geometry records (3 float4 per Gaussian)
     float4* shade = nullptr;            // shading blocks (shade_stride float4 per Gaussian)
+    float4* cull = nullptr;             // cull planes (two-phase projection)
     float4* r01 = nullptr;              // projected records (see gs_device.h)
     float4* r2 = nullptr;
     // k_project output (depth key, packed tile rect per Gaussian), then the depth sort ping-pong
@@ -149,6 +148,7 @@ struct gs_scene {
     uint32_t* hist = nullptr;
     uint32_t* bin_part = nullptr;       // bin_parts(N) + 1
     uint32_t* shade_list = nullptr;     // N: Gaussian index of each composite slot
+    uint32_t* part_count = nullptr;     // sort_parts(N): chunk-0 splats per projection partition
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tkA = nullptr, *tvA = nullptr, *tkB = nullptr, *tvB = nullptr;
@@ -350,14 +350,21 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
 
     HIPCHK(hipMemsetAsync(s->meta, 0, kMetaBytes, st));
     ProjParams pp{};
-    pp.planes = s->planes;
-    pp.plane_stride = s->stride;
+    pp.geo = s->geo;
+    pp.cull = s->cull;
     pp.n = n_tiles > 0 ? (uint32_t)s->n : 0u;
     std::memcpy(pp.V, uni + 0, 64);
     mat4_mul_ref(uni + 16, uni + 0, pp.PV);
     pp.scale_mod = uni[39];
     pp.P00 = uni[16];
     pp.P11 = uni[21];
+    pp.focal = (float)W * pp.P00 / 2.0f;
+    {
+        double f2 = 0;
+        for (int c = 0; c < 3; ++c)
+            for (int r = 0; r < 3; ++r) f2 += (double)uni[4 * c + r] * uni[4 * c + r];
+        pp.w3_fro2 = (float)(f2 * 1.0001);
+    }
     pp.W = W;
     pp.H = H;
     pp.tile_row_begin = tr_begin;
@@ -367,8 +374,19 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.rect_out = s->rectP;
     pp.rec = records(s);
     pp.ctl = s->ctl;
+    pp.thresh = T;  // first depth pass of chunk 0 fused into the projection
+    pp.c_keys = s->keysB;
+    pp.c_vals = s->valsB;
+    pp.c_rect = s->auxB;
+    pp.c_count = s->part_count;
+    pp.offsets = s->radix_offsets;
+    pp.parts_max = sort_parts(pp.n);
+    pp.hist0 = s->hist;
     mark(EV_PROJ0);
-    launch_project(pp, st);
+    // two-phase projection (cull planes first) when most Gaussians are outside this frame's
+    // rows: row strips, or a previous frame that saw under half of the scene
+    const bool two_phase = sc > 1 || (s->have_last && s->last.n_vis * 2 < s->n);
+    launch_project(pp, two_phase, st);
     mark(EV_PROJ1);
 
     // ---- per chunk: depth sort of the chunk's splats -> bin -> tile-id sort -> ranges -> composite
@@ -390,10 +408,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             break;
         }
         if (chunk == 1) launch_sat(s->done, TX, tr_end - tr_begin, s->sat, unsat_mask, s->ctl, st);
-        // (keysP, index, rectP) over N; pass 0 keeps this chunk's splats -> A -> B -> A -> B
-        const uint32_t* kin[4] = {s->keysP, s->keysA, s->keysB, s->keysA};
-        const uint32_t* vin[4] = {nullptr, s->valsA, s->valsB, s->valsA};
-        const uint32_t* ain[4] = {s->rectP, s->auxA, s->auxB, s->auxA};
+        // chunk 0: k_project compacted its splats per partition into B (and did the first upsweep);
+        // chunk 1: (keysP, index, rectP) over N, filtered by pass 0.  -> A -> B -> A -> B
+        const uint32_t* kin[4] = {chunk ? s->keysP : s->keysB, s->keysA, s->keysB, s->keysA};
+        const uint32_t* vin[4] = {chunk ? nullptr : s->valsB, s->valsA, s->valsB, s->valsA};
+        const uint32_t* ain[4] = {chunk ? s->rectP : s->auxB, s->auxA, s->auxB, s->auxA};
         uint32_t* kout[4] = {s->keysA, s->keysB, s->keysA, s->keysB};
         uint32_t* vout[4] = {s->valsA, s->valsB, s->valsA, s->valsB};
         uint32_t* aout[4] = {s->auxA, s->auxB, s->auxA, s->auxB};
@@ -411,7 +430,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.parts_max = sort_parts(pp.n);
             sp.shift = 8 * ps;
             sp.mask = 255;
-            sp.filter = ps > 0 ? kFiltNone : (chunk == 0 ? kFiltBelow : kFiltTail);
+            sp.filter = (ps == 0 && chunk == 1) ? kFiltTail : kFiltNone;
+            sp.part_count = (ps == 0 && chunk == 0) ? s->part_count : nullptr;
             sp.thresh = T;
             sp.count_out = ps == 0 ? &s->ctl->n_chunk[chunk] : nullptr;
             sp.rec = records(s);
@@ -642,9 +662,9 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
         s->n = n;
         s->n_sh = n_sh;
         try {
-            s->stride = round_up(std::max<uint64_t>(n, 1), 64);
-            dev_alloc(s->planes, (size_t)11 * s->stride);
+            dev_alloc(s->geo, 3 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->shade, (size_t)shade_stride(n_sh) * std::max<uint64_t>(n, 1));
+            dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->r01, 2 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->keysP, n); dev_alloc(s->rectP, n);
@@ -656,6 +676,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             s->hist = (uint32_t*)(s->meta + kMetaHist);
             dev_alloc(s->bin_part, 2 * ((size_t)bin_parts(n) + 1));
             dev_alloc(s->shade_list, (size_t)n);
+            dev_alloc(s->part_count, (size_t)sort_parts(n) + 1);
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hipHostMallocDefault));
             HIPCHK(hipHostMalloc((void**)&s->h_not_done, 64, hipHostMallocDefault));
             HIPCHK(hipEventCreateWithFlags(&s->mid_ev, hipEventDisableTiming));
@@ -670,7 +691,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 const uint64_t m = std::min(chunk, n - i0);
                 HIPCHK(hipMemcpyAsync(tmp, (const uint8_t*)aos + i0 * rb, m * rb, hipMemcpyHostToDevice,
                                       c->stream));
-                launch_transpose(tmp, m, n_sh, s->planes + i0, s->stride, s->shade + i0 * shade_stride(n_sh),
+                launch_transpose(tmp, m, n_sh, s->geo + 3 * i0, s->shade + i0 * shade_stride(n_sh), s->cull + i0,
                                  c->stream);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipStreamSynchronize(c->stream));
@@ -695,8 +716,9 @@ void gs_scene_free(gs_scene* s) {
         v.erase(std::remove(v.begin(), v.end(), s), v.end());
         if (s->ctx->last_scene == s) s->ctx->last_scene = nullptr;
     }
-    dev_free(s->planes);
+    dev_free(s->geo);
     dev_free(s->shade);
+    dev_free(s->cull);
     dev_free(s->r01);
     dev_free(s->r2);
     dev_free(s->keysP); dev_free(s->rectP);
@@ -706,6 +728,7 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->meta);
     dev_free(s->bin_part);
     dev_free(s->shade_list);
+    dev_free(s->part_count);
     dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB);
     dev_free(s->radix_offsets);
     dev_free(s->ranges);

@@ -11,7 +11,7 @@
 namespace gs {
 
 constexpr int kTile = 16;             // 16x16-pixel composite tile
-constexpr int kProjThreads = 256;
+constexpr int kProjThreads = 256;  // = kSortThreads: k_project works on radix partitions
 constexpr int kSortThreads = 256;     // 4 waves
 constexpr int kSortIPT = 16;          // items per thread
 constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per radix partition
@@ -52,8 +52,9 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t sat_tiles[kHistShards];  // per shard: tiles saturated by the end of the frame
 };
 
-// Scene layout in HBM: 11 SoA geometry planes (0-2 position, 3-5 log-free scale, 6-9 rotation,
-// 10 opacity logit; plane p at planes + p * plane_stride) streamed by k_project, and one
+// Scene layout in HBM: a 48-B geometry record per Gaussian (3 float4: x, y, z, opacity logit |
+// scale xyz, rot.x | rot.y, rot.z, rot.w, 0) read by k_project (streamed, or gathered for the
+// survivors of the cull), a 16-B cull plane (x, y, z, ||R(q) diag(s)||_F^2), and one
 // shading block per Gaussian [x, y, z, sh[k][c] at 3 + 3k + c] of shade_stride float4 (a power
 // of two, so a block never straddles more 128-B lines than it must; 256 B at SH degree 3).
 // The frame's projected record of Gaussian j (k_project, dense arrays indexed by j):
@@ -75,19 +76,30 @@ struct Records {
 };
 
 struct ProjParams {
-    const float* planes;
-    uint64_t plane_stride;
+    const float4* geo;        // [n][3] geometry records
+    const float4* cull;       // [n] cull planes (x, y, z, ||R(q) diag(s)||_F^2), two-phase frames
     uint32_t n;
     float V[16];              // view, column-major
     float PV[16];             // proj * view (host-computed in the reference's order)
     float scale_mod;
     float P00, P11;
+    float focal;              // W * P00 / 2 (src/simple_render.ts:273)
+    float w3_fro2;            // ||W3||_F^2 of the view's 3x3 block (conservative cull bound)
     int W, H;
     int tile_row_begin, tile_row_end, tiles_x;
     uint32_t* keys_out;       // [n]: depth key or kSentinel
     uint32_t* rect_out;       // [n]: packed tile rectangle
     Records rec;              // out: the projected record of every visible Gaussian
     FrameCtl* ctl;
+    // first depth pass of chunk 0, fused (per kSortTile partition of the Gaussians):
+    uint32_t thresh;          // chunk-0 threshold key
+    uint32_t* c_keys;         // out: chunk-0 keys, Gaussian index, tile rect, compacted in index
+    uint32_t* c_vals;         //      order to the front of each partition
+    uint32_t* c_rect;
+    uint32_t* c_count;        // out: [parts] chunk-0 elements per partition
+    uint32_t* offsets;        // out: [256][parts_max] digit-0 counts per partition
+    uint32_t parts_max;
+    uint32_t* hist0;          // out: [kHistShards][256] digit-0 histogram (zeroed)
 };
 
 // Element filter of a radix pass (the first pass of a depth chunk decides chunk membership).
@@ -108,6 +120,8 @@ struct SortPass {
     uint32_t n;               // element count, or an upper bound when n_dev is set
     const uint32_t* n_dev;    // device-side element count (nullable)
     const uint32_t* gate;     // optional: the pass is empty when *gate == 0
+    const uint32_t* part_count;  // optional: partition p holds part_count[p] elements at its front
+                                 // (input compacted by k_project; the upsweep is skipped)
     uint32_t parts_max;       // sort_parts(upper bound): stride of `offsets`, grid bound
     int shift;
     uint32_t mask;            // digit mask (<= 255)
@@ -177,9 +191,9 @@ struct CompositeParams {
 };
 
 // launchers (gs_kernels.hip)
-void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, uint64_t stride,
-                      float4* shade, hipStream_t s);
-void launch_project(const ProjParams& p, hipStream_t s);
+void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, float4* shade, float4* cull,
+                      hipStream_t s);
+void launch_project(const ProjParams& p, bool two_phase, hipStream_t s);
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, scan, emit, wide rows
 void launch_shade(const BinParams& p, hipStream_t s);  // composite records of the chunk's slots

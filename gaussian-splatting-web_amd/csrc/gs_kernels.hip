@@ -1,6 +1,7 @@
 // gs_kernels.hip — CDNA4 (gfx950) kernels of the splat forward path.
 //
-//   k_transpose   scene upload: reference AoS record (src/ply.ts:249-257) -> SoA planes
+//   k_transpose   scene upload: reference AoS record (src/ply.ts:249-257) -> geometry records,
+//                 shading blocks and cull planes
 //   k_project     per Gaussian: depth key (src/shaders.ts:36-68) + vs_points projection
 //                 (src/simple_render.ts:217-332) + tile rectangle; one streaming pass over the
 //                 geometry planes (colour is deferred to the binning).
@@ -61,23 +62,28 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp
 
 // ============================================================================ k_transpose
 __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ aos, uint64_t n,
-                                                   int n_sh, float* __restrict__ planes,
-                                                   uint64_t stride, float4* __restrict__ shade) {
+                                                   int n_sh, float4* __restrict__ geo,
+                                                   float4* __restrict__ shade,
+                                                   float4* __restrict__ cull) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float* r = (const float*)(aos + i * (uint64_t)(64 + 16 * n_sh));
     // src/ply.ts:249-257 record: pos[0:3] | scale[4:7] | rot[8:12] | opacity[12] | sh[k] at 16+4k
-    planes[0 * stride + i] = r[0];
-    planes[1 * stride + i] = r[1];
-    planes[2 * stride + i] = r[2];
-    planes[3 * stride + i] = r[4];
-    planes[4 * stride + i] = r[5];
-    planes[5 * stride + i] = r[6];
-    planes[6 * stride + i] = r[8];
-    planes[7 * stride + i] = r[9];
-    planes[8 * stride + i] = r[10];
-    planes[9 * stride + i] = r[11];
-    planes[10 * stride + i] = r[12];
+    geo[3 * i + 0] = make_float4(r[0], r[1], r[2], r[12]);  // position, opacity logit
+    geo[3 * i + 1] = make_float4(r[4], r[5], r[6], r[8]);   // scale, rot.x
+    geo[3 * i + 2] = make_float4(r[9], r[10], r[11], 0.0f); // rot.y, rot.z, rot.w
+    {  // cull plane: position and ||R(q) diag(s)||_F^2 (k_project's conservative bound)
+        const float qx = r[8], qy = r[9], qz = r[10], qw = r[11];
+        const float r00 = 1.0f - 2.0f * (qy * qy + qz * qz), r01 = 2.0f * (qx * qy - qw * qz),
+                    r02 = 2.0f * (qx * qz + qw * qy), r10 = 2.0f * (qx * qy + qw * qz),
+                    r11 = 1.0f - 2.0f * (qx * qx + qz * qz), r12 = 2.0f * (qy * qz - qw * qx),
+                    r20 = 2.0f * (qx * qz - qw * qy), r21 = 2.0f * (qy * qz + qw * qx),
+                    r22 = 1.0f - 2.0f * (qx * qx + qy * qy);
+        const float t = (r00 * r00 + r10 * r10 + r20 * r20) * r[4] * r[4] +
+                        (r01 * r01 + r11 * r11 + r21 * r21) * r[5] * r[5] +
+                        (r02 * r02 + r12 * r12 + r22 * r22) * r[6] * r[6];
+        cull[i] = make_float4(r[0], r[1], r[2], t * 1.0001f);
+    }
     const uint32_t q = shade_quads(n_sh);
     float v[4 * 13];
 #pragma unroll
@@ -201,25 +207,75 @@ __device__ __forceinline__ bool pixel_rect(float cx, float cy, float hx, float h
     return (xl <= xh) && (yl <= yh);
 }
 
-__global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
-    __shared__ unsigned long long s_k;
-    __shared__ uint32_t s_vis;
-    if (threadIdx.x == 0) { s_k = 0; s_vis = 0; }
-    __syncthreads();
+// The same conservative cull from the Gaussian's cull plane (x, y, z, ||R(q) diag(s)||_F^2),
+// written at upload: false = provably invisible in this strip.
+__device__ __forceinline__ bool cull_keep(const ProjParams& p, float4 c, int row_lo, int row_hi) {
+#pragma clang fp contract(off)
+    const float x = c.x, y = c.y, z = c.z;
+    const float vz0 = ((p.V[2] * x + p.V[6] * y) + p.V[10] * z) + p.V[14] * 1.0f;
+    const float cw = ((p.PV[3] * x + p.PV[7] * y) + p.PV[11] * z) + p.PV[15] * 1.0f;
+    const float cz = ((p.PV[2] * x + p.PV[6] * y) + p.PV[10] * z) + p.PV[14] * 1.0f;
+    if (!((cw > 0.0f) && (cz >= 0.0f) && (cz <= cw))) return false;  // :230 + near/far (exact)
+    const float cxc = ((p.PV[0] * x + p.PV[4] * y) + p.PV[8] * z) + p.PV[12];
+    const float cyc = ((p.PV[1] * x + p.PV[5] * y) + p.PV[9] * z) + p.PV[13];
+    const float a = p.focal / vz0;
+    const float trs = c.w * p.scale_mod * p.scale_mod;
+    const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w3_fro2 * trs + 0.6f)), 0.45f) * 1.02f + 2.0f;
+    const float cx0 = (cxc / cw + 1.0f) * (float)p.W * 0.5f;
+    const float cy0 = (1.0f - cyc / cw) * (float)p.H * 0.5f;
+    return !(cy0 + hb < (float)row_lo - 1.0f || cy0 - hb > (float)row_hi + 1.0f || cx0 + hb < -1.0f ||
+             cx0 - hb > (float)p.W);
+}
 
-    const uint64_t S = p.plane_stride;
-    const float* __restrict__ P = p.planes;
-    uint32_t my_vis = 0;
-    unsigned long long my_k = 0;
-    const int row_lo = p.tile_row_begin * kTile;
-    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+// One Gaussian: cull, footprint, depth key, tile rect and projected record; returns the depth key
+// (kSentinel when invisible).
+__device__ __forceinline__ uint32_t project_one(const ProjParams& p, uint32_t i, int row_lo, int row_hi,
+                                                uint32_t& my_vis, unsigned long long& my_k, bool cull) {
+    const float4 g0 = p.geo[3 * (uint64_t)i], g1 = p.geo[3 * (uint64_t)i + 1], g2 = p.geo[3 * (uint64_t)i + 2];
+        const float x = g0.x, y = g0.y, z = g0.z;
+        const float sx = g1.x, sy = g1.y, sz = g1.z;
+        const float qx = g1.w, qy = g2.x, qz = g2.y, qw = g2.z;
 
-    for (uint32_t i = blockIdx.x * kProjThreads + threadIdx.x; i < p.n;
-         i += gridDim.x * kProjThreads) {
-        const float x = P[0 * S + i], y = P[1 * S + i], z = P[2 * S + i];
-        const float sx = P[3 * S + i], sy = P[4 * S + i], sz = P[5 * S + i];
-        const float qx = P[6 * S + i], qy = P[7 * S + i], qz = P[8 * S + i], qw = P[9 * S + i];
-        const float logit = P[10 * S + i];
+        // Cheap conservative cull (a row strip, or off screen): bound the quad's half extent by
+        //   2 (s1 + s2) <= 4 max(sqrt(2 (d1 + d2)), 0.45),  d1 + d2 = C00 + C11 + 0.6,
+        //   C00 + C11 <= (focal/vz)^2 ||W3||_F^2 ||R(q) diag(s mod)||_F^2
+        // (lambda1 <= trace of the PSD 2-D covariance; C = a^2 (W3 Sigma W3^T)[0:2,0:2]) and skip
+        // the full projection when that box misses the strip; only provably invisible Gaussians
+        // are skipped, so the visible set is unchanged (a NaN bound never culls).
+        bool pre = true;
+        if (cull) {
+#pragma clang fp contract(off)
+            // clip z, w exactly as project_footprint rounds them: the near/far test is the real one
+            const float vz0 = ((p.V[2] * x + p.V[6] * y) + p.V[10] * z) + p.V[14] * 1.0f;
+            const float cw = ((p.PV[3] * x + p.PV[7] * y) + p.PV[11] * z) + p.PV[15] * 1.0f;
+            const float cz = ((p.PV[2] * x + p.PV[6] * y) + p.PV[10] * z) + p.PV[14] * 1.0f;
+            const float cxc = ((p.PV[0] * x + p.PV[4] * y) + p.PV[8] * z) + p.PV[12];
+            const float cyc = ((p.PV[1] * x + p.PV[5] * y) + p.PV[9] * z) + p.PV[13];
+            const float r00 = 1.0f - 2.0f * (qy * qy + qz * qz), r01 = 2.0f * (qx * qy - qw * qz),
+                        r02 = 2.0f * (qx * qz + qw * qy), r10 = 2.0f * (qx * qy + qw * qz),
+                        r11 = 1.0f - 2.0f * (qx * qx + qz * qz), r12 = 2.0f * (qy * qz - qw * qx),
+                        r20 = 2.0f * (qx * qz - qw * qy), r21 = 2.0f * (qy * qz + qw * qx),
+                        r22 = 1.0f - 2.0f * (qx * qx + qy * qy);
+            const float msx = sx * p.scale_mod, msy = sy * p.scale_mod, msz = sz * p.scale_mod;
+            const float trs = (r00 * r00 + r10 * r10 + r20 * r20) * msx * msx +
+                              (r01 * r01 + r11 * r11 + r21 * r21) * msy * msy +
+                              (r02 * r02 + r12 * r12 + r22 * r22) * msz * msz;
+            const float a = p.focal / vz0;
+            const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w3_fro2 * trs + 0.6f)), 0.45f) * 1.02f + 2.0f;
+            const float cx0 = (cxc / cw + 1.0f) * (float)p.W * 0.5f;
+            const float cy0 = (1.0f - cyc / cw) * (float)p.H * 0.5f;
+            if (!((cw > 0.0f) && (cz >= 0.0f) && (cz <= cw)))  // :230 + near/far: dropped anyway
+                pre = false;
+            else if (cy0 + hb < (float)row_lo - 1.0f || cy0 - hb > (float)row_hi + 1.0f ||
+                     cx0 + hb < -1.0f || cx0 - hb > (float)p.W)
+                pre = false;
+        }
+        if (!pre) {
+            p.keys_out[i] = kSentinel;
+            p.rect_out[i] = kRectEmpty;
+            return kSentinel;
+        }
+        const float logit = g0.w;
 
         float vz;
         float4 clip;
@@ -283,13 +339,106 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
         }
         p.keys_out[i] = key;
         p.rect_out[i] = prect;
+        return key;
+}
+
+// Per 4096-Gaussian partition (the radix partition of the first depth pass): project every
+// Gaussian, then do the first pass's upsweep here: the digit-0 histogram of the chunk-0 splats
+// (visible, key < thresh) and their order-preserving compaction to the front of the partition
+// in the pass-0 input arrays, so that pass reads only them.
+// TWO_PHASE (row strips, mostly off-screen frames): phase A reads only the 16-B cull planes and
+// keeps an order-preserving list of the survivors in LDS; phase B projects the survivors densely,
+// so culled Gaussians cost neither their 44 B nor divergent lanes.
+template <bool TWO_PHASE>
+__global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
+    __shared__ unsigned long long s_k;
+    __shared__ uint32_t s_vis;
+    __shared__ uint32_t s_hist[256];
+    __shared__ unsigned long long s_mask[kSortIPT][kProjThreads / 64];
+    __shared__ uint32_t s_base[kSortIPT][kProjThreads / 64];
+    __shared__ uint32_t s_total;
+    __shared__ uint16_t s_list[TWO_PHASE ? kSortTile : 1];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    if (tid == 0) { s_k = 0; s_vis = 0; }
+    uint32_t my_vis = 0;
+    unsigned long long my_k = 0;
+    const int row_lo = p.tile_row_begin * kTile;
+    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+    const uint32_t parts = sort_parts(p.n);
+    // exclusive prefix of the 16 x 4 (round, wave) ballots in s_mask: element order = index order
+    auto prefix = [&]() {
+        __syncthreads();
+        if (tid < 64) {
+            const uint32_t c = __popcll(s_mask[tid >> 2][tid & 3]);
+            const uint32_t incl = wave_incl_scan(c);
+            s_base[tid >> 2][tid & 3] = incl - c;
+            if (tid == 63) s_total = incl;
+        }
+        __syncthreads();
+    };
+    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+        const uint32_t p0 = part * kSortTile;
+        s_hist[tid] = 0;
+        uint32_t nitems = min((uint32_t)kSortTile, p.n - p0);
+        if (TWO_PHASE) {
+            for (int it = 0; it < kSortIPT; ++it) {
+                const uint32_t i = p0 + it * kProjThreads + tid;
+                bool keep = false;
+                if (i < p.n) {
+                    keep = cull_keep(p, p.cull[i], row_lo, row_hi);
+                    if (!keep) {
+                        p.keys_out[i] = kSentinel;
+                        p.rect_out[i] = kRectEmpty;
+                    }
+                }
+                const uint64_t b = __ballot(keep);
+                if (lane == 0) s_mask[it][w] = b;
+            }
+            prefix();
+            for (int it = 0; it < kSortIPT; ++it) {
+                const uint64_t b = s_mask[it][w];
+                if ((b >> lane) & 1ull) s_list[s_base[it][w] + __popcll(b & lanemask_lt())] = (uint16_t)(it * kProjThreads + tid);
+            }
+            nitems = s_total;
+            __syncthreads();
+        } else {
+            __syncthreads();
+        }
+        auto item = [&](uint32_t q) { return p0 + (TWO_PHASE ? (uint32_t)s_list[q] : q); };
+        const uint32_t rounds = (nitems + kProjThreads - 1) / kProjThreads;
+        for (uint32_t r = 0; r < (uint32_t)kSortIPT; ++r) {
+            bool keep = false;
+            const uint32_t q = r * kProjThreads + tid;
+            if (r < rounds && q < nitems) {
+                const uint32_t key = project_one(p, item(q), row_lo, row_hi, my_vis, my_k, !TWO_PHASE);
+                keep = key < p.thresh;  // kSentinel >= any threshold
+                if (keep) atomicAdd(&s_hist[key & 255u], 1u);
+            }
+            const uint64_t b = __ballot(keep);
+            if (lane == 0) s_mask[r][w] = b;
+        }
+        prefix();
+        for (uint32_t r = 0; r < rounds; ++r) {
+            const uint64_t b = s_mask[r][w];
+            if ((b >> lane) & 1ull) {
+                const uint32_t i = item(r * kProjThreads + tid);
+                const uint32_t pos = p0 + s_base[r][w] + __popcll(b & lanemask_lt());
+                p.c_keys[pos] = p.keys_out[i];  // this thread's own stores above
+                p.c_vals[pos] = i;
+                p.c_rect[pos] = p.rect_out[i];
+            }
+        }
+        p.offsets[(uint64_t)tid * p.parts_max + part] = s_hist[tid];  // digit-major, as the upsweep
+        if (s_hist[tid]) atomicAdd(&p.hist0[(part % kHistShards) * 256 + tid], s_hist[tid]);
+        if (tid == 0) p.c_count[part] = s_total;
+        __syncthreads();
     }
     if (my_vis) {
         atomicAdd(&s_vis, my_vis);
         atomicAdd(&s_k, my_k);
     }
     __syncthreads();
-    if (threadIdx.x == 0 && s_vis) {
+    if (tid == 0 && s_vis) {
         atomicAdd(&p.ctl->n_vis, s_vis);
         atomicAdd(&p.ctl->k_total, s_k);
     }
@@ -406,16 +555,18 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
         for (int t = tid; t < 1024; t += kSortThreads) (&s_wave_hist[0][0])[t] = 0;
         s_global[tid] = p.offsets[(uint64_t)tid * p.parts_max + part];
         const uint64_t wbase = (uint64_t)part * kSortTile + (uint64_t)w * (kSortIPT * 64);
+        // compacted input (k_project): only the partition's first part_count[part] elements exist
+        const uint64_t pend = (uint64_t)part * kSortTile + (p.part_count ? p.part_count[part] : (uint32_t)kSortTile);
 
         uint32_t keys[kSortIPT], vals[kSortIPT], aux[kSortIPT], rank[kSortIPT];
 #pragma unroll
         for (int it = 0; it < kSortIPT; ++it) {
             const uint64_t idx = wbase + it * 64 + lane;
-            const bool in = idx < n;
+            const bool in = idx < n && idx < pend;
             keys[it] = in ? p.keys_in[idx] : kSentinel;
             vals[it] = in ? (p.vals_in ? p.vals_in[idx] : (uint32_t)idx) : 0u;
             aux[it] = (in && has_aux) ? p.aux_in[idx] : 0u;
-            rank[it] = radix_valid(p, n, idx, keys[it], aux[it]) ? 0u : 0x80000000u;  // top bit: unsorted
+            rank[it] = (in && radix_valid(p, n, idx, keys[it], aux[it])) ? 0u : 0x80000000u;  // top bit: unsorted
         }
         __syncthreads();
         if (p.filter != kFiltNone) {
@@ -1186,21 +1337,24 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
 }  // namespace
 
 // ============================================================================ launchers
-void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float* planes, uint64_t stride,
-                      float4* shade, hipStream_t s) {
+void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, float4* shade, float4* cull,
+                      hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, aos, n, n_sh,
-                       planes, stride, shade);
+                       geo, shade, cull);
 }
-void launch_project(const ProjParams& p, hipStream_t s) {
-    const unsigned grid = (unsigned)std::max<uint64_t>(
-        1, std::min<uint64_t>(kMaxGrid, (p.n + kProjThreads - 1) / kProjThreads));
-    hipLaunchKernelGGL(k_project, dim3(grid), dim3(kProjThreads), 0, s, p);
+void launch_project(const ProjParams& p, bool two_phase, hipStream_t s) {
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, sort_parts(p.n)));
+    if (two_phase)
+        hipLaunchKernelGGL(k_project<true>, dim3(grid), dim3(kProjThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_project<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
 }
 void launch_sort_pass(const SortPass& p, hipStream_t s) {
     if (!p.parts_max) return;
     const unsigned grid = std::min<uint32_t>(p.parts_max, kMaxGrid);
-    hipLaunchKernelGGL(k_radix_upsweep, dim3(grid), dim3(kSortThreads), 0, s, p);
+    if (!p.part_count)  // else k_project produced the counts (first depth pass of chunk 0)
+        hipLaunchKernelGGL(k_radix_upsweep, dim3(grid), dim3(kSortThreads), 0, s, p);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, p);
     hipLaunchKernelGGL(k_radix_downsweep, dim3(grid), dim3(kSortThreads), 0, s, p);
 }

@@ -1,2 +1,3 @@
 set -o pipefail
-timeout -k 10 300 python tools/chunk_sweep.py --fractions 0.14,0.2,0 --frames 30
+bash tools/gpu_check.sh r1q || exit 1
+timeout -k 10 400 python tools/strip_bench.py

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Per-rank frame time of the row-strip split, measured one strip at a time on one GPU (the
+8-GPU run itself is the driver's): for G in 1, 2, 4, 8, every strip's mean frame time and stage
+times; the slowest strip bounds the G-GPU frame (plus the all-gather)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gaussian-splatting-web_amd"))
+import gsplat_amd as gs  # noqa: E402
+from gsplat_amd.strips import strip_geometry  # noqa: E402
+
+
+def main():
+    N, W, H = int(os.environ.get("N", 6_100_000)), 1920, 1080
+    aos = gs.synth_aos(N, 6, W, H)
+    u = gs.bench_uniforms(W, H)
+    ctx = gs.Context(0)
+    sc = gs.Scene(ctx, aos, N, 16)
+    for G in (1, 2, 4, 8):
+        rows = strip_geometry(H, 0, G)[1]
+        buf = gs.DeviceBuffer(rows * W * 16)
+        worst = 0.0
+        line = []
+        for g in range(G):
+            o = gs.make_opts(strip_index=g, strip_count=G, timing=1)
+            for _ in range(5):
+                sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
+            ctx.sync()
+            ctx.timings_reset()
+            t0 = time.perf_counter()
+            for _ in range(30):
+                sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
+            ctx.sync()
+            ms = (time.perf_counter() - t0) / 30 * 1e3
+            st = ctx.timings()
+            worst = max(worst, ms)
+            line.append("%d:%.3f(p%.3f s%.3f b%.3f t%.3f c%.3f)" % (g, ms, st["ms_project"], st["ms_sort"],
+                                                                  st["ms_bin"], st["ms_tile_sort"], st["ms_composite"]))
+        print("G=%d worst %.3f ms  speedup-bound %.2f  | %s" % (G, worst, 0, " ".join(line)), flush=True)
+    sc.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
