@@ -36,8 +36,8 @@ def algorithmic_bytes(stage, n, n_vis, k, W, H):
         # Gaussian; write the 48-B projected record of every visible one
         return 52 * n + 48 * n_vis
     if stage == "composite":
-        # per (tile, splat) entry: the 4-B slot and the 48-B composite record; RGBA f32 out
-        return 52 * k + 16 * W * H
+        # per (tile, splat) entry: the 4-B slot and the 48-B composite record; RGBA f16 out
+        return 52 * k + 8 * W * H
     if stage == "sort":
         # 4 LSD passes: upsweep reads the key (4 B), downsweep reads key+index+rect and writes
         # them (24 B); pass 0 runs over all N keys
@@ -116,24 +116,27 @@ def main():
     scene = gs.Scene(ctx, aos, N, 16)
 
     row0, rows_padded, t0, t1 = strip_geometry(H, rank, world)
-    opts = gs.make_opts(strip_index=rank, strip_count=world, timing=1)
-    strip_bytes = rows_padded * W * 16
+    # output RGBA f16: the reference's framebuffer format (rgba16float, src/simple_render.ts:499-505);
+    # accumulation stays fp32 (gs_opts.accum), rounded once at the store
+    opts = gs.make_opts(strip_index=rank, strip_count=world, timing=1, out_format=gs.GS_OUT_RGBA_F16)
+    strip_bytes = rows_padded * W * 8
     if launched:
         import torch
+        from gsplat_amd.strips import StripPipeline
         stream = torch.cuda.current_stream()
-        strip = torch.empty((rows_padded, W, 4), dtype=torch.float32, device="cuda")
-        full = torch.empty((world * rows_padded, W, 4), dtype=torch.float32, device="cuda")
-        from gsplat_amd.strips import gather_strips
+        pipe = StripPipeline(rows_padded, W, dtype=torch.float16)  # gather t beside render t+1
 
         def frame():
+            strip = pipe.next_strip()
             scene.render_device(u, W, H, strip.data_ptr(), strip_bytes, stream.cuda_stream, opts)
-            gather_strips(strip, full)
+            pipe.submit()
 
         def sync():
+            pipe.finish()
             torch.cuda.synchronize()
             dist.barrier()
     else:
-        buf = gs.DeviceBuffer(H * W * 16)
+        buf = gs.DeviceBuffer(H * W * 8)
 
         def frame():
             scene.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, opts)
@@ -191,7 +194,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY §8d generator, splitmix64 seed %d; bicycle PLY absent)" % args.seed,
+            "data": "synthetic (SURVEY §8d generator, splitmix64 seed %d; bicycle PLY absent); "
+                    "output RGBA f16 (the reference's rgba16float framebuffer)" % args.seed,
             "config": {"workload": "configs[3]: %d Gaussians (SH deg 3) at %dx%d, lookAt([0,0,0],[0,0,-1]) "
                                    "perspective(60deg,W/H,0.03,1000)" % (N, W, H),
                        "n_gaussians": N, "width": W, "height": H,

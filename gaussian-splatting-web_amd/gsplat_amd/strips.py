@@ -30,6 +30,60 @@ def gather_strips(strip, full=None, group=None):
     return full
 
 
+class StripPipeline:
+    """Double-buffered strips: frame t's all-gather runs on a side stream while frame t+1 renders
+    (SURVEY §8e).  Per frame: `strip = pipe.next_strip()`, render into it on the current stream,
+    then `full = pipe.submit()` (the gathered image is ready once `finish()` or a later
+    `next_strip()` for the same buffer has ordered the streams).  On CPU tensors (gloo) the
+    gather is synchronous."""
+
+    def __init__(self, rows_padded, W, channels=4, dtype=None, device=None, depth=2, group=None):
+        import torch
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+        world = dist.get_world_size(group)
+        dtype = dtype or torch.float16
+        device = torch.device(device or "cuda")
+        self.strips = [torch.zeros((rows_padded, W, channels), dtype=dtype, device=device) for _ in range(depth)]
+        self.fulls = [torch.zeros((world * rows_padded, W, channels), dtype=dtype, device=device)
+                      for _ in range(depth)]
+        self.cuda = device.type == "cuda"
+        if self.cuda:
+            self.side = torch.cuda.Stream(device=device)
+            self.rendered = [torch.cuda.Event() for _ in range(depth)]
+            self.gathered = [torch.cuda.Event() for _ in range(depth)]
+        self.k = 0
+
+    def next_strip(self):
+        """The buffer to render the next frame into (after its previous gather has finished)."""
+        import torch
+        b = self.k % len(self.strips)
+        if self.cuda and self.k >= len(self.strips):
+            torch.cuda.current_stream().wait_event(self.gathered[b])
+        return self.strips[b]
+
+    def submit(self):
+        """All-gather the strip just rendered into the current frame's full buffer; returns it."""
+        import torch
+        b = self.k % len(self.strips)
+        if self.cuda:
+            self.rendered[b].record(torch.cuda.current_stream())
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(self.rendered[b])
+                self.dist.all_gather_into_tensor(self.fulls[b], self.strips[b], group=self.group)
+                self.gathered[b].record(self.side)
+        else:
+            self.dist.all_gather_into_tensor(self.fulls[b], self.strips[b], group=self.group)
+        self.k += 1
+        return self.fulls[b]
+
+    def finish(self):
+        """Order every pending gather before the current stream's later work."""
+        import torch
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.side)
+
+
 def assemble(full, H):
     """Crop the gathered buffer to the H image rows."""
     return full[:H]
@@ -39,4 +93,4 @@ def padded_rows_total(H, count):
     return strip_geometry(H, 0, count)[1] * count
 
 
-__all__ = ["strip_geometry", "gather_strips", "assemble", "padded_rows_total"]
+__all__ = ["strip_geometry", "gather_strips", "StripPipeline", "assemble", "padded_rows_total"]

@@ -26,7 +26,7 @@ def _worker(rank, world, port, W, H, q):
     sys.path[:0] = [os.path.join(root, "gaussian-splatting-web_amd"), os.path.join(root, "tests")]
     import gsplat_amd as gs
     import oracle_py as orc
-    from gsplat_amd.strips import assemble, gather_strips, strip_geometry
+    from gsplat_amd.strips import StripPipeline, assemble, gather_strips, strip_geometry
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n = 4000
@@ -39,8 +39,18 @@ def _worker(rank, world, port, W, H, q):
     strip[:rows] = torch.from_numpy(img[row0:row0 + rows])
     full = gather_strips(strip)
     out = assemble(full, H).numpy()
+    # the double-buffered pipeline bench.py uses (synchronous on CPU tensors), two frames
+    pipe = StripPipeline(rows_padded, W, dtype=torch.float32, device="cpu")
+    ok_pipe = True
+    for _ in range(3):
+        buf = pipe.next_strip()
+        buf.zero_()
+        buf[:rows] = torch.from_numpy(img[row0:row0 + rows])
+        f = pipe.submit()
+        pipe.finish()
+        ok_pipe = ok_pipe and np.array_equal(assemble(f, H).numpy(), img)
     if rank == 0:
-        q.put(bool(np.array_equal(out, img)))
+        q.put(bool(np.array_equal(out, img)) and ok_pipe)
     dist.barrier()
     dist.destroy_process_group()
 
