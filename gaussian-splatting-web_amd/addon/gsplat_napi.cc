@@ -422,6 +422,43 @@ napi_value PackUniforms(napi_env env, napi_callback_info info) {
     return ab;
 }
 
+// PackedGaussians(arrayBuffer) (src/ply.ts:200-355): {aos, numGaussians, shDegree, nShCoeffs, minPos, maxPos}
+napi_value PlyParse(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    get_args(env, info, 1, argv);
+    void* data;
+    size_t len;
+    if (!get_bytes(env, argv[0], &data, &len)) return throw_gs(env, GS_ERR_INVALID, "plyParse: need an ArrayBuffer");
+    gs_ply_info pi;
+    int rc = gs_ply_parse(data, len, &pi, nullptr, 0);
+    if (rc) return throw_gs(env, rc, "gs_ply_parse");
+    void* out;
+    napi_value ab;
+    const size_t bytes = (size_t)(pi.num_gaussians * pi.record_bytes);
+    NAPI_OK(napi_create_arraybuffer(env, bytes, &out, &ab));
+    rc = gs_ply_parse(data, len, &pi, out, bytes);
+    if (rc) return throw_gs(env, rc, "gs_ply_parse");
+    napi_value o, v;
+    NAPI_OK(napi_create_object(env, &o));
+    napi_set_named_property(env, o, "aos", ab);
+    napi_create_double(env, (double)pi.num_gaussians, &v);
+    napi_set_named_property(env, o, "numGaussians", v);
+    napi_create_int32(env, pi.sh_degree, &v);
+    napi_set_named_property(env, o, "shDegree", v);
+    napi_create_int32(env, pi.n_sh_coeffs, &v);
+    napi_set_named_property(env, o, "nShCoeffs", v);
+    for (int k = 0; k < 2; ++k) {
+        napi_value arr;
+        napi_create_array_with_length(env, 3, &arr);
+        for (uint32_t c = 0; c < 3; ++c) {
+            napi_create_double(env, k ? pi.max_pos_d[c] : pi.min_pos_d[c], &v);
+            napi_set_element(env, arr, c, v);
+        }
+        napi_set_named_property(env, o, k ? "maxPos" : "minPos", arr);
+    }
+    return o;
+}
+
 napi_value StripRows(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     get_args(env, info, 3, argv);
@@ -448,7 +485,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"sceneFree", SceneFree}, {"render", Render}, {"renderAsync", RenderAsync},
         {"timings", Timings}, {"timingsReset", TimingsReset}, {"sync", Sync}, {"present", Present},
         {"lookAt", LookAt}, {"perspective", Perspective}, {"cameraPosition", CameraPosition},
-        {"packUniforms", PackUniforms}, {"stripRows", StripRows},
+        {"packUniforms", PackUniforms}, {"stripRows", StripRows}, {"plyParse", PlyParse},
     };
     for (const auto& f : fns) {
         napi_value fn;

@@ -4,9 +4,12 @@
 //     by src/camera.ts:101-138 and packed as src/renderer.ts:24-33 / :349-384;
 //   * seeded synthetic scenes, written in the reference AoS layout;
 //   * the present pass (src/post_process_render.ts:54-77).
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <map>
+#include <string>
 #include <vector>
 
 #include "../../include/gsplat.h"
@@ -192,6 +195,227 @@ int gs_synth_aos(uint64_t n, uint64_t seed, int W, int H, void* out_aos) {
         for (int k = 0; k < 45; ++k) rest[k] = 0.15 * r.normal();
         for (int k = 1; k < 16; ++k)
             for (int c = 0; c < 3; ++c) rec[16 + 4 * k + c] = f32(rest[c * 15 + (k - 1)]);
+    }
+    return GS_OK;
+}
+
+
+// ---- PLY ingest: PackedGaussians (src/ply.ts:54-355) restated in C++ ---------------------------
+// Same header reading (50-byte chunks until "end_header", src/ply.ts:54-102), property order (a JS
+// object: integer-like names first, then first-insertion order), only float / uchar properties
+// advance the read offset (:104-123), SH feature order f_dc_c then f_rest_{c*K+i} (:222-232),
+// rotation normalised in double, swizzled to (-x,-y,-z,w) with NaN/-0 -> 0 (:166-213, :289-297),
+// scale = |exp(s)| (:214-218), every value rounded once to f32 when packed (src/packing.ts), and
+// min_pos / max_pos by the running x+y+z comparison of src/mylib.ts:28-30 (:276-286).
+namespace {
+
+struct PlyProp {
+    std::string name, type;
+};
+
+bool js_index_key(const std::string& k, uint64_t& v) {  // canonical array index -> ordered first
+    if (k.empty() || k.size() > 10 || (k.size() > 1 && k[0] == '0')) return false;
+    v = 0;
+    for (char c : k) {
+        if (c < '0' || c > '9') return false;
+        v = v * 10 + (uint64_t)(c - '0');
+    }
+    return v < 4294967295ull;
+}
+
+bool is_word(char c) { return std::isalnum((unsigned char)c) || c == '_'; }
+
+// first match of /(\w+)\s+(\w+)\s+(\w+)/ in line: (group2, group3)
+bool match3(const std::string& l, std::string& g2, std::string& g3) {
+    for (size_t st = 0; st < l.size(); ++st) {
+        if (!is_word(l[st]) || (st > 0 && is_word(l[st - 1]) && false)) continue;
+        size_t i = st;
+        std::string g[3];
+        bool ok = true;
+        for (int k = 0; k < 3 && ok; ++k) {
+            size_t b = i;
+            while (i < l.size() && is_word(l[i])) ++i;
+            if (i == b) { ok = false; break; }
+            g[k] = l.substr(b, i - b);
+            if (k < 2) {
+                size_t ws = i;
+                while (i < l.size() && std::isspace((unsigned char)l[i])) ++i;
+                if (i == ws) ok = false;
+            }
+        }
+        if (ok) {
+            g2 = g[1];
+            g3 = g[2];
+            return true;
+        }
+    }
+    return false;
+}
+
+std::string js_trim(const std::string& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && std::isspace((unsigned char)s[a])) ++a;
+    while (b > a && std::isspace((unsigned char)s[b - 1])) --b;
+    return s.substr(a, b - a);
+}
+
+struct PlyHeader {
+    uint64_t count = 0;
+    std::vector<PlyProp> props;  // JS key order
+    uint64_t data_offset = 0;
+};
+
+int ply_header(const uint8_t* buf, uint64_t bytes, PlyHeader& h) {
+    std::string text;
+    uint64_t off = 0;
+    for (;;) {
+        if (off + 50 > bytes) return GS_ERR_INVALID;  // new Uint8Array(buf, off, 50) throws
+        text.append((const char*)buf + off, 50);
+        off += 50;
+        if (text.find("end_header") != std::string::npos) break;
+    }
+    std::vector<std::string> order;
+    std::map<std::string, std::string> types;
+    size_t pos = 0;
+    for (;;) {
+        const size_t e = text.find('\n', pos);
+        const std::string line = js_trim(text.substr(pos, e == std::string::npos ? std::string::npos : e - pos));
+        if (line.rfind("element vertex", 0) == 0) {
+            const size_t d = line.find_first_of("0123456789");
+            if (d != std::string::npos) {
+                size_t q = d;
+                uint64_t v = 0;
+                while (q < line.size() && std::isdigit((unsigned char)line[q])) v = v * 10 + (uint64_t)(line[q++] - '0');
+                h.count = v;
+            }
+        } else if (line.rfind("property", 0) == 0) {
+            std::string t, nm;
+            if (match3(line, t, nm)) {
+                if (!types.count(nm)) order.push_back(nm);
+                types[nm] = t;
+            }
+        } else if (line == "end_header") {
+            break;
+        }
+        if (e == std::string::npos) break;
+        pos = e + 1;
+    }
+    // JS property enumeration order: integer-like keys ascending, then insertion order
+    std::vector<std::pair<uint64_t, std::string>> idx;
+    std::vector<std::string> rest;
+    for (const auto& k : order) {
+        uint64_t v;
+        if (js_index_key(k, v)) idx.push_back({v, k}); else rest.push_back(k);
+    }
+    std::sort(idx.begin(), idx.end());
+    for (const auto& k : idx) h.props.push_back({k.second, types[k.second]});
+    for (const auto& k : rest) h.props.push_back({k, types[k]});
+    h.data_offset = text.find("end_header") + std::string("end_header").size() + 1;
+    return GS_OK;
+}
+
+// DataView.getFloat32 into a JS number: a signalling NaN comes back quiet (f32 -> f64 conversion)
+inline float f32_from_le(const uint8_t* p) {
+    uint32_t u;
+    std::memcpy(&u, p, 4);
+    if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) u |= 0x00400000u;
+    float v;
+    std::memcpy(&v, &u, 4);
+    return v;
+}
+
+}  // namespace
+
+int gs_ply_parse(const void* ply, uint64_t bytes, gs_ply_info* info, void* out_aos, uint64_t out_bytes) {
+    if (!ply || !info) return GS_ERR_INVALID;
+    const uint8_t* buf = (const uint8_t*)ply;
+    PlyHeader h;
+    int rc = ply_header(buf, bytes, h);
+    if (rc) return rc;
+    // per-property byte offset within a vertex (float 4, uchar 1, anything else 0 and unread)
+    std::map<std::string, int> col;       // name -> index into props
+    std::vector<uint32_t> poff(h.props.size());
+    uint64_t stride = 0;
+    int n_rest = 0;
+    for (size_t k = 0; k < h.props.size(); ++k) {
+        col[h.props[k].name] = (int)k;
+        poff[k] = (uint32_t)stride;
+        if (h.props[k].type == "float") stride += 4;
+        else if (h.props[k].type == "uchar") stride += 1;
+        if (h.props[k].name.rfind("f_rest_", 0) == 0) ++n_rest;
+    }
+    const double per_color = n_rest / 3.0;
+    const double deg = std::sqrt(per_color + 1.0) - 1.0;
+    int n_sh;
+    if (deg == 0.0) n_sh = 1;
+    else if (deg == 1.0) n_sh = 4;
+    else if (deg == 2.0) n_sh = 9;
+    else if (deg == 3.0) n_sh = 16;
+    else return GS_ERR_UNSUPPORTED;  // "Unsupported SH degree"
+    const uint64_t rec = 64 + 16 * (uint64_t)n_sh;
+    if (h.data_offset + h.count * stride > bytes && h.count > 0 && stride > 0) return GS_ERR_INVALID;
+    if (h.count > 0 && stride == 0 && h.data_offset > bytes) return GS_ERR_INVALID;
+    info->num_gaussians = h.count;
+    info->sh_degree = (int32_t)deg;
+    info->n_sh_coeffs = n_sh;
+    info->record_bytes = rec;
+    info->data_offset = h.data_offset;
+    info->vertex_stride = stride;
+    // value of property `name` of vertex v as JS sees it (missing -> NaN, as `undefined` packs)
+    auto column = [&](const std::string& name) { auto it = col.find(name); return it == col.end() ? -1 : it->second; };
+    const uint8_t* data = buf + h.data_offset;
+    auto value = [&](uint64_t v, int c) -> double {
+        if (c < 0) return NAN;
+        const PlyProp& pr = h.props[c];
+        const uint8_t* p = data + v * stride + poff[c];
+        if (pr.type == "float") return (double)f32_from_le(p);
+        if (pr.type == "uchar") return (double)p[0] / 255.0;
+        return NAN;  // never read by the reference: undefined
+    };
+    const int cx = column("x"), cy = column("y"), cz = column("z");
+    // bounding box, sequential as the reference (src/ply.ts:276-286, src/mylib.ts:28-30)
+    double mx[3] = {-99999, -99999, -99999}, mn[3] = {99999, 99999, 99999};
+    for (uint64_t v = 0; v < h.count; ++v) {
+        const double x = value(v, cx), y = value(v, cy), z = value(v, cz);
+        const double s = x + y + z;
+        if (s > mx[0] + mx[1] + mx[2]) { mx[0] = x; mx[1] = y; mx[2] = z; }
+        if (!(s > mn[0] + mn[1] + mn[2])) { mn[0] = x; mn[1] = y; mn[2] = z; }
+    }
+    for (int k = 0; k < 3; ++k) {
+        info->min_pos[k] = (float)mn[k];
+        info->max_pos[k] = (float)mx[k];
+    }
+    info->min_pos_d[0] = mn[0]; info->min_pos_d[1] = mn[1]; info->min_pos_d[2] = mn[2];
+    info->max_pos_d[0] = mx[0]; info->max_pos_d[1] = mx[1]; info->max_pos_d[2] = mx[2];
+    if (!out_aos) return GS_OK;
+    if (out_bytes < h.count * rec) return GS_ERR_INVALID;
+    std::vector<int> shc(3 * (size_t)n_sh);
+    const int K = n_rest / 3;
+    for (int c = 0; c < 3; ++c) shc[c] = column("f_dc_" + std::to_string(c));
+    for (int i = 0; i < K && 1 + i < n_sh; ++i)
+        for (int c = 0; c < 3; ++c) shc[3 * (1 + i) + c] = column("f_rest_" + std::to_string(c * K + i));
+    const int cs[3] = {column("scale_0"), column("scale_1"), column("scale_2")};
+    const int cr[4] = {column("rot_0"), column("rot_1"), column("rot_2"), column("rot_3")};
+    const int co = column("opacity");
+    uint8_t* out = (uint8_t*)out_aos;
+    std::memset(out, 0, h.count * rec);
+#pragma omp parallel for schedule(static)
+    for (int64_t vv = 0; vv < (int64_t)h.count; ++vv) {
+        const uint64_t v = (uint64_t)vv;
+        float* r = (float*)(out + v * rec);
+        r[0] = (float)value(v, cx);
+        r[1] = (float)value(v, cy);
+        r[2] = (float)value(v, cz);
+        for (int k = 0; k < 3; ++k) r[4 + k] = (float)std::fabs(std::exp(value(v, cs[k])));
+        const double q0 = value(v, cr[0]), q1 = value(v, cr[1]), q2 = value(v, cr[2]), q3 = value(v, cr[3]);
+        const double len = std::sqrt(((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3);
+        double qq[4] = {(q1 / len) * -1.0, (q2 / len) * -1.0, (q3 / len) * -1.0, q0 / len};
+        for (double& x : qq)
+            if (!(x != 0.0) || std::isnan(x)) x = 0.0;  // `qq[i] ||= 0`: NaN, 0 and -0 -> +0
+        for (int k = 0; k < 4; ++k) r[8 + k] = (float)qq[k];
+        r[12] = (float)value(v, co);
+        for (int k = 0; k < n_sh; ++k)
+            for (int c = 0; c < 3; ++c) r[16 + 4 * k + c] = (float)value(v, shc[3 * k + c]);
     }
     return GS_OK;
 }

@@ -19,15 +19,25 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libgsplat.so")
 GS_OK = 0
 GS_ACCUM_FP32, GS_ACCUM_FP16_TARGET = 0, 1
 GS_OUT_RGBA_F32, GS_OUT_RGBA_F16 = 0, 1
+GS_OK, GS_ERR_INVALID, GS_ERR_NO_DEVICE, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_DEVICE_FAULT, \
+    GS_ERR_INTERNAL = 0, -1, -2, -3, -4, -5, -6, -7
 
 # every symbol include/gsplat.h declares
 EXPORTED_SYMBOLS = (
     "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy",
     "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows",
     "gs_render", "gs_render_device", "gs_timings", "gs_timings_reset", "gs_sync", "gs_present", "gs_look_at",
-    "gs_perspective", "gs_camera_position", "gs_pack_uniforms", "gs_synth_aos",
+    "gs_perspective", "gs_camera_position", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
     "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records",
 )
+
+
+class GsPlyInfo(ctypes.Structure):
+    _fields_ = [("num_gaussians", ctypes.c_uint64), ("sh_degree", ctypes.c_int32),
+                ("n_sh_coeffs", ctypes.c_int32), ("record_bytes", ctypes.c_uint64),
+                ("data_offset", ctypes.c_uint64), ("vertex_stride", ctypes.c_uint64),
+                ("min_pos", ctypes.c_float * 3), ("max_pos", ctypes.c_float * 3),
+                ("min_pos_d", ctypes.c_double * 3), ("max_pos_d", ctypes.c_double * 3)]
 
 
 class GsOpts(ctypes.Structure):
@@ -101,6 +111,7 @@ def lib():
         L.gs_camera_position.argtypes = [P, P]
         L.gs_pack_uniforms.argtypes = [P, P, P, F, F, F, F, F, P]
         L.gs_synth_aos.argtypes = [U64, U64, I, I, P]
+        L.gs_ply_parse.argtypes = [P, U64, ctypes.POINTER(GsPlyInfo), P, U64]
         L.gs_debug_sort_pairs.argtypes = [P, P, P, U64, I, I]
         L.gs_debug_last_order.argtypes = [P, P, P, P, U64, ctypes.POINTER(U64)]
         L.gs_debug_last_records.argtypes = [P, P, P, U64]
@@ -160,6 +171,18 @@ def synth_aos(n, seed, W=1920, H=1080):
     out = np.empty(n * 80, np.float32)
     _check(lib().gs_synth_aos(int(n), int(seed), int(W), int(H), _ptr(out)))
     return out
+
+
+def parse_ply(data):
+    """PackedGaussians(arrayBuffer) (src/ply.ts): .ply bytes -> (AoS records as uint8, info dict)."""
+    buf = np.frombuffer(bytes(data), np.uint8)
+    info = GsPlyInfo()
+    _check(lib().gs_ply_parse(_ptr(buf), buf.size, ctypes.byref(info), None, 0))
+    out = np.zeros(int(info.num_gaussians * info.record_bytes), np.uint8)
+    _check(lib().gs_ply_parse(_ptr(buf), buf.size, ctypes.byref(info), _ptr(out), out.size))
+    return out, {"numGaussians": int(info.num_gaussians), "shDegree": int(info.sh_degree),
+                 "nShCoeffs": int(info.n_sh_coeffs), "record_bytes": int(info.record_bytes),
+                 "min_pos": list(info.min_pos_d), "max_pos": list(info.max_pos_d)}
 
 
 def present(rgba, W, H):

@@ -29,10 +29,13 @@ export declare class PackedGaussians {
     gaussiansBuffer: ArrayBuffer;  // AoS records, src/ply.ts:249-257
     numGaussians: number;
     nShCoeffs: number;
+    sphericalHarmonicsDegree: number;
     gaussianArrayLayout: {size: number};
-    sceneMin: number[] | null;
-    sceneMax: number[] | null;
+    min_pos: number[];
+    max_pos: number[];
     constructor(gaussiansBuffer: ArrayBuffer | ArrayBufferView, numGaussians: number, nShCoeffs?: number);
+    /** The reference's `new PackedGaussians(plyArrayBuffer)` (src/ply.ts), parsed natively. */
+    static fromPly(plyArrayBuffer: ArrayBuffer): PackedGaussians;
 }
 
 export declare class Camera {

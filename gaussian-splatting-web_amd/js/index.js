@@ -71,9 +71,21 @@ class PackedGaussians {
         this.gaussiansBuffer = gaussiansBuffer instanceof ArrayBuffer ? gaussiansBuffer : gaussiansBuffer.buffer;
         this.numGaussians = numGaussians;
         this.nShCoeffs = nShCoeffs;
+        this.sphericalHarmonicsDegree = Math.sqrt(nShCoeffs) - 1;
         this.gaussianArrayLayout = {size: numGaussians * (64 + 16 * nShCoeffs)};
-        this.sceneMin = null;
-        this.sceneMax = null;
+        this.min_pos = [99999, 99999, 99999];
+        this.max_pos = [-99999, -99999, -99999];
+    }
+
+    // new PackedGaussians(plyArrayBuffer) of the reference (src/ply.ts:200-355), parsed natively
+    // with the same semantics (gs_ply_parse); throws Error like the reference on a bad file
+    static fromPly(plyArrayBuffer) {
+        const r = addon().plyParse(plyArrayBuffer);
+        const g = new PackedGaussians(r.aos, r.numGaussians, r.nShCoeffs);
+        g.sphericalHarmonicsDegree = r.shDegree;
+        g.min_pos = r.minPos;
+        g.max_pos = r.maxPos;
+        return g;
     }
 }
 

@@ -154,6 +154,24 @@ int gs_pack_uniforms(const float view[16], const float proj[16], const float cam
 /* Writes n records of 320 bytes (SH degree 3) in the reference AoS layout. */
 int gs_synth_aos(uint64_t n, uint64_t seed, int W, int H, void* out_aos);
 
+/* ---- PLY ingest (src/ply.ts:54-355, PackedGaussians) --------------------------------------- */
+typedef struct gs_ply_info {
+    uint64_t num_gaussians;   /* PackedGaussians.numGaussians */
+    int32_t sh_degree;        /* sphericalHarmonicsDegree (0..3) */
+    int32_t n_sh_coeffs;      /* nShCoeffs: 1, 4, 9 or 16 */
+    uint64_t record_bytes;    /* 64 + 16 * n_sh_coeffs: the AoS record of gs_scene_upload */
+    uint64_t data_offset;     /* first vertex byte in the file */
+    uint64_t vertex_stride;   /* bytes per vertex in the file (float 4, uchar 1, others unread) */
+    float min_pos[3], max_pos[3];        /* PackedGaussians.min_pos / max_pos (f32) */
+    double min_pos_d[3], max_pos_d[3];   /* the same as the reference holds them (JS numbers) */
+} gs_ply_info;
+/* Parses a binary-little-endian .ply with the reference's exact semantics (header chunks, property
+ * order, float/uchar only, rotation normalise + swizzle, |exp(scale)|, SH order, f32 packing).
+ * out_aos NULL: fills `info` only (size the buffer as num_gaussians * record_bytes).  Returns
+ * GS_ERR_INVALID on a truncated file, GS_ERR_UNSUPPORTED when the f_rest count is not 0/9/24/45
+ * (the reference throws "Unsupported SH degree"). */
+int gs_ply_parse(const void* ply, uint64_t bytes, gs_ply_info* info, void* out_aos, uint64_t out_bytes);
+
 /* ---- checks used by tests ------------------------------------------------------------------ */
 /* Stable ascending GPU radix sort of (key,value) on bits [begin_bit,end_bit): host in/out. */
 int gs_debug_sort_pairs(gs_ctx* ctx, uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit,

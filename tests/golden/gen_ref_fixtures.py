@@ -13,6 +13,8 @@ What is written (data only) into tests/golden/:
                             (src/renderer.ts:24-33), found by packing sentinel values.
   * <scene>.aos.bin      -- PackedGaussians.gaussiansBuffer for public/{simple,pc_short,m3splat}.ply
   * ply_meta.json        -- numGaussians, nShCoeffs, sha256 of each AoS, min_pos/max_pos.
+  * ply_synth/          -- edge-case .ply inputs written here, with PackedGaussians output (or
+                          the error it throws) for each: <name>.aos.bin, meta.json.
   * cameras.json         -- wgpu-matrix lookAt/perspective/inverse outputs (Float32 bits) and
                             cam.json-derived view/proj through camera.ts's formulas.
 
@@ -331,6 +333,23 @@ for (const name of ['simple', 'pc_short', 'm3splat']) {
                    bytes: g.gaussiansBuffer.byteLength, min_pos: Array.from(g.min_pos), max_pos: Array.from(g.max_pos)};
 }
 
+// Synthetic edge-case PLYs (written by gen_ref_fixtures.py) through the same PackedGaussians.
+out.ply_synth = {};
+for (const f of fs.readdirSync(process.argv[4]).sort()) {
+  if (!f.endsWith('.ply')) continue;
+  const name = f.slice(0, -4);
+  const b = fs.readFileSync(process.argv[4] + '/' + f);
+  const ab = b.buffer.slice(b.byteOffset, b.byteOffset + b.byteLength);
+  try {
+    const g = new PackedGaussians(ab);
+    fs.writeFileSync(process.argv[3] + '/synth_' + name + '.aos.bin', Buffer.from(g.gaussiansBuffer));
+    out.ply_synth[name] = {numGaussians: g.numGaussians, nShCoeffs: g.nShCoeffs, shDegree: g.sphericalHarmonicsDegree,
+                           bytes: g.gaussiansBuffer.byteLength, min_pos: Array.from(g.min_pos), max_pos: Array.from(g.max_pos)};
+  } catch (e) {
+    out.ply_synth[name] = {error: String(e)};
+  }
+}
+
 // Cameras through wgpu-matrix (WM) and camera.ts's formulas (src/camera.ts:19-42, :101-138, :467-503).
 function getProjectionMatrix(znear, zfar, fovX, fovY) {
   const tanHalfFovY = Math.tan(fovY / 2), tanHalfFovX = Math.tan(fovX / 2);
@@ -379,6 +398,100 @@ fs.writeFileSync(process.argv[3] + '/driver_out.json', JSON.stringify(out));
 """
 
 
+def write_synth_plys(d):
+    """Edge-case binary PLY inputs (deterministic); the reference's PackedGaussians parses each."""
+    import random
+    import struct
+    rnd = random.Random(7)
+    os.makedirs(d, exist_ok=True)
+
+    def ply(name, props, rows, count=None, extra_header="", eol="\n", trunc=0):
+        hdr = ["ply", "format binary_little_endian 1.0", "element vertex %d" % (len(rows) if count is None else count)]
+        hdr += ["property %s %s" % (t, n) for t, n in props]
+        hdr += [x for x in extra_header.split("|") if x]
+        hdr += ["end_header"]
+        body = b""
+        for row in rows:
+            for (t, _), v in zip(props, row):
+                if t == "float":
+                    body += struct.pack("<f", v)
+                elif t == "uchar":
+                    body += struct.pack("<B", int(v) & 255)
+                elif t == "double":
+                    body += struct.pack("<d", v)
+        blob = (eol.join(hdr) + eol).encode() + body + b"\0" * 64
+        if trunc:
+            blob = blob[:len(blob) - 64 - trunc]
+        open(os.path.join(d, name + ".ply"), "wb").write(blob)
+
+    def gauss_props(n_rest, extra=()):
+        p = [("float", "x"), ("float", "y"), ("float", "z"), ("float", "nx"), ("float", "ny"), ("float", "nz")]
+        p += list(extra)
+        p += [("float", "f_dc_%d" % c) for c in range(3)]
+        p += [("float", "f_rest_%d" % k) for k in range(n_rest)]
+        p += [("float", "opacity")] + [("float", "scale_%d" % k) for k in range(3)]
+        p += [("float", "rot_%d" % k) for k in range(4)]
+        return p
+
+    def row(props):
+        out = []
+        for t, n in props:
+            if t == "uchar":
+                out.append(rnd.randrange(256))
+            elif n.startswith("scale"):
+                out.append(rnd.uniform(-6, -1))
+            elif n.startswith("rot"):
+                out.append(rnd.gauss(0, 1))
+            elif n.startswith("f_rest"):
+                out.append(rnd.gauss(0, 0.2))
+            else:
+                out.append(rnd.uniform(-2, 2))
+        return out
+
+    for deg, nr in ((0, 0), (1, 9), (2, 24)):
+        pr = gauss_props(nr)
+        ply("deg%d" % deg, pr, [row(pr) for _ in range(40)])
+    pr = gauss_props(24, extra=(("uchar", "red"), ("uchar", "green"), ("uchar", "blue")))
+    ply("deg2_uchar_rgb", pr, [row(pr) for _ in range(33)])
+    pr = gauss_props(45)
+    pr = [("uchar", n) if n in ("opacity", "rot_0", "f_dc_1") else (t, n) for t, n in pr]
+    ply("uchar_mix", pr, [row(pr) for _ in range(25)])
+    pr = gauss_props(45)
+    rows = [row(pr) for _ in range(12)]
+    ri = [i for i, (_, n) in enumerate(pr) if n.startswith("rot")]
+    si = [i for i, (_, n) in enumerate(pr) if n.startswith("scale")]
+    quats = [(0, 0, 0, 0), (-0.0, 0, 0, 0), (1, 0, 0, 0), (0, 0, 0, -1), (1e-30, 0, 0, 0), (3e38, 3e38, 0, 0),
+             (float("nan"), 1, 0, 0), (0, -0.0, -0.0, 1), (2, 0, 0, 0), (float("inf"), 0, 0, 0),
+             (-1, -1, -1, -1), (0.5, 0.5, 0.5, 0.5)]
+    for r, q in zip(rows, quats):
+        for i, v in zip(ri, q):
+            r[i] = v
+    rows[3][si[0]] = 100.0
+    rows[4][si[1]] = float("nan")
+    rows[5][0] = float("nan")
+    ply("quat_scale_edge", pr, rows)
+    pr = gauss_props(45)
+    pr = pr[-4:] + pr[-8:-4] + pr[6:-8] + pr[:6]
+    ply("reordered", pr, [row(pr) for _ in range(20)])
+    pr = gauss_props(45)
+    pr2 = pr[:3] + [("double", "weight")] + pr[3:]
+    ply("double_prop", pr2, [row(pr2) for _ in range(10)])
+    pr = gauss_props(45)
+    ply("face_element", pr, [row(pr) for _ in range(10)],
+        extra_header="element face 0|property list uchar int vertex_indices")
+    pr = gauss_props(45)
+    pr2 = pr[:3] + [("float", "7")] + pr[3:]
+    ply("integer_name", pr2, [row(pr2) for _ in range(10)])
+    pr = gauss_props(5)
+    ply("bad_degree", pr, [row(pr) for _ in range(4)])
+    pr = gauss_props(45)
+    ply("crlf", pr, [row(pr) for _ in range(8)], eol="\r\n")
+    pr = gauss_props(45)
+    ply("truncated", pr, [row(pr) for _ in range(8)], trunc=100)
+    pr = gauss_props(45)
+    ply("zero_vertices", pr, [])
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are committed, nothing to do")
@@ -394,7 +507,9 @@ def main():
         open(os.path.join(tmp, "driver.mjs"), "w").write(DRIVER)
         outdir = os.path.join(tmp, "out")
         os.makedirs(outdir)
-        r = subprocess.run(["node", "--experimental-modules", "--no-warnings", "driver.mjs", REF, outdir],
+        synth = os.path.join(HERE, "ply_synth")
+        write_synth_plys(synth)
+        r = subprocess.run(["node", "--experimental-modules", "--no-warnings", "driver.mjs", REF, outdir, synth],
                            cwd=tmp, capture_output=True, text=True)
         if r.returncode != 0:
             sys.stderr.write(r.stdout + r.stderr)
@@ -406,6 +521,12 @@ def main():
             shutil.copy(os.path.join(outdir, name + ".aos.bin"), os.path.join(HERE, name + ".aos.bin"))
         json.dump(res["layout"], open(os.path.join(HERE, "layout.json"), "w"), indent=1, sort_keys=True)
         json.dump(res["ply"], open(os.path.join(HERE, "ply_meta.json"), "w"), indent=1, sort_keys=True)
+        for name, m in res["ply_synth"].items():
+            if "error" not in m:
+                blob = open(os.path.join(outdir, "synth_" + name + ".aos.bin"), "rb").read()
+                m["sha256"] = hashlib.sha256(blob).hexdigest()
+                shutil.copy(os.path.join(outdir, "synth_" + name + ".aos.bin"), os.path.join(synth, name + ".aos.bin"))
+        json.dump(res["ply_synth"], open(os.path.join(synth, "meta.json"), "w"), indent=1, sort_keys=True)
         json.dump(res["cameras"], open(os.path.join(HERE, "cameras.json"), "w"))
         print("fixtures written to", HERE)
     finally:

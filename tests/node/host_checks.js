@@ -56,6 +56,17 @@ async function main() {
     const u = a.packUniforms(c0.viewMatrix, c0.perspective, c0.getPosition(), 0.5, 0.25, 100, 200, 1);
     out.uniforms = Array.from(new Uint32Array(u));
     out.strip = a.stripRows(1080, 3, 8);
+    // PackedGaussians.fromPly on the reference's own simple.ply (bytes compared by the caller)
+    const ply = fs.readFileSync(path.join(path.dirname(process.argv[2]), 'ply', 'simple.ply'));
+    const g = gs.PackedGaussians.fromPly(ply.buffer.slice(ply.byteOffset, ply.byteOffset + ply.byteLength));
+    out.ply = {n: g.numGaussians, nsh: g.nShCoeffs, deg: g.sphericalHarmonicsDegree, min: g.min_pos, max: g.max_pos,
+               hex: Buffer.from(g.gaussiansBuffer).toString('hex')};
+    try {
+        gs.PackedGaussians.fromPly(new ArrayBuffer(10));
+        out.plyBad = 'accepted';
+    } catch (e) {
+        out.plyBad = e instanceof Error ? e.code : typeof e;
+    }
     console.log(JSON.stringify(out));
 }
 

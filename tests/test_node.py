@@ -19,7 +19,7 @@ pytestmark = pytest.mark.skipif(not NODE or not os.path.exists(ADDON), reason="n
 
 EXPORTS = sorted(["abiVersion", "lastError", "deviceCount", "ctxCreate", "ctxDestroy", "sceneUpload", "sceneFree",
                   "render", "renderAsync", "timings", "timingsReset", "sync", "present", "lookAt", "perspective",
-                  "cameraPosition", "packUniforms", "stripRows"])
+                  "cameraPosition", "packUniforms", "stripRows", "plyParse"])
 
 
 def run_node(*args, timeout=120):
@@ -46,6 +46,12 @@ def test_node_host_cpu():
     assert np.array_equal(u[0:16].view(np.uint32), np.array(ref["view"], np.uint32))
     assert np.array_equal(u[35:40], np.array([0.5, 0.25, 100, 200, 1], np.float32))
     assert out["strip"] == {"row0": 3 * 9 * 16, "rowsPadded": 9 * 16}
+    meta = json.load(open(os.path.join(GOLDEN, "ply_meta.json")))["simple"]
+    assert bytes.fromhex(out["ply"]["hex"]) == open(os.path.join(GOLDEN, "simple.aos.bin"), "rb").read()
+    assert out["ply"]["n"] == meta["numGaussians"] and out["ply"]["nsh"] == meta["nShCoeffs"]
+    assert out["ply"]["deg"] == meta["shDegree"]
+    assert out["ply"]["min"] == meta["min_pos"] and out["ply"]["max"] == meta["max_pos"]
+    assert out["plyBad"] == -1
 
 
 @pytest.mark.gpu
