@@ -141,6 +141,7 @@ struct gs_scene {
     uint32_t *keysA = nullptr, *valsA = nullptr, *auxA = nullptr;
     uint32_t *keysB = nullptr, *valsB = nullptr, *auxB = nullptr;
     float4* crec = nullptr;             // composite records, 3 float4 per slot
+    ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     // zero-per-frame block: FrameCtl | digit histograms of the 4 depth + 2 tile passes of each
     // chunk (kHistShards x 256 words each)
     uint8_t* meta = nullptr;
@@ -407,7 +408,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             for (int e = 0; e < 5; ++e) mark(eb + e);
             break;
         }
-        if (chunk == 1) launch_sat(s->done, TX, tr_end - tr_begin, s->sat, unsat_mask, s->ctl, st);
+        if (chunk == 1) {
+            launch_sat(s->done, TX, tr_end - tr_begin, s->sat, unsat_mask, s->ctl, st);
+            // k_project stored records only for chunk 0: add those chunk 1's filter and bins read
+            ProjParams rp = pp;
+            rp.sat = s->sat;
+            rp.rec_all = 0;
+            launch_records(rp, st);
+        }
         // chunk 0: k_project compacted its splats per partition into B (and did the first upsweep);
         // chunk 1: (keysP, index, rectP) over N, filtered by pass 0.  -> A -> B -> A -> B
         const uint32_t* kin[4] = {chunk ? s->keysP : s->keysB, s->keysA, s->keysB, s->keysA};
@@ -524,6 +532,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     }
     launch_frame_stats(s->ctl, s->shade_list, records(s), st);
     mark(EV_END);
+    s->last_pp = pp;
     HIPCHK(hipGetLastError());
     if (timed) {
         fe.pending = true;
@@ -922,6 +931,10 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
         HIPCHK(hipStreamSynchronize(c->stream));
         const uint64_t m = std::min(cap, s->n);
         if (m) {  // r01 -> words [0, 8); r2 -> words [12, 16); colour below
+            ProjParams rp = s->last_pp;  // records of every visible Gaussian (a frame stores fewer)
+            rp.rec_all = 1;
+            launch_records(rp, c->stream);
+            HIPCHK(hipStreamSynchronize(c->stream));
             std::vector<float> a((size_t)m * 8), b((size_t)m * 4);
             HIPCHK(hipMemcpy(a.data(), s->r01, a.size() * 4, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(b.data(), s->r2, b.size() * 4, hipMemcpyDeviceToHost));

@@ -57,7 +57,8 @@ struct FrameCtl {                 // zeroed at the start of every frame
 // survivors of the cull), a 16-B cull plane (x, y, z, ||R(q) diag(s)||_F^2), and one
 // shading block per Gaussian [x, y, z, sh[k][c] at 3 + 3k + c] of shade_stride float4 (a power
 // of two, so a block never straddles more 128-B lines than it must; 256 B at SH degree 3).
-// The frame's projected record of Gaussian j (k_project, dense arrays indexed by j):
+// The frame's projected record of Gaussian j (dense arrays indexed by j; k_project stores it for
+// the chunk-0 splats, k_records for the chunk-1 splats it needs):
 //   r01[2j]     cx, cy, e1x', e1y'      centre (pixels); quad axes e/|e|^2 * sqrt(log2 e)
 //   r01[2j+1]   e2x', e2y', log2(op), pixel box x (x0 | x1 << 16, u32 bits)
 //   r2[j]       depth key, tile count, pixel box x, pixel box y (u32 bits)
@@ -100,6 +101,9 @@ struct ProjParams {
     uint32_t* offsets;        // out: [256][parts_max] digit-0 counts per partition
     uint32_t parts_max;
     uint32_t* hist0;          // out: [kHistShards][256] digit-0 histogram (zeroed)
+    // k_records: unsaturated-tile SAT of chunk 0 (see BinParams::sat); rec_all = every visible
+    const uint32_t* sat;
+    int rec_all;
 };
 
 // Element filter of a radix pass (the first pass of a depth chunk decides chunk membership).
@@ -194,6 +198,7 @@ struct CompositeParams {
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, float4* shade, float4* cull,
                       hipStream_t s);
 void launch_project(const ProjParams& p, bool two_phase, hipStream_t s);
+void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 (or all) projected records
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, scan, emit, wide rows
 void launch_shade(const BinParams& p, hipStream_t s);  // composite records of the chunk's slots

@@ -227,10 +227,18 @@ __device__ __forceinline__ bool cull_keep(const ProjParams& p, float4 c, int row
              cx0 - hb > (float)p.W);
 }
 
-// One Gaussian: cull, footprint, depth key, tile rect and projected record; returns the depth key
-// (kSentinel when invisible).
-__device__ __forceinline__ uint32_t project_one(const ProjParams& p, uint32_t i, int row_lo, int row_hi,
-                                                uint32_t& my_vis, unsigned long long& my_k, bool cull) {
+// One Gaussian's projection: depth key, packed tile rect, tile count and projected record.
+struct Proj {
+    uint32_t key, prect, ntiles, bbx, bby;
+    float4 r0, r1;
+};
+
+// Cull, footprint, depth key, tile rect and projected record of Gaussian i; false (key =
+// kSentinel) when invisible.  Deterministic: k_records recomputes the same record bit for bit.
+__device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, int row_lo, int row_hi,
+                                             bool cull, Proj& o) {
+    o.key = kSentinel;
+    o.prect = kRectEmpty;
     const float4 g0 = p.geo[3 * (uint64_t)i], g1 = p.geo[3 * (uint64_t)i + 1], g2 = p.geo[3 * (uint64_t)i + 2];
         const float x = g0.x, y = g0.y, z = g0.z;
         const float sx = g1.x, sy = g1.y, sz = g1.z;
@@ -270,11 +278,7 @@ __device__ __forceinline__ uint32_t project_one(const ProjParams& p, uint32_t i,
                      cx0 + hb < -1.0f || cx0 - hb > (float)p.W)
                 pre = false;
         }
-        if (!pre) {
-            p.keys_out[i] = kSentinel;
-            p.rect_out[i] = kRectEmpty;
-            return kSentinel;
-        }
+        if (!pre) return false;
         const float logit = g0.w;
 
         float vz;
@@ -303,9 +307,9 @@ __device__ __forceinline__ uint32_t project_one(const ProjParams& p, uint32_t i,
         }
         vis = vis && pixel_rect(f.cx, f.cy, qhx, qhy, p.W, row_lo, row_hi, qxl, qxh, qyl, qyh);
 
-        uint32_t key = kSentinel, prect = kRectEmpty;
-        if (vis) {
-            key = sortable_key(vz);
+        if (!vis) return false;
+        {
+            const uint32_t key = sortable_key(vz);
             // binning rectangle: quad box intersected with the alpha >= 1/255 disc box, widened by
             // a small margin so that float rounding can never drop a covered pixel
             const float R = sqrtf(fmaxf(logf(255.0f * op), 0.0f));
@@ -321,25 +325,73 @@ __device__ __forceinline__ uint32_t project_one(const ProjParams& p, uint32_t i,
                 const uint32_t tx0 = (uint32_t)xl >> 4, tx1 = (uint32_t)xh >> 4,
                                ty0 = (uint32_t)yl >> 4, ty1 = (uint32_t)yh >> 4;
                 ntiles = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
-                prect = (tx1 - tx0 < 16 && ty1 - ty0 < 16)
+                o.prect = (tx1 - tx0 < 16 && ty1 - ty0 < 16)
                             ? (tx0 | (ty0 << 12) | ((tx1 - tx0) << 24) | ((ty1 - ty0) << 28))
                             : kRectLarge;
             }
-            // composite record (colour: k_bin_emit, only for splats that receive tile entries): u' = d.(e1/|e1|^2)*sqrt(log2 e), so u'^2+v'^2 = (u^2+v^2) log2 e and
+            // projected record (colour: k_shade, only for splats that receive tile entries):
+            // u' = d.(e1/|e1|^2)*sqrt(log2 e), so u'^2+v'^2 = (u^2+v^2) log2 e and
             // alpha = op * exp(-(u^2+v^2)) = exp2(log2(op) - (u'^2+v'^2))
             const float k1 = kSqrtLog2e / (f.e1x * f.e1x + f.e1y * f.e1y);
             const float k2 = kSqrtLog2e / (f.e2x * f.e2x + f.e2y * f.e2y);
-            float4* r = p.rec.r01 + 2 * (uint64_t)i;
-            r[0] = make_float4(f.cx, f.cy, f.e1x * k1, f.e1y * k1);
-            r[1] = make_float4(f.e2x * k2, f.e2y * k2, log2f(op), __uint_as_float(bbx));
-            p.rec.r2[i] = make_float4(__uint_as_float(key), __uint_as_float(ntiles), __uint_as_float(bbx),
-                                      __uint_as_float(bby));
-            ++my_vis;
-            my_k += ntiles;
+            o.r0 = make_float4(f.cx, f.cy, f.e1x * k1, f.e1y * k1);
+            o.r1 = make_float4(f.e2x * k2, f.e2y * k2, log2f(op), __uint_as_float(bbx));
+            o.key = key;
+            o.ntiles = ntiles;
+            o.bbx = bbx;
+            o.bby = bby;
         }
-        p.keys_out[i] = key;
-        p.rect_out[i] = prect;
-        return key;
+        return true;
+}
+
+__device__ __forceinline__ void store_records(const ProjParams& p, uint32_t i, const Proj& o) {
+    float4* r = p.rec.r01 + 2 * (uint64_t)i;
+    r[0] = o.r0;
+    r[1] = o.r1;
+    p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles), __uint_as_float(o.bbx),
+                              __uint_as_float(o.bby));
+}
+
+// k_project's per-Gaussian step: key and rect of every Gaussian; the 48-B record only for the
+// chunk-0 splats (key < thresh), the only ones a frame reads unless chunk 1 runs (k_records).
+__device__ __forceinline__ uint32_t project_one(const ProjParams& p, uint32_t i, int row_lo, int row_hi,
+                                                uint32_t& my_vis, unsigned long long& my_k, bool cull) {
+    Proj o;
+    if (project_core(p, i, row_lo, row_hi, cull, o)) {
+        if (o.key < p.thresh) store_records(p, i, o);
+        ++my_vis;
+        my_k += o.ntiles;
+    }
+    p.keys_out[i] = o.key;
+    p.rect_out[i] = o.prect;
+    return o.key;
+}
+
+// Records of the splats k_project did not store, before chunk 1's depth sort: visible Gaussians
+// with key >= thresh whose rect is wide or touches an unsaturated tile (the SAT of k_sat), or,
+// with rec_all (debug), every visible Gaussian.
+__global__ __launch_bounds__(256) void k_records(ProjParams p) {
+    const int row_lo = p.tile_row_begin * kTile;
+    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+    const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += gridDim.x * blockDim.x) {
+        const uint32_t key = p.keys_out[i];
+        if (key == kSentinel) continue;
+        if (!p.rec_all) {
+            if (key < p.thresh) continue;
+            const uint32_t pr = p.rect_out[i];
+            if (pr == kRectEmpty) continue;  // as tail_overlaps: no tile, never in chunk 1
+            if (pr != kRectLarge) {
+                const uint32_t x0 = pr & 0xfffu, y0 = (pr >> 12) & 0xfffu;
+                const uint32_t x1 = x0 + ((pr >> 24) & 15u), y1 = y0 + (pr >> 28);
+                const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
+                const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
+                if ((b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]) == 0u) continue;
+            }
+        }
+        Proj o;
+        if (project_core(p, i, row_lo, row_hi, false, o)) store_records(p, i, o);
+    }
 }
 
 // Per 4096-Gaussian partition (the radix partition of the first depth pass): project every
@@ -1350,6 +1402,12 @@ void launch_project(const ProjParams& p, bool two_phase, hipStream_t s) {
     else
         hipLaunchKernelGGL(k_project<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
 }
+void launch_records(const ProjParams& p, hipStream_t s) {
+    if (!p.n) return;
+    const uint32_t grid = std::min<uint32_t>((p.n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_records, dim3(grid), dim3(256), 0, s, p);
+}
+
 void launch_sort_pass(const SortPass& p, hipStream_t s) {
     if (!p.parts_max) return;
     const unsigned grid = std::min<uint32_t>(p.parts_max, kMaxGrid);

@@ -33,7 +33,7 @@ def frames_of(rows, key_start="k_project"):
     frames, cur = [], None
     for r in rows:
         n = short(r["Kernel_Name"])
-        if n == key_start:
+        if n.split("<")[0] == key_start:
             cur = []
             frames.append(cur)
         if cur is not None:
