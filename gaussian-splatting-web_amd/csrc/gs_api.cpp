@@ -141,6 +141,7 @@ struct gs_scene {
     uint32_t *keysA = nullptr, *valsA = nullptr, *auxA = nullptr;
     uint32_t *keysB = nullptr, *valsB = nullptr, *auxB = nullptr;
     float4* crec = nullptr;             // composite records, 3 float4 per slot
+    unsigned long long* keep_mask = nullptr;  // two-phase frames: k_cull's keep bits
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     // zero-per-frame block: FrameCtl | digit histograms of the 4 depth + 2 tile passes of each
     // chunk (kHistShards x 256 words each)
@@ -353,6 +354,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     ProjParams pp{};
     pp.geo = s->geo;
     pp.cull = s->cull;
+    pp.keep_mask = s->keep_mask;
     pp.n = n_tiles > 0 ? (uint32_t)s->n : 0u;
     std::memcpy(pp.V, uni + 0, 64);
     mat4_mul_ref(uni + 16, uni + 0, pp.PV);
@@ -360,11 +362,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.P00 = uni[16];
     pp.P11 = uni[21];
     pp.focal = (float)W * pp.P00 / 2.0f;
-    {
-        double f2 = 0;
-        for (int c = 0; c < 3; ++c)
-            for (int r = 0; r < 3; ++r) f2 += (double)uni[4 * c + r] * uni[4 * c + r];
-        pp.w3_fro2 = (float)(f2 * 1.0001);
+    {  // lambda_max of the 2x2 Gram matrix of W3's rows 0 and 1 (row r = V[r], V[4 + r], V[8 + r])
+        double g[2][2];
+        for (int r = 0; r < 2; ++r)
+            for (int q = 0; q < 2; ++q)
+                g[r][q] = (double)uni[r] * uni[q] + (double)uni[4 + r] * uni[4 + q] + (double)uni[8 + r] * uni[8 + q];
+        const double m = 0.5 * (g[0][0] + g[1][1]), h = 0.5 * (g[0][0] - g[1][1]);
+        const double lmax = m + std::sqrt(h * h + g[0][1] * g[0][1]);
+        pp.w01_spec2 = std::isfinite(lmax) ? (float)(lmax * 1.0001 + 1e-30) : INFINITY;  // NaN view: never cull
     }
     pp.W = W;
     pp.H = H;
@@ -674,6 +679,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->geo, 3 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->shade, (size_t)shade_stride(n_sh) * std::max<uint64_t>(n, 1));
             dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
+            dev_alloc(s->keep_mask, (size_t)(n / 64 + 1));
             dev_alloc(s->r01, 2 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->keysP, n); dev_alloc(s->rectP, n);
@@ -728,6 +734,7 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->geo);
     dev_free(s->shade);
     dev_free(s->cull);
+    dev_free(s->keep_mask);
     dev_free(s->r01);
     dev_free(s->r2);
     dev_free(s->keysP); dev_free(s->rectP);

@@ -85,7 +85,8 @@ struct ProjParams {
     float scale_mod;
     float P00, P11;
     float focal;              // W * P00 / 2 (src/simple_render.ts:273)
-    float w3_fro2;            // ||W3||_F^2 of the view's 3x3 block (conservative cull bound)
+    float w01_spec2;          // lambda_max(W01 W01^T), W01 = rows 0-1 of the view's 3x3 block
+                              // (x 1.0001): the conservative cull bound's camera factor
     int W, H;
     int tile_row_begin, tile_row_end, tiles_x;
     uint32_t* keys_out;       // [n]: depth key or kSentinel
@@ -101,6 +102,8 @@ struct ProjParams {
     uint32_t* offsets;        // out: [256][parts_max] digit-0 counts per partition
     uint32_t parts_max;
     uint32_t* hist0;          // out: [kHistShards][256] digit-0 histogram (zeroed)
+    // two-phase frames: k_cull's keep bit per Gaussian (bit i%64 of word i/64)
+    unsigned long long* keep_mask;
     // k_records: unsaturated-tile SAT of chunk 0 (see BinParams::sat); rec_all = every visible
     const uint32_t* sat;
     int rec_all;

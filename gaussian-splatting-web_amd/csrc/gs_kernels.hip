@@ -220,7 +220,7 @@ __device__ __forceinline__ bool cull_keep(const ProjParams& p, float4 c, int row
     const float cyc = ((p.PV[1] * x + p.PV[5] * y) + p.PV[9] * z) + p.PV[13];
     const float a = p.focal / vz0;
     const float trs = c.w * p.scale_mod * p.scale_mod;
-    const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w3_fro2 * trs + 0.6f)), 0.45f) * 1.02f + 2.0f;
+    const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w01_spec2 * trs + 0.6f)), 0.45f) * 1.02f + 2.0f;
     const float cx0 = (cxc / cw + 1.0f) * (float)p.W * 0.5f;
     const float cy0 = (1.0f - cyc / cw) * (float)p.H * 0.5f;
     return !(cy0 + hb < (float)row_lo - 1.0f || cy0 - hb > (float)row_hi + 1.0f || cx0 + hb < -1.0f ||
@@ -246,8 +246,10 @@ __device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, in
 
         // Cheap conservative cull (a row strip, or off screen): bound the quad's half extent by
         //   2 (s1 + s2) <= 4 max(sqrt(2 (d1 + d2)), 0.45),  d1 + d2 = C00 + C11 + 0.6,
-        //   C00 + C11 <= (focal/vz)^2 ||W3||_F^2 ||R(q) diag(s mod)||_F^2
-        // (lambda1 <= trace of the PSD 2-D covariance; C = a^2 (W3 Sigma W3^T)[0:2,0:2]) and skip
+        //   C00 + C11 = a^2 tr(W01 Sigma W01^T) <= a^2 lambda_max(W01 W01^T) tr(Sigma),
+        //   tr(Sigma) = ||R(q) diag(s mod)||_F^2,  a = focal/vz
+        // (lambda1 <= trace of the PSD 2-D covariance; tr(A S) <= lambda_max(A) tr(S) for PSD
+        // A, S; W01 = the rows of W3 that reach C[0:2,0:2]) and skip
         // the full projection when that box misses the strip; only provably invisible Gaussians
         // are skipped, so the visible set is unchanged (a NaN bound never culls).
         bool pre = true;
@@ -269,7 +271,7 @@ __device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, in
                               (r01 * r01 + r11 * r11 + r21 * r21) * msy * msy +
                               (r02 * r02 + r12 * r12 + r22 * r22) * msz * msz;
             const float a = p.focal / vz0;
-            const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w3_fro2 * trs + 0.6f)), 0.45f) * 1.02f + 2.0f;
+            const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w01_spec2 * trs + 0.6f)), 0.45f) * 1.02f + 2.0f;
             const float cx0 = (cxc / cw + 1.0f) * (float)p.W * 0.5f;
             const float cy0 = (1.0f - cyc / cw) * (float)p.H * 0.5f;
             if (!((cw > 0.0f) && (cz >= 0.0f) && (cz <= cw)))  // :230 + near/far: dropped anyway
@@ -394,13 +396,26 @@ __global__ __launch_bounds__(256) void k_records(ProjParams p) {
     }
 }
 
+// Two-phase frames, first phase: the conservative cull of every Gaussian from its 16-B cull plane,
+// one Gaussian per thread at full occupancy (a streaming read), as a keep bitmask for k_project.
+__global__ __launch_bounds__(256) void k_cull(ProjParams p) {
+    const int row_lo = p.tile_row_begin * kTile;
+    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i - lane < p.n; i += gridDim.x * blockDim.x) {
+        const bool keep = i < p.n && cull_keep(p, p.cull[i], row_lo, row_hi);
+        const unsigned long long b = __ballot(keep);
+        if (lane == 0) p.keep_mask[i >> 6] = b;
+    }
+}
+
 // Per 4096-Gaussian partition (the radix partition of the first depth pass): project every
 // Gaussian, then do the first pass's upsweep here: the digit-0 histogram of the chunk-0 splats
 // (visible, key < thresh) and their order-preserving compaction to the front of the partition
 // in the pass-0 input arrays, so that pass reads only them.
-// TWO_PHASE (row strips, mostly off-screen frames): phase A reads only the 16-B cull planes and
-// keeps an order-preserving list of the survivors in LDS; phase B projects the survivors densely,
-// so culled Gaussians cost neither their 44 B nor divergent lanes.
+// TWO_PHASE (row strips, mostly off-screen frames): phase A reads k_cull's keep bits and keeps an
+// order-preserving list of the survivors in LDS; phase B projects the survivors densely, so culled
+// Gaussians cost neither their 48 B nor divergent lanes.
 template <bool TWO_PHASE>
 __global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
     __shared__ unsigned long long s_k;
@@ -435,15 +450,12 @@ __global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
         if (TWO_PHASE) {
             for (int it = 0; it < kSortIPT; ++it) {
                 const uint32_t i = p0 + it * kProjThreads + tid;
-                bool keep = false;
-                if (i < p.n) {
-                    keep = cull_keep(p, p.cull[i], row_lo, row_hi);
-                    if (!keep) {
-                        p.keys_out[i] = kSentinel;
-                        p.rect_out[i] = kRectEmpty;
-                    }
+                // the wave's 64 Gaussians are one mask word (zero bits past n)
+                const uint64_t b = i - lane < p.n ? p.keep_mask[(i - lane) >> 6] : 0ull;
+                if (i < p.n && !((b >> lane) & 1ull)) {
+                    p.keys_out[i] = kSentinel;
+                    p.rect_out[i] = kRectEmpty;
                 }
-                const uint64_t b = __ballot(keep);
                 if (lane == 0) s_mask[it][w] = b;
             }
             prefix();
@@ -995,70 +1007,89 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
 // projected record, written densely at the slot.  16 lanes per splat: lanes 0-12 read the
 // line-aligned shading block (one coalesced load), lanes 14-15 the 32-B record quads; each lane
 // evaluates its own coefficients' terms and the group sums them with xor shuffles.
+// Latency: a wave takes 64 slots at once (one coalesced load of their Gaussian indices) and keeps
+// kShadeU groups of 4 splats' block loads in flight before evaluating any of them.
+constexpr int kShadeU = 4;
+
+__device__ __forceinline__ void shade_eval(const BinParams& p, float4 q, uint32_t l, uint32_t nq,
+                                           uint32_t ncoef, bool active, uint32_t slot) {
+    const uint32_t gl = lane_id() & ~15u;
+    const float px = __shfl(q.x, gl, 64), py = __shfl(q.y, gl, 64), pz = __shfl(q.z, gl, 64);
+    const float dx = px - p.cam[0], dy = py - p.cam[1], dz = pz - p.cam[2];
+    const float dl = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float x = dx / dl, y = dy / dl, z = dz / dl;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
+    float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
+    const float v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uint32_t i = 4 * l + t;  // float index in the block: 3 + 3k + c
+        if (l >= nq || i < 3 || i >= 3 + ncoef) continue;
+        const uint32_t k = (i - 3) / 3, c = (i - 3) % 3;
+        float b;
+        switch (k) {
+            case 0: b = 0.28209479177387814f; break;
+            case 1: b = 0.4886025119029199f * -y; break;
+            case 2: b = 0.4886025119029199f * z; break;
+            case 3: b = 0.4886025119029199f * -x; break;
+            case 4: b = 1.0925484305920792f * xy; break;
+            case 5: b = -1.0925484305920792f * yz; break;
+            case 6: b = 0.31539156525252005f * (2.0f * zz - xx - yy); break;
+            case 7: b = -1.0925484305920792f * xz; break;
+            case 8: b = 0.5462742152960396f * (xx - yy); break;
+            case 9: b = -0.5900435899266435f * y * (3.0f * xx - yy); break;
+            case 10: b = 2.890611442640554f * xy * z; break;
+            case 11: b = -0.4570457994644658f * y * (4.0f * zz - xx - yy); break;
+            case 12: b = 0.3731763325901154f * z * (2.0f * zz - 3.0f * xx - 3.0f * yy); break;
+            case 13: b = -0.4570457994644658f * x * (4.0f * zz - xx - yy); break;
+            case 14: b = 1.445305721320277f * z * (xx - yy); break;
+            default: b = -0.5900435899266435f * x * (xx - 3.0f * yy); break;
+        }
+        const float bv = b * v[t];
+        acc0 += c == 0 ? bv : 0.0f;
+        acc1 += c == 1 ? bv : 0.0f;
+        acc2 += c == 2 ? bv : 0.0f;
+    }
+#pragma unroll
+    for (int d = 8; d >= 1; d >>= 1) {
+        acc0 += __shfl_xor(acc0, d, 64);
+        acc1 += __shfl_xor(acc1, d, 64);
+        acc2 += __shfl_xor(acc2, d, 64);
+    }
+    if (active) {
+        float4* o = p.crec + 3 * (uint64_t)slot;
+        if (l >= 14) o[l - 14] = q;
+        if (l == 0)
+            o[2] = make_float4(fmaxf(acc0 + 0.5f, 0.0f), fmaxf(acc1 + 0.5f, 0.0f), fmaxf(acc2 + 0.5f, 0.0f), 0.0f);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_shade(BinParams p) {
     const uint32_t g0 = p.chunk ? p.ctl->shade_n[0] : 0u;
     const uint32_t n = p.ctl->shade_n[p.chunk];
     const uint32_t lane = lane_id(), l = lane & 15;
     const uint32_t nq = shade_quads(p.n_sh), ncoef = 3 * (uint32_t)p.n_sh;
     const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
-    for (uint32_t base = wave * 4; base < n; base += nwaves * 4) {  // wave-uniform: shuffles below
-        const uint32_t gi = base + (lane >> 4);
-        const bool active = gi < n;
-        const uint32_t slot = g0 + gi;
-        const uint32_t j = active ? p.shade_list[slot] : 0u;
-        float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (active) {  // lanes 0..nq-1: the shading block; lanes 14, 15: record quads r01
-            if (l < nq) q = p.shade[(uint64_t)j * p.shade_stride + l];
-            else if (l >= 14) q = p.rec.r01[2 * (uint64_t)j + (l - 14)];
-        }
-        const uint32_t gl = lane & ~15u;
-        const float px = __shfl(q.x, gl, 64), py = __shfl(q.y, gl, 64), pz = __shfl(q.z, gl, 64);
-        const float dx = px - p.cam[0], dy = py - p.cam[1], dz = pz - p.cam[2];
-        const float dl = sqrtf(dx * dx + dy * dy + dz * dz);
-        const float x = dx / dl, y = dy / dl, z = dz / dl;
-        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
-        float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
-        const float v[4] = {q.x, q.y, q.z, q.w};
+    for (uint32_t base = wave * 64; base < n; base += nwaves * 64) {  // wave-uniform: shuffles below
+        const uint32_t jl = base + lane < n ? p.shade_list[g0 + base + lane] : 0u;
+        const uint32_t cnt = min(64u, n - base);
+        for (uint32_t sub = 0; sub < cnt; sub += 4 * kShadeU) {
+            float4 q[kShadeU];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const uint32_t i = 4 * l + t;  // float index in the block: 3 + 3k + c
-            if (l >= nq || i < 3 || i >= 3 + ncoef) continue;
-            const uint32_t k = (i - 3) / 3, c = (i - 3) % 3;
-            float b;
-            switch (k) {
-                case 0: b = 0.28209479177387814f; break;
-                case 1: b = 0.4886025119029199f * -y; break;
-                case 2: b = 0.4886025119029199f * z; break;
-                case 3: b = 0.4886025119029199f * -x; break;
-                case 4: b = 1.0925484305920792f * xy; break;
-                case 5: b = -1.0925484305920792f * yz; break;
-                case 6: b = 0.31539156525252005f * (2.0f * zz - xx - yy); break;
-                case 7: b = -1.0925484305920792f * xz; break;
-                case 8: b = 0.5462742152960396f * (xx - yy); break;
-                case 9: b = -0.5900435899266435f * y * (3.0f * xx - yy); break;
-                case 10: b = 2.890611442640554f * xy * z; break;
-                case 11: b = -0.4570457994644658f * y * (4.0f * zz - xx - yy); break;
-                case 12: b = 0.3731763325901154f * z * (2.0f * zz - 3.0f * xx - 3.0f * yy); break;
-                case 13: b = -0.4570457994644658f * x * (4.0f * zz - xx - yy); break;
-                case 14: b = 1.445305721320277f * z * (xx - yy); break;
-                default: b = -0.5900435899266435f * x * (xx - 3.0f * yy); break;
+            for (int u = 0; u < kShadeU; ++u) {
+                const uint32_t k = sub + 4 * u + (lane >> 4);  // splat within the 64
+                const uint32_t j = __shfl(jl, k & 63, 64);
+                q[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (k < cnt) {  // lanes 0..nq-1: the shading block; lanes 14, 15: record quads r01
+                    if (l < nq) q[u] = p.shade[(uint64_t)j * p.shade_stride + l];
+                    else if (l >= 14) q[u] = p.rec.r01[2 * (uint64_t)j + (l - 14)];
+                }
             }
-            const float bv = b * v[t];
-            acc0 += c == 0 ? bv : 0.0f;
-            acc1 += c == 1 ? bv : 0.0f;
-            acc2 += c == 2 ? bv : 0.0f;
-        }
 #pragma unroll
-        for (int d = 8; d >= 1; d >>= 1) {
-            acc0 += __shfl_xor(acc0, d, 64);
-            acc1 += __shfl_xor(acc1, d, 64);
-            acc2 += __shfl_xor(acc2, d, 64);
-        }
-        if (active) {
-            float4* o = p.crec + 3 * (uint64_t)slot;
-            if (l >= 14) o[l - 14] = q;
-            if (l == 0)
-                o[2] = make_float4(fmaxf(acc0 + 0.5f, 0.0f), fmaxf(acc1 + 0.5f, 0.0f), fmaxf(acc2 + 0.5f, 0.0f), 0.0f);
+            for (int u = 0; u < kShadeU; ++u) {
+                const uint32_t k = sub + 4 * u + (lane >> 4);
+                shade_eval(p, q[u], l, nq, ncoef, k < cnt, g0 + base + k);
+            }
         }
     }
 }
@@ -1213,7 +1244,12 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     __shared__ uint32_t sN[2][2][2];           // per half, per producing wave: list length
     __shared__ uint32_t s_sat;                 // slot that saturated the last wave
     const int tid = threadIdx.x;
-    const int tile = blockIdx.x;
+    // XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch), so XCD b % 8 gets
+    // the contiguous band of tiles [(b % 8) * per, (b % 8 + 1) * per): a splat's neighbouring
+    // tiles then read its record through one L2
+    const int per = (p.n_tiles + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= p.n_tiles) return;
     if (p.mode == kCompSecond && p.done[tile]) return;
     const int h = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
@@ -1397,8 +1433,11 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, flo
 }
 void launch_project(const ProjParams& p, bool two_phase, hipStream_t s) {
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, sort_parts(p.n)));
-    if (two_phase)
+    if (two_phase) {
+        const unsigned cgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (p.n + 255) / 256));
+        hipLaunchKernelGGL(k_cull, dim3(cgrid), dim3(256), 0, s, p);
         hipLaunchKernelGGL(k_project<true>, dim3(grid), dim3(kProjThreads), 0, s, p);
+    }
     else
         hipLaunchKernelGGL(k_project<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
 }
@@ -1440,10 +1479,11 @@ void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max,
 }
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;
+    const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);  // see k_composite's tile order
     if (accum_fp16)
-        hipLaunchKernelGGL(k_composite<true>, dim3(p.n_tiles), dim3(128), 0, s, p);
+        hipLaunchKernelGGL(k_composite<true>, dim3(grid), dim3(128), 0, s, p);
     else
-        hipLaunchKernelGGL(k_composite<false>, dim3(p.n_tiles), dim3(128), 0, s, p);
+        hipLaunchKernelGGL(k_composite<false>, dim3(grid), dim3(128), 0, s, p);
 }
 
 }  // namespace gs

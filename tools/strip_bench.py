@@ -17,13 +17,18 @@ def main():
     aos = gs.synth_aos(N, 6, W, H)
     u = gs.bench_uniforms(W, H)
     ctx = gs.Context(0)
+    base = 0.0
     sc = gs.Scene(ctx, aos, N, 16)
-    for G in (1, 2, 4, 8):
+    gl = tuple(int(x) for x in os.environ.get("GS", "1,2,4,8").split(","))
+    only = int(os.environ["STRIP"]) if "STRIP" in os.environ else None
+    for G in gl:
         rows = strip_geometry(H, 0, G)[1]
         buf = gs.DeviceBuffer(rows * W * 16)
         worst = 0.0
         line = []
         for g in range(G):
+            if only is not None and g != only:
+                continue
             o = gs.make_opts(strip_index=g, strip_count=G, timing=1)
             for _ in range(5):
                 sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
@@ -38,7 +43,9 @@ def main():
             worst = max(worst, ms)
             line.append("%d:%.3f(p%.3f s%.3f b%.3f t%.3f c%.3f)" % (g, ms, st["ms_project"], st["ms_sort"],
                                                                   st["ms_bin"], st["ms_tile_sort"], st["ms_composite"]))
-        print("G=%d worst %.3f ms  speedup-bound %.2f  | %s" % (G, worst, 0, " ".join(line)), flush=True)
+        base = worst if G == 1 else base
+        print("G=%d worst %.3f ms  speedup-bound %.2f  | %s" % (G, worst, base / worst if worst else 0.0,
+                                                            " ".join(line)), flush=True)
     sc.close()
     ctx.close()
 
