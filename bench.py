@@ -27,14 +27,16 @@ import gsplat_amd as gs  # noqa: E402
 from gsplat_amd.strips import strip_geometry  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 4 cycles at 2.4 GHz
+VALU_PEAK = 256 * 4 * 2.4e9 / 4  # wave instructions / s
 
 
-def algorithmic_bytes(stage, n, n_vis, k, W, H):
-    """Bytes a kernel must move per launch (DESIGN.md §Roofline)."""
+def algorithmic_bytes(stage, n, n_vis, k, W, H, n_chunk0=None):
+    """Bytes a kernel must move per launch (DESIGN.md §4)."""
     if stage == "project":
-        # read the 11 geometry planes (44 B) and write key + packed tile rect (8 B) of every
-        # Gaussian; write the 48-B projected record of every visible one
-        return 52 * n + 48 * n_vis
+        # read the 48-B geometry record and write key + packed tile rect (8 B) of every Gaussian;
+        # write the 48-B projected record and the 12-B compacted sort element of every chunk-0 splat
+        return 56 * n + 60 * (n_vis if n_chunk0 is None else n_chunk0)
     if stage == "composite":
         # per (tile, splat) entry: the 4-B slot and the 48-B composite record; RGBA f16 out
         return 52 * k + 8 * W * H
@@ -63,6 +65,18 @@ def pmc_traffic(kernel):
                 continue  # depth passes only
             tot += e["traffic_bytes"]
     return (tot if tot else None), prof[-1]
+
+
+def pmc_valu(kernel):
+    """VALU wave instructions per frame of `kernel` from the committed PMC profile (SQ_INSTS_VALU)."""
+    names = {"composite": "k_composite<false>", "project": "k_project", "sort": "k_radix_"}
+    prof = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc.json")) \
+        if os.path.isdir(os.path.join(ROOT, "profiles")) else []
+    if not prof:
+        return None
+    d = json.load(open(os.path.join(ROOT, "profiles", prof[-1])))
+    tot = sum(e.get("SQ_INSTS_VALU", 0.0) for lab, e in d.items() if lab.startswith(names[kernel]))
+    return tot or None
 
 
 def frame_bytes(n, n_vis, k, W, H):
@@ -175,9 +189,11 @@ def main():
     stages = {"project": st["ms_project"], "composite": st["ms_composite"], "sort": st["ms_sort"]}
     dom = max(stages, key=stages.get)
     rows_here = max(0, min(t1 * 16, H) - row0)
-    a_bytes = algorithmic_bytes(dom, N, st["n_vis"], st["k_entries"], W, rows_here)
+    a_bytes = algorithmic_bytes(dom, N, st["n_vis"], st["k_entries"], W, rows_here,
+                                n_chunk0=int(round(st["chunk_fraction"] * st["n_vis"])))
     achieved = a_bytes / (stages[dom] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dom)
+    valu = pmc_valu(dom) if world == 1 else None
     fb = frame_bytes(N, n_vis_all, k_all, W, H)
 
     if rank == 0:
@@ -214,6 +230,13 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": int(a_bytes),
                          "per": "frame (the kernel's launches in one frame, HIP events on the render stream)"},
+            # the dominant kernel's real bound: VALU issue (PMC instruction count of this command's
+            # committed profile / the live event-timed duration)
+            "valu_roofline": ({"kernel": dom, "insts_per_launch": int(valu),
+                               "achieved": round(valu / (stages[dom] * 1e-3) / 1e9, 1),
+                               "peak": VALU_PEAK / 1e9, "unit": "G wave-instr/s",
+                               "frac": round(valu / (stages[dom] * 1e-3) / VALU_PEAK, 4),
+                               "source": traffic_src} if valu else None),
             "frame_roofline": {"bytes": int(fb), "frac": round(fb / (ms * 1e-3) / (world * HBM_PEAK), 4),
                                "compulsory_frac": round((236 * N + 16 * W * H) / (ms * 1e-3) / (world * HBM_PEAK), 4),
                                "formula": "236N + 148N_vis + 48K + 16WH (SURVEY 8d)"},
