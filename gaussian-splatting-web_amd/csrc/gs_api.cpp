@@ -134,7 +134,6 @@ struct gs_scene {
     float4* geo = nullptr;              // geometry records (3 float4 per Gaussian)
     float4* shade = nullptr;            // shading blocks (shade_stride float4 per Gaussian)
     float4* cull = nullptr;             // cull planes (two-phase projection)
-    float4* r01 = nullptr;              // projected records (see gs_device.h)
     float4* r2 = nullptr;
     // k_project output (depth key, packed tile rect per Gaussian), then the depth sort ping-pong
     uint32_t *keysP = nullptr, *rectP = nullptr;
@@ -185,7 +184,9 @@ static constexpr size_t kHistWords = kHistShards * 256;
 static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 12 * kHistWords * 4;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
-static Records records(gs_scene* s) { return Records{s->r01, s->r2}; }
+static Records records(gs_scene* s) {
+    return Records{s->shade, s->r2, shade_stride(s->n_sh), shade_quads(s->n_sh)};
+}
 
 static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
     if (k <= s->kcap && s->tkA) return;
@@ -680,7 +681,6 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->shade, (size_t)shade_stride(n_sh) * std::max<uint64_t>(n, 1));
             dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->keep_mask, (size_t)(n / 64 + 1));
-            dev_alloc(s->r01, 2 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->keysP, n); dev_alloc(s->rectP, n);
             dev_alloc(s->keysA, n); dev_alloc(s->valsA, n); dev_alloc(s->auxA, n);
@@ -735,7 +735,6 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->shade);
     dev_free(s->cull);
     dev_free(s->keep_mask);
-    dev_free(s->r01);
     dev_free(s->r2);
     dev_free(s->keysP); dev_free(s->rectP);
     dev_free(s->keysA); dev_free(s->valsA); dev_free(s->auxA);
@@ -942,8 +941,9 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
             rp.rec_all = 1;
             launch_records(rp, c->stream);
             HIPCHK(hipStreamSynchronize(c->stream));
+            const Records rc = records(s);  // r01 lives in the shading blocks' padding
             std::vector<float> a((size_t)m * 8), b((size_t)m * 4);
-            HIPCHK(hipMemcpy(a.data(), s->r01, a.size() * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy2D(a.data(), 32, rc.r01 + rc.off, (size_t)rc.stride * 16, 32, m, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(b.data(), s->r2, b.size() * 4, hipMemcpyDeviceToHost));
             for (uint64_t j = 0; j < m; ++j) {
                 std::memcpy(out16 + 16 * j, &a[8 * j], 32);

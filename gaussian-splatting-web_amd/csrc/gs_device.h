@@ -57,24 +57,30 @@ struct FrameCtl {                 // zeroed at the start of every frame
 // survivors of the cull), a 16-B cull plane (x, y, z, ||R(q) diag(s)||_F^2), and one
 // shading block per Gaussian [x, y, z, sh[k][c] at 3 + 3k + c] of shade_stride float4 (a power
 // of two, so a block never straddles more 128-B lines than it must; 256 B at SH degree 3).
-// The frame's projected record of Gaussian j (dense arrays indexed by j; k_project stores it for
-// the chunk-0 splats, k_records for the chunk-1 splats it needs):
-//   r01[2j]     cx, cy, e1x', e1y'      centre (pixels); quad axes e/|e|^2 * sqrt(log2 e)
-//   r01[2j+1]   e2x', e2y', log2(op), pixel box x (x0 | x1 << 16, u32 bits)
-//   r2[j]       depth key, tile count, pixel box x, pixel box y (u32 bits)
+// The frame's projected record of Gaussian j (k_project stores it for the chunk-0 splats,
+// k_records for the chunk-1 splats it needs):
+//   r01 = quads shade_quads(n_sh), +1 of j's shading block (its padding), so k_shade reads the
+//         record with the block: cx, cy, e1x', e1y' | e2x', e2y', log2(op), pixel box x
+//         (centre in pixels; quad axes e/|e|^2 * sqrt(log2 e); box x0 | x1 << 16, u32 bits)
+//   r2[j] = depth key, tile count, pixel box x, pixel box y (u32 bits), dense
 // Composite record, 3 float4 per binned splat at its slot g (depth-rank order of the splats
 // that received entries; written by k_shade; the tile lists hold g):
-//   [0] = r01[2j], [1] = r01[2j+1], [2] r, g, b, 0
+//   [0], [1] = the r01 quads, [2] r, g, b, 0
 __host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
-__host__ __device__ inline uint32_t shade_stride(int n_sh) {
-    const uint32_t q = shade_quads(n_sh);
-    return q <= 2 ? 2 : q <= 4 ? 4 : q <= 8 ? 8 : 16;
+__host__ __device__ inline uint32_t shade_stride(int n_sh) {  // block + 2 record quads, power of 2
+    const uint32_t q = shade_quads(n_sh) + 2;
+    return q <= 4 ? 4 : q <= 8 ? 8 : 16;
 }
 
 struct Records {
-    float4* r01;
+    float4* r01;      // the shading blocks (records at quad `off` of each block)
     float4* r2;
+    uint32_t stride;  // float4 per block (shade_stride)
+    uint32_t off;     // shade_quads(n_sh)
 };
+__host__ __device__ inline float4* rec_r01(const Records& r, uint64_t j) {
+    return r.r01 + j * r.stride + r.off;
+}
 
 struct ProjParams {
     const float4* geo;        // [n][3] geometry records

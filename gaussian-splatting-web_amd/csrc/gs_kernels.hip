@@ -347,7 +347,7 @@ __device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, in
 }
 
 __device__ __forceinline__ void store_records(const ProjParams& p, uint32_t i, const Proj& o) {
-    float4* r = p.rec.r01 + 2 * (uint64_t)i;
+    float4* r = rec_r01(p.rec, i);
     r[0] = o.r0;
     r[1] = o.r1;
     p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles), __uint_as_float(o.bbx),
@@ -1004,8 +1004,8 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
 
 // Composite records of this chunk's slots: colour (src/simple_render.ts:26-66, :321-322:
 // dir = normalize(p - camPos), SH to degree 3, + 0.5, max(., 0)) plus the footprint words of the
-// projected record, written densely at the slot.  16 lanes per splat: lanes 0-12 read the
-// line-aligned shading block (one coalesced load), lanes 14-15 the 32-B record quads; each lane
+// projected record, written densely at the slot.  16 lanes per splat read the line-aligned
+// shading block with the 32-B record in its padding (one coalesced load); each lane
 // evaluates its own coefficients' terms and the group sums them with xor shuffles.
 // Latency: a wave takes 64 slots at once (one coalesced load of their Gaussian indices) and keeps
 // kShadeU groups of 4 splats' block loads in flight before evaluating any of them.
@@ -1058,7 +1058,7 @@ __device__ __forceinline__ void shade_eval(const BinParams& p, float4 q, uint32_
     }
     if (active) {
         float4* o = p.crec + 3 * (uint64_t)slot;
-        if (l >= 14) o[l - 14] = q;
+        if (l >= nq && l < nq + 2) o[l - nq] = q;
         if (l == 0)
             o[2] = make_float4(fmaxf(acc0 + 0.5f, 0.0f), fmaxf(acc1 + 0.5f, 0.0f), fmaxf(acc2 + 0.5f, 0.0f), 0.0f);
     }
@@ -1080,10 +1080,8 @@ __global__ __launch_bounds__(256) void k_shade(BinParams p) {
                 const uint32_t k = sub + 4 * u + (lane >> 4);  // splat within the 64
                 const uint32_t j = __shfl(jl, k & 63, 64);
                 q[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                if (k < cnt) {  // lanes 0..nq-1: the shading block; lanes 14, 15: record quads r01
-                    if (l < nq) q[u] = p.shade[(uint64_t)j * p.shade_stride + l];
-                    else if (l >= 14) q[u] = p.rec.r01[2 * (uint64_t)j + (l - 14)];
-                }
+                // lanes 0..nq-1: the shading block; lanes nq, nq+1: the record quads r01 in its padding
+                if (k < cnt && l < nq + 2) q[u] = p.shade[(uint64_t)j * p.shade_stride + l];
             }
 #pragma unroll
             for (int u = 0; u < kShadeU; ++u) {
