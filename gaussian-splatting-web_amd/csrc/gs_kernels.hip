@@ -1235,9 +1235,9 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <bool FP16_TARGET>
 __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
-    __shared__ float4 sA[2][kCompBatch];       // cx, cy, a, b
-    __shared__ float4 sB[2][kCompBatch];       // c, d, log2(op), composite slot (bits)
-    __shared__ float4 sC[2][kCompBatch];       // r, g, b, -
+    // staged record per batch entry: [0] c0u, c0v, a, b  [1] c, d, log2(op), slot (bits)
+    // [2] r, g, b, -   with u = a lx + b ly + c0u, v = c lx + d ly + c0v in tile-local pixels
+    __shared__ float4 sR[2][kCompBatch][3];
     __shared__ uint8_t sL[2][2][kCompBatch];   // per half: batch indices, segment = producing wave
     __shared__ uint32_t sN[2][2][2];           // per half, per producing wave: list length
     __shared__ uint32_t s_sat;                 // slot that saturated the last wave
@@ -1254,8 +1254,8 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     const int tx0 = tx * kTile, ty0 = ty * kTile;
     const int px = tx0 + h * 8 + (lane & 7), py = ty0 + (lane >> 3);  // pixels (px, py), (px, py + 8)
     const bool in0 = px < p.W && py < p.H, in1 = px < p.W && py + 8 < p.H;
-    const float fx = (float)px + 0.5f;
-    const f2 fy = {(float)py + 0.5f, (float)py + 8.5f};
+    const float lx = (float)(px - tx0) + 0.5f;  // tile-local pixel centres
+    const f2 ly = {(float)(py - ty0) + 0.5f, (float)(py - ty0) + 8.5f};
     const uint2 range = p.ranges[tile];
     const float4* __restrict__ rec = p.rec;
     const uint32_t* __restrict__ tvals = p.tvals;
@@ -1297,9 +1297,13 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
         }
     };
     auto park = [&](int buf) {
-        sA[buf][tid] = ga;
-        sB[buf][tid] = make_float4(gb.x, gb.y, gb.z, __uint_as_float(gs_));  // box x: used below only
-        sC[buf][tid] = gc;
+        // offsets of the axes' linear forms at the tile origin (explicit roundings, see blend)
+        const float cxr = ga.x - (float)tx0, cyr = ga.y - (float)ty0;
+        const float c0u = -__builtin_fmaf(cxr, ga.z, cyr * ga.w);
+        const float c0v = -__builtin_fmaf(cxr, gb.x, cyr * gb.y);
+        sR[buf][tid][0] = make_float4(c0u, c0v, ga.z, ga.w);
+        sR[buf][tid][1] = make_float4(gb.x, gb.y, gb.z, __uint_as_float(gs_));  // box x: used below only
+        sR[buf][tid][2] = gc;
         const uint32_t bx = __float_as_uint(gb.w);
         const int x0 = (int)(bx & 0xffffu), x1 = (int)(bx >> 16);
 #pragma unroll
@@ -1312,15 +1316,13 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
         }
     };
     auto blend = [&](int k, int cur) {
-        const float4 A = sA[cur][k];
-        const float4 B = sB[cur][k];
-        const float4 C = sC[cur][k];
+        const float4 A = sR[cur][k][0];
+        const float4 B = sR[cur][k][1];
+        const float4 C = sR[cur][k][2];
         // every rounding is spelled out (explicit fma or contraction off), so each inlined copy of
         // this blend rounds identically and the image cannot depend on where batches split
-        const float dx = fx - A.x;
-        const f2 dy = fy - A.y;
-        const f2 u = __builtin_elementwise_fma(dy, (f2)A.w, (f2)(dx * A.z));
-        const f2 v = __builtin_elementwise_fma(dy, (f2)B.y, (f2)(dx * B.x));
+        const f2 u = __builtin_elementwise_fma(ly, (f2)A.w, (f2)__builtin_fmaf(lx, A.z, A.x));
+        const f2 v = __builtin_elementwise_fma(ly, (f2)B.y, (f2)__builtin_fmaf(lx, B.x, A.y));
         const f2 qd = __builtin_elementwise_fma(u, u, v * v);
         const f2 e = (f2)B.z - qd;
         const float a0 = __builtin_amdgcn_exp2f(e.x), a1 = __builtin_amdgcn_exp2f(e.y);
@@ -1369,21 +1371,24 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
                 const int cnt = (int)sN[cur][h][seg];
                 const uint8_t* list = &sL[cur][h][seg * 64];
                 int k = 0;
-                for (; k + 1 < cnt; k += 2) {
-                    const int i0 = list[k], i1 = list[k + 1];
-                    blend(i0, cur);
-                    blend(i1, cur);
+                for (; k + 3 < cnt; k += 4) {  // saturation checked every 4 splats
+                    const int i3 = list[k + 3];
+                    blend(list[k], cur);
+                    blend(list[k + 1], cur);
+                    blend(list[k + 2], cur);
+                    blend(i3, cur);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sB[cur][i1].w));
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][i3][1].w));
                         break;
                     }
                 }
-                if (wave_live && k < cnt) {
-                    blend(list[k], cur);
+                for (; wave_live && k < cnt; ++k) {
+                    const int ik = list[k];
+                    blend(ik, cur);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sB[cur][list[k]].w));
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][ik][1].w));
                     }
                 }
             }

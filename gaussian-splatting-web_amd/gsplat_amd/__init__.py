@@ -14,7 +14,7 @@ import weakref
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libgsplat.so")
+LIB_PATH = os.environ.get("GSPLAT_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libgsplat.so")
 
 GS_OK = 0
 GS_ACCUM_FP32, GS_ACCUM_FP16_TARGET = 0, 1
