@@ -149,6 +149,7 @@ struct gs_scene {
     uint32_t* hist = nullptr;
     uint32_t* bin_part = nullptr;       // bin_parts(N) + 1
     uint32_t* shade_list = nullptr;     // N: Gaussian index of each composite slot
+    uint32_t* rank_cnt = nullptr;       // N: binning scratch (entries per depth rank)
     uint32_t* part_count = nullptr;     // sort_parts(N): chunk-0 splats per projection partition
     // tile lists
     uint64_t kcap = 0;
@@ -158,8 +159,7 @@ struct gs_scene {
     uint8_t* done = nullptr;
     uint32_t* sat = nullptr;            // (strip rows + 1) x (tiles_x + 1), then the bitmask
     size_t sat_cap = 0;
-    uint4* wide_items = nullptr;        // wide-splat queue (per chunk, reused)
-    uint32_t* wide_unit = nullptr;
+    uint4* wide_unit = nullptr;         // wide-splat row queue (per chunk, reused)
     uint32_t wide_cap = 0, wide_unit_cap = 0;
     int tiles_cap = 0;
     float4* state = nullptr;
@@ -220,10 +220,8 @@ static void ensure_wide(gs_scene* s, int strip_rows) {
     (void)strip_rows;
     const uint32_t items = (uint32_t)std::min<uint64_t>(1u << 20, s->kcap / kWideTiles + 1024);
     const uint32_t units = (uint32_t)std::min<uint64_t>(1u << 30, s->kcap / 8 + 4096);
-    if (s->wide_items && items <= s->wide_cap && units <= s->wide_unit_cap) return;
-    dev_free(s->wide_items);
+    if (s->wide_unit && items <= s->wide_cap && units <= s->wide_unit_cap) return;
     dev_free(s->wide_unit);
-    dev_alloc(s->wide_items, items);
     dev_alloc(s->wide_unit, units);
     s->wide_cap = items;
     s->wide_unit_cap = units;
@@ -475,6 +473,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.n_max = std::max<uint32_t>(pp.n, 1);
         bp.capacity = (uint32_t)s->kcap;
         bp.part_tot = s->bin_part;
+        bp.rank_cnt = s->rank_cnt;
         bp.part_stride = bin_parts(s->n) + 1;
         bp.tkeys = s->tkA;
         bp.tvals = s->tvA;
@@ -483,14 +482,13 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.mask_words = (TX + 63) / 64;
         bp.rows = tr_end - tr_begin;
         bp.shade_list = s->shade_list;
-        bp.wide_items = s->wide_items;
         bp.wide_cap = s->wide_cap;
         bp.wide_unit = s->wide_unit;
         bp.wide_unit_cap = s->wide_unit_cap;
-        launch_bin(bp, st);
-        // colour in the same stream: overlapping k_shade with the tile-id sort on a second stream
-        // was measured slower (both are memory-bound and contend)
+        // composite records of the chunk's depth ranks first: the binning reads them to bin each
+        // splat's ellipse, not its bounding box
         launch_shade(bp, st);
+        launch_bin(bp, st);
         mark(eb + 1);
 
         uint32_t *tk_in = s->tkA, *tv_in = s->tvA, *tk_out = s->tkB, *tv_out = s->tvB;
@@ -691,6 +689,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             s->hist = (uint32_t*)(s->meta + kMetaHist);
             dev_alloc(s->bin_part, 2 * ((size_t)bin_parts(n) + 1));
             dev_alloc(s->shade_list, (size_t)n);
+            dev_alloc(s->rank_cnt, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->part_count, (size_t)sort_parts(n) + 1);
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hipHostMallocDefault));
             HIPCHK(hipHostMalloc((void**)&s->h_not_done, 64, hipHostMallocDefault));
@@ -743,13 +742,13 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->meta);
     dev_free(s->bin_part);
     dev_free(s->shade_list);
+    dev_free(s->rank_cnt);
     dev_free(s->part_count);
     dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB);
     dev_free(s->radix_offsets);
     dev_free(s->ranges);
     dev_free(s->done);
     dev_free(s->sat);
-    dev_free(s->wide_items);
     dev_free(s->wide_unit);
     dev_free(s->state);
     for (auto& e : s->stat_ev)

@@ -43,7 +43,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t err;
     uint32_t wide_n[2];           // wide splats queued per chunk (binning)
     uint32_t wide_rows[2];        // their tile rows (work units of k_bin_wide)
-    uint32_t shade_n[2];          // splats queued for colour per chunk (binning)
+    uint32_t shade_n[2];          // composite slots per chunk (= its depth-sorted splats)
     uint32_t n_chunk[2];          // depth-sorted splats per chunk (count of radix pass 0)
     uint32_t sat_key;             // depth key of the farthest splat a tile saturated at
     uint32_t sat_slot_max;        // (k_frame_stats)
@@ -63,8 +63,8 @@ struct FrameCtl {                 // zeroed at the start of every frame
 //         record with the block: cx, cy, e1x', e1y' | e2x', e2y', log2(op), pixel box x
 //         (centre in pixels; quad axes e/|e|^2 * sqrt(log2 e); box x0 | x1 << 16, u32 bits)
 //   r2[j] = depth key, tile count, pixel box x, pixel box y (u32 bits), dense
-// Composite record, 3 float4 per binned splat at its slot g (depth-rank order of the splats
-// that received entries; written by k_shade; the tile lists hold g):
+// Composite record, 3 float4 per depth rank of the chunk at slot g = chunk base + rank (written
+// by k_shade before the binning, which reads it; the tile lists hold g):
 //   [0], [1] = the r01 quads, [2] r, g, b, 0
 __host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
 __host__ __device__ inline uint32_t shade_stride(int n_sh) {  // block + 2 record quads, power of 2
@@ -166,7 +166,8 @@ struct BinParams {
     int tile_row_begin, tiles_x;
     uint32_t n_max;               // upper bound of n_vis (grid / scratch sizing)
     uint32_t capacity;            // entry capacity of out arrays
-    uint32_t* part_tot;           // [2][part_stride] scratch: entries, then splats with entries
+    uint32_t* part_tot;           // [part_stride] scratch: entries per binning partition
+    uint32_t* rank_cnt;           // [n_max] scratch: entries of each depth rank of the chunk
     uint32_t part_stride;         // >= bin_parts(n_max)
     uint32_t* tkeys;              // out: strip-relative tile id
     uint32_t* tvals;              // out: Gaussian index
@@ -177,12 +178,11 @@ struct BinParams {
     const unsigned long long* mask;
     int mask_words;
     int rows;                     // tile rows of the strip
-    uint32_t* shade_list;         // [n] Gaussian index of each composite slot g
-    // wide splats: item = (Gaussian index, output offset, x0 | x1 << 16, y0 | y1 << 16); one
-    // work unit per tile row, unit word = item << 12 | row offset (~0u: no item)
-    uint4* wide_items;
+    uint32_t* shade_list;         // [n] Gaussian index of each composite slot g (k_shade)
+    // wide splats: one work unit per tile row, (slot, output position, xa | xb << 16, tile row)
+    // (row ~0u: no entries); wide_cap bounds the splats queued per chunk
     uint32_t wide_cap;
-    uint32_t* wide_unit;
+    uint4* wide_unit;
     uint32_t wide_unit_cap;
 };
 

@@ -787,17 +787,104 @@ __device__ __forceinline__ bool rect_wide(const TileRect& r) {
     return (r.x1 - r.x0 + 1) * (r.y1 - r.y0 + 1) >= kWideTiles;
 }
 
-// Entries of one splat in this chunk: every tile of its rectangle (chunk 0) or the unsaturated
-// ones (chunk 1: bitmask rows when narrow, the summed-area table when wide).
-__device__ __forceinline__ uint32_t rect_count(const BinParams& p, const unsigned long long* m,
-                                               const TileRect& r) {
-    const uint32_t w = r.x1 - r.x0 + 1;
-    if (p.chunk == 0) return w * (r.y1 - r.y0 + 1);
-    if (rect_wide(r)) return sat_count(p, r.x0, r.x1, r.y0, r.y1);
+// ---- exact-ish binning: the alpha >= 1/255 region of a splat is the ellipse
+//   u'^2 + v'^2 <= log2(op) + log2(255),  u' = d.e1', v' = d.e2'  (d = pixel - centre, record axes)
+// (the quad's |u|,|v| <= 2 only removes pixels from it).  It is convex, so in every tile row the
+// tiles holding one of its pixel centres form one contiguous column range, computed in closed
+// form below and widened (log2 margin, 0.02 px + relative) so that no pixel the composite would
+// blend is ever dropped.  Count, emission and the wide path call the same functions, so their
+// entry counts agree exactly.
+struct Ellipse {
+    float cx, cy, m00, m01, det, l, hy, dys, xm, rm00;  // xm: x margin; rm00 = 1 / m00
+    uint32_t px0, px1;                             // pixel box columns
+    bool ok;                                       // false: use the whole box row (degenerate)
+};
+
+// Hardware sqrt / reciprocal (about 1 ulp): the ranges only need to be conservative, and the
+// margins above are orders of magnitude wider than their error.
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+__device__ __forceinline__ Ellipse ellipse_of(const float4 q0, const float4 q1) {
+    Ellipse e;
+    const float ax = q0.z, ay = q0.w, bx = q1.x, by = q1.y;
+    const uint32_t bbx = __float_as_uint(q1.w);
+    e.cx = q0.x;
+    e.cy = q0.y;
+    e.px0 = bbx & 0xffffu;
+    e.px1 = bbx >> 16;
+    e.m00 = ax * ax + bx * bx;
+    e.m01 = ax * ay + bx * by;
+    const float m11 = ay * ay + by * by;
+    const float da = ax * by - ay * bx;
+    e.det = da * da;
+    e.l = q1.z + 7.99435343f + 2e-3f;  // log2(op) + log2(255) + margin
+    const float rdet = frcp(e.det);
+    const float hx = fsqrt(e.l * m11 * rdet);
+    e.hy = fsqrt(e.l * e.m00 * rdet) * 1.0001f + 0.02f;
+    e.dys = -e.m01 * fsqrt(e.l * rdet * frcp(m11));  // y offset of the rightmost point
+    e.xm = 0.02f + 1e-4f * hx;
+    e.rm00 = frcp(e.m00);
+    e.ok = e.l > 0.0f && e.det > 0.0f && isfinite(hx) && isfinite(e.hy) && isfinite(e.dys) &&
+           isfinite(e.rm00) && isfinite(e.cx) && isfinite(e.cy);
+    return e;
+}
+
+// Tile columns [xa, xb] of tile row ty holding a pixel centre of the ellipse (inside the box).
+__device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint32_t& xa, uint32_t& xb) {
+    if (!e.ok) {
+        xa = e.px0 >> 4;
+        xb = e.px1 >> 4;
+        return true;
+    }
+    const float lo = fmaxf((float)(ty * kTile) + 0.5f - e.cy, -e.hy);
+    const float hi = fminf((float)(ty * kTile) + 15.5f - e.cy, e.hy);
+    if (!(lo <= hi)) return false;
+    const float d1 = fminf(fmaxf(e.dys, lo), hi), d0 = fminf(fmaxf(-e.dys, lo), hi);
+    const float g1 = fsqrt(fmaxf(e.m00 * e.l - e.det * d1 * d1, 0.0f));
+    const float g0 = fsqrt(fmaxf(e.m00 * e.l - e.det * d0 * d0, 0.0f));
+    const float xmax = e.cx + (g1 - e.m01 * d1) * e.rm00 + e.xm;
+    const float xmin = e.cx - (g0 + e.m01 * d0) * e.rm00 - e.xm;
+    // pixel columns px with px + 0.5 in [xmin, xmax], inside the box
+    const float pl = fmaxf(ceilf(xmin - 0.5f), (float)e.px0), ph = fminf(floorf(xmax - 0.5f), (float)e.px1);
+    if (!(pl <= ph)) {
+        if (isfinite(xmin) && isfinite(xmax)) return false;
+        xa = e.px0 >> 4;  // NaN/inf: the whole box row (conservative)
+        xb = e.px1 >> 4;
+        return true;
+    }
+    xa = (uint32_t)pl >> 4;
+    xb = (uint32_t)ph >> 4;
+    return true;
+}
+
+// Entries of tile row ty, columns [xa, xb], in this chunk: all of them (chunk 0) or the
+// unsaturated ones (chunk 1: bitmask row when narrow, the summed-area table when wide).
+__device__ __forceinline__ uint32_t row_count(const BinParams& p, const unsigned long long* m, uint32_t ty,
+                                              uint32_t xa, uint32_t xb) {
+    const uint32_t w = xb - xa + 1;
+    if (p.chunk == 0) return w;
+    if (w > 32) return sat_count(p, xa, xb, ty, ty);
+    return __popc(mask_bits(m + (uint64_t)(ty - p.tile_row_begin) * p.mask_words, p.mask_words, xa, w));
+}
+
+// Entries of one splat in this chunk (rows of its rect, ellipse column ranges).
+__device__ __forceinline__ uint32_t splat_count(const BinParams& p, const unsigned long long* m,
+                                                const TileRect& r, const Ellipse& e) {
     uint32_t c = 0;
-    for (uint32_t ty = r.y0; ty <= r.y1; ++ty)
-        c += __popc(mask_bits(m + (uint64_t)(ty - p.tile_row_begin) * p.mask_words, p.mask_words, r.x0, w));
+    for (uint32_t ty = r.y0; ty <= r.y1; ++ty) {
+        uint32_t xa, xb;
+        if (!ellipse_row(e, ty, xa, xb)) continue;
+        xa = max(xa, r.x0);
+        xb = min(xb, r.x1);
+        if (xa <= xb) c += row_count(p, m, ty, xa, xb);
+    }
     return c;
+}
+
+// The chunk's composite records start at slot base: chunk 0 at 0, chunk 1 after chunk 0.
+__device__ __forceinline__ uint32_t slot_base(const BinParams& p) {
+    return p.chunk ? p.ctl->n_chunk[0] : 0u;
 }
 
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
@@ -808,27 +895,26 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     const uint32_t parts = bin_parts(r1 - r0);
     if (blockIdx.x >= parts) return;
     const unsigned long long* m = stage_mask(p, s_mask);
+    const uint32_t g0 = slot_base(p);
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        uint32_t sum = 0, nsh = 0;
+        uint32_t sum = 0;
 #pragma unroll
         for (int k = 0; k < kBinIPT; ++k) {
             const uint32_t r = r0 + part * kBinTile + k * kBinThreads + threadIdx.x;
             if (r < r1) {
                 TileRect tr;
+                uint32_t c = 0;
                 if (rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) {
-                    const uint32_t c = rect_count(p, m, tr);
-                    sum += c;
-                    nsh += c ? 1u : 0u;
+                    const float4* q = p.crec + 3 * (uint64_t)(g0 + r);
+                    c = splat_count(p, m, tr, ellipse_of(q[0], q[1]));
                 }
+                p.rank_cnt[r - r0] = c;  // k_bin_emit's counts
+                sum += c;
             }
         }
-        uint32_t total, total_sh;
+        uint32_t total;
         block_excl_scan256(sum, s_tmp, &total);
-        block_excl_scan256(nsh, s_tmp, &total_sh);
-        if (threadIdx.x == 0) {
-            p.part_tot[part] = total;
-            p.part_tot[p.part_stride + part] = total_sh;
-        }
+        if (threadIdx.x == 0) p.part_tot[part] = total;
     }
 }
 
@@ -863,18 +949,16 @@ __device__ unsigned long long scan_parts(uint32_t* a, uint32_t parts, uint32_t c
     return total;
 }
 
-// single workgroup: partition bases of the entries (capacity-clamped, overflow flagged) and of
-// the colour queue
+// single workgroup: partition bases of the entries (capacity-clamped, overflow flagged)
 __global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
     __shared__ unsigned long long s_wsum[16];
     uint32_t r0, r1;
     chunk_range(p, r0, r1);
     const uint32_t parts = bin_parts(r1 - r0);
     const unsigned long long total = scan_parts(p.part_tot, parts, p.capacity, s_wsum);
-    const unsigned long long nsh = scan_parts(p.part_tot + p.part_stride, parts, 0xFFFFFFFFu, s_wsum);
     if (threadIdx.x == 0) {
         p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
-        p.ctl->shade_n[p.chunk] = (uint32_t)nsh;
+        p.ctl->shade_n[p.chunk] = r1 - r0;  // every depth rank has a composite slot
     }
     if (p.chunk == 0 && threadIdx.x < 8 && r1 > 0) {  // quantile keys (fixed-fraction chunking)
         const uint32_t q = (r1 + (1u << threadIdx.x) - 1) >> threadIdx.x;
@@ -883,44 +967,61 @@ __global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
     if (threadIdx.x == 0 && total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
 }
 
-// Queue a wide splat (composite slot g) for k_bin_wide; false when the queue is full (the caller
-// emits it itself).
-__device__ bool wide_push(const BinParams& p, uint32_t j, uint32_t out, const TileRect& r) {
+// Queue the tile rows of a wide splat (composite slot g, first output position out) for
+// k_bin_wide, one unit per row: (slot, output position of the row, xa | xb << 16, tile row).
+// False when the queue is full (the caller emits it itself).
+__device__ bool wide_push(const BinParams& p, const unsigned long long* m, uint32_t g, uint32_t out,
+                          const TileRect& r, const Ellipse& e) {
     const uint32_t h = r.y1 - r.y0 + 1;
     const uint32_t slot = atomicAdd(&p.ctl->wide_n[p.chunk], 1u);
     const uint32_t u0 = atomicAdd(&p.ctl->wide_rows[p.chunk], h);
-    const bool ok = slot < p.wide_cap && slot < (1u << 20) && (uint64_t)u0 + h <= p.wide_unit_cap;
-    for (uint32_t t = 0; t < h && u0 + t < p.wide_unit_cap; ++t)
-        p.wide_unit[u0 + t] = ok ? (slot << 12 | t) : 0xFFFFFFFFu;
-    if (ok) p.wide_items[slot] = make_uint4(j, out, r.x0 | (r.x1 << 16), r.y0 | (r.y1 << 16));
+    const bool ok = slot < p.wide_cap && (uint64_t)u0 + h <= p.wide_unit_cap;
+    uint32_t o = out;
+    for (uint32_t t = 0; t < h && u0 + t < p.wide_unit_cap; ++t) {
+        const uint32_t ty = r.y0 + t;
+        uint32_t xa, xb, c = 0;
+        if (ellipse_row(e, ty, xa, xb)) {
+            xa = max(xa, r.x0);
+            xb = min(xb, r.x1);
+            if (xa <= xb) c = row_count(p, m, ty, xa, xb);
+        }
+        p.wide_unit[u0 + t] = (ok && c) ? make_uint4(g, o, xa | (xb << 16), ty) : make_uint4(0, 0, 0, 0xFFFFFFFFu);
+        o += c;
+    }
     return ok;
 }
 
 // Entries [k0, k1) of a splat emitted here (local positions o + k) into the LDS stage at o + k - R0.
 __device__ __forceinline__ void stage_narrow(const BinParams& p, const unsigned long long* m, const TileRect& tr,
-                                             uint32_t o, uint32_t k0, uint32_t k1, uint32_t R0,
-                                             uint32_t* s_key) {
-    const uint32_t w = tr.x1 - tr.x0 + 1;
-    if (p.chunk == 0) {
-        for (uint32_t k = k0; k < k1; ++k) s_key[o + k - R0] = tile_id(p, tr.x0 + k % w, tr.y0 + k / w);
-        return;
-    }
+                                             const Ellipse& e, uint32_t o, uint32_t k0, uint32_t k1,
+                                             uint32_t R0, uint32_t* s_key) {
     uint32_t k = 0;
     for (uint32_t ty = tr.y0; ty <= tr.y1 && k < k1; ++ty) {
-        const uint32_t t0 = tile_id(p, tr.x0, ty);
-        if (w > 32) {  // a wide splat the queue could not take
-            for (uint32_t x = 0; x < w && k < k1; ++x) {
+        uint32_t xa, xb;
+        if (!ellipse_row(e, ty, xa, xb)) continue;
+        xa = max(xa, tr.x0);
+        xb = min(xb, tr.x1);
+        if (xa > xb) continue;
+        const uint32_t t0 = tile_id(p, 0, ty);
+        if (p.chunk == 0) {
+            for (uint32_t x = xa; x <= xb && k < k1; ++x, ++k)
+                if (k >= k0) s_key[o + k - R0] = t0 + x;
+            continue;
+        }
+        const uint32_t w = xb - xa + 1;
+        if (w > 32) {  // a wide row (the queue could not take the splat): unsaturated tiles
+            for (uint32_t x = xa; x <= xb && k < k1; ++x) {
                 if (p.done[t0 + x]) continue;
                 if (k >= k0) s_key[o + k - R0] = t0 + x;
                 ++k;
             }
             continue;
         }
-        uint32_t bits = mask_bits(m + (uint64_t)(ty - p.tile_row_begin) * p.mask_words, p.mask_words, tr.x0, w);
+        uint32_t bits = mask_bits(m + (uint64_t)(ty - p.tile_row_begin) * p.mask_words, p.mask_words, xa, w);
         while (bits && k < k1) {
             const uint32_t x = __ffs(bits) - 1;
             bits &= bits - 1;
-            if (k >= k0) s_key[o + k - R0] = t0 + x;
+            if (k >= k0) s_key[o + k - R0] = t0 + xa + x;
             ++k;
         }
     }
@@ -928,9 +1029,9 @@ __device__ __forceinline__ void stage_narrow(const BinParams& p, const unsigned 
 
 constexpr uint32_t kEmitStage = 2048;  // entries staged in LDS per round
 
-// Per depth rank: colour (when it has entries), then its entries at the scanned output position.
-// Narrow splats' entries are staged in LDS and written out coalesced, round by round; the
-// positions of wide splats are left for k_bin_wide (queued here, written after this kernel).
+// Per depth rank r (composite slot g = base + r): its entries at the scanned output position.
+// Narrow splats' entries are staged in LDS and written out coalesced, round by round; the rows
+// of wide splats are queued for k_bin_wide (written after this kernel).
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_tmp[8];
     __shared__ unsigned long long s_mask[kMaskLdsWords];
@@ -942,18 +1043,23 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     const uint32_t parts = bin_parts(r1 - r0);
     if (blockIdx.x >= parts) return;
     const unsigned long long* m = stage_mask(p, s_mask);
+    const uint32_t g0 = slot_base(p);
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         const uint32_t base_r = r0 + part * kBinTile;
-        uint32_t cnt[kBinIPT], j[kBinIPT];
+        uint32_t cnt[kBinIPT], g[kBinIPT];
         bool narrow[kBinIPT];
         TileRect tr[kBinIPT];
+        Ellipse el[kBinIPT];
 #pragma unroll
         for (int k = 0; k < kBinIPT; ++k) {
             const uint32_t r = base_r + k * kBinThreads + tid;
             cnt[k] = 0;
-            if (r < r1) {
-                j[k] = p.sorted_vals[r];
-                if (rect_unpack(p, p.sorted_rect[r], j[k], tr[k])) cnt[k] = rect_count(p, m, tr[k]);
+            g[k] = g0 + r;
+            if (r < r1) cnt[k] = p.rank_cnt[r - r0];  // k_bin_count's
+            if (cnt[k]) {
+                rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr[k]);
+                const float4* q = p.crec + 3 * (uint64_t)g[k];
+                el[k] = ellipse_of(q[0], q[1]);
             }
         }
         // local output offsets: ranks in order (k, tid) within the partition, as in k_bin_count
@@ -965,18 +1071,10 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
             T += total;
         }
         const uint32_t obase = p.part_tot[part];
-        uint32_t sb = p.part_tot[p.part_stride + part] + (p.chunk ? p.ctl->shade_n[0] : 0u);
-        uint32_t g[kBinIPT];
 #pragma unroll
         for (int k = 0; k < kBinIPT; ++k) {
-            // every splat with entries gets a composite slot (rank order); lists carry the slot
-            uint32_t nsh;
-            const uint32_t so = block_excl_scan256(cnt[k] ? 1u : 0u, s_tmp, &nsh);
-            g[k] = sb + so;
-            if (cnt[k]) p.shade_list[g[k]] = j[k];
-            sb += nsh;
             narrow[k] = cnt[k] != 0;
-            if (cnt[k] && rect_wide(tr[k]) && wide_push(p, g[k], obase + o[k], tr[k])) narrow[k] = false;
+            if (cnt[k] && rect_wide(tr[k]) && wide_push(p, m, g[k], obase + o[k], tr[k], el[k])) narrow[k] = false;
         }
         for (uint32_t R0 = 0; R0 < T; R0 += kEmitStage) {
             const uint32_t R1 = min(T, R0 + kEmitStage);
@@ -984,12 +1082,12 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
             for (int k = 0; k < kBinIPT; ++k) {
                 if (!narrow[k] || o[k] >= R1 || o[k] + cnt[k] <= R0) continue;
                 const uint32_t k0 = R0 > o[k] ? R0 - o[k] : 0u, k1 = min(cnt[k], R1 - o[k]);
-                stage_narrow(p, m, tr[k], o[k], k0, k1, R0, s_key);
+                stage_narrow(p, m, tr[k], el[k], o[k], k0, k1, R0, s_key);
                 for (uint32_t q = k0; q < k1; ++q) s_val[o[k] + q - R0] = g[k];
             }
             __syncthreads();
-            // coalesced copy; slots of queued wide splats carry stale LDS words and are rewritten
-            // by k_bin_wide
+            // coalesced copy; positions of queued wide splats carry stale LDS words and are
+            // rewritten by k_bin_wide
             for (uint32_t q = R0 + tid; q < R1; q += kBinThreads) {
                 const uint32_t oe = obase + q;
                 if (oe < p.capacity) {
@@ -1002,13 +1100,14 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     }
 }
 
-// Composite records of this chunk's slots: colour (src/simple_render.ts:26-66, :321-322:
-// dir = normalize(p - camPos), SH to degree 3, + 0.5, max(., 0)) plus the footprint words of the
-// projected record, written densely at the slot.  16 lanes per splat read the line-aligned
-// shading block with the 32-B record in its padding (one coalesced load); each lane
-// evaluates its own coefficients' terms and the group sums them with xor shuffles.
-// Latency: a wave takes 64 slots at once (one coalesced load of their Gaussian indices) and keeps
-// kShadeU groups of 4 splats' block loads in flight before evaluating any of them.
+// Composite records of this chunk's depth ranks (slot g = base + rank): colour
+// (src/simple_render.ts:26-66, :321-322: dir = normalize(p - camPos), SH to degree 3, + 0.5,
+// max(., 0)) plus the footprint words of the projected record, written densely.  16 lanes per
+// splat read the line-aligned shading block with the 32-B record in its padding (one coalesced
+// load); each lane evaluates its own coefficients' terms and the group sums them with xor
+// shuffles.  Latency: a wave takes 64 ranks at once (one coalesced load of their Gaussian
+// indices) and keeps kShadeU groups of 4 splats' block loads in flight before evaluating any.
+// Runs before the binning, which reads the records to bin each splat's ellipse exactly.
 constexpr int kShadeU = 4;
 
 __device__ __forceinline__ void shade_eval(const BinParams& p, float4 q, uint32_t l, uint32_t nq,
@@ -1065,13 +1164,16 @@ __device__ __forceinline__ void shade_eval(const BinParams& p, float4 q, uint32_
 }
 
 __global__ __launch_bounds__(256) void k_shade(BinParams p) {
-    const uint32_t g0 = p.chunk ? p.ctl->shade_n[0] : 0u;
-    const uint32_t n = p.ctl->shade_n[p.chunk];
+    uint32_t r0, r1;
+    chunk_range(p, r0, r1);
+    const uint32_t g0 = slot_base(p);
+    const uint32_t n = r1 - r0;
     const uint32_t lane = lane_id(), l = lane & 15;
     const uint32_t nq = shade_quads(p.n_sh), ncoef = 3 * (uint32_t)p.n_sh;
     const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
     for (uint32_t base = wave * 64; base < n; base += nwaves * 64) {  // wave-uniform: shuffles below
-        const uint32_t jl = base + lane < n ? p.shade_list[g0 + base + lane] : 0u;
+        const uint32_t jl = base + lane < n ? p.sorted_vals[r0 + base + lane] : 0u;
+        if (base + lane < n) p.shade_list[g0 + base + lane] = jl;
         const uint32_t cnt = min(64u, n - base);
         for (uint32_t sub = 0; sub < cnt; sub += 4 * kShadeU) {
             float4 q[kShadeU];
@@ -1092,8 +1194,8 @@ __global__ __launch_bounds__(256) void k_shade(BinParams p) {
     }
 }
 
-// Tile rows of wide splats, one row per work unit: each wave prefetches 64 units lane-parallel
-// (unit word, item, chunk-1 row count and prefix), then writes them one by one across its lanes.
+// Tile rows of wide splats, one row per work unit (slot, output position, xa | xb << 16, row):
+// each wave prefetches 64 units lane-parallel, then writes them one by one across its lanes.
 __global__ __launch_bounds__(kBinThreads) void k_bin_wide(BinParams p) {
     __shared__ unsigned long long s_mask[kMaskLdsWords];
     const uint32_t units = min(p.ctl->wide_rows[p.chunk], p.wide_unit_cap);
@@ -1104,38 +1206,23 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_wide(BinParams p) {
     const uint32_t nwaves = gridDim.x * (kBinThreads / 64);
     for (uint32_t u0 = wave * 64; u0 < units; u0 += nwaves * 64) {
         const uint32_t u = u0 + lane;
-        uint32_t code = 0xFFFFFFFFu;
-        uint4 it = make_uint4(0, 0, 0, 0);
-        uint32_t rowcnt = 0, pre = 0;
-        if (u < units) code = p.wide_unit[u];
-        if (code != 0xFFFFFFFFu) {
-            it = p.wide_items[code >> 12];
-            const uint32_t x0 = it.z & 0xffffu, x1 = it.z >> 16, y0 = it.w & 0xffffu;
-            const uint32_t row = y0 + (code & 4095u);
-            if (p.chunk == 0) {
-                rowcnt = x1 - x0 + 1;
-                pre = (code & 4095u) * rowcnt;
-            } else {
-                rowcnt = sat_count(p, x0, x1, row, row);
-                pre = row > y0 ? sat_count(p, x0, x1, y0, row - 1) : 0u;
-            }
-        }
-        uint64_t todo = __ballot(rowcnt != 0);
+        uint4 it = make_uint4(0, 0, 0, 0xFFFFFFFFu);
+        if (u < units) it = p.wide_unit[u];
+        uint64_t todo = __ballot(it.w != 0xFFFFFFFFu);
         while (todo) {
             const int src = __ffsll((long long)todo) - 1;
             todo &= todo - 1;
-            const uint32_t c = __shfl(code, src, 64);
-            const uint32_t gj = __shfl(it.x, src, 64), go = __shfl(it.y, src, 64) + __shfl(pre, src, 64);
-            const uint32_t gz = __shfl(it.z, src, 64), gw = __shfl(it.w, src, 64);
-            const uint32_t x0 = gz & 0xffffu, x1 = gz >> 16, row = (gw & 0xffffu) + (c & 4095u);
-            const uint32_t w = x1 - x0 + 1, t0 = tile_id(p, x0, row);
+            const uint32_t gj = __shfl(it.x, src, 64), go = __shfl(it.y, src, 64);
+            const uint32_t gz = __shfl(it.z, src, 64), row = __shfl(it.w, src, 64);
+            const uint32_t xa = gz & 0xffffu, xb = gz >> 16;
+            const uint32_t w = xb - xa + 1, t0 = tile_id(p, xa, row);
             uint32_t o = go;
             for (uint32_t xs = 0; xs < w; xs += 64) {
                 const uint32_t x = xs + lane;
                 bool f = x < w;
                 if (p.chunk == 1 && f) {
                     const unsigned long long* mr = m + (uint64_t)(row - p.tile_row_begin) * p.mask_words;
-                    f = (mr[(x0 + x) >> 6] >> ((x0 + x) & 63)) & 1ull;
+                    f = (mr[(xa + x) >> 6] >> ((xa + x) & 63)) & 1ull;
                 }
                 const uint64_t b = __ballot(f);
                 const uint32_t e = o + __popcll(b & lanemask_lt());

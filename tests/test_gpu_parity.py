@@ -173,7 +173,9 @@ def test_synthetic_1m_1080p(gpu_ctx):
     st_gpu = gpu_ctx.timings()
     ref, st = orc.render(aos.view(np.uint8), 1_000_000, 16, u, W, H, accum=0, t_min=1e-4)
     assert st_gpu["n_vis"] == st["n_vis"]
-    assert st["k_tiles"] <= st_gpu["k_entries"] <= st["k_tiles"] * 1.02
+    # the oracle counts every tile of each binning box; the GPU bins each splat's alpha >= 1/255
+    # ellipse row by row (a subset), and the image check below shows no contributing tile is lost
+    assert 0.4 * st["k_tiles"] <= st_gpu["k_entries"] <= st["k_tiles"]
     mse, bad, ok = image_close_fp32(img, ref, name="synth1m")
     assert ok, (mse, bad)
     keys, idx = sc.last_order()
@@ -240,6 +242,36 @@ def test_odd_sizes(gpu_ctx, size):
     ref, _ = orc.render(aos.view(np.uint8), 20_000, 16, u, W, H)
     r = image_close_fp32(img, ref, name="odd_%dx%d" % (W, H))
     assert r[2], r
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_thin_rotated_splats_binning(gpu_ctx, seed):
+    """Ellipse binning is conservative: sparse, thin, rotated, mostly opaque splats on an empty
+    background with no early termination, so a tile dropped from a splat's list would change
+    pixels at T ~ 1; at most 2 pixels may differ by more than 1e-3 (alpha-threshold rounding)."""
+    W, H = 512, 384
+    n = 400
+    rng = np.random.default_rng(seed)
+    aos = np.zeros((n, 80), np.float32)
+    z = rng.uniform(3.0, 8.0, n)
+    aos[:, 0] = rng.uniform(-0.6, 0.6, n) * z
+    aos[:, 1] = rng.uniform(-0.45, 0.45, n) * z
+    aos[:, 2] = -z
+    aos[:, 4] = rng.uniform(0.2, 0.9, n)
+    aos[:, 5] = rng.uniform(0.005, 0.04, n)
+    aos[:, 6] = rng.uniform(0.005, 0.04, n)
+    q = rng.normal(size=(n, 4))
+    aos[:, 8:12] = q / np.linalg.norm(q, axis=1, keepdims=True)
+    aos[:, 12] = rng.uniform(-2.0, 6.0, n)
+    aos[:, 16:19] = rng.uniform(0.5, 2.0, (n, 3))
+    aos = aos.reshape(-1)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    img = sc.render(u, W, H, gs.make_opts(t_min=0.0))
+    ref, st = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=0.0)
+    d = np.abs(img.astype(np.float64) - ref.astype(np.float64)).max(axis=-1)
+    assert st["n_vis"] > n // 2
+    assert int((d > 1e-3).sum()) <= 2, (int((d > 1e-3).sum()), float(d.max()))
 
 
 def test_huge_splats(gpu_ctx):
