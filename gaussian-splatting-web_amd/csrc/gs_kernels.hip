@@ -830,11 +830,12 @@ __device__ __forceinline__ Ellipse ellipse_of(const float4 q0, const float4 q1) 
     return e;
 }
 
-// Tile columns [xa, xb] of tile row ty holding a pixel centre of the ellipse (inside the box).
-__device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint32_t& xa, uint32_t& xb) {
+// Pixel columns [pl, ph] of tile row ty (pixel rows 16 ty .. 16 ty + 15) holding a pixel centre of
+// the ellipse, inside the box; false when there is none.
+__device__ __forceinline__ bool ellipse_cols(const Ellipse& e, uint32_t ty, uint32_t& pl_, uint32_t& ph_) {
     if (!e.ok) {
-        xa = e.px0 >> 4;
-        xb = e.px1 >> 4;
+        pl_ = e.px0;
+        ph_ = e.px1;
         return true;
     }
     const float lo = fmaxf((float)(ty * kTile) + 0.5f - e.cy, -e.hy);
@@ -849,12 +850,21 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
     const float pl = fmaxf(ceilf(xmin - 0.5f), (float)e.px0), ph = fminf(floorf(xmax - 0.5f), (float)e.px1);
     if (!(pl <= ph)) {
         if (isfinite(xmin) && isfinite(xmax)) return false;
-        xa = e.px0 >> 4;  // NaN/inf: the whole box row (conservative)
-        xb = e.px1 >> 4;
+        pl_ = e.px0;  // NaN/inf: the whole box row (conservative)
+        ph_ = e.px1;
         return true;
     }
-    xa = (uint32_t)pl >> 4;
-    xb = (uint32_t)ph >> 4;
+    pl_ = (uint32_t)pl;
+    ph_ = (uint32_t)ph;
+    return true;
+}
+
+// Tile columns [xa, xb] of tile row ty holding a pixel centre of the ellipse (inside the box).
+__device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint32_t& xa, uint32_t& xb) {
+    uint32_t pl, ph;
+    if (!ellipse_cols(e, ty, pl, ph)) return false;
+    xa = pl >> 4;
+    xb = ph >> 4;
     return true;
 }
 
@@ -1391,12 +1401,14 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
         sR[buf][tid][0] = make_float4(c0u, c0v, ga.z, ga.w);
         sR[buf][tid][1] = make_float4(gb.x, gb.y, gb.z, __uint_as_float(gs_));  // box x: used below only
         sR[buf][tid][2] = gc;
-        const uint32_t bx = __float_as_uint(gb.w);
-        const int x0 = (int)(bx & 0xffffu), x1 = (int)(bx >> 16);
+        // the splat's pixel columns within this tile's rows (ellipse; the binning's margins)
+        uint32_t ul = 0u, uh = 0u;
+        const bool cols = gv && ellipse_cols(ellipse_of(ga, gb), (uint32_t)(ty0 >> 4), ul, uh);
+        const int x0 = (int)ul, x1 = (int)uh;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int qx = tx0 + q * 8;
-            const bool hit = gv && x0 <= qx + 7 && x1 >= qx;
+            const bool hit = cols && x0 <= qx + 7 && x1 >= qx;
             const uint64_t b = __ballot(hit);
             if (hit) sL[buf][q][h * 64 + __popcll(b & lanemask_lt())] = (uint8_t)tid;
             if (lane == 0) sN[buf][q][h] = (uint32_t)__popcll(b);
