@@ -181,6 +181,16 @@ struct gs_scene {
 };
 
 static constexpr size_t kHistWords = kHistShards * 256;
+// radix partition sizes (items per thread x 256): small partitions keep every CU busy on the
+// short depth sorts; the tile-id sort is long enough for 4096-element partitions
+#ifndef GS_DEPTH_IPT
+#define GS_DEPTH_IPT 8
+#endif
+#ifndef GS_TILE_IPT
+#define GS_TILE_IPT 8
+#endif
+static constexpr int kDepthSortIpt = GS_DEPTH_IPT, kTileSortIpt = GS_TILE_IPT;
+static constexpr int kMinSortIpt = kDepthSortIpt < kTileSortIpt ? kDepthSortIpt : kTileSortIpt;
 static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 12 * kHistWords * 4;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
@@ -194,7 +204,7 @@ static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
     const uint64_t cap = std::min<uint64_t>(0xFFFFFFFEull, std::max<uint64_t>(k + k / 2, 1u << 20));
     dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB); dev_free(s->radix_offsets);
     dev_alloc(s->tkA, cap); dev_alloc(s->tvA, cap); dev_alloc(s->tkB, cap); dev_alloc(s->tvB, cap);
-    dev_alloc(s->radix_offsets, 256 * (size_t)sort_parts(std::max<uint64_t>(cap, s->n)));
+    dev_alloc(s->radix_offsets, 256 * (size_t)sort_parts(std::max<uint64_t>(cap, s->n), kMinSortIpt));
     s->kcap = cap;
 }
 
@@ -439,7 +449,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.n = pp.n;
             sp.n_dev = ps == 0 ? nullptr : &s->ctl->n_chunk[chunk];
             sp.gate = chunk == 1 ? &s->ctl->not_done : nullptr;  // chunk 1: only with unsaturated tiles
-            sp.parts_max = sort_parts(pp.n);
+            sp.ipt = (ps == 0 && chunk == 0) ? 16 : kDepthSortIpt;
+            sp.parts_max = sort_parts(pp.n, sp.ipt);
             sp.shift = 8 * ps;
             sp.mask = 255;
             sp.filter = (ps == 0 && chunk == 1) ? kFiltTail : kFiltNone;
@@ -500,7 +511,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.vals_out = tv_out;
             sp.n = (uint32_t)s->kcap;
             sp.n_dev = &s->ctl->k_chunk[chunk];
-            sp.parts_max = sort_parts(s->kcap);
+            sp.ipt = kTileSortIpt;
+            sp.parts_max = sort_parts(s->kcap, sp.ipt);
             sp.shift = 8 * ps;
             sp.mask = 255;
             sp.hist = s->hist + (6 * chunk + 4 + ps) * kHistWords;
@@ -883,7 +895,7 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
         uint32_t *kA, *vA, *kB, *vB, *hist, *offs;
         dev_alloc(kA, n); dev_alloc(vA, n); dev_alloc(kB, n); dev_alloc(vB, n);
         dev_alloc(hist, (size_t)npass * kHistWords);
-        dev_alloc(offs, (size_t)256 * sort_parts(n));
+        dev_alloc(offs, (size_t)256 * sort_parts(n, kDepthSortIpt));
         hipStream_t st = c->stream;
         HIPCHK(hipMemcpyAsync(kA, keys, n * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(vA, vals, n * 4, hipMemcpyHostToDevice, st));
@@ -893,7 +905,8 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
             SortPass sp{};
             sp.keys_in = ki; sp.vals_in = vi; sp.keys_out = ko; sp.vals_out = vo;
             sp.n = (uint32_t)n;
-            sp.parts_max = sort_parts(n);
+            sp.ipt = kDepthSortIpt;
+            sp.parts_max = sort_parts(n, sp.ipt);
             sp.shift = begin_bit + 8 * ps;
             const int bits = std::min(8, end_bit - sp.shift);
             sp.mask = (1u << bits) - 1u;

@@ -135,7 +135,9 @@ struct SortPass {
     const uint32_t* gate;     // optional: the pass is empty when *gate == 0
     const uint32_t* part_count;  // optional: partition p holds part_count[p] elements at its front
                                  // (input compacted by k_project; the upsweep is skipped)
-    uint32_t parts_max;       // sort_parts(upper bound): stride of `offsets`, grid bound
+    uint32_t parts_max;       // partitions of the upper bound: stride of `offsets`, grid bound
+    int ipt;                  // items per thread: partitions of 256 * ipt elements (4, 8 or 16;
+                              // 16 when part_count is set, k_project's partitions)
     int shift;
     uint32_t mask;            // digit mask (<= 255)
     int filter;               // RadixFilter
@@ -219,6 +221,10 @@ void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max,
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);
 
 __host__ __device__ inline uint32_t sort_parts(uint64_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }
+__host__ __device__ inline uint32_t sort_parts(uint64_t n, int ipt) {
+    const uint64_t t = (uint64_t)kSortThreads * (uint64_t)ipt;
+    return (uint32_t)((n + t - 1) / t);
+}
 __host__ __device__ inline uint32_t bin_parts(uint64_t n) { return (uint32_t)((n + kBinTile - 1) / kBinTile); }
 
 }  // namespace gs

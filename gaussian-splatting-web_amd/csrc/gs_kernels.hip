@@ -549,17 +549,19 @@ __device__ __forceinline__ bool radix_valid(const SortPass& p, uint32_t n, uint6
     }
 }
 
+template <int IPT>
 __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(SortPass p) {
+    constexpr int kTileN = kSortThreads * IPT;
     __shared__ uint32_t s_hist[4][256];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const uint32_t n = radix_n(p), parts = sort_parts(n);
+    const uint32_t n = radix_n(p), parts = (n + kTileN - 1) / kTileN;
     uint32_t total = 0;  // this workgroup's count of digit `tid` over all its partitions
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         for (int t = tid; t < 1024; t += kSortThreads) (&s_hist[0][0])[t] = 0;
         __syncthreads();
-        const uint64_t wbase = (uint64_t)part * kSortTile + (uint64_t)w * (kSortIPT * 64);
+        const uint64_t wbase = (uint64_t)part * kTileN + (uint64_t)w * (IPT * 64);
 #pragma unroll 4
-        for (int it = 0; it < kSortIPT; ++it) {
+        for (int it = 0; it < IPT; ++it) {
             const uint64_t idx = wbase + it * 64 + lane;
             const uint32_t key = idx < n ? p.keys_in[idx] : kSentinel;
             const uint32_t aux = (p.filter == kFiltTail && idx < n) ? p.aux_in[idx] : 0u;
@@ -581,7 +583,8 @@ __global__ __launch_bounds__(256) void k_radix_scan(SortPass p) {
     __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_base;
     const int d = blockIdx.x, tid = threadIdx.x;
-    const uint32_t parts = sort_parts(radix_n(p));
+    const uint32_t tile_n = (uint32_t)kSortThreads * (uint32_t)p.ipt;
+    const uint32_t parts = (radix_n(p) + tile_n - 1) / tile_n;
     uint32_t tot = 0;
     for (int sh = 0; sh < kHistShards; ++sh) tot += p.hist[sh * 256 + tid];
     uint32_t gtotal;
@@ -603,28 +606,30 @@ __global__ __launch_bounds__(256) void k_radix_scan(SortPass p) {
     }
 }
 
+template <int IPT>
 __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
+    constexpr int kTileN = kSortThreads * IPT;
     __shared__ uint32_t s_wave_hist[4][256];
     __shared__ uint32_t s_digit_start[256];
     __shared__ uint32_t s_global[256];
-    __shared__ uint32_t s_keys[kSortTile];
-    __shared__ uint32_t s_vals[kSortTile];
-    __shared__ uint32_t s_aux[kSortTile];
+    __shared__ uint32_t s_keys[kTileN];
+    __shared__ uint32_t s_vals[kTileN];
+    __shared__ uint32_t s_aux[kTileN];
     __shared__ uint32_t s_tmp[8];
 
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    const uint32_t n = radix_n(p), parts = sort_parts(n);
+    const uint32_t n = radix_n(p), parts = (n + kTileN - 1) / kTileN;
     const bool has_aux = p.aux_in != nullptr;
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         for (int t = tid; t < 1024; t += kSortThreads) (&s_wave_hist[0][0])[t] = 0;
         s_global[tid] = p.offsets[(uint64_t)tid * p.parts_max + part];
-        const uint64_t wbase = (uint64_t)part * kSortTile + (uint64_t)w * (kSortIPT * 64);
+        const uint64_t wbase = (uint64_t)part * kTileN + (uint64_t)w * (IPT * 64);
         // compacted input (k_project): only the partition's first part_count[part] elements exist
-        const uint64_t pend = (uint64_t)part * kSortTile + (p.part_count ? p.part_count[part] : (uint32_t)kSortTile);
+        const uint64_t pend = (uint64_t)part * kTileN + (p.part_count ? p.part_count[part] : (uint32_t)kTileN);
 
-        uint32_t keys[kSortIPT], vals[kSortIPT], aux[kSortIPT], rank[kSortIPT];
+        uint32_t keys[IPT], vals[IPT], aux[IPT], rank[IPT];
 #pragma unroll
-        for (int it = 0; it < kSortIPT; ++it) {
+        for (int it = 0; it < IPT; ++it) {
             const uint64_t idx = wbase + it * 64 + lane;
             const bool in = idx < n && idx < pend;
             keys[it] = in ? p.keys_in[idx] : kSentinel;
@@ -637,12 +642,12 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
             // filtered pass: compact each wave's kept elements, in order, into the front rows of its
             // slice of the stage (order within the partition is unchanged), so ranking only visits
             // rows that hold kept elements
-            uint32_t* wk = s_keys + w * (kSortIPT * 64);
-            uint32_t* wv = s_vals + w * (kSortIPT * 64);
-            uint32_t* wa = s_aux + w * (kSortIPT * 64);
+            uint32_t* wk = s_keys + w * (IPT * 64);
+            uint32_t* wv = s_vals + w * (IPT * 64);
+            uint32_t* wa = s_aux + w * (IPT * 64);
             uint32_t m = 0;
 #pragma unroll
-            for (int it = 0; it < kSortIPT; ++it) {
+            for (int it = 0; it < IPT; ++it) {
                 const bool valid = (rank[it] & 0x80000000u) == 0u;
                 const uint64_t b = __ballot(valid);
                 if (valid) {
@@ -655,7 +660,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
             }
             __syncthreads();
 #pragma unroll
-            for (int it = 0; it < kSortIPT; ++it) {
+            for (int it = 0; it < IPT; ++it) {
                 const uint32_t q = it * 64 + lane;
                 const bool valid = q < m;
                 keys[it] = valid ? wk[q] : kSentinel;
@@ -666,7 +671,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
             __syncthreads();
         }
 #pragma unroll
-        for (int it = 0; it < kSortIPT; ++it) {
+        for (int it = 0; it < IPT; ++it) {
             const bool valid = (rank[it] & 0x80000000u) == 0u;
             const uint32_t digit = (keys[it] >> p.shift) & p.mask;
             uint64_t peers = __ballot(valid);
@@ -699,7 +704,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
         s_wave_hist[3][d] = c0 + c1 + c2;
         __syncthreads();
 #pragma unroll
-        for (int it = 0; it < kSortIPT; ++it) {
+        for (int it = 0; it < IPT; ++it) {
             if ((rank[it] & 0x80000000u) == 0u) {
                 const uint32_t digit = (keys[it] >> p.shift) & p.mask;
                 const uint32_t pos = s_digit_start[digit] + s_wave_hist[w][digit] + rank[it];
@@ -1549,13 +1554,22 @@ void launch_records(const ProjParams& p, hipStream_t s) {
     hipLaunchKernelGGL(k_records, dim3(grid), dim3(256), 0, s, p);
 }
 
-void launch_sort_pass(const SortPass& p, hipStream_t s) {
-    if (!p.parts_max) return;
+template <int IPT>
+static void sort_pass_ipt(const SortPass& p, hipStream_t s) {
     const unsigned grid = std::min<uint32_t>(p.parts_max, kMaxGrid);
     if (!p.part_count)  // else k_project produced the counts (first depth pass of chunk 0)
-        hipLaunchKernelGGL(k_radix_upsweep, dim3(grid), dim3(kSortThreads), 0, s, p);
+        hipLaunchKernelGGL(k_radix_upsweep<IPT>, dim3(grid), dim3(kSortThreads), 0, s, p);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(k_radix_downsweep, dim3(grid), dim3(kSortThreads), 0, s, p);
+    hipLaunchKernelGGL(k_radix_downsweep<IPT>, dim3(grid), dim3(kSortThreads), 0, s, p);
+}
+
+void launch_sort_pass(const SortPass& p, hipStream_t s) {
+    if (!p.parts_max) return;
+    switch (p.ipt) {
+        case 4: sort_pass_ipt<4>(p, s); break;
+        case 8: sort_pass_ipt<8>(p, s); break;
+        default: sort_pass_ipt<16>(p, s); break;
+    }
 }
 void launch_bin(const BinParams& p, hipStream_t s) {
     const unsigned grid = std::max<uint32_t>(1, std::min<uint32_t>(bin_parts(p.n_max), kMaxGrid));
