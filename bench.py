@@ -14,6 +14,7 @@ Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -60,7 +61,8 @@ def pmc_traffic(kernel):
     tot = 0.0
     for lab, e in d.items():
         if lab.startswith(names[kernel]) and "traffic_bytes" in e:
-            if kernel == "sort" and not any(lab.startswith("k_radix_%s#%d" % (k, i)) for k in
+            base = re.sub(r"<[^>]*>", "", lab)  # k_radix_downsweep<8>#2 -> k_radix_downsweep#2
+            if kernel == "sort" and not any(base == "k_radix_%s#%d" % (k, i) for k in
                                             ("upsweep", "scan", "downsweep") for i in range(4)):
                 continue  # depth passes only
             tot += e["traffic_bytes"]
