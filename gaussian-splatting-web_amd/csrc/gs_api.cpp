@@ -406,6 +406,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
 
     // ---- per chunk: depth sort of the chunk's splats -> bin -> tile-id sort -> ranges -> composite
     const int tile_passes = n_tiles > 256 ? 2 : 1;
+    // chunk 0's first depth pass reads k_project's partitions, each holding only its chunk-0
+    // splats at the front: one downsweep workgroup takes as many as (on the last frame's count)
+    // fill about 3/4 of its 4096-element tile; rounds keep it exact whatever this frame holds
+    int pass0_merge = 1;
+    if (s->have_last && s->last.n_vis > 0 && pp.n > 0) {
+        const double per = std::max(1.0, (double)s->last.n_chunk[0] / (double)sort_parts(pp.n));
+        pass0_merge = (int)std::max(1.0, std::min((double)kMaxMerge, 3072.0 / per));
+    }
     const size_t sat_words = (size_t)(tr_end - tr_begin + 1) * (TX + 1);
     unsigned long long* unsat_mask = (unsigned long long*)(s->sat + ((sat_words + 1) & ~(size_t)1));
     for (int chunk = 0; chunk < 2; ++chunk) {
@@ -450,6 +458,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.n_dev = ps == 0 ? nullptr : &s->ctl->n_chunk[chunk];
             sp.gate = chunk == 1 ? &s->ctl->not_done : nullptr;  // chunk 1: only with unsaturated tiles
             sp.ipt = (ps == 0 && chunk == 0) ? 16 : kDepthSortIpt;
+            sp.merge = ps == 0 && chunk == 0 ? pass0_merge : 1;
             sp.parts_max = sort_parts(pp.n, sp.ipt);
             sp.shift = 8 * ps;
             sp.mask = 255;

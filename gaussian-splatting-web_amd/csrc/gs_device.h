@@ -25,6 +25,7 @@ constexpr int kMaxGrid = 2048;        // persistent grids: 8 workgroups per CU
 constexpr uint32_t kWideTiles = 32;     // splats binding >= this many tiles are emitted row-wise
 constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
 constexpr int kMaskLdsWords = 2048;     // unsaturated-tile bitmask cached in LDS up to this size
+constexpr int kMaxMerge = 16;           // compacted radix input: partitions per downsweep workgroup
 
 // Packed tile rectangle carried through the depth sort (32 bits): tx0[0:12) ty0[12:24)
 // (w-1)[24:28) (h-1)[28:32).  Rectangles wider or taller than 16 tiles use kRectLarge (the
@@ -138,6 +139,7 @@ struct SortPass {
     uint32_t parts_max;       // partitions of the upper bound: stride of `offsets`, grid bound
     int ipt;                  // items per thread: partitions of 256 * ipt elements (4, 8 or 16;
                               // 16 when part_count is set, k_project's partitions)
+    int merge;                // part_count set: partitions per downsweep workgroup (<= kMaxMerge)
     int shift;
     uint32_t mask;            // digit mask (<= 255)
     int filter;               // RadixFilter

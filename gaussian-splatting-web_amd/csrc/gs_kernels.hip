@@ -617,21 +617,49 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
     __shared__ uint32_t s_aux[kTileN];
     __shared__ uint32_t s_tmp[8];
 
+    __shared__ uint32_t s_sub[kMaxMerge + 1];  // element prefix of the round's partitions
+    __shared__ uint32_t s_nsub;
+
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t n = radix_n(p), parts = (n + kTileN - 1) / kTileN;
     const bool has_aux = p.aux_in != nullptr;
-    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+    // A workgroup takes `merge` consecutive partitions and ranks them in rounds of whole
+    // partitions whose elements fit the tile: the scan's offsets of a round's first partition
+    // place the round's digit-d elements contiguously, since the partitions follow each other.
+    // (merge > 1 only for the compacted input of k_project, whose partitions are mostly empty.)
+    const uint32_t M = p.part_count ? max(1u, min((uint32_t)p.merge, (uint32_t)kMaxMerge)) : 1u;
+    const uint32_t units = (parts + M - 1) / M;
+    for (uint32_t unit = blockIdx.x; unit < units; unit += gridDim.x) {
+      const uint32_t se = min((unit + 1) * M, parts);
+      for (uint32_t sp = unit * M; sp < se;) {  // workgroup-uniform
+        if (tid == 0) {
+            uint32_t tot = 0, k = 0;
+            s_sub[0] = 0;
+            for (uint32_t q = sp; q < se; ++q) {
+                // compacted input (k_project): only partition q's first part_count[q] elements exist
+                const uint32_t c = p.part_count ? p.part_count[q] : min((uint32_t)kTileN, n - q * kTileN);
+                if (k > 0 && tot + c > (uint32_t)kTileN) break;
+                tot += c;
+                s_sub[++k] = tot;
+            }
+            s_nsub = k;
+        }
         for (int t = tid; t < 1024; t += kSortThreads) (&s_wave_hist[0][0])[t] = 0;
-        s_global[tid] = p.offsets[(uint64_t)tid * p.parts_max + part];
-        const uint64_t wbase = (uint64_t)part * kTileN + (uint64_t)w * (IPT * 64);
-        // compacted input (k_project): only the partition's first part_count[part] elements exist
-        const uint64_t pend = (uint64_t)part * kTileN + (p.part_count ? p.part_count[part] : (uint32_t)kTileN);
+        s_global[tid] = p.offsets[(uint64_t)tid * p.parts_max + sp];
+        __syncthreads();
+        const uint32_t nsub = s_nsub, total = s_sub[nsub];
 
         uint32_t keys[IPT], vals[IPT], aux[IPT], rank[IPT];
 #pragma unroll
         for (int it = 0; it < IPT; ++it) {
-            const uint64_t idx = wbase + it * 64 + lane;
-            const bool in = idx < n && idx < pend;
+            const uint32_t slot = (uint32_t)w * (IPT * 64) + it * 64 + lane;
+            const bool in = slot < total;
+            uint64_t idx = 0;
+            if (in) {
+                uint32_t k = 0;
+                while (k + 1 < nsub && slot >= s_sub[k + 1]) ++k;
+                idx = (uint64_t)(sp + k) * kTileN + (slot - s_sub[k]);
+            }
             keys[it] = in ? p.keys_in[idx] : kSentinel;
             vals[it] = in ? (p.vals_in ? p.vals_in[idx] : (uint32_t)idx) : 0u;
             aux[it] = (in && has_aux) ? p.aux_in[idx] : 0u;
@@ -723,6 +751,8 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
             if (has_aux) p.aux_out[dest] = s_aux[q];
         }
         __syncthreads();
+        sp += nsub;
+      }
     }
 }
 
@@ -1560,7 +1590,9 @@ static void sort_pass_ipt(const SortPass& p, hipStream_t s) {
     if (!p.part_count)  // else k_project produced the counts (first depth pass of chunk 0)
         hipLaunchKernelGGL(k_radix_upsweep<IPT>, dim3(grid), dim3(kSortThreads), 0, s, p);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(k_radix_downsweep<IPT>, dim3(grid), dim3(kSortThreads), 0, s, p);
+    const uint32_t m = p.part_count ? std::max(1, std::min(p.merge, kMaxMerge)) : 1;
+    const unsigned dgrid = std::min<uint32_t>((p.parts_max + m - 1) / m, kMaxGrid);
+    hipLaunchKernelGGL(k_radix_downsweep<IPT>, dim3(dgrid), dim3(kSortThreads), 0, s, p);
 }
 
 void launch_sort_pass(const SortPass& p, hipStream_t s) {
