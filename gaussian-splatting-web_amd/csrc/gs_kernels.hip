@@ -632,12 +632,16 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
     for (uint32_t unit = blockIdx.x; unit < units; unit += gridDim.x) {
       const uint32_t se = min((unit + 1) * M, parts);
       for (uint32_t sp = unit * M; sp < se;) {  // workgroup-uniform
+        // element counts of partitions sp .. se-1 (compacted input: only partition q's first
+        // part_count[q] elements exist), loaded in parallel, then cut into the round
+        if (tid < (int)(se - sp))
+            s_sub[tid + 1] = p.part_count ? p.part_count[sp + tid] : min((uint32_t)kTileN, n - (sp + tid) * kTileN);
+        __syncthreads();
         if (tid == 0) {
             uint32_t tot = 0, k = 0;
             s_sub[0] = 0;
             for (uint32_t q = sp; q < se; ++q) {
-                // compacted input (k_project): only partition q's first part_count[q] elements exist
-                const uint32_t c = p.part_count ? p.part_count[q] : min((uint32_t)kTileN, n - q * kTileN);
+                const uint32_t c = s_sub[k + 1];
                 if (k > 0 && tot + c > (uint32_t)kTileN) break;
                 tot += c;
                 s_sub[++k] = tot;
