@@ -1244,19 +1244,22 @@ __global__ __launch_bounds__(256) void k_shade(BinParams p) {
 }
 
 // Tile rows of wide splats, one row per work unit (slot, output position, xa | xb << 16, row):
-// each wave prefetches 64 units lane-parallel, then writes them one by one across its lanes.
+// each wave prefetches kWideUnits units lane-parallel, then writes them one by one across its
+// lanes (few units per wave: the rows are short and the wave's loop is the latency).
+constexpr uint32_t kWideUnits = 16;
+
 __global__ __launch_bounds__(kBinThreads) void k_bin_wide(BinParams p) {
     __shared__ unsigned long long s_mask[kMaskLdsWords];
     const uint32_t units = min(p.ctl->wide_rows[p.chunk], p.wide_unit_cap);
-    if (blockIdx.x * (kBinThreads / 64) * 64 >= units) return;
+    if (blockIdx.x * (kBinThreads / 64) * kWideUnits >= units) return;
     const unsigned long long* m = stage_mask(p, s_mask);
     const uint32_t lane = lane_id();
     const uint32_t wave = blockIdx.x * (kBinThreads / 64) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (kBinThreads / 64);
-    for (uint32_t u0 = wave * 64; u0 < units; u0 += nwaves * 64) {
+    for (uint32_t u0 = wave * kWideUnits; u0 < units; u0 += nwaves * kWideUnits) {
         const uint32_t u = u0 + lane;
         uint4 it = make_uint4(0, 0, 0, 0xFFFFFFFFu);
-        if (u < units) it = p.wide_unit[u];
+        if (lane < kWideUnits && u < units) it = p.wide_unit[u];
         uint64_t todo = __ballot(it.w != 0xFFFFFFFFu);
         while (todo) {
             const int src = __ffsll((long long)todo) - 1;
