@@ -459,6 +459,27 @@ napi_value PlyParse(napi_env env, napi_callback_info info) {
     return o;
 }
 
+// encodePng(rgba8, W, H) -> ArrayBuffer: PNG of an RGBA8 image (row 0 = top), gs_encode_png
+napi_value EncodePng(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    get_args(env, info, 3, argv);
+    void* data;
+    size_t len;
+    if (!get_bytes(env, argv[0], &data, &len)) return throw_gs(env, GS_ERR_INVALID, "encodePng: need RGBA8 bytes");
+    const int W = (int)num(env, argv[1], 0), H = (int)num(env, argv[2], 0);
+    if (W <= 0 || H <= 0 || (uint64_t)len < 4ull * (uint64_t)W * (uint64_t)H)
+        return throw_gs(env, GS_ERR_INVALID, "encodePng: buffer smaller than W*H*4");
+    uint64_t need = 0;
+    int rc = gs_encode_png((const uint8_t*)data, W, H, nullptr, 0, &need);
+    if (rc) return throw_gs(env, rc, "gs_encode_png");
+    void* out;
+    napi_value ab;
+    NAPI_OK(napi_create_arraybuffer(env, (size_t)need, &out, &ab));
+    rc = gs_encode_png((const uint8_t*)data, W, H, (uint8_t*)out, need, &need);
+    if (rc) return throw_gs(env, rc, "gs_encode_png");
+    return ab;
+}
+
 napi_value StripRows(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     get_args(env, info, 3, argv);
@@ -485,7 +506,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"sceneFree", SceneFree}, {"render", Render}, {"renderAsync", RenderAsync},
         {"timings", Timings}, {"timingsReset", TimingsReset}, {"sync", Sync}, {"present", Present},
         {"lookAt", LookAt}, {"perspective", Perspective}, {"cameraPosition", CameraPosition},
-        {"packUniforms", PackUniforms}, {"stripRows", StripRows}, {"plyParse", PlyParse},
+        {"packUniforms", PackUniforms}, {"stripRows", StripRows}, {"plyParse", PlyParse}, {"encodePng", EncodePng},
     };
     for (const auto& f : fns) {
         napi_value fn;

@@ -811,6 +811,30 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
     });
 }
 
+int gs_present_device(gs_ctx* c, const void* fb_dev, int fb_format, int W, int H, int out_format,
+                      void* out_dev, uint64_t out_bytes, void* stream) {
+    return guarded([&] {
+        if (!c || !fb_dev || !out_dev) throw GsError(GS_ERR_INVALID, "null argument");
+        if (W <= 0 || H <= 0 || W > 65535 || H > 65535) throw GsError(GS_ERR_INVALID, "bad image size");
+        if (fb_format != GS_OUT_RGBA_F32 && fb_format != GS_OUT_RGBA_F16)
+            throw GsError(GS_ERR_INVALID, "bad framebuffer format");
+        uint64_t px_bytes;
+        switch (out_format) {
+            case GS_PRESENT_RGBA_F32: px_bytes = 16; break;
+            case GS_PRESENT_RGBA_F16: px_bytes = 8; break;
+            case GS_PRESENT_RGBA8: px_bytes = 4; break;
+            default: throw GsError(GS_ERR_INVALID, "bad present format");
+        }
+        if (out_bytes < px_bytes * (uint64_t)W * (uint64_t)H) throw GsError(GS_ERR_INVALID, "output buffer too small");
+        if (fb_dev == out_dev) throw GsError(GS_ERR_INVALID, "present cannot run in place");
+        HIPCHK(hipSetDevice(c->device));
+        launch_present(fb_dev, fb_format == GS_OUT_RGBA_F16, W, H, out_format, out_dev,
+                       stream ? (hipStream_t)stream : c->stream);
+        HIPCHK(hipGetLastError());
+        return GS_OK;
+    });
+}
+
 int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_opts* opts, void* out_host) {
     return guarded([&] {
         validate_render_args(c, s, uni, W, H, opts);

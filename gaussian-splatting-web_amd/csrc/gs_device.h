@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "../../include/gsplat.h"
+
 namespace gs {
 
 constexpr int kTile = 16;             // 16x16-pixel composite tile
@@ -221,6 +223,7 @@ void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsig
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
                    hipStream_t s);
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);
+void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void* out, hipStream_t s);
 
 __host__ __device__ inline uint32_t sort_parts(uint64_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }
 __host__ __device__ inline uint32_t sort_parts(uint64_t n, int ipt) {

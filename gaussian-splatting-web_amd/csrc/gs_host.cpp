@@ -155,11 +155,92 @@ int gs_present(const float* in, int W, int H, float* out) {
             dst[4 * x + 1] = src[4 * x + 1];
             dst[4 * x + 2] = src[4 * x + 2];
             float a = std::fmin(std::fmax(src[4 * x + 3] * 1.5f, 0.0f), 1.0f);
-            if (a < 0.99f) a = std::pow(a, 4.0f);
+            if (a < 0.99f) {  // pow(a, 4) as (a^2)^2: the device kernel rounds identically
+                const float a2 = a * a;
+                a = a2 * a2;
+            }
             dst[4 * x + 3] = a;
         }
     }
     return GS_OK;
+}
+
+// ---- PNG (RGBA8, zlib stream of stored deflate blocks) -------------------------------------
+static uint32_t crc32_update(uint32_t c, const uint8_t* p, size_t n) {
+    static uint32_t table[256];
+    static bool init = false;
+    if (!init) {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t v = i;
+            for (int k = 0; k < 8; ++k) v = (v & 1) ? 0xEDB88320u ^ (v >> 1) : v >> 1;
+            table[i] = v;
+        }
+        init = true;
+    }
+    c = ~c;
+    for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    return ~c;
+}
+
+static uint64_t png_size(int W, int H) {
+    const uint64_t raw = (uint64_t)H * (1 + 4 * (uint64_t)W);
+    const uint64_t blocks = raw ? (raw + 65534) / 65535 : 1;
+    return 8 + 25 + (12 + 2 + raw + 5 * blocks + 4) + 12;
+}
+
+int gs_encode_png(const uint8_t* rgba8, int W, int H, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    if (!out_len || W <= 0 || H <= 0 || (!rgba8 && out)) return GS_ERR_INVALID;
+    const uint64_t need = png_size(W, H);
+    *out_len = need;
+    if (!out) return GS_OK;
+    if (cap < need) return GS_ERR_INVALID;
+    uint8_t* o = out;
+    auto be32 = [&](uint32_t v) {
+        o[0] = v >> 24; o[1] = (v >> 16) & 0xFF; o[2] = (v >> 8) & 0xFF; o[3] = v & 0xFF;
+        o += 4;
+    };
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+    std::memcpy(o, sig, 8);
+    o += 8;
+    auto chunk = [&](const char* type, uint64_t len, auto&& body) {
+        be32((uint32_t)len);
+        uint8_t* start = o;
+        std::memcpy(o, type, 4);
+        o += 4;
+        body();
+        be32(crc32_update(0, start, (size_t)(o - start)));
+    };
+    chunk("IHDR", 13, [&] {
+        be32((uint32_t)W);
+        be32((uint32_t)H);
+        *o++ = 8;  // bit depth
+        *o++ = 6;  // colour type RGBA
+        *o++ = 0; *o++ = 0; *o++ = 0;  // deflate, adaptive filtering, no interlace
+    });
+    const uint64_t row = 1 + 4 * (uint64_t)W, raw = (uint64_t)H * row;
+    const uint64_t blocks = (raw + 65534) / 65535;
+    chunk("IDAT", 2 + raw + 5 * blocks + 4, [&] {
+        *o++ = 0x78;  // zlib: deflate, 32 K window
+        *o++ = 0x01;
+        uint32_t s1 = 1, s2 = 0;  // Adler-32
+        uint64_t pos = 0;         // position in the filtered raw stream
+        for (uint64_t b = 0; b < blocks; ++b) {
+            const uint32_t len = (uint32_t)std::min<uint64_t>(65535, raw - pos);
+            *o++ = b + 1 == blocks ? 1 : 0;  // BFINAL, BTYPE = stored
+            *o++ = len & 0xFF; *o++ = len >> 8;
+            *o++ = ~len & 0xFF; *o++ = (~len >> 8) & 0xFF;
+            for (uint32_t k = 0; k < len; ++k, ++pos) {
+                const uint64_t y = pos / row, c = pos % row;
+                const uint8_t v = c == 0 ? 0 : rgba8[y * 4 * (uint64_t)W + (c - 1)];  // filter 0
+                *o++ = v;
+                s1 = (s1 + v) % 65521;
+                s2 = (s2 + s1) % 65521;
+            }
+        }
+        be32((s2 << 16) | s1);
+    });
+    chunk("IEND", 0, [] {});
+    return (uint64_t)(o - out) == need ? GS_OK : GS_ERR_INTERNAL;
 }
 
 // Synthetic scene, SURVEY §8d / BASELINE.md §4: camera lookAt([0,0,0],[0,0,-1],[0,1,0]), depth

@@ -1566,9 +1566,50 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     }
 }
 
+// ============================================================================ k_present
+// PostProcessRenderer.fragmentMain (src/post_process_render.ts:62-77) per pixel: the sampler
+// reads texel (x, H-1-y) at its centre (exact), a' = saturate(1.5 a), a' = a'^4 (as (a'^2)^2,
+// gs_present's rounding) when a' < 0.99; stored as f32, f16 (the rgba16float canvas) or unorm8.
+__global__ __launch_bounds__(256) void k_present(const void* __restrict__ in, int in_f16, int W, int H,
+                                                 int out_kind, void* __restrict__ out) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const uint64_t npx = (uint64_t)W * H;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < npx; i += (uint64_t)gridDim.x * 256ull) {
+        const uint32_t y = (uint32_t)(i / (uint32_t)W), x = (uint32_t)(i % (uint32_t)W);
+        const uint64_t src = (uint64_t)(H - 1 - y) * W + x;
+        float4 c;
+        if (in_f16) {
+            const h4 v = ((const h4*)in)[src];
+            c = make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
+        } else {
+            c = ((const float4*)in)[src];
+        }
+        float a = fminf(fmaxf(c.w * 1.5f, 0.0f), 1.0f);
+        if (a < 0.99f) {
+            const float a2 = a * a;
+            a = a2 * a2;
+        }
+        c.w = a;
+        if (out_kind == GS_PRESENT_RGBA_F32) {
+            ((float4*)out)[i] = c;
+        } else if (out_kind == GS_PRESENT_RGBA_F16) {
+            ((h4*)out)[i] = h4{(_Float16)c.x, (_Float16)c.y, (_Float16)c.z, (_Float16)c.w};
+        } else {
+            auto u8 = [](float v) { return (uint32_t)rintf(fminf(fmaxf(v, 0.0f), 1.0f) * 255.0f); };
+            ((uint32_t*)out)[i] = u8(c.x) | (u8(c.y) << 8) | (u8(c.z) << 16) | (u8(c.w) << 24);
+        }
+    }
+}
+
 }  // namespace
 
 // ============================================================================ launchers
+void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void* out, hipStream_t s) {
+    const uint64_t npx = (uint64_t)W * H;
+    if (!npx) return;
+    const unsigned grid = (unsigned)std::min<uint64_t>(8192, (npx + 255) / 256);
+    hipLaunchKernelGGL(k_present, dim3(grid), dim3(256), 0, s, in, in_f16, W, H, out_kind, out);
+}
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, float4* shade, float4* cull,
                       hipStream_t s) {
     if (!n) return;

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("GSPLAT_LIB") or os.path.join(os.path.dirname(_HERE), 
 GS_OK = 0
 GS_ACCUM_FP32, GS_ACCUM_FP16_TARGET = 0, 1
 GS_OUT_RGBA_F32, GS_OUT_RGBA_F16 = 0, 1
+GS_PRESENT_RGBA_F32, GS_PRESENT_RGBA_F16, GS_PRESENT_RGBA8 = 0, 1, 2
 GS_OK, GS_ERR_INVALID, GS_ERR_NO_DEVICE, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_DEVICE_FAULT, \
     GS_ERR_INTERNAL = 0, -1, -2, -3, -4, -5, -6, -7
 
@@ -26,7 +27,8 @@ GS_OK, GS_ERR_INVALID, GS_ERR_NO_DEVICE, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPOR
 EXPORTED_SYMBOLS = (
     "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy",
     "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows",
-    "gs_render", "gs_render_device", "gs_timings", "gs_timings_reset", "gs_sync", "gs_present", "gs_look_at",
+    "gs_render", "gs_render_device", "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
+    "gs_present_device", "gs_encode_png", "gs_look_at",
     "gs_perspective", "gs_camera_position", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
     "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records",
 )
@@ -106,6 +108,8 @@ def lib():
         L.gs_timings_reset.argtypes = [P]
         L.gs_sync.argtypes = [P]
         L.gs_present.argtypes = [P, I, I, P]
+        L.gs_present_device.argtypes = [P, P, I, I, I, I, P, U64, P]
+        L.gs_encode_png.argtypes = [P, I, I, P, U64, ctypes.POINTER(U64)]
         L.gs_look_at.argtypes = [P, P, P, P]
         L.gs_perspective.argtypes = [D, D, D, D, P]
         L.gs_camera_position.argtypes = [P, P]
@@ -192,6 +196,22 @@ def present(rgba, W, H):
     return out.reshape(H, W, 4)
 
 
+def encode_png(rgba8):
+    """PNG bytes of an (H, W, 4) uint8 image (row 0 = top), via gs_encode_png."""
+    img = np.ascontiguousarray(rgba8, np.uint8)
+    H, W = img.shape[0], img.shape[1]
+    n = ctypes.c_uint64()
+    _check(lib().gs_encode_png(None, W, H, None, 0, ctypes.byref(n)))
+    out = np.empty(n.value, np.uint8)
+    _check(lib().gs_encode_png(_ptr(img), W, H, _ptr(out), n.value, ctypes.byref(n)))
+    return out.tobytes()
+
+
+def write_png(path, rgba8):
+    with open(path, "wb") as f:
+        f.write(encode_png(rgba8))
+
+
 def strip_rows(H, strip_index, strip_count):
     r0, rp = ctypes.c_int(), ctypes.c_int()
     _check(lib().gs_strip_rows(int(H), int(strip_index), int(strip_count), ctypes.byref(r0), ctypes.byref(rp)))
@@ -254,6 +274,11 @@ class Context:
 
     def timings_reset(self):
         _check(lib().gs_timings_reset(self.handle))
+
+    def present_device(self, fb_ptr, fb_format, W, H, out_format, out_ptr, out_bytes, stream_ptr=None):
+        """PostProcessRenderer on the device (gs_present_device): framebuffer -> presented image."""
+        _check(lib().gs_present_device(self.handle, fb_ptr, int(fb_format), int(W), int(H), int(out_format),
+                                       out_ptr, int(out_bytes), stream_ptr))
 
     def sort_pairs(self, keys, vals, begin_bit=0, end_bit=32):
         k = np.array(keys, np.uint32, copy=True)

@@ -16,7 +16,8 @@
  *   gs_look_at / gs_perspective /
  *   gs_camera_position              <- wgpu-matrix lookAt/perspective/inverse+getTranslation as used by
  *                                      src/camera.ts:101-138 (f32 storage semantics)
- *   gs_present                      <- PostProcessRenderer.draw               (src/post_process_render.ts:54-77)
+ *   gs_present / gs_present_device  <- PostProcessRenderer.draw               (src/post_process_render.ts:54-77)
+ *   gs_encode_png                   <- (new: PNG dumps of the presented image for visual diffs)
  *
  * Conventions: every function returns 0 on success and a negative gs_status on failure; no C++
  * exception crosses the ABI; gs_last_error() returns a thread-local message for the last failure.
@@ -139,8 +140,26 @@ int gs_timings_reset(gs_ctx* ctx);
 int gs_sync(gs_ctx* ctx);
 
 /* PostProcessRenderer (src/post_process_render.ts:54-77) on the host-visible image: y flip,
- * a' = sat(1.5a), a' = a'^4 if a' < 0.99.  rgba_in/out: W*H f32x4 host buffers. */
+ * a' = sat(1.5a), a' = a'^4 (computed as (a'^2)^2) if a' < 0.99.  rgba_in/out: W*H f32x4 host
+ * buffers. */
 int gs_present(const float* rgba_in, int W, int H, float* rgba_out);
+
+typedef enum {
+    GS_PRESENT_RGBA_F32 = 0,  /* f32x4 */
+    GS_PRESENT_RGBA_F16 = 1,  /* f16x4: the reference's rgba16float canvas (src/post_process_render.ts:24) */
+    GS_PRESENT_RGBA8 = 2      /* unorm8x4 = round(sat(v) * 255), for PNG dumps */
+} gs_present_format;
+
+/* The same transform on the device, from a framebuffer gs_render_device wrote (fb_format =
+ * GS_OUT_RGBA_F32 or GS_OUT_RGBA_F16, W*H pixels, row 0 = top) into out_dev (>= out_bytes) in
+ * out_format, on hip_stream (NULL = the ctx's stream); returns when the work is enqueued.  For
+ * the same input it equals gs_present bit for bit (f32), or that result rounded (f16, unorm8). */
+int gs_present_device(gs_ctx* ctx, const void* fb_dev, int fb_format, int W, int H, int out_format,
+                      void* out_dev, uint64_t out_bytes, void* hip_stream);
+
+/* PNG (RGBA, 8 bits, stored deflate blocks, no external library) of a W*H RGBA8 image, row 0 =
+ * top.  out == NULL: *out_len = bytes needed.  GS_ERR_INVALID when cap is too small. */
+int gs_encode_png(const uint8_t* rgba8, int W, int H, uint8_t* out, uint64_t cap, uint64_t* out_len);
 
 /* ---- camera / uniforms (headless producer; wgpu-matrix 2.9.1 semantics, f32 storage) ------- */
 int gs_look_at(const double eye[3], const double target[3], const double up[3], float out_view[16]);

@@ -61,6 +61,8 @@ async function main() {
     const g = gs.PackedGaussians.fromPly(ply.buffer.slice(ply.byteOffset, ply.byteOffset + ply.byteLength));
     out.ply = {n: g.numGaussians, nsh: g.nShCoeffs, deg: g.sphericalHarmonicsDegree, min: g.min_pos, max: g.max_pos,
                hex: Buffer.from(g.gaussiansBuffer).toString('hex')};
+    const px = new Uint8Array(3 * 2 * 4).map((_, i) => i);
+    out.png = Buffer.from(a.encodePng(px, 3, 2)).toString('hex');
     try {
         gs.PackedGaussians.fromPly(new ArrayBuffer(10));
         out.plyBad = 'accepted';

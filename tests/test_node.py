@@ -19,7 +19,7 @@ pytestmark = pytest.mark.skipif(not NODE or not os.path.exists(ADDON), reason="n
 
 EXPORTS = sorted(["abiVersion", "lastError", "deviceCount", "ctxCreate", "ctxDestroy", "sceneUpload", "sceneFree",
                   "render", "renderAsync", "timings", "timingsReset", "sync", "present", "lookAt", "perspective",
-                  "cameraPosition", "packUniforms", "stripRows", "plyParse"])
+                  "cameraPosition", "packUniforms", "stripRows", "plyParse", "encodePng"])
 
 
 def run_node(*args, timeout=120):
@@ -52,6 +52,9 @@ def test_node_host_cpu():
     assert out["ply"]["deg"] == meta["shDegree"]
     assert out["ply"]["min"] == meta["min_pos"] and out["ply"]["max"] == meta["max_pos"]
     assert out["plyBad"] == -1
+    import gsplat_amd as gs
+    png = bytes.fromhex(out["png"])
+    assert png == gs.encode_png(np.arange(3 * 2 * 4, dtype=np.uint8).reshape(2, 3, 4))
 
 
 @pytest.mark.gpu

@@ -1,0 +1,101 @@
+"""Present + readback: PostProcessRenderer (src/post_process_render.ts:54-77)
+on the device, and the PNG encoder used for visual diffs.
+
+CPU: gs_encode_png decodes (PIL, and an independent zlib parse) to the exact input pixels.
+GPU: gs_present_device equals the host gs_present bit for bit (f32 out), or that result rounded
+to f16 (the reference's rgba16float canvas) / unorm8, from f32 and f16 framebuffers."""
+import os
+import struct
+import sys
+import zlib
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gaussian-splatting-web_amd"))
+import gsplat_amd as gs  # noqa: E402
+
+
+def _decode_png_stored(data):
+    """Minimal PNG reader for 8-bit RGBA, filter 0 (independent of PIL)."""
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, W, H = 8, b"", None, None
+    while pos < len(data):
+        ln, = struct.unpack(">I", data[pos:pos + 4])
+        typ, body = data[pos + 4:pos + 8], data[pos + 8:pos + 8 + ln]
+        crc, = struct.unpack(">I", data[pos + 8 + ln:pos + 12 + ln])
+        assert zlib.crc32(typ + body) & 0xFFFFFFFF == crc, typ
+        if typ == b"IHDR":
+            W, H, depth, ctype = struct.unpack(">IIBB", body[:10])
+            assert (depth, ctype) == (8, 6)
+        elif typ == b"IDAT":
+            idat += body
+        pos += 12 + ln
+    raw = zlib.decompress(idat)
+    rows = np.frombuffer(raw, np.uint8).reshape(H, 1 + 4 * W)
+    assert np.all(rows[:, 0] == 0)
+    return rows[:, 1:].reshape(H, W, 4)
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (3, 5), (64, 48), (300, 400)])
+def test_png_roundtrip(shape):
+    H, W = shape
+    rng = np.random.default_rng(H * 1000 + W)
+    img = rng.integers(0, 256, (H, W, 4), dtype=np.uint8)
+    png = gs.encode_png(img)
+    assert np.array_equal(_decode_png_stored(png), img)
+    from io import BytesIO
+    try:
+        from PIL import Image
+    except ImportError:
+        return
+    im = Image.open(BytesIO(png))
+    assert im.mode == "RGBA" and im.size == (W, H)
+    assert np.array_equal(np.asarray(im), img)
+
+
+def test_png_multi_block():
+    """Raw stream above one stored block (65535 B) splits into several."""
+    img = np.arange(200 * 120 * 4, dtype=np.uint32).astype(np.uint8).reshape(120, 200, 4)
+    assert np.array_equal(_decode_png_stored(gs.encode_png(img)), img)
+
+
+def test_png_bad_args():
+    n = __import__("ctypes").c_uint64()
+    assert gs.lib().gs_encode_png(None, 0, 4, None, 0, __import__("ctypes").byref(n)) == gs.GS_ERR_INVALID
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fb_format", [gs.GS_OUT_RGBA_F32, gs.GS_OUT_RGBA_F16])
+def test_present_device_matches_host(gpu_ctx, fb_format):
+    W, H = 320, 200
+    aos = gs.synth_aos(50_000, 4, W, H)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, 50_000, 16)
+    bpp = 16 if fb_format == gs.GS_OUT_RGBA_F32 else 8
+    fb = gs.DeviceBuffer(W * H * bpp)
+    sc.render_device(u, W, H, fb.ptr.value, fb.nbytes, opts=gs.make_opts(out_format=fb_format))
+    gpu_ctx.sync()
+    fb_host = np.empty((H, W, 4), np.float32 if bpp == 16 else np.float16)
+    fb.to_host(fb_host)
+    ref = gs.present(fb_host.astype(np.float32), W, H)  # host PostProcessRenderer
+    assert ref[..., 3].max() > 0.5  # a non-trivial image
+    for fmt, dt in ((gs.GS_PRESENT_RGBA_F32, np.float32), (gs.GS_PRESENT_RGBA_F16, np.float16),
+                    (gs.GS_PRESENT_RGBA8, np.uint8)):
+        out = gs.DeviceBuffer(W * H * 4 * np.dtype(dt).itemsize)
+        gpu_ctx.present_device(fb.ptr, fb_format, W, H, fmt, out.ptr, out.nbytes)
+        gpu_ctx.sync()
+        got = np.empty((H, W, 4), dt)
+        out.to_host(got)
+        if dt == np.float32:
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+        elif dt == np.float16:
+            assert np.array_equal(got.view(np.uint16), ref.astype(np.float16).view(np.uint16))
+        else:
+            assert np.array_equal(got, np.rint(np.clip(ref, 0.0, 1.0) * 255.0).astype(np.uint8))
+        out.free()
+    bad = gs.lib().gs_present_device(gpu_ctx.handle, fb.ptr, fb_format, W, H, 7, fb.ptr, fb.nbytes, None)
+    assert bad == gs.GS_ERR_INVALID
+    fb.free()
+    sc.close()
