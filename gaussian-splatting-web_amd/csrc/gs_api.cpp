@@ -190,6 +190,11 @@ static constexpr size_t kHistWords = kHistShards * 256;
 #define GS_TILE_IPT 8
 #endif
 static constexpr int kDepthSortIpt = GS_DEPTH_IPT, kTileSortIpt = GS_TILE_IPT;
+// chunk-0 threshold: the farthest saturation key of the last frame, its depth scaled by this
+#ifndef GS_CHUNK_MARGIN
+#define GS_CHUNK_MARGIN 1.15f
+#endif
+static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
 static constexpr int kMinSortIpt = kDepthSortIpt < kTileSortIpt ? kDepthSortIpt : kTileSortIpt;
 static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 12 * kHistWords * 4;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
@@ -313,7 +318,7 @@ static void collect_stats(gs_scene* s, bool wait) {
         for (int k = 0; k < kHistShards; ++k) sat_tiles += l.sat_tiles[k];
         uint32_t target = kNoSplit;
         if (l.n_vis > 0 && l.sat_key != 0 && sat_tiles >= 0.5 * std::max(1, s->last_tiles))
-            target = scaled_threshold(l.sat_key, 1.15f);
+            target = scaled_threshold(l.sat_key, kChunkMargin);
         if (target >= s->chunk_T || s->chunk_T == kNoSplit)
             s->chunk_T = target;
         else
