@@ -154,7 +154,9 @@ struct gs_scene {
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tkA = nullptr, *tvA = nullptr, *tkB = nullptr, *tvB = nullptr;
-    uint32_t* radix_offsets = nullptr;  // 256 x sort_parts(max(N, kcap))
+    uint32_t* radix_offsets = nullptr;  // 256 x sort_parts(max(N, kcap)): partition counts
+    uint32_t* gsum = nullptr;           // 12 regions (chunk x 6 passes) of group sums, zero between uses
+    size_t gsum_region = 0;             // words per region
     uint2* ranges = nullptr;
     uint8_t* done = nullptr;
     uint32_t* sat = nullptr;            // (strip rows + 1) x (tiles_x + 1), then the bitmask
@@ -210,6 +212,12 @@ static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
     dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB); dev_free(s->radix_offsets);
     dev_alloc(s->tkA, cap); dev_alloc(s->tvA, cap); dev_alloc(s->tkB, cap); dev_alloc(s->tvB, cap);
     dev_alloc(s->radix_offsets, 256 * (size_t)sort_parts(std::max<uint64_t>(cap, s->n), kMinSortIpt));
+    // group sums: every pass's partitions fit a region (kept zero: k_ranges resets after use)
+    dev_free(s->gsum);
+    const size_t parts = sort_parts(std::max<uint64_t>(cap, s->n), kMinSortIpt);
+    s->gsum_region = 256 * ((parts + kGroupParts - 1) / kGroupParts + 1);
+    dev_alloc(s->gsum, 12 * s->gsum_region);
+    HIPCHK(hipMemset(s->gsum, 0, 12 * s->gsum_region * sizeof(uint32_t)));
     s->kcap = cap;
 }
 
@@ -400,6 +408,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.c_rect = s->auxB;
     pp.c_count = s->part_count;
     pp.offsets = s->radix_offsets;
+    pp.gsum = s->gsum;  // chunk 0, pass 0's region
     pp.parts_max = sort_parts(pp.n);
     pp.hist0 = s->hist;
     mark(EV_PROJ0);
@@ -477,6 +486,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.tile_row_begin = tr_begin;
             sp.hist = s->hist + (6 * chunk + ps) * kHistWords;
             sp.offsets = s->radix_offsets;
+            sp.gsum = s->gsum + (size_t)(6 * chunk + ps) * s->gsum_region;
             launch_sort_pass(sp, st);
         }
         mark(eb);
@@ -531,13 +541,15 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.mask = 255;
             sp.hist = s->hist + (6 * chunk + 4 + ps) * kHistWords;
             sp.offsets = s->radix_offsets;
+            sp.gsum = s->gsum + (size_t)(6 * chunk + 4 + ps) * s->gsum_region;
             launch_sort_pass(sp, st);
             std::swap(tk_in, tk_out);
             std::swap(tv_in, tv_out);
         }
         mark(eb + 2);
         HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)std::max(n_tiles, 1) * sizeof(uint2), st));
-        launch_ranges(tk_in, &s->ctl->k_chunk[chunk], (uint32_t)s->kcap, s->ranges, st);
+        launch_ranges(tk_in, &s->ctl->k_chunk[chunk], (uint32_t)s->kcap, s->ranges,
+                      s->gsum + (size_t)(6 * chunk) * s->gsum_region, 6 * s->gsum_region, st);
         mark(eb + 3);
 
         CompositeParams cp{};
@@ -772,6 +784,7 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->part_count);
     dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB);
     dev_free(s->radix_offsets);
+    dev_free(s->gsum);
     dev_free(s->ranges);
     dev_free(s->done);
     dev_free(s->sat);
@@ -930,14 +943,17 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
         if (n == 0) return GS_OK;
         HIPCHK(hipSetDevice(c->device));
         const int npass = (end_bit - begin_bit + 7) / 8;
-        uint32_t *kA, *vA, *kB, *vB, *hist, *offs;
+        uint32_t *kA, *vA, *kB, *vB, *hist, *offs, *gsum;
         dev_alloc(kA, n); dev_alloc(vA, n); dev_alloc(kB, n); dev_alloc(vB, n);
         dev_alloc(hist, (size_t)npass * kHistWords);
         dev_alloc(offs, (size_t)256 * sort_parts(n, kDepthSortIpt));
+        const size_t region = 256 * ((sort_parts(n, kDepthSortIpt) + kGroupParts - 1) / kGroupParts + 1);
+        dev_alloc(gsum, (size_t)npass * region);
         hipStream_t st = c->stream;
         HIPCHK(hipMemcpyAsync(kA, keys, n * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(vA, vals, n * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemsetAsync(hist, 0, (size_t)npass * kHistWords * 4, st));
+        HIPCHK(hipMemsetAsync(gsum, 0, (size_t)npass * region * 4, st));
         uint32_t *ki = kA, *vi = vA, *ko = kB, *vo = vB;
         for (int ps = 0; ps < npass; ++ps) {
             SortPass sp{};
@@ -950,6 +966,7 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
             sp.mask = (1u << bits) - 1u;
             sp.hist = hist + ps * kHistWords;
             sp.offsets = offs;
+            sp.gsum = gsum + (size_t)ps * region;
             launch_sort_pass(sp, st);
             std::swap(ki, ko);
             std::swap(vi, vo);
@@ -959,6 +976,7 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
         HIPCHK(hipMemcpyAsync(vals, vi, n * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         dev_free(kA); dev_free(vA); dev_free(kB); dev_free(vB); dev_free(hist); dev_free(offs);
+        dev_free(gsum);
         return GS_OK;
     });
 }

@@ -28,6 +28,7 @@ constexpr uint32_t kWideTiles = 32;     // splats binding >= this many tiles are
 constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
 constexpr int kMaskLdsWords = 2048;     // unsaturated-tile bitmask cached in LDS up to this size
 constexpr int kMaxMerge = 16;           // compacted radix input: partitions per downsweep workgroup
+constexpr uint32_t kGroupParts = 32;    // radix partitions per group sum (the downsweep's offsets)
 
 // Packed tile rectangle carried through the depth sort (32 bits): tx0[0:12) ty0[12:24)
 // (w-1)[24:28) (h-1)[28:32).  Rectangles wider or taller than 16 tiles use kRectLarge (the
@@ -108,7 +109,8 @@ struct ProjParams {
     uint32_t* c_vals;         //      order to the front of each partition
     uint32_t* c_rect;
     uint32_t* c_count;        // out: [parts] chunk-0 elements per partition
-    uint32_t* offsets;        // out: [256][parts_max] digit-0 counts per partition
+    uint32_t* offsets;        // out: [parts][256] digit-0 counts per partition
+    uint32_t* gsum;           // out: [parts / kGroupParts][256] their group sums (zeroed)
     uint32_t parts_max;
     uint32_t* hist0;          // out: [kHistShards][256] digit-0 histogram (zeroed)
     // two-phase frames: k_cull's keep bit per Gaussian (bit i%64 of word i/64)
@@ -146,14 +148,16 @@ struct SortPass {
     uint32_t mask;            // digit mask (<= 255)
     int filter;               // RadixFilter
     uint32_t thresh;          // chunk threshold key (kFiltBelow / kFiltTail)
-    uint32_t* count_out;      // optional: number of elements kept (written by the scan)
+    uint32_t* count_out;      // optional: number of elements kept (written by the downsweep)
     // kFiltTail: the element's tile rect is aux; wide rects from the record; unsaturated-tile SAT
     Records rec;
     const uint32_t* sat;
     int tiles_x, tile_row_begin;
     uint32_t* hist;           // [kHistShards][256] digit histogram of this pass (zeroed; the
-                              // upsweep accumulates it, the scan turns it into digit bases)
-    uint32_t* offsets;        // [256][parts_max] scratch: partition counts, then offsets
+                              // upsweep accumulates it, the downsweep scans it into digit bases)
+    uint32_t* offsets;        // [parts][256] scratch: partition counts (upsweep)
+    uint32_t* gsum;           // [parts / kGroupParts][256] group sums of the counts (zeroed; reset
+                              // by k_ranges after the chunk's passes)
 };
 
 struct BinParams {
@@ -221,7 +225,7 @@ void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, Records rec, 
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s);
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
-                   hipStream_t s);
+                   uint32_t* zero_words, uint64_t zero_n, hipStream_t s);  // zero_n % 4 == 0
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);
 void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void* out, hipStream_t s);
 

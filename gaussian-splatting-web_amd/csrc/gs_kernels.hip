@@ -492,8 +492,11 @@ __global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
                 p.c_rect[pos] = p.rect_out[i];
             }
         }
-        p.offsets[(uint64_t)tid * p.parts_max + part] = s_hist[tid];  // digit-major, as the upsweep
-        if (s_hist[tid]) atomicAdd(&p.hist0[(part % kHistShards) * 256 + tid], s_hist[tid]);
+        p.offsets[(uint64_t)part * 256 + tid] = s_hist[tid];  // partition-major, as the upsweep
+        if (s_hist[tid]) {
+            atomicAdd(&p.gsum[(part / kGroupParts) * 256 + tid], s_hist[tid]);
+            atomicAdd(&p.hist0[(part % kHistShards) * 256 + tid], s_hist[tid]);
+        }
         if (tid == 0) p.c_count[part] = s_total;
         __syncthreads();
     }
@@ -509,12 +512,26 @@ __global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
 }
 
 // ============================================================================ radix pass
-// One stable LSD pass = three launches, no inter-workgroup waiting:
-//   k_radix_upsweep    per 4096-element partition: digit histogram -> counts[digit][part]
-//   k_radix_scan       per digit: offsets[digit][part] = base[digit] + sum of earlier partitions
-//   k_radix_downsweep  per partition: stable local ranks (wave ballots, element order inside the
-//                      partition = (wave, item, lane)), LDS staging, contiguous writes per digit run
+// One stable LSD pass = two launches, no inter-workgroup waiting:
+//   k_radix_upsweep    per partition (256 x IPT elements): digit histogram -> counts[part][digit],
+//                      the pass's global histogram and group sums gsum[part / 32][digit] (atomics)
+//   k_radix_downsweep  per partition: its offsets (digit base from the global histogram + earlier
+//                      groups' sums + earlier partitions of its group), stable local ranks (wave
+//                      ballots, element order inside the partition = (wave, item, lane)), LDS
+//                      staging, contiguous writes per digit run
 // This replaces webgpu-radix-sort's 16 x 2-bit passes (RS:621-654) with 8-bit digits.
+
+// Sum of column entries a[0], a[256], ..., a[256 (m - 1)]: 8 independent loads in flight.
+__device__ __forceinline__ uint32_t sum_column(const uint32_t* __restrict__ a, uint32_t m) {
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t k = 0;
+    for (; k + 8 <= m; k += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] += a[(uint64_t)(k + u) * 256];
+    }
+    for (; k < m; ++k) acc[0] += a[(uint64_t)k * 256];
+    return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
 
 __device__ __forceinline__ uint32_t radix_n(const SortPass& p) {
     if (p.gate && *p.gate == 0) return 0;
@@ -569,41 +586,13 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(SortPass p) {
         }
         __syncthreads();
         const uint32_t c = s_hist[0][tid] + s_hist[1][tid] + s_hist[2][tid] + s_hist[3][tid];
-        p.offsets[(uint64_t)tid * p.parts_max + part] = c;  // digit-major
+        p.offsets[(uint64_t)part * 256 + tid] = c;  // partition-major
+        if (c) atomicAdd(&p.gsum[(part / kGroupParts) * 256 + tid], c);
         total += c;
         __syncthreads();
     }
     // global digit histogram of this pass (kHistShards shards, zeroed with the frame)
     if (total) atomicAdd(&p.hist[(blockIdx.x % kHistShards) * 256 + tid], total);
-}
-
-// Block d scans column d over partitions and adds the global digit base (exclusive scan of the
-// global histogram, which the producing kernel accumulated in kHistShards shards).
-__global__ __launch_bounds__(256) void k_radix_scan(SortPass p) {
-    __shared__ uint32_t s_tmp[8];
-    __shared__ uint32_t s_base;
-    const int d = blockIdx.x, tid = threadIdx.x;
-    const uint32_t tile_n = (uint32_t)kSortThreads * (uint32_t)p.ipt;
-    const uint32_t parts = (radix_n(p) + tile_n - 1) / tile_n;
-    uint32_t tot = 0;
-    for (int sh = 0; sh < kHistShards; ++sh) tot += p.hist[sh * 256 + tid];
-    uint32_t gtotal;
-    const uint32_t gbase = block_excl_scan256(tot, s_tmp, &gtotal);
-    if (tid == d) s_base = gbase;
-    if (d == 0 && tid == 0 && p.count_out) *p.count_out = gtotal;  // elements kept by this pass
-    __syncthreads();
-    uint32_t* col = p.offsets + (uint64_t)d * p.parts_max;
-    const uint32_t per = (parts + 255) / 256;
-    const uint32_t b0 = min(parts, tid * per), b1 = min(parts, b0 + per);
-    uint32_t sum = 0;
-    for (uint32_t i = b0; i < b1; ++i) sum += col[i];
-    uint32_t total;
-    uint32_t run = s_base + block_excl_scan256(sum, s_tmp, &total);
-    for (uint32_t i = b0; i < b1; ++i) {
-        const uint32_t c = col[i];
-        col[i] = run;
-        run += c;
-    }
 }
 
 template <int IPT>
@@ -629,6 +618,16 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
     // (merge > 1 only for the compacted input of k_project, whose partitions are mostly empty.)
     const uint32_t M = p.part_count ? max(1u, min((uint32_t)p.merge, (uint32_t)kMaxMerge)) : 1u;
     const uint32_t units = (parts + M - 1) / M;
+    // digit d's base: exclusive scan of the pass's global histogram (every workgroup computes it;
+    // workgroup 0 also reports the elements this pass keeps)
+    uint32_t dbase;
+    {
+        uint32_t tot = 0;
+        for (int sh = 0; sh < kHistShards; ++sh) tot += p.hist[sh * 256 + tid];
+        uint32_t gtotal;
+        dbase = block_excl_scan256(tot, s_tmp, &gtotal);
+        if (blockIdx.x == 0 && tid == 0 && p.count_out) *p.count_out = gtotal;
+    }
     for (uint32_t unit = blockIdx.x; unit < units; unit += gridDim.x) {
       const uint32_t se = min((unit + 1) * M, parts);
       for (uint32_t sp = unit * M; sp < se;) {  // workgroup-uniform
@@ -649,7 +648,12 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
             s_nsub = k;
         }
         for (int t = tid; t < 1024; t += kSortThreads) (&s_wave_hist[0][0])[t] = 0;
-        s_global[tid] = p.offsets[(uint64_t)tid * p.parts_max + sp];
+        {   // digit tid's first output position for partition sp: its base, the group sums of the
+            // earlier groups and the counts of the earlier partitions of sp's group (no scan launch)
+            const uint32_t g = sp / kGroupParts;
+            s_global[tid] = dbase + sum_column(p.gsum + tid, g) +
+                            sum_column(p.offsets + (uint64_t)g * kGroupParts * 256 + tid, sp - g * kGroupParts);
+        }
         __syncthreads();
         const uint32_t nsub = s_nsub, total = s_sub[nsub];
 
@@ -1343,7 +1347,11 @@ __global__ __launch_bounds__(1024) void k_sat(const uint8_t* __restrict__ done, 
 // ============================================================================ k_ranges
 __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tkeys,
                                                 const uint32_t* __restrict__ k_dev,
-                                                uint2* __restrict__ ranges) {
+                                                uint2* __restrict__ ranges, uint4* __restrict__ zero,
+                                                uint32_t zero_n) {
+    // the chunk's radix passes are done: reset their group sums for the next use
+    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < zero_n; q += gridDim.x * 256)
+        zero[q] = make_uint4(0, 0, 0, 0);
     const uint32_t k = *k_dev;
     for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < k; q += gridDim.x * 256) {
         const uint32_t t = tkeys[q];
@@ -1637,7 +1645,6 @@ static void sort_pass_ipt(const SortPass& p, hipStream_t s) {
     const unsigned grid = std::min<uint32_t>(p.parts_max, kMaxGrid);
     if (!p.part_count)  // else k_project produced the counts (first depth pass of chunk 0)
         hipLaunchKernelGGL(k_radix_upsweep<IPT>, dim3(grid), dim3(kSortThreads), 0, s, p);
-    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, p);
     const uint32_t m = p.part_count ? std::max(1, std::min(p.merge, kMaxMerge)) : 1;
     const unsigned dgrid = std::min<uint32_t>((p.parts_max + m - 1) / m, kMaxGrid);
     hipLaunchKernelGGL(k_radix_downsweep<IPT>, dim3(dgrid), dim3(kSortThreads), 0, s, p);
@@ -1669,9 +1676,10 @@ void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsig
     hipLaunchKernelGGL(k_sat, dim3(1), dim3(1024), 0, s, done, tiles_x, rows, sat, mask, ctl);
 }
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
-                   hipStream_t s) {
+                   uint32_t* zero_words, uint64_t zero_n, hipStream_t s) {
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (k_max + 255) / 256));
-    hipLaunchKernelGGL(k_ranges, dim3(grid), dim3(256), 0, s, tkeys, k_dev, ranges);
+    hipLaunchKernelGGL(k_ranges, dim3(grid), dim3(256), 0, s, tkeys, k_dev, ranges, (uint4*)zero_words,
+                       (uint32_t)(zero_n / 4));
 }
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;
