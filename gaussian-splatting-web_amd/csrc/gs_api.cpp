@@ -155,7 +155,8 @@ struct gs_scene {
     uint64_t kcap = 0;
     uint32_t *tkA = nullptr, *tvA = nullptr, *tkB = nullptr, *tvB = nullptr;
     uint32_t* radix_offsets = nullptr;  // 256 x sort_parts(max(N, kcap)): partition counts
-    uint32_t* gsum = nullptr;           // 12 regions (chunk x 6 passes) of group sums, zero between uses
+    uint32_t* gsum = nullptr;           // 12 regions (chunk x 6 radix passes) of group sums, zero
+                                        // between uses
     size_t gsum_region = 0;             // words per region
     uint2* ranges = nullptr;
     uint8_t* done = nullptr;
@@ -197,6 +198,8 @@ static constexpr int kDepthSortIpt = GS_DEPTH_IPT, kTileSortIpt = GS_TILE_IPT;
 #define GS_CHUNK_MARGIN 1.15f
 #endif
 static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
+// group-sum regions per chunk: 4 depth passes, 2 tile-id passes
+static constexpr size_t kGsumRegions = 6;
 static constexpr int kMinSortIpt = kDepthSortIpt < kTileSortIpt ? kDepthSortIpt : kTileSortIpt;
 static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 12 * kHistWords * 4;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
@@ -216,8 +219,8 @@ static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
     dev_free(s->gsum);
     const size_t parts = sort_parts(std::max<uint64_t>(cap, s->n), kMinSortIpt);
     s->gsum_region = 256 * ((parts + kGroupParts - 1) / kGroupParts + 1);
-    dev_alloc(s->gsum, 12 * s->gsum_region);
-    HIPCHK(hipMemset(s->gsum, 0, 12 * s->gsum_region * sizeof(uint32_t)));
+    dev_alloc(s->gsum, 2 * kGsumRegions * s->gsum_region);
+    HIPCHK(hipMemset(s->gsum, 0, 2 * kGsumRegions * s->gsum_region * sizeof(uint32_t)));
     s->kcap = cap;
 }
 
@@ -486,7 +489,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.tile_row_begin = tr_begin;
             sp.hist = s->hist + (6 * chunk + ps) * kHistWords;
             sp.offsets = s->radix_offsets;
-            sp.gsum = s->gsum + (size_t)(6 * chunk + ps) * s->gsum_region;
+            sp.gsum = s->gsum + (kGsumRegions * chunk + ps) * s->gsum_region;
             launch_sort_pass(sp, st);
         }
         mark(eb);
@@ -508,6 +511,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.n_max = std::max<uint32_t>(pp.n, 1);
         bp.capacity = (uint32_t)s->kcap;
         bp.part_tot = s->bin_part;
+        bp.ranges = s->ranges;
+        bp.n_tiles = (uint32_t)n_tiles;
         bp.rank_cnt = s->rank_cnt;
         bp.part_stride = bin_parts(s->n) + 1;
         bp.tkeys = s->tkA;
@@ -541,15 +546,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             sp.mask = 255;
             sp.hist = s->hist + (6 * chunk + 4 + ps) * kHistWords;
             sp.offsets = s->radix_offsets;
-            sp.gsum = s->gsum + (size_t)(6 * chunk + 4 + ps) * s->gsum_region;
+            sp.gsum = s->gsum + (kGsumRegions * chunk + 4 + ps) * s->gsum_region;
             launch_sort_pass(sp, st);
             std::swap(tk_in, tk_out);
             std::swap(tv_in, tv_out);
         }
         mark(eb + 2);
-        HIPCHK(hipMemsetAsync(s->ranges, 0, (size_t)std::max(n_tiles, 1) * sizeof(uint2), st));
         launch_ranges(tk_in, &s->ctl->k_chunk[chunk], (uint32_t)s->kcap, s->ranges,
-                      s->gsum + (size_t)(6 * chunk) * s->gsum_region, 6 * s->gsum_region, st);
+                      s->gsum + kGsumRegions * chunk * s->gsum_region, kGsumRegions * s->gsum_region, st);
         mark(eb + 3);
 
         CompositeParams cp{};

@@ -177,6 +177,8 @@ struct BinParams {
     uint32_t n_max;               // upper bound of n_vis (grid / scratch sizing)
     uint32_t capacity;            // entry capacity of out arrays
     uint32_t* part_tot;           // [part_stride] scratch: entries per binning partition
+    uint2* ranges;                // [n_tiles] tile ranges, emptied by k_bin_count
+    uint32_t n_tiles;
     uint32_t* rank_cnt;           // [n_max] scratch: entries of each depth rank of the chunk
     uint32_t part_stride;         // >= bin_parts(n_max)
     uint32_t* tkeys;              // out: strip-relative tile id
@@ -219,7 +221,7 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, flo
 void launch_project(const ProjParams& p, bool two_phase, hipStream_t s);
 void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 (or all) projected records
 void launch_sort_pass(const SortPass& p, hipStream_t s);
-void launch_bin(const BinParams& p, hipStream_t s);    // count, scan, emit, wide rows
+void launch_bin(const BinParams& p, hipStream_t s);    // count, emit, wide rows
 void launch_shade(const BinParams& p, hipStream_t s);  // composite records of the chunk's slots
 void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, Records rec, hipStream_t s);
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,

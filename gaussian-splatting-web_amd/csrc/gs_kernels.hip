@@ -943,6 +943,9 @@ __device__ __forceinline__ uint32_t slot_base(const BinParams& p) {
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     __shared__ uint32_t s_tmp[8];
     __shared__ unsigned long long s_mask[kMaskLdsWords];
+    // the chunk's tile ranges start empty (k_ranges writes the non-empty ones)
+    for (uint32_t q = blockIdx.x * kBinThreads + threadIdx.x; q < p.n_tiles; q += gridDim.x * kBinThreads)
+        p.ranges[q] = make_uint2(0u, 0u);
     uint32_t r0, r1;
     chunk_range(p, r0, r1);
     const uint32_t parts = bin_parts(r1 - r0);
@@ -971,53 +974,14 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     }
 }
 
-// Exclusive scan of `parts` 32-bit counts in place (one 1024-thread workgroup), clamped to
-// `clamp`; returns the 64-bit total to every thread.
-__device__ unsigned long long scan_parts(uint32_t* a, uint32_t parts, uint32_t clamp,
-                                         unsigned long long* s_wsum) {
-    const uint32_t tid = threadIdx.x, per = (parts + 1023) / 1024;
-    const uint32_t b0 = min(parts, tid * per), b1 = min(parts, b0 + per);
-    unsigned long long sum = 0;
-    for (uint32_t i = b0; i < b1; ++i) sum += a[i];
-    unsigned long long incl = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned long long t = __shfl_up(incl, d, 64);
-        if ((int)lane_id() >= d) incl += t;
-    }
-    if (lane_id() == 63) s_wsum[tid >> 6] = incl;
+// Sum of one 64-bit value per thread of a 256-thread workgroup (every thread gets it).
+__device__ __forceinline__ unsigned long long block_sum64(unsigned long long v, unsigned long long* s_red) {
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (lane_id() == 0) s_red[threadIdx.x >> 6] = v;
     __syncthreads();
-    unsigned long long base = 0, total = 0;
-    for (uint32_t i = 0; i < 16; ++i) {
-        if (i < (tid >> 6)) base += s_wsum[i];
-        total += s_wsum[i];
-    }
+    const unsigned long long t = s_red[0] + s_red[1] + s_red[2] + s_red[3];
     __syncthreads();
-    unsigned long long run = base + incl - sum;
-    for (uint32_t i = b0; i < b1; ++i) {
-        const uint32_t c = a[i];
-        a[i] = (uint32_t)min(run, (unsigned long long)clamp);
-        run += c;
-    }
-    return total;
-}
-
-// single workgroup: partition bases of the entries (capacity-clamped, overflow flagged)
-__global__ __launch_bounds__(1024) void k_bin_scan(BinParams p) {
-    __shared__ unsigned long long s_wsum[16];
-    uint32_t r0, r1;
-    chunk_range(p, r0, r1);
-    const uint32_t parts = bin_parts(r1 - r0);
-    const unsigned long long total = scan_parts(p.part_tot, parts, p.capacity, s_wsum);
-    if (threadIdx.x == 0) {
-        p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
-        p.ctl->shade_n[p.chunk] = r1 - r0;  // every depth rank has a composite slot
-    }
-    if (p.chunk == 0 && threadIdx.x < 8 && r1 > 0) {  // quantile keys (fixed-fraction chunking)
-        const uint32_t q = (r1 + (1u << threadIdx.x) - 1) >> threadIdx.x;
-        p.ctl->quant_key[threadIdx.x] = p.sorted_keys[q - 1];
-    }
-    if (threadIdx.x == 0 && total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
+    return t;
 }
 
 // Queue the tile rows of a wide splat (composite slot g, first output position out) for
@@ -1087,6 +1051,7 @@ constexpr uint32_t kEmitStage = 2048;  // entries staged in LDS per round
 // of wide splats are queued for k_bin_wide (written after this kernel).
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_tmp[8];
+    __shared__ unsigned long long s_red[4];
     __shared__ unsigned long long s_mask[kMaskLdsWords];
     __shared__ uint32_t s_key[kEmitStage];
     __shared__ uint32_t s_val[kEmitStage];
@@ -1097,6 +1062,20 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     if (blockIdx.x >= parts) return;
     const unsigned long long* m = stage_mask(p, s_mask);
     const uint32_t g0 = slot_base(p);
+    if (blockIdx.x == 0) {  // the chunk's totals (what a separate scan launch would write)
+        unsigned long long v = 0;
+        for (uint32_t k = tid; k < parts; k += kBinThreads) v += p.part_tot[k];
+        const unsigned long long total = block_sum64(v, s_red);
+        if (tid == 0) {
+            p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
+            p.ctl->shade_n[p.chunk] = r1 - r0;  // every depth rank has a composite slot
+            if (total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
+        }
+        if (p.chunk == 0 && tid < 8 && r1 > 0) {  // quantile keys (fixed-fraction chunking)
+            const uint32_t q = (r1 + (1u << tid) - 1) >> tid;
+            p.ctl->quant_key[tid] = p.sorted_keys[q - 1];
+        }
+    }
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         const uint32_t base_r = r0 + part * kBinTile;
         uint32_t cnt[kBinIPT], g[kBinIPT];
@@ -1123,7 +1102,13 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
             o[k] = block_excl_scan256(cnt[k], s_tmp, &total) + T;
             T += total;
         }
-        const uint32_t obase = p.part_tot[part];
+        // output base: the entries of all earlier partitions, summed by the whole workgroup
+        uint32_t obase;
+        {
+            unsigned long long v = 0;
+            for (uint32_t k = tid; k < part; k += kBinThreads) v += p.part_tot[k];
+            obase = (uint32_t)min(block_sum64(v, s_red), (unsigned long long)p.capacity);
+        }
 #pragma unroll
         for (int k = 0; k < kBinIPT; ++k) {
             narrow[k] = cnt[k] != 0;
@@ -1661,7 +1646,6 @@ void launch_sort_pass(const SortPass& p, hipStream_t s) {
 void launch_bin(const BinParams& p, hipStream_t s) {
     const unsigned grid = std::max<uint32_t>(1, std::min<uint32_t>(bin_parts(p.n_max), kMaxGrid));
     hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(kBinThreads), 0, s, p);
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, p);
     hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);
     hipLaunchKernelGGL(k_bin_wide, dim3(kMaxGrid), dim3(kBinThreads), 0, s, p);
 }
