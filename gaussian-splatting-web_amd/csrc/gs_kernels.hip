@@ -873,16 +873,17 @@ __device__ __forceinline__ Ellipse ellipse_of(const float4 q0, const float4 q1) 
     return e;
 }
 
-// Pixel columns [pl, ph] of tile row ty (pixel rows 16 ty .. 16 ty + 15) holding a pixel centre of
-// the ellipse, inside the box; false when there is none.
-__device__ __forceinline__ bool ellipse_cols(const Ellipse& e, uint32_t ty, uint32_t& pl_, uint32_t& ph_) {
+// Pixel columns [pl, ph] of a band of pixel rows (a tile row: 16 ty .. 16 ty + 15) holding a
+// pixel centre of the ellipse, inside the box; false when there is none.
+__device__ __forceinline__ bool ellipse_cols_band(const Ellipse& e, uint32_t y0, uint32_t y1, uint32_t& pl_,
+                                                  uint32_t& ph_) {  // pixel rows y0 .. y1
     if (!e.ok) {
         pl_ = e.px0;
         ph_ = e.px1;
         return true;
     }
-    const float lo = fmaxf((float)(ty * kTile) + 0.5f - e.cy, -e.hy);
-    const float hi = fminf((float)(ty * kTile) + 15.5f - e.cy, e.hy);
+    const float lo = fmaxf((float)y0 + 0.5f - e.cy, -e.hy);
+    const float hi = fminf((float)y1 + 0.5f - e.cy, e.hy);
     if (!(lo <= hi)) return false;
     const float d1 = fminf(fmaxf(e.dys, lo), hi), d0 = fminf(fmaxf(-e.dys, lo), hi);
     const float g1 = fsqrt(fmaxf(e.m00 * e.l - e.det * d1 * d1, 0.0f));
@@ -900,6 +901,10 @@ __device__ __forceinline__ bool ellipse_cols(const Ellipse& e, uint32_t ty, uint
     pl_ = (uint32_t)pl;
     ph_ = (uint32_t)ph;
     return true;
+}
+
+__device__ __forceinline__ bool ellipse_cols(const Ellipse& e, uint32_t ty, uint32_t& pl_, uint32_t& ph_) {
+    return ellipse_cols_band(e, ty * kTile, ty * kTile + kTile - 1, pl_, ph_);
 }
 
 // Tile columns [xa, xb] of tile row ty holding a pixel centre of the ellipse (inside the box).
@@ -1363,6 +1368,10 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tke
 // Chunked frames: mode kCompFirst marks saturated tiles done (and writes them out) and parks the
 // per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
 constexpr int kCompBatch = 128;
+#ifndef GS_QUARTER_TILES
+#define GS_QUARTER_TILES 1536
+#endif
+constexpr int kQuarterTiles = GS_QUARTER_TILES;  // at most this many tiles: k_composite_q
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <bool FP16_TARGET>
@@ -1559,6 +1568,179 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     }
 }
 
+
+// Quarter variant for frames with few tiles (row strips): 4 waves per tile, wave q owns the 8x8
+// quarter (q & 1, q >> 1) at one pixel per lane, and each splat is listed only for the quarters
+// its ellipse reaches (columns within the quarter's rows).  Per pixel it performs the same
+// operations in the same order as k_composite, so the image is bit-identical; it shortens the
+// slowest tile's chain when there are too few tiles to fill the chip.
+constexpr int kCompBatchQ = 256;
+
+template <bool FP16_TARGET>
+__global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
+    __shared__ float4 sR[2][kCompBatchQ][3];
+    __shared__ uint8_t sL[2][4][kCompBatchQ];  // per quarter: batch indices, segment = producing wave
+    __shared__ uint32_t sN[2][4][4];           // per quarter, per producing wave: list length
+    __shared__ uint32_t s_sat;
+    const int tid = threadIdx.x;
+    const int per = (p.n_tiles + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= p.n_tiles) return;
+    if (p.mode == kCompSecond && p.done[tile]) return;
+    const int qw = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
+    const int tx0 = tx * kTile, ty0 = ty * kTile;
+    const int px = tx0 + (qw & 1) * 8 + (lane & 7), py = ty0 + (qw >> 1) * 8 + (lane >> 3);
+    const bool in = px < p.W && py < p.H;
+    const float lx = (float)(px - tx0) + 0.5f, ly = (float)(py - ty0) + 0.5f;
+    const uint2 range = p.ranges[tile];
+    const float4* __restrict__ rec = p.rec;
+    const uint32_t* __restrict__ tvals = p.tvals;
+    const float L = 2.0f * kSqrtLog2e, amin = 1.0f / 255.0f, t_min = p.t_min;
+    const uint64_t pix = (uint64_t)py * p.W + px;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f, T = 1.0f, ca = 0.0f;
+    if (p.mode == kCompSecond && in) {
+        const float4 st = p.state[pix];
+        cr = st.x; cg = st.y; cb = st.z;
+        if (FP16_TARGET) ca = st.w; else T = st.w;
+    }
+    bool live = in && (FP16_TARGET ? ca < 1.0f : T >= t_min);
+    bool wave_live = __any(live);
+
+    const uint32_t n = range.y - range.x;
+    const uint32_t nb = (n + kCompBatchQ - 1) / kCompBatchQ;
+    float4 ga, gb, gc;
+    uint32_t gs_ = 0;
+    bool gv = false;
+    auto gather = [&](uint32_t batch) {
+        const uint32_t e = range.x + batch * kCompBatchQ + tid;
+        gv = e < range.y;
+        if (gv) {
+            gs_ = tvals[e];
+            const float4* r = rec + 3 * (uint64_t)gs_;
+            ga = r[0];
+            gb = r[1];
+            gc = r[2];
+        }
+    };
+    auto park = [&](int buf) {
+        const float cxr = ga.x - (float)tx0, cyr = ga.y - (float)ty0;
+        const float c0u = -__builtin_fmaf(cxr, ga.z, cyr * ga.w);
+        const float c0v = -__builtin_fmaf(cxr, gb.x, cyr * gb.y);
+        sR[buf][tid][0] = make_float4(c0u, c0v, ga.z, ga.w);
+        sR[buf][tid][1] = make_float4(gb.x, gb.y, gb.z, __uint_as_float(gs_));
+        sR[buf][tid][2] = gc;
+        const Ellipse el = ellipse_of(ga, gb);
+#pragma unroll
+        for (int hy = 0; hy < 2; ++hy) {  // the splat's columns within the quarter row band
+            uint32_t ul = 0u, uh = 0u;
+            const bool cols = gv && ellipse_cols_band(el, (uint32_t)(ty0 + 8 * hy), (uint32_t)(ty0 + 8 * hy + 7), ul, uh);
+#pragma unroll
+            for (int hx = 0; hx < 2; ++hx) {
+                const int q = hy * 2 + hx, qx = tx0 + hx * 8;
+                const bool hit = cols && (int)ul <= qx + 7 && (int)uh >= qx;
+                const uint64_t b = __ballot(hit);
+                if (hit) sL[buf][q][qw * 64 + __popcll(b & lanemask_lt())] = (uint8_t)tid;
+                if (lane == 0) sN[buf][q][qw] = (uint32_t)__popcll(b);
+            }
+        }
+    };
+    auto blend = [&](int k, int cur) {
+        const float4 A = sR[cur][k][0];
+        const float4 B = sR[cur][k][1];
+        const float4 C = sR[cur][k][2];
+        // the same roundings as k_composite's packed pair
+        const float u = __builtin_fmaf(ly, A.w, __builtin_fmaf(lx, A.z, A.x));
+        const float v = __builtin_fmaf(ly, B.y, __builtin_fmaf(lx, B.x, A.y));
+        const float qd = __builtin_fmaf(u, u, v * v);
+        const float e = B.z - qd;
+        const float a = __builtin_amdgcn_exp2f(e);
+        const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && a >= amin;
+        if (FP16_TARGET) {
+#pragma clang fp contract(off)
+            if (hit) {
+                const float om = 1.0f - ca;
+                cr = (float)(_Float16)((C.x * a) * om + cr);
+                cg = (float)(_Float16)((C.y * a) * om + cg);
+                cb = (float)(_Float16)((C.z * a) * om + cb);
+                ca = (float)(_Float16)(a * om + ca);
+                live = ca < 1.0f;
+            }
+        } else {
+            const float s = hit ? a * T : 0.0f;
+            cr = __builtin_fmaf(C.x, s, cr);
+            cg = __builtin_fmaf(C.y, s, cg);
+            cb = __builtin_fmaf(C.z, s, cb);
+            T = T - s;
+            live = live && T >= t_min;
+        }
+    };
+    if (tid == 0) s_sat = 0;
+    if (nb > 0) {
+        gather(0);
+        park(0);
+    }
+    __syncthreads();
+    for (uint32_t b = 0; b < nb; ++b) {
+        const int cur = b & 1;
+        if (b + 1 < nb) gather(b + 1);
+        if (wave_live) {
+            for (int seg = 0; seg < 4 && wave_live; ++seg) {
+                const int cnt = (int)sN[cur][qw][seg];
+                const uint8_t* list = &sL[cur][qw][seg * 64];
+                int k = 0;
+                for (; k + 3 < cnt; k += 4) {
+                    const int i3 = list[k + 3];
+                    blend(list[k], cur);
+                    blend(list[k + 1], cur);
+                    blend(list[k + 2], cur);
+                    blend(i3, cur);
+                    if (!__any(live)) {
+                        wave_live = false;
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][i3][1].w));
+                        break;
+                    }
+                }
+                for (; wave_live && k < cnt; ++k) {
+                    const int ik = list[k];
+                    blend(ik, cur);
+                    if (!__any(live)) {
+                        wave_live = false;
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][ik][1].w));
+                    }
+                }
+            }
+        }
+        if (b + 1 < nb) park(cur ^ 1);
+        if (__syncthreads_count(wave_live) == 0) break;
+    }
+    const bool tile_done = __syncthreads_count(live) == 0;
+    if (tile_done && tid == 0 && n > 0) {
+        atomicAdd(&p.ctl->sat_tiles[tile % kHistShards], 1u);
+        atomicMax(&p.ctl->sat_slot[tile % kHistShards], s_sat);
+    }
+    if (p.mode == kCompFirst) {
+        if (!tile_done) {
+            if (in) p.state[pix] = make_float4(cr, cg, cb, FP16_TARGET ? ca : T);
+            if (tid == 0) {
+                p.done[tile] = 0;
+                atomicAdd(&p.ctl->not_done, 1u);
+            }
+            return;
+        }
+        if (tid == 0) p.done[tile] = 1;
+    }
+    if (!FP16_TARGET) ca = 1.0f - T;
+    const uint64_t o = (uint64_t)(py - p.row0) * p.W + px;
+    if (!in) return;
+    if (p.out_f16) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        ((h4*)p.out)[o] = h4{(_Float16)cr, (_Float16)cg, (_Float16)cb, (_Float16)ca};
+    } else {
+        ((float4*)p.out)[o] = make_float4(cr, cg, cb, ca);
+    }
+}
+
 // ============================================================================ k_present
 // PostProcessRenderer.fragmentMain (src/post_process_render.ts:62-77) per pixel: the sampler
 // reads texel (x, H-1-y) at its centre (exact), a' = saturate(1.5 a), a' = a'^4 (as (a'^2)^2,
@@ -1668,10 +1850,16 @@ void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max,
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);  // see k_composite's tile order
-    if (accum_fp16)
+    if (p.n_tiles <= kQuarterTiles) {  // few tiles (row strips): 4 waves per tile
+        if (accum_fp16)
+            hipLaunchKernelGGL(k_composite_q<true>, dim3(grid), dim3(256), 0, s, p);
+        else
+            hipLaunchKernelGGL(k_composite_q<false>, dim3(grid), dim3(256), 0, s, p);
+    } else if (accum_fp16) {
         hipLaunchKernelGGL(k_composite<true>, dim3(grid), dim3(128), 0, s, p);
-    else
+    } else {
         hipLaunchKernelGGL(k_composite<false>, dim3(grid), dim3(128), 0, s, p);
+    }
 }
 
 }  // namespace gs
