@@ -384,6 +384,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     std::memcpy(pp.V, uni + 0, 64);
     mat4_mul_ref(uni + 16, uni + 0, pp.PV);
     pp.scale_mod = uni[39];
+    std::memcpy(pp.cam, uni + 32, 12);
     pp.P00 = uni[16];
     pp.P11 = uni[21];
     pp.focal = (float)W * pp.P00 / 2.0f;
@@ -527,7 +528,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.wide_unit_cap = s->wide_unit_cap;
         // composite records of the chunk's depth ranks first: the binning reads them to bin each
         // splat's ellipse, not its bounding box
-        launch_shade(bp, st);
+        launch_shade(bp, !two_phase, st);  // two-phase frames: k_colour stored the colours
         launch_bin(bp, st);
         mark(eb + 1);
 

@@ -63,16 +63,18 @@ struct FrameCtl {                 // zeroed at the start of every frame
 // of two, so a block never straddles more 128-B lines than it must; 256 B at SH degree 3).
 // The frame's projected record of Gaussian j (k_project stores it for the chunk-0 splats,
 // k_records for the chunk-1 splats it needs):
-//   r01 = quads shade_quads(n_sh), +1 of j's shading block (its padding), so k_shade reads the
-//         record with the block: cx, cy, e1x', e1y' | e2x', e2y', log2(op), pixel box x
-//         (centre in pixels; quad axes e/|e|^2 * sqrt(log2 e); box x0 | x1 << 16, u32 bits)
+//   r01 = quads shade_quads(n_sh), +1 of j's shading block (its padding): cx, cy, e1x', e1y' |
+//         e2x', e2y', log2(op), pixel box x (centre in pixels; quad axes e/|e|^2 * sqrt(log2 e);
+//         box x0 | x1 << 16, u32 bits)
+//   colour = quad shade_quads(n_sh) + 2: r, g, b, 0 (SH at the frame's view direction), stored
+//         with r01, so k_shade gathers one 48-B record per splat
 //   r2[j] = depth key, tile count, pixel box x, pixel box y (u32 bits), dense
 // Composite record, 3 float4 per depth rank of the chunk at slot g = chunk base + rank (written
 // by k_shade before the binning, which reads it; the tile lists hold g):
-//   [0], [1] = the r01 quads, [2] r, g, b, 0
+//   [0], [1], [2] = the r01 quads and the colour
 __host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
-__host__ __device__ inline uint32_t shade_stride(int n_sh) {  // block + 2 record quads, power of 2
-    const uint32_t q = shade_quads(n_sh) + 2;
+__host__ __device__ inline uint32_t shade_stride(int n_sh) {  // block + 3 record quads, power of 2
+    const uint32_t q = shade_quads(n_sh) + 3;
     return q <= 4 ? 4 : q <= 8 ? 8 : 16;
 }
 
@@ -118,6 +120,7 @@ struct ProjParams {
     // k_records: unsaturated-tile SAT of chunk 0 (see BinParams::sat); rec_all = every visible
     const uint32_t* sat;
     int rec_all;
+    float cam[3];             // camera position (SH view direction)
 };
 
 // Element filter of a radix pass (the first pass of a depth chunk decides chunk membership).
@@ -222,7 +225,7 @@ void launch_project(const ProjParams& p, bool two_phase, hipStream_t s);
 void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 (or all) projected records
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, emit, wide rows
-void launch_shade(const BinParams& p, hipStream_t s);  // composite records of the chunk's slots
+void launch_shade(const BinParams& p, bool colour, hipStream_t s);  // composite records of the chunk's slots
 void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, Records rec, hipStream_t s);
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s);

@@ -331,7 +331,7 @@ __device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, in
                             ? (tx0 | (ty0 << 12) | ((tx1 - tx0) << 24) | ((ty1 - ty0) << 28))
                             : kRectLarge;
             }
-            // projected record (colour: k_shade, only for splats that receive tile entries):
+            // projected record (colour: store_colour, for the splats whose records are stored):
             // u' = d.(e1/|e1|^2)*sqrt(log2 e), so u'^2+v'^2 = (u^2+v^2) log2 e and
             // alpha = op * exp(-(u^2+v^2)) = exp2(log2(op) - (u'^2+v'^2))
             const float k1 = kSqrtLog2e / (f.e1x * f.e1x + f.e1y * f.e1y);
@@ -344,6 +344,53 @@ __device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, in
             o.bby = bby;
         }
         return true;
+}
+
+// SH colour of a Gaussian from its shading block blk (nq quads: position, coefficients),
+// src/simple_render.ts:5-67, :321: one thread, the reference's expression order with contraction
+// off (bit-identical to the oracle).
+__device__ __forceinline__ float4 sh_colour(const float4* __restrict__ blk, uint32_t nq, const float* cam) {
+#pragma clang fp contract(off)
+    float f[52];
+#pragma unroll
+    for (uint32_t t = 0; t < 13; ++t) {
+        const float4 q = t < nq ? blk[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+        f[4 * t] = q.x;
+        f[4 * t + 1] = q.y;
+        f[4 * t + 2] = q.z;
+        f[4 * t + 3] = q.w;
+    }
+    const float dx = f[0] - cam[0], dy = f[1] - cam[1], dz = f[2] - cam[2];
+    const float l = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float X = dx / l, Y = dy / l, Z = dz / l;
+    const float xx = X * X, yy = Y * Y, zz = Z * Z, xy = X * Y, xz = X * Z, yz = Y * Z;
+    const float C0 = 0.28209479177387814f, C1 = 0.4886025119029199f;
+    const float C20 = 1.0925484305920792f, C21 = -1.0925484305920792f, C22 = 0.31539156525252005f,
+                C23 = -1.0925484305920792f, C24 = 0.5462742152960396f;
+    const float C30 = -0.5900435899266435f, C31 = 2.890611442640554f, C32 = -0.4570457994644658f,
+                C33 = 0.3731763325901154f, C34 = -0.4570457994644658f, C35 = 1.445305721320277f,
+                C36 = -0.5900435899266435f;
+    float col[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float* sh = f + 3 + c;  // sh[3 k] = coefficient k, channel c
+        float r = C0 * sh[0];
+        r = r + C1 * (-Y * sh[3] + Z * sh[6] - X * sh[9]);
+        r = r + C20 * xy * sh[12] + C21 * yz * sh[15] + C22 * (2.0f * zz - xx - yy) * sh[18] +
+            C23 * xz * sh[21] + C24 * (xx - yy) * sh[24];
+        r = r + C30 * Y * (3.0f * xx - yy) * sh[27] + C31 * xy * Z * sh[30] +
+            C32 * Y * (4.0f * zz - xx - yy) * sh[33] + C33 * Z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * sh[36] +
+            C34 * X * (4.0f * zz - xx - yy) * sh[39] + C35 * Z * (xx - yy) * sh[42] +
+            C36 * X * (xx - 3.0f * yy) * sh[45];
+        r = r + 0.5f;
+        col[c] = fmaxf(r, 0.0f);
+    }
+    return make_float4(col[0], col[1], col[2], 0.0f);
+}
+
+// Gaussian j's colour, stored after its record quads (k_colour, k_records).
+__device__ __forceinline__ void store_colour(const ProjParams& p, uint32_t j) {
+    rec_r01(p.rec, j)[2] = sh_colour(p.rec.r01 + (uint64_t)j * p.rec.stride, p.rec.off, p.cam);
 }
 
 __device__ __forceinline__ void store_records(const ProjParams& p, uint32_t i, const Proj& o) {
@@ -392,7 +439,10 @@ __global__ __launch_bounds__(256) void k_records(ProjParams p) {
             }
         }
         Proj o;
-        if (project_core(p, i, row_lo, row_hi, false, o)) store_records(p, i, o);
+        if (project_core(p, i, row_lo, row_hi, false, o)) {
+            store_records(p, i, o);
+            store_colour(p, i);
+        }
     }
 }
 
@@ -508,6 +558,16 @@ __global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
     if (tid == 0 && s_vis) {
         atomicAdd(&p.ctl->n_vis, s_vis);
         atomicAdd(&p.ctl->k_total, s_k);
+    }
+}
+
+// Colours of the chunk-0 splats (k_project's compacted list per partition, in index order), one
+// thread per splat: their shading blocks are read in index order, not in depth order.
+__global__ __launch_bounds__(256) void k_colour(ProjParams p) {
+    const uint32_t parts = sort_parts(p.n);
+    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+        const uint32_t cnt = p.c_count[part], p0 = part * kSortTile;
+        for (uint32_t q = threadIdx.x; q < cnt; q += 256) store_colour(p, p.c_vals[p0 + q]);
     }
 }
 
@@ -1143,95 +1203,52 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     }
 }
 
-// Composite records of this chunk's depth ranks (slot g = base + rank): colour
-// (src/simple_render.ts:26-66, :321-322: dir = normalize(p - camPos), SH to degree 3, + 0.5,
-// max(., 0)) plus the footprint words of the projected record, written densely.  16 lanes per
-// splat read the line-aligned shading block with the 32-B record in its padding (one coalesced
-// load); each lane evaluates its own coefficients' terms and the group sums them with xor
-// shuffles.  Latency: a wave takes 64 ranks at once (one coalesced load of their Gaussian
-// indices) and keeps kShadeU groups of 4 splats' block loads in flight before evaluating any.
+// Composite records of this chunk's depth ranks (slot g = base + rank): the projected record
+// quads r01 and the colour of each rank's Gaussian, written densely in rank order.  A wave takes
+// 64 ranks at once (one coalesced load of their Gaussian indices).
+//   COLOUR (one-phase frames): one thread per rank gathers the Gaussian's shading block with the
+//     record in its padding and evaluates the colour (sh_colour): one 240-B gather per splat.
+//   else (row strips): k_colour stored the colour after the record quads in index order; 4 lanes
+//     per rank copy the 48 B, 4 groups of 16 ranks' gathers in flight.
 // Runs before the binning, which reads the records to bin each splat's ellipse exactly.
-constexpr int kShadeU = 4;
-
-__device__ __forceinline__ void shade_eval(const BinParams& p, float4 q, uint32_t l, uint32_t nq,
-                                           uint32_t ncoef, bool active, uint32_t slot) {
-    const uint32_t gl = lane_id() & ~15u;
-    const float px = __shfl(q.x, gl, 64), py = __shfl(q.y, gl, 64), pz = __shfl(q.z, gl, 64);
-    const float dx = px - p.cam[0], dy = py - p.cam[1], dz = pz - p.cam[2];
-    const float dl = sqrtf(dx * dx + dy * dy + dz * dz);
-    const float x = dx / dl, y = dy / dl, z = dz / dl;
-    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
-    float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;
-    const float v[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const uint32_t i = 4 * l + t;  // float index in the block: 3 + 3k + c
-        if (l >= nq || i < 3 || i >= 3 + ncoef) continue;
-        const uint32_t k = (i - 3) / 3, c = (i - 3) % 3;
-        float b;
-        switch (k) {
-            case 0: b = 0.28209479177387814f; break;
-            case 1: b = 0.4886025119029199f * -y; break;
-            case 2: b = 0.4886025119029199f * z; break;
-            case 3: b = 0.4886025119029199f * -x; break;
-            case 4: b = 1.0925484305920792f * xy; break;
-            case 5: b = -1.0925484305920792f * yz; break;
-            case 6: b = 0.31539156525252005f * (2.0f * zz - xx - yy); break;
-            case 7: b = -1.0925484305920792f * xz; break;
-            case 8: b = 0.5462742152960396f * (xx - yy); break;
-            case 9: b = -0.5900435899266435f * y * (3.0f * xx - yy); break;
-            case 10: b = 2.890611442640554f * xy * z; break;
-            case 11: b = -0.4570457994644658f * y * (4.0f * zz - xx - yy); break;
-            case 12: b = 0.3731763325901154f * z * (2.0f * zz - 3.0f * xx - 3.0f * yy); break;
-            case 13: b = -0.4570457994644658f * x * (4.0f * zz - xx - yy); break;
-            case 14: b = 1.445305721320277f * z * (xx - yy); break;
-            default: b = -0.5900435899266435f * x * (xx - 3.0f * yy); break;
-        }
-        const float bv = b * v[t];
-        acc0 += c == 0 ? bv : 0.0f;
-        acc1 += c == 1 ? bv : 0.0f;
-        acc2 += c == 2 ? bv : 0.0f;
-    }
-#pragma unroll
-    for (int d = 8; d >= 1; d >>= 1) {
-        acc0 += __shfl_xor(acc0, d, 64);
-        acc1 += __shfl_xor(acc1, d, 64);
-        acc2 += __shfl_xor(acc2, d, 64);
-    }
-    if (active) {
-        float4* o = p.crec + 3 * (uint64_t)slot;
-        if (l >= nq && l < nq + 2) o[l - nq] = q;
-        if (l == 0)
-            o[2] = make_float4(fmaxf(acc0 + 0.5f, 0.0f), fmaxf(acc1 + 0.5f, 0.0f), fmaxf(acc2 + 0.5f, 0.0f), 0.0f);
-    }
-}
-
+template <bool COLOUR>
 __global__ __launch_bounds__(256) void k_shade(BinParams p) {
     uint32_t r0, r1;
     chunk_range(p, r0, r1);
     const uint32_t g0 = slot_base(p);
     const uint32_t n = r1 - r0;
-    const uint32_t lane = lane_id(), l = lane & 15;
-    const uint32_t nq = shade_quads(p.n_sh), ncoef = 3 * (uint32_t)p.n_sh;
+    const uint32_t lane = lane_id(), qd = lane & 3;
     const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+    const uint32_t nq = p.rec.off;
     for (uint32_t base = wave * 64; base < n; base += nwaves * 64) {  // wave-uniform: shuffles below
-        const uint32_t jl = base + lane < n ? p.sorted_vals[r0 + base + lane] : 0u;
-        if (base + lane < n) p.shade_list[g0 + base + lane] = jl;
-        const uint32_t cnt = min(64u, n - base);
-        for (uint32_t sub = 0; sub < cnt; sub += 4 * kShadeU) {
-            float4 q[kShadeU];
+        const bool mine = base + lane < n;
+        const uint32_t jl = mine ? p.sorted_vals[r0 + base + lane] : 0u;
+        if (mine) p.shade_list[g0 + base + lane] = jl;
+        float4* o = p.crec + 3 * (uint64_t)(g0 + base);
+        if (COLOUR) {
+            if (mine) {
+                const float4* blk = p.rec.r01 + (uint64_t)jl * p.rec.stride;
+                const float4 a = blk[nq], b = blk[nq + 1];
+                const float4 c = sh_colour(blk, nq, p.cam);
+                o[3 * lane] = a;
+                o[3 * lane + 1] = b;
+                o[3 * lane + 2] = c;
+            }
+        } else {
+            const uint32_t cnt = min(64u, n - base);
+            const float4* __restrict__ rec = p.rec.r01 + nq;
+            float4 q[4];
 #pragma unroll
-            for (int u = 0; u < kShadeU; ++u) {
-                const uint32_t k = sub + 4 * u + (lane >> 4);  // splat within the 64
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = 16 * u + (lane >> 2);  // rank within the 64
                 const uint32_t j = __shfl(jl, k & 63, 64);
                 q[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                // lanes 0..nq-1: the shading block; lanes nq, nq+1: the record quads r01 in its padding
-                if (k < cnt && l < nq + 2) q[u] = p.shade[(uint64_t)j * p.shade_stride + l];
+                if (k < cnt && qd < 3) q[u] = rec[(uint64_t)j * p.rec.stride + qd];
             }
 #pragma unroll
-            for (int u = 0; u < kShadeU; ++u) {
-                const uint32_t k = sub + 4 * u + (lane >> 4);
-                shade_eval(p, q[u], l, nq, ncoef, k < cnt, g0 + base + k);
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = 16 * u + (lane >> 2);
+                if (k < cnt && qd < 3) o[3 * k + qd] = q[u];
             }
         }
     }
@@ -1800,6 +1817,8 @@ void launch_project(const ProjParams& p, bool two_phase, hipStream_t s) {
     }
     else
         hipLaunchKernelGGL(k_project<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
+    if (two_phase)  // else k_shade<true> evaluates the colours
+        hipLaunchKernelGGL(k_colour, dim3(grid), dim3(256), 0, s, p);
 }
 void launch_records(const ProjParams& p, hipStream_t s) {
     if (!p.n) return;
@@ -1831,8 +1850,11 @@ void launch_bin(const BinParams& p, hipStream_t s) {
     hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);
     hipLaunchKernelGGL(k_bin_wide, dim3(kMaxGrid), dim3(kBinThreads), 0, s, p);
 }
-void launch_shade(const BinParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_shade, dim3(kMaxGrid), dim3(256), 0, s, p);
+void launch_shade(const BinParams& p, bool colour, hipStream_t s) {
+    if (colour)
+        hipLaunchKernelGGL(k_shade<true>, dim3(kMaxGrid), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_shade<false>, dim3(kMaxGrid), dim3(256), 0, s, p);
 }
 void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, Records rec, hipStream_t s) {
     hipLaunchKernelGGL(k_frame_stats, dim3(1), dim3(64), 0, s, ctl, shade_list, rec);
