@@ -86,6 +86,8 @@ enum { ST_TOTAL, ST_PROJECT, ST_SORT, ST_BIN, ST_TSORT, ST_RANGES, ST_COMPOSITE,
 struct FrameEvents {
     hipEvent_t ev[EV_COUNT] = {};
     bool pending = false;
+    int level = 0;        // opts.timing of the frame: 1 every stage, 2 the composite only
+    bool chunk1 = false;  // chunk 1 ran (its composite events were recorded)
 };
 
 constexpr uint32_t kNoSplit = 0xFFFFFFFFu;  // chunk threshold: every visible splat in chunk 0
@@ -121,7 +123,9 @@ struct gs_ctx {
     FrameEvents fe[2];  // ping-pong: frame t's events are read once frame t+1 needs the slot
     int fe_cur = 0;
     double acc_ms[ST_COUNT] = {};
-    uint32_t acc_frames = 0;
+    uint32_t acc_frames = 0;    // frames timed at level 1 (every stage)
+    double acc_comp_ms = 0.0;   // composite time of every timed frame (levels 1 and 2)
+    uint32_t comp_frames = 0;
     gs_stats stats{};
     gs_scene* last_scene = nullptr;
     std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
@@ -167,11 +171,15 @@ struct gs_scene {
     int tiles_cap = 0;
     float4* state = nullptr;
     uint64_t state_cap = 0;
-    // asynchronous frame statistics (chunk controller, capacity)
-    FrameCtl* h_ctl = nullptr;  // pinned, 2 slots
-    hipEvent_t stat_ev[2] = {};
-    uint32_t* h_not_done = nullptr;  // pinned: chunk 0's unsaturated-tile count, read mid-frame
-    hipEvent_t mid_ev = nullptr;
+    // asynchronous frame statistics (chunk controller, capacity): k_frame_end stores FrameCtl into
+    // a pinned slot and then publishes a sequence number there; two slots (two frames in flight)
+    FrameCtl* h_ctl = nullptr;    // pinned, coherent, device-mapped (d_ctl_slot): 2 slots
+    uint32_t* h_seq = nullptr;    // pinned, coherent, device-mapped (d_seq): per slot
+    FrameCtl* d_ctl_slot = nullptr;
+    uint32_t* d_seq = nullptr;
+    uint32_t seq_next = 1;
+    bool meta_clean = false;      // the last frame's k_frame_end zeroed meta (see render_frame)
+    uint32_t stat_want[2] = {};   // sequence number that completes the slot's frame
     bool stat_pending[2] = {};
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
@@ -287,21 +295,50 @@ static void strip_geometry(int H, int si, int sc, int& tr_begin, int& tr_end, in
 
 static void harvest(gs_ctx* c, FrameEvents& f) {
     if (!f.pending) return;
-    HIPCHK(hipEventSynchronize(f.ev[EV_END]));
     auto el = [&](int a, int b) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, f.ev[a], f.ev[b]));
         return (double)ms;
     };
+    HIPCHK(hipEventSynchronize(f.ev[f.level == 1 ? EV_END : f.chunk1 ? EV_COMP_1 : EV_COMP_0]));
+    c->acc_comp_ms += el(EV_RANGES_0, EV_COMP_0) + (f.chunk1 ? el(EV_RANGES_1, EV_COMP_1) : 0.0);
+    c->comp_frames++;
+    if (f.level != 1) {
+        f.pending = false;
+        return;
+    }
     c->acc_ms[ST_TOTAL] += el(EV_BEGIN, EV_END);
     c->acc_ms[ST_PROJECT] += el(EV_PROJ0, EV_PROJ1);
     c->acc_ms[ST_SORT] += el(EV_PROJ1, EV_DSORT_0) + el(EV_COMP_0, EV_DSORT_1);
     c->acc_ms[ST_BIN] += el(EV_DSORT_0, EV_BIN_0) + el(EV_DSORT_1, EV_BIN_1);
     c->acc_ms[ST_TSORT] += el(EV_BIN_0, EV_TSORT_0) + el(EV_BIN_1, EV_TSORT_1);
     c->acc_ms[ST_RANGES] += el(EV_TSORT_0, EV_RANGES_0) + el(EV_TSORT_1, EV_RANGES_1);
-    c->acc_ms[ST_COMPOSITE] += el(EV_RANGES_0, EV_COMP_0) + el(EV_RANGES_1, EV_COMP_1);
     c->acc_frames++;
     f.pending = false;
+}
+
+static bool seq_arrived(const gs_scene* s, int slot) {
+    return __atomic_load_n(&s->h_seq[slot], __ATOMIC_ACQUIRE) == s->stat_want[slot];
+}
+
+// Spin until k_frame_end published `slot`'s sequence number.  `st` (nullable) is a stream the
+// signal is queued on: polled now and then, so a fault surfaces as an error, not a hang.
+// Without a stream: a device synchronize if the signal is late.  False: it never came.
+static bool wait_slot(gs_scene* s, int slot, hipStream_t st) {
+    for (uint32_t it = 1;; ++it) {
+        if (seq_arrived(s, slot)) return true;
+        if ((it & 255u) == 0) {
+            if (st) {
+                const hipError_t e = hipStreamQuery(st);
+                if (e == hipSuccess) return seq_arrived(s, slot);
+                if (e != hipErrorNotReady) HIPCHK(e);
+            } else {
+                HIPCHK(hipDeviceSynchronize());
+                return seq_arrived(s, slot);
+            }
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 // Latest frame statistics that have arrived on the host; `wait` blocks for the newest frame.
@@ -309,10 +346,12 @@ static void collect_stats(gs_scene* s, bool wait) {
     for (int k = 0; k < 2; ++k) {
         const int slot = (s->stat_cur + k) & 1;  // older slot first
         if (!s->stat_pending[slot]) continue;
-        if (wait) {
-            HIPCHK(hipEventSynchronize(s->stat_ev[slot]));
-        } else if (hipEventQuery(s->stat_ev[slot]) != hipSuccess) {
-            continue;
+        if (!seq_arrived(s, slot)) {
+            if (!wait) continue;
+            if (!wait_slot(s, slot, nullptr)) {  // the frame never completed (an error mid-frame)
+                s->stat_pending[slot] = false;
+                continue;
+            }
         }
         s->last = s->h_ctl[slot];
         s->have_last = true;
@@ -346,6 +385,20 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     const int TX = (W + kTile - 1) / kTile;
     const int n_tiles = TX * (tr_end - tr_begin);
     collect_stats(s, false);
+    const int slot = s->stat_cur;  // this frame's statistics slot
+    if (s->stat_pending[slot]) {  // two frames in flight: the older one's statistics first
+        wait_slot(s, slot, nullptr);
+        collect_stats(s, false);
+        s->stat_pending[slot] = false;
+    }
+    auto frame_end = [&](int zero_mode) {  // statistics into the slot (then meta zeroed, see k_frame_end)
+        const uint32_t q = s->seq_next++;
+        s->stat_want[slot] = q;
+        launch_frame_end(s->ctl, s->shade_list, records(s), s->d_ctl_slot + slot, s->d_seq + slot, q,
+                         (uint4*)s->meta, (uint32_t)(kMetaBytes / 16), zero_mode, st);
+        return q;
+    };
+    bool ended = false;
     if (s->have_last && s->last.k_total > s->kcap) ensure_tile_capacity(s, s->last.k_total);
     ensure_tiles(s, std::max(n_tiles, 1));
     s->last_tiles = n_tiles;
@@ -367,15 +420,26 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     }
     ensure_wide(s, tr_end - tr_begin);
 
+    // timing 1: events between every stage; 2: around the composite only (each event record costs
+    // the stream a few microseconds, so a frame timed at level 1 runs ~35 us slower)
     const bool timed = o.timing != 0;
     FrameEvents& fe = c->fe[c->fe_cur];
     auto mark = [&](int e) {
-        if (timed) HIPCHK(hipEventRecord(fe.ev[e], st));
+        if (!timed) return;
+        if (o.timing != 1 && e != EV_RANGES_0 && e != EV_COMP_0 && e != EV_RANGES_1 && e != EV_COMP_1) return;
+        HIPCHK(hipEventRecord(fe.ev[e], st));
     };
-    if (timed) harvest(c, fe);  // slot reuse: its frame completed long ago (or wait for it)
+    if (timed) {
+        harvest(c, fe);  // slot reuse: its frame completed long ago (or wait for it)
+        fe.level = o.timing;
+        fe.chunk1 = false;
+    }
     mark(EV_BEGIN);
 
-    HIPCHK(hipMemsetAsync(s->meta, 0, kMetaBytes, st));
+    // meta (FrameCtl, histograms) is zero at a frame's start: k_frame_end of the last frame cleared
+    // it, unless that frame never ended (first frame, an error mid-frame)
+    if (!s->meta_clean) HIPCHK(hipMemsetAsync(s->meta, 0, kMetaBytes, st));
+    s->meta_clean = false;
     ProjParams pp{};
     pp.geo = s->geo;
     pp.cull = s->cull;
@@ -436,18 +500,23 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     unsigned long long* unsat_mask = (unsigned long long*)(s->sat + ((sat_words + 1) & ~(size_t)1));
     for (int chunk = 0; chunk < 2; ++chunk) {
         const int eb = chunk == 0 ? EV_DSORT_0 : EV_DSORT_1;
+        uint32_t not_done = 0;
         if (chunk == 1 && two_chunks) {
-            // chunk 1 only when chunk 0 left a tile unsaturated: read that count back (4 B, pinned)
-            // and decide here.  Enqueued but empty, chunk 1's ~26 launches cost ~0.13 ms of GPU
-            // time; this costs one short wait for chunk 0 (host run-ahead is lost for it).
-            HIPCHK(hipMemcpyAsync(s->h_not_done, &s->ctl->not_done, 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipEventRecord(s->mid_ev, st));
-            HIPCHK(hipEventSynchronize(s->mid_ev));
+            // chunk 1 only when chunk 0 left a tile unsaturated: k_frame_end publishes chunk 0's
+            // statistics to the host, which spins on them and decides here.  Enqueued but empty,
+            // chunk 1's ~26 launches cost ~0.13 ms of GPU time; this costs one short wait for
+            // chunk 0 (host run-ahead is lost for it).  Without chunk 1 the frame ends here.
+            frame_end(1);  // zeroes meta on the device iff not_done == 0 (the host's test below)
+            if (!wait_slot(s, slot, st)) throw GsError(GS_ERR_HIP, "chunk-0 statistics never arrived");
+            not_done = s->h_ctl[slot].not_done;
+            ended = not_done == 0;
         }
-        if (chunk == 1 && (!two_chunks || *s->h_not_done == 0)) {
-            for (int e = 0; e < 5; ++e) mark(eb + e);
+        if (chunk == 1 && (!two_chunks || not_done == 0)) {
+            if (o.timing == 1)
+                for (int e = 0; e < 5; ++e) mark(eb + e);
             break;
         }
+        if (chunk == 1) fe.chunk1 = true;
         if (chunk == 1) {
             launch_sat(s->done, TX, tr_end - tr_begin, s->sat, unsat_mask, s->ctl, st);
             // k_project stored records only for chunk 0: add those chunk 1's filter and bins read
@@ -577,7 +646,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
         mark(eb + 4);
     }
-    launch_frame_stats(s->ctl, s->shade_list, records(s), st);
+    if (!ended) frame_end(2);
+    s->meta_clean = true;  // k_frame_end zeroes it for the next frame
     mark(EV_END);
     s->last_pp = pp;
     HIPCHK(hipGetLastError());
@@ -585,15 +655,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         fe.pending = true;
         c->fe_cur ^= 1;
     }
-    // frame statistics back to the host, asynchronously
-    const int slot = s->stat_cur;
-    if (s->stat_pending[slot]) {  // two frames in flight: wait for the older one
-        HIPCHK(hipEventSynchronize(s->stat_ev[slot]));
-        collect_stats(s, false);
-    }
-    HIPCHK(hipMemcpyAsync(&s->h_ctl[slot], s->ctl, sizeof(FrameCtl), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipEventRecord(s->stat_ev[slot], st));
-    s->stat_pending[slot] = true;
+    s->stat_pending[slot] = true;  // frame statistics arrive asynchronously (k_frame_end)
     s->stat_cur ^= 1;
     s->have_frame = true;
     c->last_scene = s;
@@ -616,6 +678,7 @@ static void validate_render_args(gs_ctx* c, gs_scene* s, const void* uni, int W,
         if (o->out_format != GS_OUT_RGBA_F32 && o->out_format != GS_OUT_RGBA_F16)
             throw GsError(GS_ERR_INVALID, "bad out_format");
         if (!(o->t_min >= 0.0f && o->t_min < 1.0f)) throw GsError(GS_ERR_INVALID, "t_min must be in [0,1)");
+        if (o->timing < 0 || o->timing > 2) throw GsError(GS_ERR_INVALID, "timing must be 0, 1 or 2");
         if (!(o->chunk_fraction >= 0.0f)) throw GsError(GS_ERR_INVALID, "chunk_fraction must be >= 0");
         if (o->ref_quirks) throw GsError(GS_ERR_UNSUPPORTED, "ref_quirks not built in this version");
     }
@@ -734,10 +797,12 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->shade_list, (size_t)n);
             dev_alloc(s->rank_cnt, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->part_count, (size_t)sort_parts(n) + 1);
-            HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hipHostMallocDefault));
-            HIPCHK(hipHostMalloc((void**)&s->h_not_done, 64, hipHostMallocDefault));
-            HIPCHK(hipEventCreateWithFlags(&s->mid_ev, hipEventDisableTiming));
-            for (auto& e : s->stat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
+            HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hf));
+            HIPCHK(hipHostMalloc((void**)&s->h_seq, 64, hf));
+            std::memset(s->h_seq, 0, 64);
+            HIPCHK(hipHostGetDevicePointer((void**)&s->d_ctl_slot, s->h_ctl, 0));
+            HIPCHK(hipHostGetDevicePointer((void**)&s->d_seq, s->h_seq, 0));
             ensure_tile_capacity(s, 4 * n + (1u << 20));
             // AoS -> SoA on device, in chunks of 4M records
             const uint64_t rb = 64 + 16 * (uint64_t)n_sh;
@@ -795,11 +860,8 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->sat);
     dev_free(s->wide_unit);
     dev_free(s->state);
-    for (auto& e : s->stat_ev)
-        if (e) (void)hipEventDestroy(e);
     if (s->h_ctl) (void)hipHostFree(s->h_ctl);
-    if (s->h_not_done) (void)hipHostFree(s->h_not_done);
-    if (s->mid_ev) (void)hipEventDestroy(s->mid_ev);
+    if (s->h_seq) (void)hipHostFree(s->h_seq);
     delete s;
 }
 
@@ -912,7 +974,7 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
             st.wide_chunk1 = l.wide_n[1];
             st.chunk_fraction = l.n_vis ? (float)l.n_chunk[0] / (float)l.n_vis : 0.0f;
         }
-        st.frames = (int32_t)c->acc_frames;
+        st.frames = (int32_t)c->comp_frames;
         const double k = c->acc_frames ? 1.0 / c->acc_frames : 0.0;
         st.ms_total = (float)(c->acc_ms[ST_TOTAL] * k);
         st.ms_project = (float)(c->acc_ms[ST_PROJECT] * k);
@@ -920,9 +982,10 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
         st.ms_bin = (float)(c->acc_ms[ST_BIN] * k);
         st.ms_tile_sort = (float)(c->acc_ms[ST_TSORT] * k);
         st.ms_ranges = (float)(c->acc_ms[ST_RANGES] * k);
-        st.ms_composite = (float)(c->acc_ms[ST_COMPOSITE] * k);
-        st.ms_other = st.ms_total - (st.ms_project + st.ms_sort + st.ms_bin + st.ms_tile_sort +
-                                     st.ms_ranges + st.ms_composite);
+        st.ms_composite = (float)(c->comp_frames ? c->acc_comp_ms / c->comp_frames : 0.0);
+        st.ms_other = c->acc_frames ? st.ms_total - (st.ms_project + st.ms_sort + st.ms_bin + st.ms_tile_sort +
+                                                     st.ms_ranges + st.ms_composite)
+                                    : 0.0f;
         *out = st;
         return GS_OK;
     });
@@ -936,6 +999,8 @@ int gs_timings_reset(gs_ctx* c) {
         harvest(c, c->fe[1]);
         for (auto& v : c->acc_ms) v = 0.0;
         c->acc_frames = 0;
+        c->acc_comp_ms = 0.0;
+        c->comp_frames = 0;
         return GS_OK;
     });
 }

@@ -50,7 +50,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t shade_n[2];          // composite slots per chunk (= its depth-sorted splats)
     uint32_t n_chunk[2];          // depth-sorted splats per chunk (count of radix pass 0)
     uint32_t sat_key;             // depth key of the farthest splat a tile saturated at
-    uint32_t sat_slot_max;        // (k_frame_stats)
+    uint32_t sat_slot_max;        // (k_frame_end)
     uint32_t quant_key[8];        // key at rank ceil(n_chunk[0] / 2^t) - 1 of chunk 0, t = 0..7
     uint32_t sat_slot[kHistShards];   // per shard: max composite slot at which a tile saturated
     uint32_t sat_tiles[kHistShards];  // per shard: tiles saturated by the end of the frame
@@ -226,7 +226,10 @@ void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 (or all) pr
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, emit, wide rows
 void launch_shade(const BinParams& p, bool colour, hipStream_t s);  // composite records of the chunk's slots
-void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, Records rec, hipStream_t s);
+// stats -> host slot + seq; then meta zeroed (zero_mode 2, or 1 when ctl->not_done == 0)
+void launch_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec, FrameCtl* host_ctl,
+                      uint32_t* host_seq, uint32_t seq, uint4* meta, uint32_t meta_quads, int zero_mode,
+                      hipStream_t s);
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s);
 void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,

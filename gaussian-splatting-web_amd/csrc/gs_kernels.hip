@@ -1299,17 +1299,40 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_wide(BinParams p) {
     }
 }
 
-// End of frame: the depth key of the farthest splat any tile saturated at (chunk controller).
-__global__ __launch_bounds__(64) void k_frame_stats(FrameCtl* ctl, const uint32_t* shade_list,
-                                                    Records rec) {
-    if (threadIdx.x != 0) return;
-    uint32_t slot = 0, tiles = 0;
-    for (int k = 0; k < kHistShards; ++k) {
-        slot = max(slot, ctl->sat_slot[k]);
-        tiles += ctl->sat_tiles[k];
+// End of a chunk (the frame's last, or chunk 0 when the host decides on chunk 1): the frame
+// statistics (depth key of the farthest splat a tile saturated at), then FrameCtl stored into the
+// host's pinned slot (mapped, fine-grained) and the sequence number published with a system-scope
+// release; the host spins on it instead of a copy + event.  Then, when the frame ends here
+// (zero_mode 2, or 1 and chunk 0 left no tile unsaturated), the frame's meta block (FrameCtl and
+// histograms) is zeroed for the next frame.
+__global__ __launch_bounds__(256) void k_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec,
+                                                  FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq,
+                                                  uint4* meta, uint32_t meta_quads, int zero_mode) {
+    __shared__ uint32_t s_slot, s_key, s_not_done;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        uint32_t slot = 0, tiles = 0;
+        for (int k = 0; k < kHistShards; ++k) {
+            slot = max(slot, ctl->sat_slot[k]);
+            tiles += ctl->sat_tiles[k];
+        }
+        s_slot = slot;
+        s_key = tiles ? __float_as_uint(rec.r2[shade_list[slot]].x) : 0u;
+        s_not_done = ctl->not_done;
+        ctl->sat_slot_max = s_slot;
+        ctl->sat_key = s_key;
     }
-    ctl->sat_slot_max = slot;
-    ctl->sat_key = tiles ? __float_as_uint(rec.r2[shade_list[slot]].x) : 0u;
+    __syncthreads();
+    constexpr uint32_t kWords = sizeof(FrameCtl) / 4;
+    constexpr uint32_t kSlotW = offsetof(FrameCtl, sat_slot_max) / 4, kKeyW = offsetof(FrameCtl, sat_key) / 4;
+    const uint32_t* src = (const uint32_t*)ctl;
+    uint32_t* dst = (uint32_t*)host_ctl;
+    for (uint32_t w = tid; w < kWords; w += 256) dst[w] = w == kSlotW ? s_slot : w == kKeyW ? s_key : src[w];
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (zero_mode == 2 || (zero_mode == 1 && s_not_done == 0))
+        for (uint32_t i = tid; i < meta_quads; i += 256) meta[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // Summed-area table and bitmask of the tiles chunk 0 left unsaturated (done == 0): one
@@ -1856,8 +1879,11 @@ void launch_shade(const BinParams& p, bool colour, hipStream_t s) {
     else
         hipLaunchKernelGGL(k_shade<false>, dim3(kMaxGrid), dim3(256), 0, s, p);
 }
-void launch_frame_stats(FrameCtl* ctl, const uint32_t* shade_list, Records rec, hipStream_t s) {
-    hipLaunchKernelGGL(k_frame_stats, dim3(1), dim3(64), 0, s, ctl, shade_list, rec);
+void launch_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec, FrameCtl* host_ctl,
+                      uint32_t* host_seq, uint32_t seq, uint4* meta, uint32_t meta_quads, int zero_mode,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(256), 0, s, ctl, shade_list, rec, host_ctl, host_seq, seq,
+                       meta, meta_quads, zero_mode);
 }
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s) {

@@ -77,7 +77,8 @@ typedef struct gs_opts {
                              frame's sorted (key,value) (zero on the first frame).  State lives in the scene. */
     int32_t strip_index;  /* row strip rendered by this call, 0 <= strip_index < strip_count */
     int32_t strip_count;  /* number of equal row strips (16-px tile rows, see gs_strip_rows); 1 = whole image */
-    int32_t timing;       /* 1: record per-stage hipEvent timings (gs_timings) */
+    int32_t timing;       /* 1: record per-stage hipEvent timings (gs_timings); 2: the composite's only
+                             (each event costs the stream a few microseconds) */
     float chunk_fraction; /* depth split between the two chunks (the image never depends on it):
                              0 = adaptive (from the depth at which tiles saturated last frame),
                              >= 1 = one chunk, (0,1) = fixed split at the depth-rank quantile
@@ -93,7 +94,8 @@ typedef struct gs_stats {
     float chunk_fraction; /* fraction of the visible splats sorted in chunk 0 (last frame) */
     int32_t tile_row_begin, tile_row_end;  /* tile rows rendered by the last call */
     int32_t tiles_x;
-    int32_t frames;       /* timed frames averaged below (opts.timing = 1) since gs_timings_reset */
+    int32_t frames;       /* timed frames since gs_timings_reset; ms_composite averages all of them, the
+                             other stage times the frames timed with opts.timing = 1 */
     float ms_total;       /* mean HIP-event times per timed frame: whole frame and per stage; */
     float ms_project, ms_sort, ms_bin, ms_tile_sort, ms_ranges, ms_composite, ms_other;
                           /* project / composite are single kernels, the others kernel groups */
