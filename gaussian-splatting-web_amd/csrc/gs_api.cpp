@@ -151,23 +151,21 @@ struct gs_scene {
     uint8_t* meta = nullptr;
     FrameCtl* ctl = nullptr;
     uint32_t* hist = nullptr;
-    uint32_t* bin_part = nullptr;       // bin_parts(N) + 1
     uint32_t* shade_list = nullptr;     // N: Gaussian index of each composite slot
-    uint32_t* rank_cnt = nullptr;       // N: binning scratch (entries per depth rank)
     uint32_t* part_count = nullptr;     // sort_parts(N): chunk-0 splats per projection partition
     // tile lists
     uint64_t kcap = 0;
-    uint32_t *tkA = nullptr, *tvA = nullptr, *tkB = nullptr, *tvB = nullptr;
+    uint32_t *tvA = nullptr, *tvB = nullptr;  // tile lists: unordered (binning), sorted
     uint32_t* radix_offsets = nullptr;  // 256 x sort_parts(max(N, kcap)): partition counts
     uint32_t* gsum = nullptr;           // 12 regions (chunk x 6 radix passes) of group sums, zero
                                         // between uses
     size_t gsum_region = 0;             // words per region
     uint2* ranges = nullptr;
+    uint32_t* bmat = nullptr;           // [kBinParts][n_tiles] binning partition counts / offsets
+    uint32_t* tbase = nullptr;          // [n_tiles] tile totals, then list begins
     uint8_t* done = nullptr;
     uint32_t* sat = nullptr;            // (strip rows + 1) x (tiles_x + 1), then the bitmask
     size_t sat_cap = 0;
-    uint4* wide_unit = nullptr;         // wide-splat row queue (per chunk, reused)
-    uint32_t wide_cap = 0, wide_unit_cap = 0;
     int tiles_cap = 0;
     float4* state = nullptr;
     uint64_t state_cap = 0;
@@ -217,11 +215,11 @@ static Records records(gs_scene* s) {
 }
 
 static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
-    if (k <= s->kcap && s->tkA) return;
+    if (k <= s->kcap && s->tvA) return;
     if (k >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "more than 2^32 tile entries");
     const uint64_t cap = std::min<uint64_t>(0xFFFFFFFEull, std::max<uint64_t>(k + k / 2, 1u << 20));
-    dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB); dev_free(s->radix_offsets);
-    dev_alloc(s->tkA, cap); dev_alloc(s->tvA, cap); dev_alloc(s->tkB, cap); dev_alloc(s->tvB, cap);
+    dev_free(s->tvA); dev_free(s->tvB); dev_free(s->radix_offsets);
+    dev_alloc(s->tvA, cap); dev_alloc(s->tvB, cap);
     dev_alloc(s->radix_offsets, 256 * (size_t)sort_parts(std::max<uint64_t>(cap, s->n), kMinSortIpt));
     // group sums: every pass's partitions fit a region (kept zero: k_ranges resets after use)
     dev_free(s->gsum);
@@ -236,8 +234,12 @@ static void ensure_tiles(gs_scene* s, int n_tiles) {
     if (n_tiles <= s->tiles_cap && s->ranges) return;
     dev_free(s->ranges);
     dev_free(s->done);
+    dev_free(s->bmat);
+    dev_free(s->tbase);
     dev_alloc(s->ranges, (size_t)n_tiles);
     dev_alloc(s->done, (size_t)n_tiles);
+    dev_alloc(s->bmat, (size_t)kBinParts * n_tiles);
+    dev_alloc(s->tbase, (size_t)n_tiles);
     s->tiles_cap = n_tiles;
 }
 
@@ -246,19 +248,6 @@ static void ensure_sat(gs_scene* s, size_t words) {
     dev_free(s->sat);
     dev_alloc(s->sat, words);
     s->sat_cap = words;
-}
-
-// Wide-splat queue: items <= entries / kWideTiles; one unit per tile row.  Overflowing splats
-// are emitted by the binning itself (slower, still exact).
-static void ensure_wide(gs_scene* s, int strip_rows) {
-    (void)strip_rows;
-    const uint32_t items = (uint32_t)std::min<uint64_t>(1u << 20, s->kcap / kWideTiles + 1024);
-    const uint32_t units = (uint32_t)std::min<uint64_t>(1u << 30, s->kcap / 8 + 4096);
-    if (s->wide_unit && items <= s->wide_cap && units <= s->wide_unit_cap) return;
-    dev_free(s->wide_unit);
-    dev_alloc(s->wide_unit, units);
-    s->wide_cap = items;
-    s->wide_unit_cap = units;
 }
 
 static void ensure_state(gs_scene* s, uint64_t pixels) {
@@ -418,7 +407,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         ensure_state(s, (uint64_t)W * H);
         ensure_sat(s, (size_t)(tr_end - tr_begin + 1) * (TX + 1) + 2 + (size_t)(tr_end - tr_begin) * ((TX + 63) / 64) * 2);
     }
-    ensure_wide(s, tr_end - tr_begin);
 
     // timing 1: events between every stage; 2: around the composite only (each event record costs
     // the stream a few microseconds, so a frame timed at level 1 runs ~35 us slower)
@@ -487,7 +475,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     mark(EV_PROJ1);
 
     // ---- per chunk: depth sort of the chunk's splats -> bin -> tile-id sort -> ranges -> composite
-    const int tile_passes = n_tiles > 256 ? 2 : 1;
     // chunk 0's first depth pass reads k_project's partitions, each holding only its chunk-0
     // splats at the front: one downsweep workgroup takes as many as (on the last frame's count)
     // fill about 3/4 of its 4096-element tile; rounds keep it exact whatever this frame holds
@@ -580,55 +567,34 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         bp.tiles_x = TX;
         bp.n_max = std::max<uint32_t>(pp.n, 1);
         bp.capacity = (uint32_t)s->kcap;
-        bp.part_tot = s->bin_part;
         bp.ranges = s->ranges;
         bp.n_tiles = (uint32_t)n_tiles;
-        bp.rank_cnt = s->rank_cnt;
-        bp.part_stride = bin_parts(s->n) + 1;
-        bp.tkeys = s->tkA;
+        bp.bmat = s->bmat;
+        bp.tbase = s->tbase;
         bp.tvals = s->tvA;
-        bp.sat = s->sat;
-        bp.mask = unsat_mask;
-        bp.mask_words = (TX + 63) / 64;
+        bp.gsum_zero = (uint4*)(s->gsum + kGsumRegions * chunk * s->gsum_region);
+        bp.gsum_zero_quads = (uint32_t)(4 * s->gsum_region / 4);  // the chunk's 4 depth passes
         bp.rows = tr_end - tr_begin;
         bp.shade_list = s->shade_list;
-        bp.wide_cap = s->wide_cap;
-        bp.wide_unit = s->wide_unit;
-        bp.wide_unit_cap = s->wide_unit_cap;
         // composite records of the chunk's depth ranks first: the binning reads them to bin each
         // splat's ellipse, not its bounding box
         launch_shade(bp, !two_phase, st);  // two-phase frames: k_colour stored the colours
         launch_bin(bp, st);
         mark(eb + 1);
 
-        uint32_t *tk_in = s->tkA, *tv_in = s->tvA, *tk_out = s->tkB, *tv_out = s->tvB;
-        for (int ps = 0; ps < tile_passes; ++ps) {
-            SortPass sp{};
-            sp.keys_in = tk_in;
-            sp.vals_in = tv_in;
-            sp.keys_out = tk_out;
-            sp.vals_out = tv_out;
-            sp.n = (uint32_t)s->kcap;
-            sp.n_dev = &s->ctl->k_chunk[chunk];
-            sp.ipt = kTileSortIpt;
-            sp.parts_max = sort_parts(s->kcap, sp.ipt);
-            sp.shift = 8 * ps;
-            sp.mask = 255;
-            sp.hist = s->hist + (6 * chunk + 4 + ps) * kHistWords;
-            sp.offsets = s->radix_offsets;
-            sp.gsum = s->gsum + (kGsumRegions * chunk + 4 + ps) * s->gsum_region;
-            launch_sort_pass(sp, st);
-            std::swap(tk_in, tk_out);
-            std::swap(tv_in, tv_out);
-        }
+        TileSortParams tsp{};  // each tile's list into depth (slot) order
+        tsp.ranges = s->ranges;
+        tsp.in = s->tvA;
+        tsp.out = s->tvB;
+        tsp.done = chunk == 1 ? s->done : nullptr;
+        tsp.n_tiles = n_tiles;
+        launch_tile_sort(tsp, st);
         mark(eb + 2);
-        launch_ranges(tk_in, &s->ctl->k_chunk[chunk], (uint32_t)s->kcap, s->ranges,
-                      s->gsum + kGsumRegions * chunk * s->gsum_region, kGsumRegions * s->gsum_region, st);
         mark(eb + 3);
 
         CompositeParams cp{};
         cp.ranges = s->ranges;
-        cp.tvals = tv_in;
+        cp.tvals = s->tvB;
         cp.rec = s->crec;
         cp.W = W;
         cp.H = H;
@@ -793,9 +759,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->meta, kMetaBytes);
             s->ctl = (FrameCtl*)(s->meta + kMetaCtl);
             s->hist = (uint32_t*)(s->meta + kMetaHist);
-            dev_alloc(s->bin_part, 2 * ((size_t)bin_parts(n) + 1));
             dev_alloc(s->shade_list, (size_t)n);
-            dev_alloc(s->rank_cnt, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->part_count, (size_t)sort_parts(n) + 1);
             const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hf));
@@ -848,17 +812,16 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->keysB); dev_free(s->valsB); dev_free(s->auxB);
     dev_free(s->crec);
     dev_free(s->meta);
-    dev_free(s->bin_part);
     dev_free(s->shade_list);
-    dev_free(s->rank_cnt);
     dev_free(s->part_count);
-    dev_free(s->tkA); dev_free(s->tvA); dev_free(s->tkB); dev_free(s->tvB);
+    dev_free(s->tvA); dev_free(s->tvB);
     dev_free(s->radix_offsets);
     dev_free(s->gsum);
     dev_free(s->ranges);
+    dev_free(s->bmat);
+    dev_free(s->tbase);
     dev_free(s->done);
     dev_free(s->sat);
-    dev_free(s->wide_unit);
     dev_free(s->state);
     if (s->h_ctl) (void)hipHostFree(s->h_ctl);
     if (s->h_seq) (void)hipHostFree(s->h_seq);

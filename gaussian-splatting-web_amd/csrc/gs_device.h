@@ -17,16 +17,15 @@ constexpr int kProjThreads = 256;  // = kSortThreads: k_project works on radix p
 constexpr int kSortThreads = 256;     // 4 waves
 constexpr int kSortIPT = 16;          // items per thread
 constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per radix partition
-constexpr int kBinThreads = 256;
-constexpr int kBinIPT = 2;
-constexpr int kBinTile = kBinThreads * kBinIPT;     // 512 ranks per binning partition
+constexpr int kBinThreads = 1024;     // binning workgroup (one partition of the chunk's ranks)
+constexpr int kBinParts = 256;        // binning partitions per chunk (rows of BinParams::bmat)
+constexpr int kBandTiles = 8192;      // tiles per binning band (LDS counters / cursors)
 constexpr int kHistShards = 8;        // global histograms sharded by blockIdx % 8 (XCD group)
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // key of a culled Gaussian (no visible splat has it)
 constexpr int kRecFloats = 16;        // 64-B projected record
 constexpr int kMaxGrid = 2048;        // persistent grids: 8 workgroups per CU
 constexpr uint32_t kWideTiles = 32;     // splats binding >= this many tiles are emitted row-wise
 constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
-constexpr int kMaskLdsWords = 2048;     // unsaturated-tile bitmask cached in LDS up to this size
 constexpr int kMaxMerge = 16;           // compacted radix input: partitions per downsweep workgroup
 constexpr uint32_t kGroupParts = 32;    // radix partitions per group sum (the downsweep's offsets)
 
@@ -177,28 +176,29 @@ struct BinParams {
     int chunk;                    // 0 or 1
     const uint32_t* sorted_keys;  // [n_chunk] depth keys in order (chunk 0: quantile keys)
     int tile_row_begin, tiles_x;
-    uint32_t n_max;               // upper bound of n_vis (grid / scratch sizing)
-    uint32_t capacity;            // entry capacity of out arrays
-    uint32_t* part_tot;           // [part_stride] scratch: entries per binning partition
-    uint2* ranges;                // [n_tiles] tile ranges, emptied by k_bin_count
+    uint32_t n_max;               // upper bound of n_vis (grid sizing)
+    uint32_t capacity;            // entry capacity of the tile-list arrays
+    uint2* ranges;                // [n_tiles] out (k_tile_scan): [begin, end) of each tile's list
     uint32_t n_tiles;
-    uint32_t* rank_cnt;           // [n_max] scratch: entries of each depth rank of the chunk
-    uint32_t part_stride;         // >= bin_parts(n_max)
-    uint32_t* tkeys;              // out: strip-relative tile id
-    uint32_t* tvals;              // out: Gaussian index
-    // chunk 1: summed-area table of unsaturated tiles, (rows + 1) x (tiles_x + 1),
-    // sat[y][x] = unsaturated tiles in strip rows < y and columns < x; and the same set as a
-    // bitmask, mask_words 64-bit words per strip row (bit x of row y = tile (x, y) unsaturated)
-    const uint32_t* sat;
-    const unsigned long long* mask;
-    int mask_words;
+    uint32_t* bmat;               // [kBinParts][n_tiles] entries of binning partition p in tile t,
+                                  // then (k_bin_colscan) the entries of the earlier partitions
+    uint32_t* tbase;              // [n_tiles] entries per tile, then (k_tile_scan) the tile's begin
+    uint32_t* tvals;              // out: composite slots, grouped by tile, unordered in a tile
+    uint4* gsum_zero;             // the chunk's depth-pass group sums, zeroed by k_bin_count
+    uint32_t gsum_zero_quads;
     int rows;                     // tile rows of the strip
     uint32_t* shade_list;         // [n] Gaussian index of each composite slot g (k_shade)
-    // wide splats: one work unit per tile row, (slot, output position, xa | xb << 16, tile row)
-    // (row ~0u: no entries); wide_cap bounds the splats queued per chunk
-    uint32_t wide_cap;
-    uint4* wide_unit;
-    uint32_t wide_unit_cap;
+};
+
+// Per-tile sort of the tile lists (k_tile_sort): each tile's slots ordered by their sort key,
+// key(g) = g (slots are depth ranks) or, with skey, (skey[g].x << 32) | skey[g].y.
+struct TileSortParams {
+    const uint2* ranges;          // [n_tiles]
+    const uint32_t* in;           // unordered lists (k_bin_emit / k_bin_wide)
+    uint32_t* out;                // the same lists, each in ascending key order
+    const uint2* skey;            // nullable
+    const uint8_t* done;          // chunk 1: saturated tiles are skipped (nullable)
+    int n_tiles;
 };
 
 enum CompositeMode { kCompSingle = 0, kCompFirst = 1, kCompSecond = 2 };
@@ -224,7 +224,7 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, flo
 void launch_project(const ProjParams& p, bool two_phase, hipStream_t s);
 void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 (or all) projected records
 void launch_sort_pass(const SortPass& p, hipStream_t s);
-void launch_bin(const BinParams& p, hipStream_t s);    // count, emit, wide rows
+void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit, wide rows
 void launch_shade(const BinParams& p, bool colour, hipStream_t s);  // composite records of the chunk's slots
 // stats -> host slot + seq; then meta zeroed (zero_mode 2, or 1 when ctl->not_done == 0)
 void launch_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec, FrameCtl* host_ctl,
@@ -232,8 +232,7 @@ void launch_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec, Fr
                       hipStream_t s);
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s);
-void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
-                   uint32_t* zero_words, uint64_t zero_n, hipStream_t s);  // zero_n % 4 == 0
+void launch_tile_sort(const TileSortParams& p, hipStream_t s);
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);
 void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void* out, hipStream_t s);
 
@@ -242,6 +241,6 @@ __host__ __device__ inline uint32_t sort_parts(uint64_t n, int ipt) {
     const uint64_t t = (uint64_t)kSortThreads * (uint64_t)ipt;
     return (uint32_t)((n + t - 1) / t);
 }
-__host__ __device__ inline uint32_t bin_parts(uint64_t n) { return (uint32_t)((n + kBinTile - 1) / kBinTile); }
+__host__ __device__ inline uint32_t bin_bands(uint32_t n_tiles) { return (n_tiles + kBandTiles - 1) / kBandTiles; }
 
 }  // namespace gs

@@ -859,33 +859,6 @@ __device__ __forceinline__ uint32_t tile_id(const BinParams& p, uint32_t tx, uin
     return (ty - (uint32_t)p.tile_row_begin) * (uint32_t)p.tiles_x + tx;
 }
 
-// unsaturated tiles in columns [x0, x1], absolute tile rows [y0, y1] (chunk 1)
-__device__ __forceinline__ uint32_t sat_count(const BinParams& p, uint32_t x0, uint32_t x1, uint32_t y0,
-                                              uint32_t y1) {
-    const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
-    const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
-    const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
-    return (b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]);
-}
-
-// bits [x0, x0 + w) of a bitmask row (w <= 32), bit i = column x0 + i
-__device__ __forceinline__ uint32_t mask_bits(const unsigned long long* row, int words, uint32_t x0, uint32_t w) {
-    const uint32_t wi = x0 >> 6, sh = x0 & 63;
-    unsigned long long v = row[wi] >> sh;
-    if (sh && (int)wi + 1 < words) v |= row[wi + 1] << (64 - sh);
-    return (uint32_t)v & (w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u));
-}
-
-// Block-wide view of the chunk-1 bitmask: LDS copy when it fits.
-__device__ __forceinline__ const unsigned long long* stage_mask(const BinParams& p, unsigned long long* lds) {
-    const int words = p.mask_words * p.rows;
-    if (p.chunk == 0) return nullptr;
-    if (words > kMaskLdsWords) return p.mask;
-    for (int q = threadIdx.x; q < words; q += blockDim.x) lds[q] = p.mask[q];
-    __syncthreads();
-    return lds;
-}
-
 __device__ __forceinline__ bool rect_wide(const TileRect& r) {
     return (r.x1 - r.x0 + 1) * (r.y1 - r.y0 + 1) >= kWideTiles;
 }
@@ -976,229 +949,222 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
     return true;
 }
 
-// Entries of tile row ty, columns [xa, xb], in this chunk: all of them (chunk 0) or the
-// unsaturated ones (chunk 1: bitmask row when narrow, the summed-area table when wide).
-__device__ __forceinline__ uint32_t row_count(const BinParams& p, const unsigned long long* m, uint32_t ty,
-                                              uint32_t xa, uint32_t xb) {
-    const uint32_t w = xb - xa + 1;
-    if (p.chunk == 0) return w;
-    if (w > 32) return sat_count(p, xa, xb, ty, ty);
-    return __popc(mask_bits(m + (uint64_t)(ty - p.tile_row_begin) * p.mask_words, p.mask_words, xa, w));
-}
-
-// Entries of one splat in this chunk (rows of its rect, ellipse column ranges).
-__device__ __forceinline__ uint32_t splat_count(const BinParams& p, const unsigned long long* m,
-                                                const TileRect& r, const Ellipse& e) {
-    uint32_t c = 0;
-    for (uint32_t ty = r.y0; ty <= r.y1; ++ty) {
-        uint32_t xa, xb;
-        if (!ellipse_row(e, ty, xa, xb)) continue;
-        xa = max(xa, r.x0);
-        xb = min(xb, r.x1);
-        if (xa <= xb) c += row_count(p, m, ty, xa, xb);
-    }
-    return c;
-}
-
 // The chunk's composite records start at slot base: chunk 0 at 0, chunk 1 after chunk 0.
 __device__ __forceinline__ uint32_t slot_base(const BinParams& p) {
     return p.chunk ? p.ctl->n_chunk[0] : 0u;
 }
 
-__global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
-    __shared__ uint32_t s_tmp[8];
-    __shared__ unsigned long long s_mask[kMaskLdsWords];
-    // the chunk's tile ranges start empty (k_ranges writes the non-empty ones)
-    for (uint32_t q = blockIdx.x * kBinThreads + threadIdx.x; q < p.n_tiles; q += gridDim.x * kBinThreads)
-        p.ranges[q] = make_uint2(0u, 0u);
-    uint32_t r0, r1;
-    chunk_range(p, r0, r1);
-    const uint32_t parts = bin_parts(r1 - r0);
-    if (blockIdx.x >= parts) return;
-    const unsigned long long* m = stage_mask(p, s_mask);
-    const uint32_t g0 = slot_base(p);
-    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        uint32_t sum = 0;
-#pragma unroll
-        for (int k = 0; k < kBinIPT; ++k) {
-            const uint32_t r = r0 + part * kBinTile + k * kBinThreads + threadIdx.x;
-            if (r < r1) {
-                TileRect tr;
-                uint32_t c = 0;
-                if (rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) {
-                    const float4* q = p.crec + 3 * (uint64_t)(g0 + r);
-                    c = splat_count(p, m, tr, ellipse_of(q[0], q[1]));
-                }
-                p.rank_cnt[r - r0] = c;  // k_bin_emit's counts
-                sum += c;
-            }
-        }
-        uint32_t total;
-        block_excl_scan256(sum, s_tmp, &total);
-        if (threadIdx.x == 0) p.part_tot[part] = total;
-    }
+// ---- binning into per-tile lists, a two-level counting sort without global atomics.  The
+// chunk's ranks are cut into kBinParts partitions; the tiles into bands of <= kBandTiles.
+//   k_bin_count    workgroup (partition p, band): LDS counters of its splats' entries per tile
+//                  (ellipse rows; chunk 1: unsaturated tiles only) -> bmat[p][t]
+//   k_bin_colscan  per tile: exclusive prefix of bmat[.][t] over the partitions, tile totals
+//   k_tile_scan    one workgroup: exclusive scan of the totals in tile order -> ranges, tbase
+//   k_bin_emit     workgroup (p, band): LDS cursors tbase[t] + bmat[p][t]; each entry takes a
+//                  slot with an LDS atomic (lists are unordered inside a tile: k_tile_sort)
+// Count and emission walk the same ellipse rows, so a tile's count and its entries agree.
+__device__ __forceinline__ void bin_partition(const BinParams& p, uint32_t part, uint32_t& r0, uint32_t& r1) {
+    const uint32_t n = p.ctl->n_chunk[p.chunk];
+    const uint32_t per = (n + kBinParts - 1) / kBinParts;
+    r0 = min(n, part * per);
+    r1 = min(n, r0 + per);
 }
 
-// Sum of one 64-bit value per thread of a 256-thread workgroup (every thread gets it).
-__device__ __forceinline__ unsigned long long block_sum64(unsigned long long v, unsigned long long* s_red) {
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    if (lane_id() == 0) s_red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    const unsigned long long t = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-    __syncthreads();
-    return t;
-}
-
-// Queue the tile rows of a wide splat (composite slot g, first output position out) for
-// k_bin_wide, one unit per row: (slot, output position of the row, xa | xb << 16, tile row).
-// False when the queue is full (the caller emits it itself).
-__device__ bool wide_push(const BinParams& p, const unsigned long long* m, uint32_t g, uint32_t out,
-                          const TileRect& r, const Ellipse& e) {
-    const uint32_t h = r.y1 - r.y0 + 1;
-    const uint32_t slot = atomicAdd(&p.ctl->wide_n[p.chunk], 1u);
-    const uint32_t u0 = atomicAdd(&p.ctl->wide_rows[p.chunk], h);
-    const bool ok = slot < p.wide_cap && (uint64_t)u0 + h <= p.wide_unit_cap;
-    uint32_t o = out;
-    for (uint32_t t = 0; t < h && u0 + t < p.wide_unit_cap; ++t) {
-        const uint32_t ty = r.y0 + t;
-        uint32_t xa, xb, c = 0;
-        if (ellipse_row(e, ty, xa, xb)) {
-            xa = max(xa, r.x0);
-            xb = min(xb, r.x1);
-            if (xa <= xb) c = row_count(p, m, ty, xa, xb);
-        }
-        p.wide_unit[u0 + t] = (ok && c) ? make_uint4(g, o, xa | (xb << 16), ty) : make_uint4(0, 0, 0, 0xFFFFFFFFu);
-        o += c;
-    }
-    return ok;
-}
-
-// Entries [k0, k1) of a splat emitted here (local positions o + k) into the LDS stage at o + k - R0.
-__device__ __forceinline__ void stage_narrow(const BinParams& p, const unsigned long long* m, const TileRect& tr,
-                                             const Ellipse& e, uint32_t o, uint32_t k0, uint32_t k1,
-                                             uint32_t R0, uint32_t* s_key) {
-    uint32_t k = 0;
-    for (uint32_t ty = tr.y0; ty <= tr.y1 && k < k1; ++ty) {
+// Entries of one splat (composite slot g) in tiles [t_lo, t_hi): f(tile) per entry.  Rows whose
+// column range is wide are left to `wide` (returns false: not handled) when it accepts them.
+template <class F>
+__device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect& tr, const Ellipse& e,
+                                              uint32_t t_lo, uint32_t t_hi, F&& f) {
+    const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
+    const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
+    for (uint32_t ty = ya; ty <= yb; ++ty) {
         uint32_t xa, xb;
         if (!ellipse_row(e, ty, xa, xb)) continue;
         xa = max(xa, tr.x0);
         xb = min(xb, tr.x1);
-        if (xa > xb) continue;
-        const uint32_t t0 = tile_id(p, 0, ty);
-        if (p.chunk == 0) {
-            for (uint32_t x = xa; x <= xb && k < k1; ++x, ++k)
-                if (k >= k0) s_key[o + k - R0] = t0 + x;
-            continue;
-        }
-        const uint32_t w = xb - xa + 1;
-        if (w > 32) {  // a wide row (the queue could not take the splat): unsaturated tiles
-            for (uint32_t x = xa; x <= xb && k < k1; ++x) {
-                if (p.done[t0 + x]) continue;
-                if (k >= k0) s_key[o + k - R0] = t0 + x;
-                ++k;
-            }
-            continue;
-        }
-        uint32_t bits = mask_bits(m + (uint64_t)(ty - p.tile_row_begin) * p.mask_words, p.mask_words, xa, w);
-        while (bits && k < k1) {
-            const uint32_t x = __ffs(bits) - 1;
-            bits &= bits - 1;
-            if (k >= k0) s_key[o + k - R0] = t0 + xa + x;
-            ++k;
+        const uint32_t t0 = (ty - rb) * tx;
+        for (uint32_t x = xa; x <= xb; ++x) {
+            const uint32_t t = t0 + x;
+            if (t < t_lo || t >= t_hi) continue;
+            if (p.chunk == 1 && p.done[t]) continue;
+            f(t);
         }
     }
 }
 
-constexpr uint32_t kEmitStage = 2048;  // entries staged in LDS per round
-
-// Per depth rank r (composite slot g = base + r): its entries at the scanned output position.
-// Narrow splats' entries are staged in LDS and written out coalesced, round by round; the rows
-// of wide splats are queued for k_bin_wide (written after this kernel).
-__global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
-    __shared__ uint32_t s_tmp[8];
-    __shared__ unsigned long long s_red[4];
-    __shared__ unsigned long long s_mask[kMaskLdsWords];
-    __shared__ uint32_t s_key[kEmitStage];
-    __shared__ uint32_t s_val[kEmitStage];
-    const int tid = threadIdx.x;
+__global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
+    __shared__ uint32_t s_cnt[kBandTiles];
+    // the chunk's depth passes are done: reset their group sums for the next use
+    for (uint32_t q = blockIdx.x * kBinThreads + threadIdx.x; q < p.gsum_zero_quads; q += gridDim.x * kBinThreads)
+        p.gsum_zero[q] = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t part = blockIdx.x % kBinParts, band = blockIdx.x / kBinParts;
+    const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
+    for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += kBinThreads) s_cnt[t] = 0;
+    __syncthreads();
     uint32_t r0, r1;
-    chunk_range(p, r0, r1);
-    const uint32_t parts = bin_parts(r1 - r0);
-    if (blockIdx.x >= parts) return;
-    const unsigned long long* m = stage_mask(p, s_mask);
+    bin_partition(p, part, r0, r1);
     const uint32_t g0 = slot_base(p);
-    if (blockIdx.x == 0) {  // the chunk's totals (what a separate scan launch would write)
-        unsigned long long v = 0;
-        for (uint32_t k = tid; k < parts; k += kBinThreads) v += p.part_tot[k];
-        const unsigned long long total = block_sum64(v, s_red);
-        if (tid == 0) {
-            p.ctl->k_chunk[p.chunk] = (uint32_t)min(total, (unsigned long long)p.capacity);
-            p.ctl->shade_n[p.chunk] = r1 - r0;  // every depth rank has a composite slot
-            if (total > p.capacity) atomicOr(&p.ctl->err, kErrOverflow);
-        }
-        if (p.chunk == 0 && tid < 8 && r1 > 0) {  // quantile keys (fixed-fraction chunking)
-            const uint32_t q = (r1 + (1u << tid) - 1) >> tid;
-            p.ctl->quant_key[tid] = p.sorted_keys[q - 1];
-        }
+    for (uint32_t r = r0 + threadIdx.x; r < r1; r += kBinThreads) {
+        TileRect tr;
+        if (!rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) continue;
+        const float4* q = p.crec + 3 * (uint64_t)(g0 + r);
+        splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
     }
-    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        const uint32_t base_r = r0 + part * kBinTile;
-        uint32_t cnt[kBinIPT], g[kBinIPT];
-        bool narrow[kBinIPT];
-        TileRect tr[kBinIPT];
-        Ellipse el[kBinIPT];
+    __syncthreads();
+    uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
+    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += kBinThreads) row[t] = s_cnt[t - t_lo];
+}
+
+// Per tile: exclusive prefix of its column of bmat over the partitions (in place) and the tile's
+// total into tbase.  The prefix runs XCD-major: partition p is emitted by workgroup p (and
+// p + kBinParts ...) on XCD p % 8, so ordering the partitions (p % 8, p / 8) gives every XCD one
+// contiguous sub-range of each tile's list and its L2 merges the scattered 4-B stores into whole
+// lines.  Workgroup = 64 tiles x 4 waves; wave w sums ordered partitions [64 w, 64 w + 64).
+constexpr int kColTiles = 64;
+constexpr int kColRows = kBinParts / 4;
+static_assert(kBinParts % 8 == 0, "binning partitions must split evenly over the 8 XCDs");
+__device__ __forceinline__ uint32_t colscan_part(uint32_t q) {  // q-th partition in XCD-major order
+    return (q % (kBinParts / 8)) * 8 + q / (kBinParts / 8);
+}
+
+__global__ __launch_bounds__(256) void k_bin_colscan(BinParams p) {
+    __shared__ uint32_t s_sum[4][kColTiles];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t t = blockIdx.x * kColTiles + lane;
+    const bool ok = t < p.n_tiles;
+    uint32_t v[kColRows], sum = 0;
 #pragma unroll
-        for (int k = 0; k < kBinIPT; ++k) {
-            const uint32_t r = base_r + k * kBinThreads + tid;
-            cnt[k] = 0;
-            g[k] = g0 + r;
-            if (r < r1) cnt[k] = p.rank_cnt[r - r0];  // k_bin_count's
-            if (cnt[k]) {
-                rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr[k]);
-                const float4* q = p.crec + 3 * (uint64_t)g[k];
-                el[k] = ellipse_of(q[0], q[1]);
+    for (int k = 0; k < kColRows; ++k) {
+        v[k] = ok ? p.bmat[(uint64_t)colscan_part(w * kColRows + k) * p.n_tiles + t] : 0u;
+        sum += v[k];
+    }
+    s_sum[w][lane] = sum;
+    __syncthreads();
+    uint32_t run = 0;
+    for (int i = 0; i < w; ++i) run += s_sum[i][lane];
+    if (!ok) return;
+#pragma unroll
+    for (int k = 0; k < kColRows; ++k) {
+        p.bmat[(uint64_t)colscan_part(w * kColRows + k) * p.n_tiles + t] = run;
+        run += v[k];
+    }
+    if (w == 3) p.tbase[t] = run;
+}
+
+// One workgroup: exclusive scan of the tile totals in tile order -> ranges [begin, end) and
+// tbase = begin; the chunk's totals.
+constexpr int kScanThreads = 1024;
+
+__global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
+    __shared__ uint32_t s_w[kScanThreads / 64];
+    __shared__ uint32_t s_carry;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    constexpr int nw = kScanThreads / 64;
+    constexpr int ipt = 8;
+    const uint32_t cap = p.capacity;
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < p.n_tiles; t0 += kScanThreads * ipt) {
+        uint32_t v[ipt], sum = 0;
+#pragma unroll
+        for (int k = 0; k < ipt; ++k) {
+            const uint32_t t = t0 + (uint32_t)tid * ipt + k;
+            v[k] = t < p.n_tiles ? p.tbase[t] : 0u;
+            sum += v[k];
+        }
+        const uint32_t incl = wave_incl_scan(sum);
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        uint32_t base = carry + incl - sum, total = 0;
+        for (int i = 0; i < nw; ++i) {
+            if (i < w) base += s_w[i];
+            total += s_w[i];
+        }
+#pragma unroll
+        for (int k = 0; k < ipt; ++k) {
+            const uint32_t t = t0 + (uint32_t)tid * ipt + k;
+            if (t < p.n_tiles) {
+                const uint32_t bb = min(base, cap);
+                p.ranges[t] = make_uint2(bb, min(base + v[k], cap));
+                p.tbase[t] = bb;
+            }
+            base += v[k];
+        }
+        carry += total;
+        __syncthreads();
+    }
+    (void)s_carry;
+    const uint32_t n = p.ctl->n_chunk[p.chunk];
+    if (tid == 0) {
+        p.ctl->k_chunk[p.chunk] = min(carry, cap);
+        p.ctl->shade_n[p.chunk] = n;  // every depth rank has a composite slot
+        if (carry > cap) atomicOr(&p.ctl->err, kErrOverflow);
+    }
+    if (p.chunk == 0 && tid < 8 && n > 0) {  // quantile keys (fixed-fraction chunking)
+        const uint32_t q = (n + (1u << tid) - 1) >> tid;
+        p.ctl->quant_key[tid] = p.sorted_keys[q - 1];
+    }
+}
+
+// Wide splats (>= kWideTiles box tiles) are queued in LDS by the thread that meets them and
+// emitted row by row by whole waves (lanes over columns); the queue holds kWideQueue splats,
+// beyond that the thread emits its splat itself.
+constexpr uint32_t kWideQueue = 512;
+
+__global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
+    __shared__ uint32_t s_cur[kBandTiles];
+    __shared__ uint32_t s_wide[kWideQueue];
+    __shared__ uint32_t s_nw;
+    const uint32_t part = blockIdx.x % kBinParts, band = blockIdx.x / kBinParts;
+    const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
+    const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
+    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += kBinThreads) s_cur[t - t_lo] = p.tbase[t] + row[t];
+    if (threadIdx.x == 0) s_nw = 0;
+    __syncthreads();
+    uint32_t r0, r1;
+    bin_partition(p, part, r0, r1);
+    const uint32_t g0 = slot_base(p);
+    const uint32_t cap = p.capacity;
+    for (uint32_t r = r0 + threadIdx.x; r < r1; r += kBinThreads) {
+        TileRect tr;
+        if (!rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) continue;
+        const uint32_t g = g0 + r;
+        if (rect_wide(tr)) {
+            const uint32_t qi = atomicAdd(&s_nw, 1u);
+            if (qi < kWideQueue) {
+                s_wide[qi] = r;
+                continue;
             }
         }
-        // local output offsets: ranks in order (k, tid) within the partition, as in k_bin_count
-        uint32_t o[kBinIPT];
-        uint32_t total, T = 0;
-#pragma unroll
-        for (int k = 0; k < kBinIPT; ++k) {
-            o[k] = block_excl_scan256(cnt[k], s_tmp, &total) + T;
-            T += total;
-        }
-        // output base: the entries of all earlier partitions, summed by the whole workgroup
-        uint32_t obase;
-        {
-            unsigned long long v = 0;
-            for (uint32_t k = tid; k < part; k += kBinThreads) v += p.part_tot[k];
-            obase = (uint32_t)min(block_sum64(v, s_red), (unsigned long long)p.capacity);
-        }
-#pragma unroll
-        for (int k = 0; k < kBinIPT; ++k) {
-            narrow[k] = cnt[k] != 0;
-            if (cnt[k] && rect_wide(tr[k]) && wide_push(p, m, g[k], obase + o[k], tr[k], el[k])) narrow[k] = false;
-        }
-        for (uint32_t R0 = 0; R0 < T; R0 += kEmitStage) {
-            const uint32_t R1 = min(T, R0 + kEmitStage);
-#pragma unroll
-            for (int k = 0; k < kBinIPT; ++k) {
-                if (!narrow[k] || o[k] >= R1 || o[k] + cnt[k] <= R0) continue;
-                const uint32_t k0 = R0 > o[k] ? R0 - o[k] : 0u, k1 = min(cnt[k], R1 - o[k]);
-                stage_narrow(p, m, tr[k], el[k], o[k], k0, k1, R0, s_key);
-                for (uint32_t q = k0; q < k1; ++q) s_val[o[k] + q - R0] = g[k];
+        const float4* q = p.crec + 3 * (uint64_t)g;
+        splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, [&](uint32_t t) {
+            const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
+            if (pos < cap) p.tvals[pos] = g;
+        });
+    }
+    __syncthreads();
+    const uint32_t nq = min(s_nw, kWideQueue);
+    if (threadIdx.x == 0 && s_nw) atomicAdd(&p.ctl->wide_n[p.chunk], s_nw);  // statistics
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
+    for (uint32_t qi = wave; qi < nq; qi += kBinThreads / 64) {  // wave-uniform
+        const uint32_t r = s_wide[qi], g = g0 + r;
+        TileRect tr;
+        rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr);
+        const float4* q = p.crec + 3 * (uint64_t)g;
+        const Ellipse e = ellipse_of(q[0], q[1]);
+        const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
+        for (uint32_t ty = ya; ty <= yb; ++ty) {
+            uint32_t xa, xb;
+            if (!ellipse_row(e, ty, xa, xb)) continue;
+            xa = max(xa, tr.x0);
+            xb = min(xb, tr.x1);
+            const uint32_t t0 = (ty - rb) * tx;
+            for (uint32_t x = xa + lane; x <= xb; x += 64) {
+                const uint32_t t = t0 + x;
+                if (t < t_lo || t >= t_hi || (p.chunk == 1 && p.done[t])) continue;
+                const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
+                if (pos < cap) p.tvals[pos] = g;
             }
-            __syncthreads();
-            // coalesced copy; positions of queued wide splats carry stale LDS words and are
-            // rewritten by k_bin_wide
-            for (uint32_t q = R0 + tid; q < R1; q += kBinThreads) {
-                const uint32_t oe = obase + q;
-                if (oe < p.capacity) {
-                    p.tkeys[oe] = s_key[q - R0];
-                    p.tvals[oe] = s_val[q - R0];
-                }
-            }
-            __syncthreads();
         }
     }
 }
@@ -1249,51 +1215,6 @@ __global__ __launch_bounds__(256) void k_shade(BinParams p) {
             for (int u = 0; u < 4; ++u) {
                 const uint32_t k = 16 * u + (lane >> 2);
                 if (k < cnt && qd < 3) o[3 * k + qd] = q[u];
-            }
-        }
-    }
-}
-
-// Tile rows of wide splats, one row per work unit (slot, output position, xa | xb << 16, row):
-// each wave prefetches kWideUnits units lane-parallel, then writes them one by one across its
-// lanes (few units per wave: the rows are short and the wave's loop is the latency).
-constexpr uint32_t kWideUnits = 16;
-
-__global__ __launch_bounds__(kBinThreads) void k_bin_wide(BinParams p) {
-    __shared__ unsigned long long s_mask[kMaskLdsWords];
-    const uint32_t units = min(p.ctl->wide_rows[p.chunk], p.wide_unit_cap);
-    if (blockIdx.x * (kBinThreads / 64) * kWideUnits >= units) return;
-    const unsigned long long* m = stage_mask(p, s_mask);
-    const uint32_t lane = lane_id();
-    const uint32_t wave = blockIdx.x * (kBinThreads / 64) + (threadIdx.x >> 6);
-    const uint32_t nwaves = gridDim.x * (kBinThreads / 64);
-    for (uint32_t u0 = wave * kWideUnits; u0 < units; u0 += nwaves * kWideUnits) {
-        const uint32_t u = u0 + lane;
-        uint4 it = make_uint4(0, 0, 0, 0xFFFFFFFFu);
-        if (lane < kWideUnits && u < units) it = p.wide_unit[u];
-        uint64_t todo = __ballot(it.w != 0xFFFFFFFFu);
-        while (todo) {
-            const int src = __ffsll((long long)todo) - 1;
-            todo &= todo - 1;
-            const uint32_t gj = __shfl(it.x, src, 64), go = __shfl(it.y, src, 64);
-            const uint32_t gz = __shfl(it.z, src, 64), row = __shfl(it.w, src, 64);
-            const uint32_t xa = gz & 0xffffu, xb = gz >> 16;
-            const uint32_t w = xb - xa + 1, t0 = tile_id(p, xa, row);
-            uint32_t o = go;
-            for (uint32_t xs = 0; xs < w; xs += 64) {
-                const uint32_t x = xs + lane;
-                bool f = x < w;
-                if (p.chunk == 1 && f) {
-                    const unsigned long long* mr = m + (uint64_t)(row - p.tile_row_begin) * p.mask_words;
-                    f = (mr[(xa + x) >> 6] >> ((xa + x) & 63)) & 1ull;
-                }
-                const uint64_t b = __ballot(f);
-                const uint32_t e = o + __popcll(b & lanemask_lt());
-                if (f && e < p.capacity) {
-                    p.tkeys[e] = t0 + x;
-                    p.tvals[e] = gj;
-                }
-                o += __popcll(b);
             }
         }
     }
@@ -1375,18 +1296,253 @@ __global__ __launch_bounds__(1024) void k_sat(const uint8_t* __restrict__ done, 
 }
 
 // ============================================================================ k_ranges
-__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ tkeys,
-                                                const uint32_t* __restrict__ k_dev,
-                                                uint2* __restrict__ ranges, uint4* __restrict__ zero,
-                                                uint32_t zero_n) {
-    // the chunk's radix passes are done: reset their group sums for the next use
-    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < zero_n; q += gridDim.x * 256)
-        zero[q] = make_uint4(0, 0, 0, 0);
-    const uint32_t k = *k_dev;
-    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < k; q += gridDim.x * 256) {
-        const uint32_t t = tkeys[q];
-        if (q == 0 || tkeys[q - 1] != t) ranges[t].x = q;
-        if (q == k - 1 || tkeys[q + 1] != t) ranges[t].y = q + 1;
+// ============================================================================ k_tile_sort
+// One workgroup per tile orders the tile's list by key (the slot itself, or (skey.x, skey.y)),
+// ascending; keys are unique.  Lists of up to kTsCap entries are sorted in one round: 1024
+// buckets over [kmin, kmax] (a power-of-two width), a counting scatter into LDS, and each
+// element's rank = its bucket's start + the smaller keys in its bucket (a bitonic sort in LDS
+// when a bucket is heavy).  Longer lists go in rounds of <= kTsCap consecutive keys: a bucket
+// histogram of the remaining keys picks the round's upper bound, the round's elements are
+// gathered into LDS and sorted the same way.  The output depends only on the keys.
+constexpr int kTsThreads = 256;
+constexpr int kTsIpt = 8;
+constexpr uint32_t kTsCap = kTsThreads * kTsIpt;  // entries per round
+constexpr int kTsBucketBits = 10;
+constexpr uint32_t kTsBuckets = 1u << kTsBucketBits;
+constexpr uint32_t kTsHeavy = 64;  // largest bucket ranked by counting
+
+struct TsShared {
+    unsigned long long k[kTsCap];
+    uint32_t v[kTsCap];
+    uint32_t cnt[kTsBuckets];
+    uint32_t start[kTsBuckets];
+    unsigned long long red[8];
+    uint32_t tmp[8];
+};
+
+__device__ __forceinline__ unsigned long long ts_key(const TileSortParams& p, uint32_t g) {
+    if (!p.skey) return g;
+    const uint2 k = p.skey[g];
+    return ((unsigned long long)k.x << 32) | k.y;
+}
+
+__device__ __forceinline__ void block_minmax64(unsigned long long& mn, unsigned long long& mx, unsigned long long* s) {
+    for (int d = 32; d >= 1; d >>= 1) {
+        mn = min(mn, (unsigned long long)__shfl_xor(mn, d, 64));
+        mx = max(mx, (unsigned long long)__shfl_xor(mx, d, 64));
+    }
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+        s[w] = mn;
+        s[4 + w] = mx;
+    }
+    __syncthreads();
+    mn = min(min(s[0], s[1]), min(s[2], s[3]));
+    mx = max(max(s[4], s[5]), max(s[6], s[7]));
+    __syncthreads();
+}
+
+__device__ __forceinline__ int ts_shift(unsigned long long span) {
+    return span == 0 ? 0 : max(0, 64 - (int)__clzll(span) - kTsBucketBits);
+}
+
+// Sort n <= kTsCap elements held in registers (element j*256 + tid of k/v) with keys in
+// [kmin, kmax]; out[rank] = value.
+__device__ void ts_segment(TsShared& S, const unsigned long long (&k)[kTsIpt], const uint32_t (&v)[kTsIpt],
+                           uint32_t n, unsigned long long kmin, unsigned long long kmax, uint32_t* __restrict__ out) {
+    const int tid = threadIdx.x;
+    const int s = ts_shift(kmax - kmin);
+    for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;
+    __syncthreads();
+    uint32_t bk[kTsIpt];
+#pragma unroll
+    for (int j = 0; j < kTsIpt; ++j) {
+        bk[j] = 0;
+        if (j * kTsThreads + tid < (int)n) {
+            bk[j] = (uint32_t)((k[j] - kmin) >> s);
+            atomicAdd(&S.cnt[bk[j]], 1u);
+        }
+    }
+    __syncthreads();
+    constexpr int per = kTsBuckets / kTsThreads;
+    uint32_t c[per], sum = 0, big = 0;
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+        c[q] = S.cnt[per * tid + q];
+        sum += c[q];
+        big = max(big, c[q]);
+    }
+    uint32_t total;
+    uint32_t b = block_excl_scan256(sum, S.tmp, &total);
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+        S.start[per * tid + q] = b;
+        S.cnt[per * tid + q] = b;  // scatter cursor
+        b += c[q];
+    }
+    const bool heavy = __syncthreads_or(big > kTsHeavy);
+#pragma unroll
+    for (int j = 0; j < kTsIpt; ++j) {
+        if (j * kTsThreads + tid < (int)n) {
+            const uint32_t pos = atomicAdd(&S.cnt[bk[j]], 1u);
+            S.k[pos] = k[j];
+            S.v[pos] = v[j];
+        }
+    }
+    __syncthreads();
+    if (!heavy) {
+#pragma unroll
+        for (int j = 0; j < kTsIpt; ++j) {
+            if (j * kTsThreads + tid < (int)n) {
+                const uint32_t b0 = S.start[bk[j]], b1 = bk[j] + 1 < kTsBuckets ? S.start[bk[j] + 1] : n;
+                uint32_t r = b0;
+                for (uint32_t q = b0; q < b1; ++q) r += S.k[q] < k[j] ? 1u : 0u;
+                out[r] = v[j];
+            }
+        }
+    } else {  // bitonic sort of the (bucket-ordered) elements, padded to a power of two
+        uint32_t P = 1;
+        while (P < n) P <<= 1;
+        for (uint32_t i = n + tid; i < P; i += kTsThreads) {
+            S.k[i] = ~0ull;
+            S.v[i] = 0u;
+        }
+        __syncthreads();
+        for (uint32_t size = 2; size <= P; size <<= 1) {
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t i = tid; i < (P >> 1); i += kTsThreads) {
+                    const uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+                    const bool asc = (lo & size) == 0;
+                    const unsigned long long a = S.k[lo], bb = S.k[hi];
+                    if ((a > bb) == asc) {
+                        S.k[lo] = bb;
+                        S.k[hi] = a;
+                        const uint32_t t = S.v[lo];
+                        S.v[lo] = S.v[hi];
+                        S.v[hi] = t;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t i = tid; i < n; i += kTsThreads) out[i] = S.v[i];
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kTsThreads) void k_tile_sort(TileSortParams p) {
+    __shared__ TsShared S;
+    const int per = (p.n_tiles + 7) >> 3;  // XCD-banded, as k_composite
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= p.n_tiles) return;
+    if (p.done && p.done[tile]) return;
+    const uint2 range = p.ranges[tile];
+    const uint32_t L = range.y - range.x;
+    if (L == 0) return;
+    const uint32_t* __restrict__ in = p.in + range.x;
+    uint32_t* __restrict__ out = p.out + range.x;
+    const int tid = threadIdx.x;
+    unsigned long long k[kTsIpt];
+    uint32_t v[kTsIpt];
+    if (L == 1) {
+        if (tid == 0) out[0] = in[0];
+        return;
+    }
+    if (L <= kTsCap) {
+        unsigned long long mn = ~0ull, mx = 0ull;
+#pragma unroll
+        for (int j = 0; j < kTsIpt; ++j) {
+            const uint32_t i = j * kTsThreads + tid;
+            k[j] = 0ull;
+            v[j] = 0u;
+            if (i < L) {
+                v[j] = in[i];
+                k[j] = ts_key(p, v[j]);
+                mn = min(mn, k[j]);
+                mx = max(mx, k[j]);
+            }
+        }
+        block_minmax64(mn, mx, S.red);
+        ts_segment(S, k, v, L, mn, mx, out);
+        return;
+    }
+    // long list: rounds of <= kTsCap consecutive keys
+    unsigned long long kmin = ~0ull, kmax = 0ull;
+    for (uint32_t i = tid; i < L; i += kTsThreads) {
+        const unsigned long long key = ts_key(p, in[i]);
+        kmin = min(kmin, key);
+        kmax = max(kmax, key);
+    }
+    block_minmax64(kmin, kmax, S.red);
+    unsigned long long lo = kmin, hi = 0ull;
+    uint32_t done_n = 0;
+    constexpr int perb = kTsBuckets / kTsThreads;
+    while (done_n < L) {
+        const bool bounded = L - done_n > kTsCap;
+        if (bounded) {  // hi: the largest bucket boundary with <= kTsCap keys in [lo, hi)
+            unsigned long long span = kmax - lo;
+            for (;;) {
+                const int s = ts_shift(span);
+                for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;
+                __syncthreads();
+                for (uint32_t i = tid; i < L; i += kTsThreads) {
+                    const unsigned long long key = ts_key(p, in[i]);
+                    if (key >= lo && key - lo <= span) atomicAdd(&S.cnt[(uint32_t)((key - lo) >> s)], 1u);
+                }
+                __syncthreads();
+                uint32_t c[perb], sum = 0;
+#pragma unroll
+                for (int q = 0; q < perb; ++q) {
+                    c[q] = S.cnt[perb * tid + q];
+                    sum += c[q];
+                }
+                uint32_t total;
+                uint32_t run = block_excl_scan256(sum, S.tmp, &total);
+                uint32_t fit = 0;
+#pragma unroll
+                for (int q = 0; q < perb; ++q) {
+                    run += c[q];
+                    fit += run <= kTsCap ? 1u : 0u;
+                }
+                uint32_t m;
+                block_excl_scan256(fit, S.tmp, &m);  // buckets whose prefix fits (a prefix of them)
+                if (m >= 1) {
+                    hi = lo + ((unsigned long long)m << s);
+                    break;
+                }
+                span = (1ull << s) - 1ull;  // the first bucket alone overflows: narrow to it (s > 0)
+            }
+        }
+        if (tid == 0) S.tmp[4] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < L; i += kTsThreads) {
+            const uint32_t g = in[i];
+            const unsigned long long key = ts_key(p, g);
+            if (key >= lo && (!bounded || key < hi)) {
+                const uint32_t pos = atomicAdd(&S.tmp[4], 1u);
+                S.k[pos] = key;
+                S.v[pos] = g;
+            }
+        }
+        __syncthreads();
+        const uint32_t nc = S.tmp[4];
+        unsigned long long mn = ~0ull, mx = 0ull;
+#pragma unroll
+        for (int j = 0; j < kTsIpt; ++j) {
+            const uint32_t i = j * kTsThreads + tid;
+            k[j] = 0ull;
+            v[j] = 0u;
+            if (i < nc) {
+                k[j] = S.k[i];
+                v[j] = S.v[i];
+                mn = min(mn, k[j]);
+                mx = max(mx, k[j]);
+            }
+        }
+        block_minmax64(mn, mx, S.red);  // (its barriers order the LDS reads before ts_segment)
+        ts_segment(S, k, v, nc, mn, mx, out + done_n);
+        done_n += nc;
+        lo = hi;
     }
 }
 
@@ -1868,10 +2024,17 @@ void launch_sort_pass(const SortPass& p, hipStream_t s) {
     }
 }
 void launch_bin(const BinParams& p, hipStream_t s) {
-    const unsigned grid = std::max<uint32_t>(1, std::min<uint32_t>(bin_parts(p.n_max), kMaxGrid));
+    if (p.n_tiles == 0) return;
+    const unsigned grid = kBinParts * bin_bands(p.n_tiles);
     hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(kBinThreads), 0, s, p);
+    hipLaunchKernelGGL(k_bin_colscan, dim3((p.n_tiles + kColTiles - 1) / kColTiles), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, s, p);
     hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);
-    hipLaunchKernelGGL(k_bin_wide, dim3(kMaxGrid), dim3(kBinThreads), 0, s, p);
+}
+void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
+    if (p.n_tiles <= 0) return;
+    const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
+    hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(kTsThreads), 0, s, p);
 }
 void launch_shade(const BinParams& p, bool colour, hipStream_t s) {
     if (colour)
@@ -1888,12 +2051,6 @@ void launch_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec, Fr
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s) {
     hipLaunchKernelGGL(k_sat, dim3(1), dim3(1024), 0, s, done, tiles_x, rows, sat, mask, ctl);
-}
-void launch_ranges(const uint32_t* tkeys, const uint32_t* k_dev, uint32_t k_max, uint2* ranges,
-                   uint32_t* zero_words, uint64_t zero_n, hipStream_t s) {
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (k_max + 255) / 256));
-    hipLaunchKernelGGL(k_ranges, dim3(grid), dim3(256), 0, s, tkeys, k_dev, ranges, (uint4*)zero_words,
-                       (uint32_t)(zero_n / 4));
 }
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;
