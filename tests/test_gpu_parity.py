@@ -373,3 +373,60 @@ def test_chunked_strips(gpu_ctx):
     parts = [sc.render(u, W, H, gs.make_opts(strip_index=g, strip_count=4, chunk_fraction=0.2))
              for g in range(4)]
     assert np.array_equal(np.concatenate(parts, axis=0)[:H], full)
+
+
+def test_long_tile_lists(gpu_ctx):
+    """Every tile's list far longer than one LDS round of k_tile_sort (rounds of consecutive
+    keys), faint splats so the composite walks the whole list; against the fp32 oracle."""
+    W, H = 64, 64
+    n = 10_000
+    rng = np.random.default_rng(41)
+    aos = gs.synth_aos(n, 41, W, H).reshape(n, 80)
+    d = rng.uniform(4.0, 12.0, n).astype(np.float32)
+    t = np.float32(np.tan(np.pi / 6))
+    aos[:, 0] = rng.uniform(-0.3, 0.3, n) * d * t
+    aos[:, 1] = rng.uniform(-0.3, 0.3, n) * d * t
+    aos[:, 2] = -d
+    aos[:, 4:7] = (1.5 * d * t)[:, None]  # about the image's size
+    aos[:, 12] = -3.9  # op ~ 0.02
+    aos = aos.reshape(-1)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    img = sc.render(u, W, H, gs.make_opts(t_min=0.0, chunk_fraction=1.0, timing=1))
+    assert gpu_ctx.timings()["k_entries"] >= 16 * 2 * 2048
+    ref, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=0.0)
+    r = image_close_fp32(img, ref, name="long_lists")
+    assert r[2], r
+
+
+def test_skewed_tile_keys(gpu_ctx):
+    """Tile (0, 0) holds 1000 near splats and one far splat: its keys crowd a few of
+    k_tile_sort's buckets (the bitonic path); the other tiles hold mid-depth splats."""
+    W, H = 64, 64
+    n = 200_000
+    rng = np.random.default_rng(43)
+    aos = gs.synth_aos(n, 43, W, H).reshape(n, 80)
+    t = np.float32(np.tan(np.pi / 6))
+    near = np.arange(1000)
+    d = rng.uniform(2.0, 2.5, near.size).astype(np.float32)
+    aos[near, 0] = (-1.0 + rng.uniform(0.1, 0.4, near.size)) * d * t
+    aos[near, 1] = (1.0 - rng.uniform(0.1, 0.4, near.size)) * d * t
+    aos[near, 2] = -d
+    aos[near, 4:7] = 0.004
+    aos[near, 12] = -3.0
+    mid = np.arange(1000, n - 1)
+    d = rng.uniform(8.0, 20.0, mid.size).astype(np.float32)
+    aos[mid, 0] = rng.uniform(0.1, 0.9, mid.size) * d * t
+    aos[mid, 1] = rng.uniform(-0.9, 0.9, mid.size) * d * t
+    aos[mid, 2] = -d
+    aos[mid, 4:7] = (0.002 * d)[:, None]
+    aos[n - 1, 0:3] = (0.0, 0.0, -40.0)
+    aos[n - 1, 4:7] = 30.0
+    aos[n - 1, 12] = 0.0
+    aos = aos.reshape(-1)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    img = sc.render(u, W, H, gs.make_opts(t_min=0.0, chunk_fraction=1.0))
+    ref, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=0.0)
+    r = image_close_fp32(img, ref, name="skewed_keys")
+    assert r[2], r
