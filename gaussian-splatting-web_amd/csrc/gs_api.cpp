@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -139,27 +140,19 @@ struct gs_scene {
     float4* shade = nullptr;            // shading blocks (shade_stride float4 per Gaussian)
     float4* cull = nullptr;             // cull planes (two-phase projection)
     float4* r2 = nullptr;
-    // k_project output (depth key, packed tile rect per Gaussian), then the depth sort ping-pong
+    // k_project output: depth key, packed tile rect per Gaussian
     uint32_t *keysP = nullptr, *rectP = nullptr;
-    uint32_t *keysA = nullptr, *valsA = nullptr, *auxA = nullptr;
-    uint32_t *keysB = nullptr, *valsB = nullptr, *auxB = nullptr;
-    float4* crec = nullptr;             // composite records, 3 float4 per slot
+    // composite slots (slot_c0 / slot_c1): records (3 float4), (depth key, index), packed rect
+    float4* crec = nullptr;
+    uint2* skey = nullptr;
+    uint32_t* srect = nullptr;
+    uint32_t *c0 = nullptr, *c1 = nullptr;  // [parts]: slots per projection partition and chunk
     unsigned long long* keep_mask = nullptr;  // two-phase frames: k_cull's keep bits
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
-    // zero-per-frame block: FrameCtl | digit histograms of the 4 depth + 2 tile passes of each
-    // chunk (kHistShards x 256 words each)
-    uint8_t* meta = nullptr;
-    FrameCtl* ctl = nullptr;
-    uint32_t* hist = nullptr;
-    uint32_t* shade_list = nullptr;     // N: Gaussian index of each composite slot
-    uint32_t* part_count = nullptr;     // sort_parts(N): chunk-0 splats per projection partition
+    FrameCtl* ctl = nullptr;            // zero at a frame's start (k_frame_end clears it)
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tvA = nullptr, *tvB = nullptr;  // tile lists: unordered (binning), sorted
-    uint32_t* radix_offsets = nullptr;  // 256 x sort_parts(max(N, kcap)): partition counts
-    uint32_t* gsum = nullptr;           // 12 regions (chunk x 6 radix passes) of group sums, zero
-                                        // between uses
-    size_t gsum_region = 0;             // words per region
     uint2* ranges = nullptr;
     uint32_t* bmat = nullptr;           // [kBinParts][n_tiles] binning partition counts / offsets
     uint32_t* tbase = nullptr;          // [n_tiles] tile totals, then list begins
@@ -176,15 +169,15 @@ struct gs_scene {
     FrameCtl* d_ctl_slot = nullptr;
     uint32_t* d_seq = nullptr;
     uint32_t seq_next = 1;
-    bool meta_clean = false;      // the last frame's k_frame_end zeroed meta (see render_frame)
+    bool meta_clean = false;      // the last frame's k_frame_end zeroed FrameCtl (see render_frame)
     uint32_t stat_want[2] = {};   // sequence number that completes the slot's frame
     bool stat_pending[2] = {};
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
     bool have_last = false;
     uint32_t chunk_T = kNoSplit;        // adaptive chunk threshold for the next frame
-    uint32_t full_quant[8] = {};        // quantile keys of the last frame sorted in one chunk
-    bool have_quant = false;
+    uint32_t key_lo = 0, key_hi = 0;    // depth-key range of the last frame's visible splats
+    bool have_krange = false;
     int last_tiles = 0;                 // tiles of the last frame's strip
     bool have_frame = false;
 };
@@ -192,22 +185,13 @@ struct gs_scene {
 static constexpr size_t kHistWords = kHistShards * 256;
 // radix partition sizes (items per thread x 256): small partitions keep every CU busy on the
 // short depth sorts; the tile-id sort is long enough for 4096-element partitions
-#ifndef GS_DEPTH_IPT
-#define GS_DEPTH_IPT 8
-#endif
-#ifndef GS_TILE_IPT
-#define GS_TILE_IPT 8
-#endif
-static constexpr int kDepthSortIpt = GS_DEPTH_IPT, kTileSortIpt = GS_TILE_IPT;
+// radix partition size of gs_debug_sort_pairs (items per thread x 256)
+static constexpr int kDepthSortIpt = 8;
 // chunk-0 threshold: the farthest saturation key of the last frame, its depth scaled by this
 #ifndef GS_CHUNK_MARGIN
 #define GS_CHUNK_MARGIN 1.15f
 #endif
 static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
-// group-sum regions per chunk: 4 depth passes, 2 tile-id passes
-static constexpr size_t kGsumRegions = 6;
-static constexpr int kMinSortIpt = kDepthSortIpt < kTileSortIpt ? kDepthSortIpt : kTileSortIpt;
-static constexpr size_t kMetaCtl = 0, kMetaHist = 256, kMetaBytes = kMetaHist + 12 * kHistWords * 4;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
 static Records records(gs_scene* s) {
@@ -218,15 +202,8 @@ static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
     if (k <= s->kcap && s->tvA) return;
     if (k >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "more than 2^32 tile entries");
     const uint64_t cap = std::min<uint64_t>(0xFFFFFFFEull, std::max<uint64_t>(k + k / 2, 1u << 20));
-    dev_free(s->tvA); dev_free(s->tvB); dev_free(s->radix_offsets);
+    dev_free(s->tvA); dev_free(s->tvB);
     dev_alloc(s->tvA, cap); dev_alloc(s->tvB, cap);
-    dev_alloc(s->radix_offsets, 256 * (size_t)sort_parts(std::max<uint64_t>(cap, s->n), kMinSortIpt));
-    // group sums: every pass's partitions fit a region (kept zero: k_ranges resets after use)
-    dev_free(s->gsum);
-    const size_t parts = sort_parts(std::max<uint64_t>(cap, s->n), kMinSortIpt);
-    s->gsum_region = 256 * ((parts + kGroupParts - 1) / kGroupParts + 1);
-    dev_alloc(s->gsum, 2 * kGsumRegions * s->gsum_region);
-    HIPCHK(hipMemset(s->gsum, 0, 2 * kGsumRegions * s->gsum_region * sizeof(uint32_t)));
     s->kcap = cap;
 }
 
@@ -349,9 +326,10 @@ static void collect_stats(gs_scene* s, bool wait) {
         // tile saturated (measured by the composite), rising at once, decaying slowly (3 % of
         // depth per frame); frames where most tiles never saturate use one chunk
         const FrameCtl& l = s->last;
-        if (l.n_vis > 0 && l.n_chunk[0] == l.n_vis) {  // one-chunk frame: quantiles of every rank
-            std::memcpy(s->full_quant, l.quant_key, sizeof(s->full_quant));
-            s->have_quant = true;
+        if (l.n_vis > 0 && ~l.key_min_inv <= l.key_max) {  // depth range (fixed-fraction chunking)
+            s->key_lo = ~l.key_min_inv;
+            s->key_hi = l.key_max;
+            s->have_krange = true;
         }
         uint32_t sat_tiles = 0;
         for (int k = 0; k < kHistShards; ++k) sat_tiles += l.sat_tiles[k];
@@ -380,27 +358,24 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         collect_stats(s, false);
         s->stat_pending[slot] = false;
     }
-    auto frame_end = [&](int zero_mode) {  // statistics into the slot (then meta zeroed, see k_frame_end)
-        const uint32_t q = s->seq_next++;
-        s->stat_want[slot] = q;
-        launch_frame_end(s->ctl, s->shade_list, records(s), s->d_ctl_slot + slot, s->d_seq + slot, q,
-                         (uint4*)s->meta, (uint32_t)(kMetaBytes / 16), zero_mode, st);
-        return q;
-    };
-    bool ended = false;
     if (s->have_last && s->last.k_total > s->kcap) ensure_tile_capacity(s, s->last.k_total);
     ensure_tiles(s, std::max(n_tiles, 1));
     s->last_tiles = n_tiles;
     // chunk threshold: adaptive, one chunk (chunk_fraction >= 1), or a fixed split for tests and
-    // diagnostics (chunk_fraction in (0,1): the depth key at quantile 2^-t <= chunk_fraction of
-    // the last one-chunk frame; one chunk until such a frame exists)
+    // diagnostics (chunk_fraction in (0,1): the depth 2^-t <= chunk_fraction of the way from the
+    // last frame's nearest to its farthest visible splat; one chunk until a frame was seen)
     uint32_t T = s->chunk_T;
     if (o.chunk_fraction >= 1.0f) {
         T = kNoSplit;
     } else if (o.chunk_fraction > 0.0f) {
         const int t = std::min(7, std::max(0, (int)std::ceil(-std::log2((double)o.chunk_fraction))));
-        T = s->have_quant ? s->full_quant[t] + 1u : kNoSplit;
-        if (T == 0) T = kNoSplit;
+        T = kNoSplit;
+        if (s->have_krange) {
+            const float v0 = key_to_float(s->key_lo), v1 = key_to_float(s->key_hi);
+            const float v = v0 + (v1 - v0) * std::ldexp(1.0f, -t);
+            const uint32_t k = float_to_key(v);
+            if (std::isfinite(v) && k < kNoSplit - 1) T = k + 1;
+        }
     }
     const bool two_chunks = T != kNoSplit;
     if (two_chunks) {
@@ -409,7 +384,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     }
 
     // timing 1: events between every stage; 2: around the composite only (each event record costs
-    // the stream a few microseconds, so a frame timed at level 1 runs ~35 us slower)
+    // the stream a few microseconds, so a frame timed at level 1 runs slower)
     const bool timed = o.timing != 0;
     FrameEvents& fe = c->fe[c->fe_cur];
     auto mark = [&](int e) {
@@ -420,13 +395,13 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     if (timed) {
         harvest(c, fe);  // slot reuse: its frame completed long ago (or wait for it)
         fe.level = o.timing;
-        fe.chunk1 = false;
+        fe.chunk1 = two_chunks;
     }
     mark(EV_BEGIN);
 
-    // meta (FrameCtl, histograms) is zero at a frame's start: k_frame_end of the last frame cleared
-    // it, unless that frame never ended (first frame, an error mid-frame)
-    if (!s->meta_clean) HIPCHK(hipMemsetAsync(s->meta, 0, kMetaBytes, st));
+    // FrameCtl is zero at a frame's start: k_frame_end of the last frame cleared it, unless that
+    // frame never ended (first frame, an error mid-frame)
+    if (!s->meta_clean) HIPCHK(hipMemsetAsync(s->ctl, 0, sizeof(FrameCtl), st));
     s->meta_clean = false;
     ProjParams pp{};
     pp.geo = s->geo;
@@ -458,134 +433,61 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.rect_out = s->rectP;
     pp.rec = records(s);
     pp.ctl = s->ctl;
-    pp.thresh = T;  // first depth pass of chunk 0 fused into the projection
-    pp.c_keys = s->keysB;
-    pp.c_vals = s->valsB;
-    pp.c_rect = s->auxB;
-    pp.c_count = s->part_count;
-    pp.offsets = s->radix_offsets;
-    pp.gsum = s->gsum;  // chunk 0, pass 0's region
-    pp.parts_max = sort_parts(pp.n);
-    pp.hist0 = s->hist;
+    pp.thresh = T;
+    pp.crec = s->crec;
+    pp.skey = s->skey;
+    pp.srect = s->srect;
+    pp.c0 = s->c0;
+    pp.c1 = s->c1;
     mark(EV_PROJ0);
     // two-phase projection (cull planes first) when most Gaussians are outside this frame's
     // rows: row strips, or a previous frame that saw under half of the scene
     const bool two_phase = sc > 1 || (s->have_last && s->last.n_vis * 2 < s->n);
     launch_project(pp, two_phase, st);
+    launch_colour(pp, st);
     mark(EV_PROJ1);
 
-    // ---- per chunk: depth sort of the chunk's splats -> bin -> tile-id sort -> ranges -> composite
-    // chunk 0's first depth pass reads k_project's partitions, each holding only its chunk-0
-    // splats at the front: one downsweep workgroup takes as many as (on the last frame's count)
-    // fill about 3/4 of its 4096-element tile; rounds keep it exact whatever this frame holds
-    int pass0_merge = 1;
-    if (s->have_last && s->last.n_vis > 0 && pp.n > 0) {
-        const double per = std::max(1.0, (double)s->last.n_chunk[0] / (double)sort_parts(pp.n));
-        pass0_merge = (int)std::max(1.0, std::min((double)kMaxMerge, 3072.0 / per));
-    }
+    // ---- per chunk: bin -> per-tile sort -> composite.  Chunk 1 (the splats at or past T that
+    // touch a tile chunk 0 left unsaturated) is enqueued with chunk 0 and gated on the device:
+    // every kernel of it returns at once when chunk 0 saturated every tile.
     const size_t sat_words = (size_t)(tr_end - tr_begin + 1) * (TX + 1);
     unsigned long long* unsat_mask = (unsigned long long*)(s->sat + ((sat_words + 1) & ~(size_t)1));
-    for (int chunk = 0; chunk < 2; ++chunk) {
+    for (int chunk = 0; chunk < (two_chunks ? 2 : 1); ++chunk) {
         const int eb = chunk == 0 ? EV_DSORT_0 : EV_DSORT_1;
-        uint32_t not_done = 0;
-        if (chunk == 1 && two_chunks) {
-            // chunk 1 only when chunk 0 left a tile unsaturated: k_frame_end publishes chunk 0's
-            // statistics to the host, which spins on them and decides here.  Enqueued but empty,
-            // chunk 1's ~26 launches cost ~0.13 ms of GPU time; this costs one short wait for
-            // chunk 0 (host run-ahead is lost for it).  Without chunk 1 the frame ends here.
-            frame_end(1);  // zeroes meta on the device iff not_done == 0 (the host's test below)
-            if (!wait_slot(s, slot, st)) throw GsError(GS_ERR_HIP, "chunk-0 statistics never arrived");
-            not_done = s->h_ctl[slot].not_done;
-            ended = not_done == 0;
-        }
-        if (chunk == 1 && (!two_chunks || not_done == 0)) {
-            if (o.timing == 1)
-                for (int e = 0; e < 5; ++e) mark(eb + e);
-            break;
-        }
-        if (chunk == 1) fe.chunk1 = true;
         if (chunk == 1) {
             launch_sat(s->done, TX, tr_end - tr_begin, s->sat, unsat_mask, s->ctl, st);
-            // k_project stored records only for chunk 0: add those chunk 1's filter and bins read
             ProjParams rp = pp;
             rp.sat = s->sat;
             rp.rec_all = 0;
             launch_records(rp, st);
         }
-        // chunk 0: k_project compacted its splats per partition into B (and did the first upsweep);
-        // chunk 1: (keysP, index, rectP) over N, filtered by pass 0.  -> A -> B -> A -> B
-        const uint32_t* kin[4] = {chunk ? s->keysP : s->keysB, s->keysA, s->keysB, s->keysA};
-        const uint32_t* vin[4] = {chunk ? nullptr : s->valsB, s->valsA, s->valsB, s->valsA};
-        const uint32_t* ain[4] = {chunk ? s->rectP : s->auxB, s->auxA, s->auxB, s->auxA};
-        uint32_t* kout[4] = {s->keysA, s->keysB, s->keysA, s->keysB};
-        uint32_t* vout[4] = {s->valsA, s->valsB, s->valsA, s->valsB};
-        uint32_t* aout[4] = {s->auxA, s->auxB, s->auxA, s->auxB};
-        for (int ps = 0; ps < 4; ++ps) {
-            SortPass sp{};
-            sp.keys_in = kin[ps];
-            sp.vals_in = vin[ps];
-            sp.aux_in = ain[ps];
-            sp.keys_out = kout[ps];
-            sp.vals_out = vout[ps];
-            sp.aux_out = aout[ps];
-            sp.n = pp.n;
-            sp.n_dev = ps == 0 ? nullptr : &s->ctl->n_chunk[chunk];
-            sp.gate = chunk == 1 ? &s->ctl->not_done : nullptr;  // chunk 1: only with unsaturated tiles
-            sp.ipt = (ps == 0 && chunk == 0) ? 16 : kDepthSortIpt;
-            sp.merge = ps == 0 && chunk == 0 ? pass0_merge : 1;
-            sp.parts_max = sort_parts(pp.n, sp.ipt);
-            sp.shift = 8 * ps;
-            sp.mask = 255;
-            sp.filter = (ps == 0 && chunk == 1) ? kFiltTail : kFiltNone;
-            sp.part_count = (ps == 0 && chunk == 0) ? s->part_count : nullptr;
-            sp.thresh = T;
-            sp.count_out = ps == 0 ? &s->ctl->n_chunk[chunk] : nullptr;
-            sp.rec = records(s);
-            sp.sat = s->sat;
-            sp.tiles_x = TX;
-            sp.tile_row_begin = tr_begin;
-            sp.hist = s->hist + (6 * chunk + ps) * kHistWords;
-            sp.offsets = s->radix_offsets;
-            sp.gsum = s->gsum + (kGsumRegions * chunk + ps) * s->gsum_region;
-            launch_sort_pass(sp, st);
-        }
         mark(eb);
         BinParams bp{};
-        bp.sorted_vals = s->valsB;
-        bp.sorted_rect = s->auxB;
-        bp.sorted_keys = s->keysB;
+        bp.skey = s->skey;
+        bp.srect = s->srect;
+        bp.cnt = chunk == 0 ? s->c0 : s->c1;
+        bp.parts = sort_parts(pp.n);
         bp.rec = records(s);
-        bp.shade = s->shade;
-        bp.shade_stride = shade_stride(s->n_sh);
         bp.crec = s->crec;
-        bp.n_sh = s->n_sh;
-        std::memcpy(bp.cam, uni + 32, 12);
         bp.done = s->done;
         bp.ctl = s->ctl;
         bp.chunk = chunk;
         bp.tile_row_begin = tr_begin;
         bp.tiles_x = TX;
-        bp.n_max = std::max<uint32_t>(pp.n, 1);
         bp.capacity = (uint32_t)s->kcap;
         bp.ranges = s->ranges;
         bp.n_tiles = (uint32_t)n_tiles;
         bp.bmat = s->bmat;
         bp.tbase = s->tbase;
         bp.tvals = s->tvA;
-        bp.gsum_zero = (uint4*)(s->gsum + kGsumRegions * chunk * s->gsum_region);
-        bp.gsum_zero_quads = (uint32_t)(4 * s->gsum_region / 4);  // the chunk's 4 depth passes
         bp.rows = tr_end - tr_begin;
-        bp.shade_list = s->shade_list;
-        // composite records of the chunk's depth ranks first: the binning reads them to bin each
-        // splat's ellipse, not its bounding box
-        launch_shade(bp, !two_phase, st);  // two-phase frames: k_colour stored the colours
         launch_bin(bp, st);
         mark(eb + 1);
-
-        TileSortParams tsp{};  // each tile's list into depth (slot) order
+        TileSortParams tsp{};  // each tile's list into (depth key, index) order
         tsp.ranges = s->ranges;
         tsp.in = s->tvA;
         tsp.out = s->tvB;
+        tsp.skey = s->skey;
         tsp.done = chunk == 1 ? s->done : nullptr;
         tsp.n_tiles = n_tiles;
         launch_tile_sort(tsp, st);
@@ -612,8 +514,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
         mark(eb + 4);
     }
-    if (!ended) frame_end(2);
-    s->meta_clean = true;  // k_frame_end zeroes it for the next frame
+    if (!two_chunks && o.timing == 1)
+        for (int e = 0; e < 5; ++e) mark(EV_DSORT_1 + e);
+    {  // statistics into the slot, FrameCtl zeroed for the next frame
+        const uint32_t q = s->seq_next++;
+        s->stat_want[slot] = q;
+        launch_frame_end(s->ctl, s->d_ctl_slot + slot, s->d_seq + slot, q, st);
+    }
+    s->meta_clean = true;
     mark(EV_END);
     s->last_pp = pp;
     HIPCHK(hipGetLastError());
@@ -753,14 +661,14 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->keep_mask, (size_t)(n / 64 + 1));
             dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->keysP, n); dev_alloc(s->rectP, n);
-            dev_alloc(s->keysA, n); dev_alloc(s->valsA, n); dev_alloc(s->auxA, n);
-            dev_alloc(s->keysB, n); dev_alloc(s->valsB, n); dev_alloc(s->auxB, n);
-            dev_alloc(s->crec, 3 * (size_t)std::max<uint64_t>(n, 1));
-            dev_alloc(s->meta, kMetaBytes);
-            s->ctl = (FrameCtl*)(s->meta + kMetaCtl);
-            s->hist = (uint32_t*)(s->meta + kMetaHist);
-            dev_alloc(s->shade_list, (size_t)n);
-            dev_alloc(s->part_count, (size_t)sort_parts(n) + 1);
+            dev_alloc(s->crec, 3 * ((size_t)sort_parts(n) * kSortTile + 1));
+            dev_alloc(s->ctl, 1);
+            // slots: part * kSortTile + q < sort_parts(n) * kSortTile
+            const size_t nslots = (size_t)sort_parts(n) * kSortTile + 1;
+            dev_alloc(s->skey, nslots);
+            dev_alloc(s->srect, nslots);
+            dev_alloc(s->c0, (size_t)sort_parts(n) + 1);
+            dev_alloc(s->c1, (size_t)sort_parts(n) + 1);
             const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hf));
             HIPCHK(hipHostMalloc((void**)&s->h_seq, 64, hf));
@@ -808,15 +716,13 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->keep_mask);
     dev_free(s->r2);
     dev_free(s->keysP); dev_free(s->rectP);
-    dev_free(s->keysA); dev_free(s->valsA); dev_free(s->auxA);
-    dev_free(s->keysB); dev_free(s->valsB); dev_free(s->auxB);
     dev_free(s->crec);
-    dev_free(s->meta);
-    dev_free(s->shade_list);
-    dev_free(s->part_count);
+    dev_free(s->ctl);
+    dev_free(s->skey);
+    dev_free(s->srect);
+    dev_free(s->c0);
+    dev_free(s->c1);
     dev_free(s->tvA); dev_free(s->tvB);
-    dev_free(s->radix_offsets);
-    dev_free(s->gsum);
     dev_free(s->ranges);
     dev_free(s->bmat);
     dev_free(s->tbase);
@@ -1014,6 +920,27 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
     });
 }
 
+// The last frame's composite slots as (slot, depth key, Gaussian index), chunk 0 then chunk 1.
+static std::vector<std::array<uint32_t, 3>> frame_slots(gs_scene* s) {
+    collect_stats(s, true);
+    const uint32_t parts = sort_parts(s->n);
+    std::vector<std::array<uint32_t, 3>> out;
+    if (!parts) return out;
+    std::vector<uint32_t> c0(parts), c1(parts);
+    std::vector<uint2> sk((size_t)parts * kSortTile);
+    HIPCHK(hipMemcpy(c0.data(), s->c0, parts * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c1.data(), s->c1, parts * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(sk.data(), s->skey, sk.size() * sizeof(uint2), hipMemcpyDeviceToHost));
+    const bool chunk1 = s->last.n_chunk[1] > 0;
+    for (int ch = 0; ch < (chunk1 ? 2 : 1); ++ch)
+        for (uint32_t p = 0; p < parts; ++p)
+            for (uint32_t q = 0; q < (ch ? c1[p] : c0[p]); ++q) {
+                const uint32_t g = ch ? slot_c1(p, q) : slot_c0(p, q);
+                out.push_back({g, sk[g].x, sk[g].y});
+            }
+    return out;
+}
+
 int gs_debug_last_order(gs_ctx* c, gs_scene* s, uint32_t* out_keys, uint32_t* out_index, uint64_t cap,
                         uint64_t* out_n) {
     return guarded([&] {
@@ -1021,11 +948,16 @@ int gs_debug_last_order(gs_ctx* c, gs_scene* s, uint32_t* out_keys, uint32_t* ou
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipStreamSynchronize(c->stream));
-        collect_stats(s, true);
-        *out_n = s->last.n_vis;
-        const uint64_t m = std::min<uint64_t>(cap, s->last.n_vis);
-        if (m && out_keys) HIPCHK(hipMemcpy(out_keys, s->keysB, m * 4, hipMemcpyDeviceToHost));
-        if (m && out_index) HIPCHK(hipMemcpy(out_index, s->valsB, m * 4, hipMemcpyDeviceToHost));
+        auto sl = frame_slots(s);  // every composite slot, in the composite's (key, index) order
+        std::sort(sl.begin(), sl.end(), [](const std::array<uint32_t, 3>& a, const std::array<uint32_t, 3>& b) {
+            return a[1] != b[1] ? a[1] < b[1] : a[2] < b[2];
+        });
+        *out_n = sl.size();
+        const uint64_t m = std::min<uint64_t>(cap, sl.size());
+        for (uint64_t k = 0; k < m; ++k) {
+            if (out_keys) out_keys[k] = sl[k][1];
+            if (out_index) out_index[k] = sl[k][2];
+        }
         return GS_OK;
     });
 }
@@ -1037,6 +969,7 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipStreamSynchronize(c->stream));
         const uint64_t m = std::min(cap, s->n);
+        const auto sl = frame_slots(s);
         if (m) {  // r01 -> words [0, 8); r2 -> words [12, 16); colour below
             ProjParams rp = s->last_pp;  // records of every visible Gaussian (a frame stores fewer)
             rp.rec_all = 1;
@@ -1052,16 +985,13 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
                 std::memcpy(out16 + 16 * j + 12, &b[4 * j], 16);
             }
         }
-        // colour words [8, 12): from the composite record of each binned splat
-        collect_stats(s, true);
-        const uint64_t slots = (uint64_t)s->last.shade_n[0] + s->last.shade_n[1];
-        if (slots) {
-            std::vector<uint32_t> js(slots);
-            std::vector<float> cr(slots * 12);
-            HIPCHK(hipMemcpy(js.data(), s->shade_list, slots * 4, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(cr.data(), s->crec, slots * 48, hipMemcpyDeviceToHost));
-            for (uint64_t g = 0; g < slots; ++g)
-                if (js[g] < m) std::memcpy(out16 + 16 * (uint64_t)js[g] + 8, &cr[12 * g + 8], 16);
+        // colour words [8, 11): from the composite record of each slot of the frame
+        if (!sl.empty()) {
+            const size_t ns = (size_t)sort_parts(s->n) * kSortTile;
+            std::vector<float> cr(ns * 12);
+            HIPCHK(hipMemcpy(cr.data(), s->crec, ns * 48, hipMemcpyDeviceToHost));
+            for (const auto& e : sl)
+                if (e[2] < m) std::memcpy(out16 + 16 * (uint64_t)e[2] + 8, &cr[12 * (size_t)e[0] + 8], 12);
         }
         return GS_OK;
     });

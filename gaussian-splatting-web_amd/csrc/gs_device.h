@@ -44,16 +44,25 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t k_chunk[2];          // (tile, splat) entries per chunk (binning scan)
     uint32_t not_done;            // tiles still accepting splats after chunk 0
     uint32_t err;
-    uint32_t wide_n[2];           // wide splats queued per chunk (binning)
-    uint32_t wide_rows[2];        // their tile rows (work units of k_bin_wide)
-    uint32_t shade_n[2];          // composite slots per chunk (= its depth-sorted splats)
-    uint32_t n_chunk[2];          // depth-sorted splats per chunk (count of radix pass 0)
-    uint32_t sat_key;             // depth key of the farthest splat a tile saturated at
-    uint32_t sat_slot_max;        // (k_frame_end)
-    uint32_t quant_key[8];        // key at rank ceil(n_chunk[0] / 2^t) - 1 of chunk 0, t = 0..7
-    uint32_t sat_slot[kHistShards];   // per shard: max composite slot at which a tile saturated
-    uint32_t sat_tiles[kHistShards];  // per shard: tiles saturated by the end of the frame
+    uint32_t wide_n[2];           // wide splats per chunk (binning statistics)
+    uint32_t n_chunk[2];          // splats (composite slots) per chunk
+    uint32_t key_min_inv;         // ~(smallest depth key of a visible splat) (project)
+    uint32_t key_max;             // largest depth key of a visible splat (project)
+    uint32_t sat_key;             // depth key of the farthest splat a tile saturated at (k_frame_end)
+    uint32_t sat_key_shard[kHistShards];  // per shard: the same, max over the shard's tiles
+    uint32_t sat_tiles[kHistShards];      // per shard: tiles saturated by the end of the frame
 };
+
+// Composite slots.  k_project gives the chunk-0 splats of projection partition `part` (kSortTile
+// Gaussians) the slots part * kSortTile + q, q < c0[part] (in arrival order); k_records gives the
+// chunk-1 splats of that partition part * kSortTile + kSortTile - 1 - q, q < c1[part].  A
+// Gaussian is in at most one chunk, so the two never meet.  Per slot: the composite record
+// (3 float4), skey = (depth key, Gaussian index) (the per-tile sort key: ties in depth fall back
+// to the index, as the reference's stable sort over index-ordered slots) and the packed rect.
+__host__ __device__ inline uint32_t slot_c0(uint32_t part, uint32_t q) { return part * (uint32_t)kSortTile + q; }
+__host__ __device__ inline uint32_t slot_c1(uint32_t part, uint32_t q) {
+    return part * (uint32_t)kSortTile + (uint32_t)kSortTile - 1u - q;
+}
 
 // Scene layout in HBM: a 48-B geometry record per Gaussian (3 float4: x, y, z, opacity logit |
 // scale xyz, rot.x | rot.y, rot.z, rot.w, 0) read by k_project (streamed, or gathered for the
@@ -102,21 +111,18 @@ struct ProjParams {
     int tile_row_begin, tile_row_end, tiles_x;
     uint32_t* keys_out;       // [n]: depth key or kSentinel
     uint32_t* rect_out;       // [n]: packed tile rectangle
-    Records rec;              // out: the projected record of every visible Gaussian
+    Records rec;              // out: r2 of every visible Gaussian (k_records: r01 too)
     FrameCtl* ctl;
-    // first depth pass of chunk 0, fused (per kSortTile partition of the Gaussians):
-    uint32_t thresh;          // chunk-0 threshold key
-    uint32_t* c_keys;         // out: chunk-0 keys, Gaussian index, tile rect, compacted in index
-    uint32_t* c_vals;         //      order to the front of each partition
-    uint32_t* c_rect;
-    uint32_t* c_count;        // out: [parts] chunk-0 elements per partition
-    uint32_t* offsets;        // out: [parts][256] digit-0 counts per partition
-    uint32_t* gsum;           // out: [parts / kGroupParts][256] their group sums (zeroed)
-    uint32_t parts_max;
-    uint32_t* hist0;          // out: [kHistShards][256] digit-0 histogram (zeroed)
+    uint32_t thresh;          // chunk-0 threshold key: chunk 0 = visible splats with key < thresh
+    // composite slots (see slot_c0): records, sort keys, rects, per-partition counts
+    float4* crec;
+    uint2* skey;
+    uint32_t* srect;
+    uint32_t* c0;             // [parts] chunk-0 splats per projection partition (k_project)
+    uint32_t* c1;             // [parts] chunk-1 splats per projection partition (k_records; zeroed by k_project)
     // two-phase frames: k_cull's keep bit per Gaussian (bit i%64 of word i/64)
     unsigned long long* keep_mask;
-    // k_records: unsaturated-tile SAT of chunk 0 (see BinParams::sat); rec_all = every visible
+    // k_records: unsaturated-tile SAT of chunk 0 (k_sat); rec_all = every visible (debug)
     const uint32_t* sat;
     int rec_all;
     float cam[3];             // camera position (SH view direction)
@@ -163,20 +169,16 @@ struct SortPass {
 };
 
 struct BinParams {
-    const uint32_t* sorted_vals;  // [n_vis] Gaussian index in depth order
-    const uint32_t* sorted_rect;  // [n_vis] packed tile rectangle in depth order
-    Records rec;                  // projected records (k_shade input, wide rects)
-    const float4* shade;          // shading blocks
-    uint32_t shade_stride;        // float4 per block
-    float4* crec;                 // out: composite records, 3 float4 per slot
-    int n_sh;
-    float cam[3];
+    const uint2* skey;            // [slots] (depth key, Gaussian index)
+    const uint32_t* srect;        // [slots] packed tile rectangle
+    const uint32_t* cnt;          // [parts] the chunk's splats per projection partition (c0 or c1)
+    uint32_t parts;               // projection partitions
+    Records rec;                  // r2 (wide rects)
+    const float4* crec;           // composite records, 3 float4 per slot
     const uint8_t* done;          // chunk 1: per-tile "saturated after chunk 0"
     FrameCtl* ctl;
     int chunk;                    // 0 or 1
-    const uint32_t* sorted_keys;  // [n_chunk] depth keys in order (chunk 0: quantile keys)
     int tile_row_begin, tiles_x;
-    uint32_t n_max;               // upper bound of n_vis (grid sizing)
     uint32_t capacity;            // entry capacity of the tile-list arrays
     uint2* ranges;                // [n_tiles] out (k_tile_scan): [begin, end) of each tile's list
     uint32_t n_tiles;
@@ -184,10 +186,7 @@ struct BinParams {
                                   // then (k_bin_colscan) the entries of the earlier partitions
     uint32_t* tbase;              // [n_tiles] entries per tile, then (k_tile_scan) the tile's begin
     uint32_t* tvals;              // out: composite slots, grouped by tile, unordered in a tile
-    uint4* gsum_zero;             // the chunk's depth-pass group sums, zeroed by k_bin_count
-    uint32_t gsum_zero_quads;
     int rows;                     // tile rows of the strip
-    uint32_t* shade_list;         // [n] Gaussian index of each composite slot g (k_shade)
 };
 
 // Per-tile sort of the tile lists (k_tile_sort): each tile's slots ordered by their sort key,
@@ -222,14 +221,12 @@ struct CompositeParams {
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, float4* shade, float4* cull,
                       hipStream_t s);
 void launch_project(const ProjParams& p, bool two_phase, hipStream_t s);
-void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 (or all) projected records
+void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 slots (or, rec_all, every record)
+void launch_colour(const ProjParams& p, hipStream_t s);   // colours of the chunk-0 slots
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit, wide rows
-void launch_shade(const BinParams& p, bool colour, hipStream_t s);  // composite records of the chunk's slots
-// stats -> host slot + seq; then meta zeroed (zero_mode 2, or 1 when ctl->not_done == 0)
-void launch_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec, FrameCtl* host_ctl,
-                      uint32_t* host_seq, uint32_t seq, uint4* meta, uint32_t meta_quads, int zero_mode,
-                      hipStream_t s);
+// stats -> host slot + seq; then FrameCtl zeroed for the next frame
+void launch_frame_end(FrameCtl* ctl, FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq, hipStream_t s);
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s);
 void launch_tile_sort(const TileSortParams& p, hipStream_t s);

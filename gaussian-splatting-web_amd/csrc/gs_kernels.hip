@@ -393,55 +393,74 @@ __device__ __forceinline__ void store_colour(const ProjParams& p, uint32_t j) {
     rec_r01(p.rec, j)[2] = sh_colour(p.rec.r01 + (uint64_t)j * p.rec.stride, p.rec.off, p.cam);
 }
 
-__device__ __forceinline__ void store_records(const ProjParams& p, uint32_t i, const Proj& o) {
-    float4* r = rec_r01(p.rec, i);
+// A visible splat's composite slot: records r0, r1 (the colour quad follows: k_colour or
+// k_records), its sort key (depth key, index) and packed rect; and its per-Gaussian r2.
+__device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, uint32_t i, const Proj& o) {
+    float4* r = p.crec + 3 * (uint64_t)slot;
     r[0] = o.r0;
     r[1] = o.r1;
+    p.skey[slot] = make_uint2(o.key, i);
+    p.srect[slot] = o.prect;
     p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles), __uint_as_float(o.bbx),
                               __uint_as_float(o.bby));
 }
 
-// k_project's per-Gaussian step: key and rect of every Gaussian; the 48-B record only for the
-// chunk-0 splats (key < thresh), the only ones a frame reads unless chunk 1 runs (k_records).
-__device__ __forceinline__ uint32_t project_one(const ProjParams& p, uint32_t i, int row_lo, int row_hi,
-                                                uint32_t& my_vis, unsigned long long& my_k, bool cull) {
-    Proj o;
-    if (project_core(p, i, row_lo, row_hi, cull, o)) {
-        if (o.key < p.thresh) store_records(p, i, o);
-        ++my_vis;
-        my_k += o.ntiles;
-    }
-    p.keys_out[i] = o.key;
-    p.rect_out[i] = o.prect;
-    return o.key;
-}
-
-// Records of the splats k_project did not store, before chunk 1's depth sort: visible Gaussians
-// with key >= thresh whose rect is wide or touches an unsaturated tile (the SAT of k_sat), or,
-// with rec_all (debug), every visible Gaussian.
+// Chunk 1 (after chunk 0 left tiles unsaturated), or every visible Gaussian's per-Gaussian
+// record (rec_all, debug): visible Gaussians with key >= thresh whose rect touches an unsaturated
+// tile (the SAT of k_sat) get a chunk-1 slot (slot_c1) with their record and colour.  Waves
+// cover 64 consecutive Gaussians of one projection partition: one counter add per wave.
 __global__ __launch_bounds__(256) void k_records(ProjParams p) {
+    if (!p.rec_all && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += gridDim.x * blockDim.x) {
-        const uint32_t key = p.keys_out[i];
-        if (key == kSentinel) continue;
-        if (!p.rec_all) {
-            if (key < p.thresh) continue;
-            const uint32_t pr = p.rect_out[i];
-            if (pr == kRectEmpty) continue;  // as tail_overlaps: no tile, never in chunk 1
-            if (pr != kRectLarge) {
-                const uint32_t x0 = pr & 0xfffu, y0 = (pr >> 12) & 0xfffu;
-                const uint32_t x1 = x0 + ((pr >> 24) & 15u), y1 = y0 + (pr >> 28);
-                const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
-                const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
-                if ((b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]) == 0u) continue;
+    const uint32_t lane = lane_id();
+    for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < p.n; i0 += gridDim.x * blockDim.x) {
+        const uint32_t i = i0 + lane;
+        bool want = false;
+        const uint32_t key = i < p.n ? p.keys_out[i] : kSentinel;
+        if (key != kSentinel) {
+            want = true;
+            if (!p.rec_all) {
+                const uint32_t pr = p.rect_out[i];
+                want = key >= p.thresh && pr != kRectEmpty;
+                if (want && pr != kRectLarge) {
+                    const uint32_t x0 = pr & 0xfffu, y0 = (pr >> 12) & 0xfffu;
+                    const uint32_t x1 = x0 + ((pr >> 24) & 15u), y1 = y0 + (pr >> 28);
+                    const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
+                    const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
+                    want = (b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]) != 0u;
+                }
             }
         }
         Proj o;
-        if (project_core(p, i, row_lo, row_hi, false, o)) {
-            store_records(p, i, o);
-            store_colour(p, i);
+        want = want && project_core(p, i, row_lo, row_hi, false, o);
+        if (p.rec_all) {
+            if (want) {
+                float4* r = rec_r01(p.rec, i);
+                r[0] = o.r0;
+                r[1] = o.r1;
+                p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles),
+                                          __uint_as_float(o.bbx), __uint_as_float(o.bby));
+                store_colour(p, i);
+            }
+            continue;
+        }
+        const uint64_t b = __ballot(want);
+        if (!b) continue;
+        uint32_t base = 0;
+        if (lane == 0) {
+            const uint32_t c = (uint32_t)__popcll(b);
+            base = atomicAdd(&p.c1[i0 / kSortTile], c);
+            atomicAdd(&p.ctl->n_chunk[1], c);
+        }
+        base = __shfl(base, 0, 64);
+        if (want) {
+            const uint32_t slot = slot_c1(i0 / kSortTile, base + (uint32_t)__popcll(b & lanemask_lt()));
+            store_slot(p, slot, i, o);
+            float4 c = sh_colour(p.rec.r01 + (uint64_t)i * p.rec.stride, p.rec.off, p.cam);
+            c.w = __uint_as_float(o.key);
+            p.crec[3 * (uint64_t)slot + 2] = c;
         }
     }
 }
@@ -459,44 +478,33 @@ __global__ __launch_bounds__(256) void k_cull(ProjParams p) {
     }
 }
 
-// Per 4096-Gaussian partition (the radix partition of the first depth pass): project every
-// Gaussian, then do the first pass's upsweep here: the digit-0 histogram of the chunk-0 splats
-// (visible, key < thresh) and their order-preserving compaction to the front of the partition
-// in the pass-0 input arrays, so that pass reads only them.
+// Per projection partition (kSortTile Gaussians): project every Gaussian (key and packed rect
+// of each; kSentinel when invisible) and give each chunk-0 splat (visible, key < thresh) a
+// composite slot of the partition (slot_c0, arrival order: the per-tile sort orders them) with
+// its records.  Visible count, tile total, the depth-key range and c0 / c1 are published.
 // TWO_PHASE (row strips, mostly off-screen frames): phase A reads k_cull's keep bits and keeps an
 // order-preserving list of the survivors in LDS; phase B projects the survivors densely, so culled
 // Gaussians cost neither their 48 B nor divergent lanes.
 template <bool TWO_PHASE>
 __global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
     __shared__ unsigned long long s_k;
-    __shared__ uint32_t s_vis;
-    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
+    __shared__ uint32_t s_cnt;
     __shared__ unsigned long long s_mask[kSortIPT][kProjThreads / 64];
     __shared__ uint32_t s_base[kSortIPT][kProjThreads / 64];
     __shared__ uint32_t s_total;
     __shared__ uint16_t s_list[TWO_PHASE ? kSortTile : 1];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    if (tid == 0) { s_k = 0; s_vis = 0; }
-    uint32_t my_vis = 0;
+    if (tid == 0) { s_k = 0; s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
+    uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
     unsigned long long my_k = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = sort_parts(p.n);
-    // exclusive prefix of the 16 x 4 (round, wave) ballots in s_mask: element order = index order
-    auto prefix = [&]() {
-        __syncthreads();
-        if (tid < 64) {
-            const uint32_t c = __popcll(s_mask[tid >> 2][tid & 3]);
-            const uint32_t incl = wave_incl_scan(c);
-            s_base[tid >> 2][tid & 3] = incl - c;
-            if (tid == 63) s_total = incl;
-        }
-        __syncthreads();
-    };
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         const uint32_t p0 = part * kSortTile;
-        s_hist[tid] = 0;
         uint32_t nitems = min((uint32_t)kSortTile, p.n - p0);
+        if (tid == 0) s_cnt = 0;
         if (TWO_PHASE) {
             for (int it = 0; it < kSortIPT; ++it) {
                 const uint32_t i = p0 + it * kProjThreads + tid;
@@ -508,66 +516,83 @@ __global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
                 }
                 if (lane == 0) s_mask[it][w] = b;
             }
-            prefix();
+            __syncthreads();
+            if (tid < 64) {  // exclusive prefix of the 16 x 4 (round, wave) ballots: index order
+                const uint32_t c = __popcll(s_mask[tid >> 2][tid & 3]);
+                const uint32_t incl = wave_incl_scan(c);
+                s_base[tid >> 2][tid & 3] = incl - c;
+                if (tid == 63) s_total = incl;
+            }
+            __syncthreads();
             for (int it = 0; it < kSortIPT; ++it) {
                 const uint64_t b = s_mask[it][w];
                 if ((b >> lane) & 1ull) s_list[s_base[it][w] + __popcll(b & lanemask_lt())] = (uint16_t)(it * kProjThreads + tid);
             }
             nitems = s_total;
-            __syncthreads();
-        } else {
-            __syncthreads();
         }
-        auto item = [&](uint32_t q) { return p0 + (TWO_PHASE ? (uint32_t)s_list[q] : q); };
-        const uint32_t rounds = (nitems + kProjThreads - 1) / kProjThreads;
-        for (uint32_t r = 0; r < (uint32_t)kSortIPT; ++r) {
-            bool keep = false;
-            const uint32_t q = r * kProjThreads + tid;
-            if (r < rounds && q < nitems) {
-                const uint32_t key = project_one(p, item(q), row_lo, row_hi, my_vis, my_k, !TWO_PHASE);
-                keep = key < p.thresh;  // kSentinel >= any threshold
-                if (keep) atomicAdd(&s_hist[key & 255u], 1u);
-            }
-            const uint64_t b = __ballot(keep);
-            if (lane == 0) s_mask[r][w] = b;
-        }
-        prefix();
-        for (uint32_t r = 0; r < rounds; ++r) {
-            const uint64_t b = s_mask[r][w];
-            if ((b >> lane) & 1ull) {
-                const uint32_t i = item(r * kProjThreads + tid);
-                const uint32_t pos = p0 + s_base[r][w] + __popcll(b & lanemask_lt());
-                p.c_keys[pos] = p.keys_out[i];  // this thread's own stores above
-                p.c_vals[pos] = i;
-                p.c_rect[pos] = p.rect_out[i];
-            }
-        }
-        p.offsets[(uint64_t)part * 256 + tid] = s_hist[tid];  // partition-major, as the upsweep
-        if (s_hist[tid]) {
-            atomicAdd(&p.gsum[(part / kGroupParts) * 256 + tid], s_hist[tid]);
-            atomicAdd(&p.hist0[(part % kHistShards) * 256 + tid], s_hist[tid]);
-        }
-        if (tid == 0) p.c_count[part] = s_total;
         __syncthreads();
+        const uint32_t rounds = (nitems + kProjThreads - 1) / kProjThreads;
+        for (uint32_t r = 0; r < rounds; ++r) {  // block-uniform
+            const uint32_t q = r * kProjThreads + tid;
+            Proj o;
+            bool c0 = false;
+            uint32_t i = 0;
+            if (q < nitems) {
+                i = p0 + (TWO_PHASE ? (uint32_t)s_list[q] : q);
+                if (project_core(p, i, row_lo, row_hi, !TWO_PHASE, o)) {
+                    ++my_vis;
+                    my_k += o.ntiles;
+                    my_kmin_inv = max(my_kmin_inv, ~o.key);
+                    my_kmax = max(my_kmax, o.key);
+                    c0 = o.key < p.thresh;
+                }
+                p.keys_out[i] = o.key;
+                p.rect_out[i] = o.prect;
+            }
+            const uint64_t b = __ballot(c0);
+            if (b) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&s_cnt, (uint32_t)__popcll(b));
+                base = __shfl(base, 0, 64);
+                if (c0) store_slot(p, slot_c0(part, base + (uint32_t)__popcll(b & lanemask_lt())), i, o);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            p.c0[part] = s_cnt;
+            p.c1[part] = 0;
+            if (s_cnt) atomicAdd(&p.ctl->n_chunk[0], s_cnt);
+        }
     }
     if (my_vis) {
         atomicAdd(&s_vis, my_vis);
         atomicAdd(&s_k, my_k);
+        atomicMax(&s_kmin_inv, my_kmin_inv);
+        atomicMax(&s_kmax, my_kmax);
     }
     __syncthreads();
     if (tid == 0 && s_vis) {
         atomicAdd(&p.ctl->n_vis, s_vis);
         atomicAdd(&p.ctl->k_total, s_k);
+        atomicMax(&p.ctl->key_min_inv, s_kmin_inv);
+        atomicMax(&p.ctl->key_max, s_kmax);
     }
 }
 
-// Colours of the chunk-0 splats (k_project's compacted list per partition, in index order), one
-// thread per splat: their shading blocks are read in index order, not in depth order.
+// Colours of the chunk-0 slots, one thread per slot, partition by partition (the shading blocks
+// of a partition's splats are read in roughly index order): the SH colour and the depth key
+// (the composite's saturation statistic) into the record's third quad.
 __global__ __launch_bounds__(256) void k_colour(ProjParams p) {
     const uint32_t parts = sort_parts(p.n);
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        const uint32_t cnt = p.c_count[part], p0 = part * kSortTile;
-        for (uint32_t q = threadIdx.x; q < cnt; q += 256) store_colour(p, p.c_vals[p0 + q]);
+        const uint32_t cnt = p.c0[part];
+        for (uint32_t q = threadIdx.x; q < cnt; q += 256) {
+            const uint32_t slot = slot_c0(part, q);
+            const uint2 k = p.skey[slot];
+            float4 c = sh_colour(p.rec.r01 + (uint64_t)k.y * p.rec.stride, p.rec.off, p.cam);
+            c.w = __uint_as_float(k.x);
+            p.crec[3 * (uint64_t)slot + 2] = c;
+        }
     }
 }
 
@@ -831,11 +856,6 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(SortPass p) {
 // Launches per chunk, no inter-workgroup waiting: per-partition entry counts, one scan, the
 // emission in depth order, then the row-wise emission of wide splats.  Entry positions come from
 // the scan alone, so whichever kernel writes an entry, every tile's list stays in depth order.
-__device__ __forceinline__ void chunk_range(const BinParams& p, uint32_t& r0, uint32_t& r1) {
-    r0 = 0;
-    r1 = p.ctl->n_chunk[p.chunk];
-}
-
 struct TileRect {
     uint32_t x0, y0, x1, y1;  // inclusive, absolute tile coordinates
 };
@@ -949,25 +969,60 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
     return true;
 }
 
-// The chunk's composite records start at slot base: chunk 0 at 0, chunk 1 after chunk 0.
-__device__ __forceinline__ uint32_t slot_base(const BinParams& p) {
-    return p.chunk ? p.ctl->n_chunk[0] : 0u;
-}
-
-// ---- binning into per-tile lists, a two-level counting sort without global atomics.  The
-// chunk's ranks are cut into kBinParts partitions; the tiles into bands of <= kBandTiles.
-//   k_bin_count    workgroup (partition p, band): LDS counters of its splats' entries per tile
-//                  (ellipse rows; chunk 1: unsaturated tiles only) -> bmat[p][t]
+// ---- binning into per-tile lists, a two-level counting sort without global atomics.  Binning
+// partition b (of kBinParts) takes the chunk's slots of projection partitions b, b + kBinParts,
+// ... (interleaved: balanced whatever the scene order); the tiles are cut into bands of
+// <= kBandTiles.
+//   k_bin_count    workgroup (partition b, band): LDS counters of its splats' entries per tile
+//                  (ellipse rows; chunk 1: unsaturated tiles only) -> bmat[b][t]
 //   k_bin_colscan  per tile: exclusive prefix of bmat[.][t] over the partitions, tile totals
 //   k_tile_scan    one workgroup: exclusive scan of the totals in tile order -> ranges, tbase
-//   k_bin_emit     workgroup (p, band): LDS cursors tbase[t] + bmat[p][t]; each entry takes a
-//                  slot with an LDS atomic (lists are unordered inside a tile: k_tile_sort)
+//   k_bin_emit     workgroup (b, band): LDS cursors tbase[t] + bmat[b][t]; each entry takes a
+//                  position with an LDS atomic (lists are unordered inside a tile: k_tile_sort)
 // Count and emission walk the same ellipse rows, so a tile's count and its entries agree.
-__device__ __forceinline__ void bin_partition(const BinParams& p, uint32_t part, uint32_t& r0, uint32_t& r1) {
-    const uint32_t n = p.ctl->n_chunk[p.chunk];
-    const uint32_t per = (n + kBinParts - 1) / kBinParts;
-    r0 = min(n, part * per);
-    r1 = min(n, r0 + per);
+constexpr uint32_t kBinMaxPP = 4096;  // projection partitions per binning partition (2^32 / 4096 / 256)
+
+// The slots of binning partition b: s_pref[k] = splats of its first k projection partitions
+// (b + j kBinParts, j < k); returns the total.  Contains barriers.
+__device__ uint32_t bin_slots(const BinParams& p, uint32_t b, uint32_t* s_pref, uint32_t* s_tmp) {
+    const uint32_t m = p.parts > b ? (p.parts - b + kBinParts - 1) / kBinParts : 0u;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    constexpr int per = kBinMaxPP / kBinThreads;
+    uint32_t c[per], sum = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        const uint32_t j = (uint32_t)tid * per + k;
+        c[k] = j < m ? p.cnt[b + j * kBinParts] : 0u;
+        sum += c[k];
+    }
+    const uint32_t incl = wave_incl_scan(sum);
+    if (lane == 63) s_tmp[w] = incl;
+    __syncthreads();
+    uint32_t base = incl - sum, total = 0;
+    for (int i = 0; i < kBinThreads / 64; ++i) {
+        if (i < w) base += s_tmp[i];
+        total += s_tmp[i];
+    }
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        const uint32_t j = (uint32_t)tid * per + k;
+        if (j <= m) s_pref[j] = base;
+        base += c[k];
+    }
+    __syncthreads();
+    return total;
+}
+
+// The r-th slot of binning partition b (r < total of bin_slots).
+__device__ __forceinline__ uint32_t bin_slot(const BinParams& p, uint32_t b, const uint32_t* s_pref, uint32_t r) {
+    const uint32_t m = p.parts > b ? (p.parts - b + kBinParts - 1) / kBinParts : 0u;
+    uint32_t lo = 0, hi = m;  // largest k < m with s_pref[k] <= r
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_pref[mid] <= r) lo = mid; else hi = mid;
+    }
+    const uint32_t part = b + lo * kBinParts, q = r - s_pref[lo];
+    return p.chunk ? slot_c1(part, q) : slot_c0(part, q);
 }
 
 // Entries of one splat (composite slot g) in tiles [t_lo, t_hi): f(tile) per entry.  Rows whose
@@ -994,20 +1049,18 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
 
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     __shared__ uint32_t s_cnt[kBandTiles];
-    // the chunk's depth passes are done: reset their group sums for the next use
-    for (uint32_t q = blockIdx.x * kBinThreads + threadIdx.x; q < p.gsum_zero_quads; q += gridDim.x * kBinThreads)
-        p.gsum_zero[q] = make_uint4(0u, 0u, 0u, 0u);
+    __shared__ uint32_t s_pref[kBinMaxPP + 1];
+    __shared__ uint32_t s_tmp[kBinThreads / 64];
+    if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
     const uint32_t part = blockIdx.x % kBinParts, band = blockIdx.x / kBinParts;
     const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
     for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += kBinThreads) s_cnt[t] = 0;
-    __syncthreads();
-    uint32_t r0, r1;
-    bin_partition(p, part, r0, r1);
-    const uint32_t g0 = slot_base(p);
-    for (uint32_t r = r0 + threadIdx.x; r < r1; r += kBinThreads) {
+    const uint32_t total = bin_slots(p, part, s_pref, s_tmp);
+    for (uint32_t r = threadIdx.x; r < total; r += kBinThreads) {
+        const uint32_t g = bin_slot(p, part, s_pref, r);
         TileRect tr;
-        if (!rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) continue;
-        const float4* q = p.crec + 3 * (uint64_t)(g0 + r);
+        if (!rect_unpack(p, p.srect[g], p.skey[g].y, tr)) continue;
+        const float4* q = p.crec + 3 * (uint64_t)g;
         splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
     }
     __syncthreads();
@@ -1029,6 +1082,7 @@ __device__ __forceinline__ uint32_t colscan_part(uint32_t q) {  // q-th partitio
 
 __global__ __launch_bounds__(256) void k_bin_colscan(BinParams p) {
     __shared__ uint32_t s_sum[4][kColTiles];
+    if (p.chunk == 1 && p.ctl->not_done == 0) return;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t = blockIdx.x * kColTiles + lane;
     const bool ok = t < p.n_tiles;
@@ -1057,7 +1111,7 @@ constexpr int kScanThreads = 1024;
 
 __global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
     __shared__ uint32_t s_w[kScanThreads / 64];
-    __shared__ uint32_t s_carry;
+    if (p.chunk == 1 && p.ctl->not_done == 0) return;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     constexpr int nw = kScanThreads / 64;
     constexpr int ipt = 8;
@@ -1092,16 +1146,9 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
         carry += total;
         __syncthreads();
     }
-    (void)s_carry;
-    const uint32_t n = p.ctl->n_chunk[p.chunk];
     if (tid == 0) {
         p.ctl->k_chunk[p.chunk] = min(carry, cap);
-        p.ctl->shade_n[p.chunk] = n;  // every depth rank has a composite slot
         if (carry > cap) atomicOr(&p.ctl->err, kErrOverflow);
-    }
-    if (p.chunk == 0 && tid < 8 && n > 0) {  // quantile keys (fixed-fraction chunking)
-        const uint32_t q = (n + (1u << tid) - 1) >> tid;
-        p.ctl->quant_key[tid] = p.sorted_keys[q - 1];
     }
 }
 
@@ -1112,26 +1159,26 @@ constexpr uint32_t kWideQueue = 512;
 
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_cur[kBandTiles];
+    __shared__ uint32_t s_pref[kBinMaxPP + 1];
+    __shared__ uint32_t s_tmp[kBinThreads / 64];
     __shared__ uint32_t s_wide[kWideQueue];
     __shared__ uint32_t s_nw;
+    if (p.chunk == 1 && p.ctl->not_done == 0) return;
     const uint32_t part = blockIdx.x % kBinParts, band = blockIdx.x / kBinParts;
     const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
     const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += kBinThreads) s_cur[t - t_lo] = p.tbase[t] + row[t];
     if (threadIdx.x == 0) s_nw = 0;
-    __syncthreads();
-    uint32_t r0, r1;
-    bin_partition(p, part, r0, r1);
-    const uint32_t g0 = slot_base(p);
+    const uint32_t total = bin_slots(p, part, s_pref, s_tmp);
     const uint32_t cap = p.capacity;
-    for (uint32_t r = r0 + threadIdx.x; r < r1; r += kBinThreads) {
+    for (uint32_t r = threadIdx.x; r < total; r += kBinThreads) {
+        const uint32_t g = bin_slot(p, part, s_pref, r);
         TileRect tr;
-        if (!rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr)) continue;
-        const uint32_t g = g0 + r;
+        if (!rect_unpack(p, p.srect[g], p.skey[g].y, tr)) continue;
         if (rect_wide(tr)) {
             const uint32_t qi = atomicAdd(&s_nw, 1u);
             if (qi < kWideQueue) {
-                s_wide[qi] = r;
+                s_wide[qi] = g;
                 continue;
             }
         }
@@ -1147,9 +1194,9 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
     for (uint32_t qi = wave; qi < nq; qi += kBinThreads / 64) {  // wave-uniform
-        const uint32_t r = s_wide[qi], g = g0 + r;
+        const uint32_t g = s_wide[qi];
         TileRect tr;
-        rect_unpack(p, p.sorted_rect[r], p.sorted_vals[r], tr);
+        rect_unpack(p, p.srect[g], p.skey[g].y, tr);
         const float4* q = p.crec + 3 * (uint64_t)g;
         const Ellipse e = ellipse_of(q[0], q[1]);
         const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
@@ -1169,91 +1216,25 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     }
 }
 
-// Composite records of this chunk's depth ranks (slot g = base + rank): the projected record
-// quads r01 and the colour of each rank's Gaussian, written densely in rank order.  A wave takes
-// 64 ranks at once (one coalesced load of their Gaussian indices).
-//   COLOUR (one-phase frames): one thread per rank gathers the Gaussian's shading block with the
-//     record in its padding and evaluates the colour (sh_colour): one 240-B gather per splat.
-//   else (row strips): k_colour stored the colour after the record quads in index order; 4 lanes
-//     per rank copy the 48 B, 4 groups of 16 ranks' gathers in flight.
-// Runs before the binning, which reads the records to bin each splat's ellipse exactly.
-template <bool COLOUR>
-__global__ __launch_bounds__(256) void k_shade(BinParams p) {
-    uint32_t r0, r1;
-    chunk_range(p, r0, r1);
-    const uint32_t g0 = slot_base(p);
-    const uint32_t n = r1 - r0;
-    const uint32_t lane = lane_id(), qd = lane & 3;
-    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
-    const uint32_t nq = p.rec.off;
-    for (uint32_t base = wave * 64; base < n; base += nwaves * 64) {  // wave-uniform: shuffles below
-        const bool mine = base + lane < n;
-        const uint32_t jl = mine ? p.sorted_vals[r0 + base + lane] : 0u;
-        if (mine) p.shade_list[g0 + base + lane] = jl;
-        float4* o = p.crec + 3 * (uint64_t)(g0 + base);
-        if (COLOUR) {
-            if (mine) {
-                const float4* blk = p.rec.r01 + (uint64_t)jl * p.rec.stride;
-                const float4 a = blk[nq], b = blk[nq + 1];
-                const float4 c = sh_colour(blk, nq, p.cam);
-                o[3 * lane] = a;
-                o[3 * lane + 1] = b;
-                o[3 * lane + 2] = c;
-            }
-        } else {
-            const uint32_t cnt = min(64u, n - base);
-            const float4* __restrict__ rec = p.rec.r01 + nq;
-            float4 q[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t k = 16 * u + (lane >> 2);  // rank within the 64
-                const uint32_t j = __shfl(jl, k & 63, 64);
-                q[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                if (k < cnt && qd < 3) q[u] = rec[(uint64_t)j * p.rec.stride + qd];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t k = 16 * u + (lane >> 2);
-                if (k < cnt && qd < 3) o[3 * k + qd] = q[u];
-            }
-        }
-    }
-}
-
-// End of a chunk (the frame's last, or chunk 0 when the host decides on chunk 1): the frame
-// statistics (depth key of the farthest splat a tile saturated at), then FrameCtl stored into the
-// host's pinned slot (mapped, fine-grained) and the sequence number published with a system-scope
-// release; the host spins on it instead of a copy + event.  Then, when the frame ends here
-// (zero_mode 2, or 1 and chunk 0 left no tile unsaturated), the frame's meta block (FrameCtl and
-// histograms) is zeroed for the next frame.
-__global__ __launch_bounds__(256) void k_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec,
-                                                  FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq,
-                                                  uint4* meta, uint32_t meta_quads, int zero_mode) {
-    __shared__ uint32_t s_slot, s_key, s_not_done;
-    const int tid = threadIdx.x;
-    if (tid == 0) {
-        uint32_t slot = 0, tiles = 0;
-        for (int k = 0; k < kHistShards; ++k) {
-            slot = max(slot, ctl->sat_slot[k]);
-            tiles += ctl->sat_tiles[k];
-        }
-        s_slot = slot;
-        s_key = tiles ? __float_as_uint(rec.r2[shade_list[slot]].x) : 0u;
-        s_not_done = ctl->not_done;
-        ctl->sat_slot_max = s_slot;
-        ctl->sat_key = s_key;
-    }
-    __syncthreads();
+// End of a frame: the saturation statistic (depth key of the farthest splat a tile saturated
+// at), then FrameCtl stored into the host's pinned slot (mapped, fine-grained) and the sequence
+// number published with a system-scope release; the host reads it a frame or two later.  Then
+// FrameCtl is zeroed for the next frame.
+__global__ __launch_bounds__(64) void k_frame_end(FrameCtl* ctl, FrameCtl* host_ctl, uint32_t* host_seq,
+                                                 uint32_t seq) {
     constexpr uint32_t kWords = sizeof(FrameCtl) / 4;
-    constexpr uint32_t kSlotW = offsetof(FrameCtl, sat_slot_max) / 4, kKeyW = offsetof(FrameCtl, sat_key) / 4;
-    const uint32_t* src = (const uint32_t*)ctl;
-    uint32_t* dst = (uint32_t*)host_ctl;
-    for (uint32_t w = tid; w < kWords; w += 256) dst[w] = w == kSlotW ? s_slot : w == kKeyW ? s_key : src[w];
+    static_assert(kWords <= 64, "FrameCtl is copied by one wave");
+    constexpr uint32_t kKeyW = offsetof(FrameCtl, sat_key) / 4;
+    const uint32_t lane = threadIdx.x;
+    uint32_t key = 0;
+    for (int k = 0; k < kHistShards; ++k) key = max(key, ctl->sat_key_shard[k]);
+    uint32_t* src = (uint32_t*)ctl;
+    const uint32_t v = lane < kWords ? (lane == kKeyW ? key : src[lane]) : 0u;
+    if (lane < kWords) ((uint32_t*)host_ctl)[lane] = v;
     __threadfence_system();
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (zero_mode == 2 || (zero_mode == 1 && s_not_done == 0))
-        for (uint32_t i = tid; i < meta_quads; i += 256) meta[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane < kWords) src[lane] = 0u;
 }
 
 // Summed-area table and bitmask of the tiles chunk 0 left unsaturated (done == 0): one
@@ -1577,7 +1558,7 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     __shared__ float4 sR[2][kCompBatch][3];
     __shared__ uint8_t sL[2][2][kCompBatch];   // per half: batch indices, segment = producing wave
     __shared__ uint32_t sN[2][2][2];           // per half, per producing wave: list length
-    __shared__ uint32_t s_sat;                 // slot that saturated the last wave
+    __shared__ uint32_t s_sat;                 // depth key of the splat that saturated the last wave
     const int tid = threadIdx.x;
     // XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch), so XCD b % 8 gets
     // the contiguous band of tiles [(b % 8) * per, (b % 8 + 1) * per): a splat's neighbouring
@@ -1718,7 +1699,7 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
                     blend(i3, cur);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][i3][1].w));
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][i3][2].w));
                         break;
                     }
                 }
@@ -1727,7 +1708,7 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
                     blend(ik, cur);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][ik][1].w));
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][ik][2].w));
                     }
                 }
             }
@@ -1738,7 +1719,7 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     const bool tile_done = __syncthreads_count(live0 || live1) == 0;
     if (tile_done && tid == 0 && n > 0) {  // saturation statistics for the chunk controller
         atomicAdd(&p.ctl->sat_tiles[tile % kHistShards], 1u);
-        atomicMax(&p.ctl->sat_slot[tile % kHistShards], s_sat);
+        atomicMax(&p.ctl->sat_key_shard[tile % kHistShards], s_sat);
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {  // park the pixels for chunk 1
@@ -1893,7 +1874,7 @@ __global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
                     blend(i3, cur);
                     if (!__any(live)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][i3][1].w));
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][i3][2].w));
                         break;
                     }
                 }
@@ -1902,7 +1883,7 @@ __global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
                     blend(ik, cur);
                     if (!__any(live)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][ik][1].w));
+                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][ik][2].w));
                     }
                 }
             }
@@ -1913,7 +1894,7 @@ __global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
     const bool tile_done = __syncthreads_count(live) == 0;
     if (tile_done && tid == 0 && n > 0) {
         atomicAdd(&p.ctl->sat_tiles[tile % kHistShards], 1u);
-        atomicMax(&p.ctl->sat_slot[tile % kHistShards], s_sat);
+        atomicMax(&p.ctl->sat_key_shard[tile % kHistShards], s_sat);
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {
@@ -1993,11 +1974,13 @@ void launch_project(const ProjParams& p, bool two_phase, hipStream_t s) {
         const unsigned cgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (p.n + 255) / 256));
         hipLaunchKernelGGL(k_cull, dim3(cgrid), dim3(256), 0, s, p);
         hipLaunchKernelGGL(k_project<true>, dim3(grid), dim3(kProjThreads), 0, s, p);
-    }
-    else
+    } else {
         hipLaunchKernelGGL(k_project<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
-    if (two_phase)  // else k_shade<true> evaluates the colours
-        hipLaunchKernelGGL(k_colour, dim3(grid), dim3(256), 0, s, p);
+    }
+}
+void launch_colour(const ProjParams& p, hipStream_t s) {
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, sort_parts(p.n)));
+    hipLaunchKernelGGL(k_colour, dim3(grid), dim3(256), 0, s, p);
 }
 void launch_records(const ProjParams& p, hipStream_t s) {
     if (!p.n) return;
@@ -2036,17 +2019,8 @@ void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
     hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(kTsThreads), 0, s, p);
 }
-void launch_shade(const BinParams& p, bool colour, hipStream_t s) {
-    if (colour)
-        hipLaunchKernelGGL(k_shade<true>, dim3(kMaxGrid), dim3(256), 0, s, p);
-    else
-        hipLaunchKernelGGL(k_shade<false>, dim3(kMaxGrid), dim3(256), 0, s, p);
-}
-void launch_frame_end(FrameCtl* ctl, const uint32_t* shade_list, Records rec, FrameCtl* host_ctl,
-                      uint32_t* host_seq, uint32_t seq, uint4* meta, uint32_t meta_quads, int zero_mode,
-                      hipStream_t s) {
-    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(256), 0, s, ctl, shade_list, rec, host_ctl, host_seq, seq,
-                       meta, meta_quads, zero_mode);
+void launch_frame_end(FrameCtl* ctl, FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, ctl, host_ctl, host_seq, seq);
 }
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s) {
