@@ -140,16 +140,15 @@ struct gs_scene {
     float4* shade = nullptr;            // shading blocks (shade_stride float4 per Gaussian)
     float4* cull = nullptr;             // cull planes (two-phase projection)
     float4* r2 = nullptr;
-    // k_project output: depth key, packed tile rect per Gaussian
-    uint32_t *keysP = nullptr, *rectP = nullptr;
     // composite slots (slot_c0 / slot_c1): records (3 float4), (depth key, index), packed rect
     float4* crec = nullptr;
     uint2* skey = nullptr;
     uint32_t* srect = nullptr;
     uint32_t *c0 = nullptr, *c1 = nullptr;  // [parts]: slots per projection partition and chunk
-    unsigned long long* keep_mask = nullptr;  // two-phase frames: k_cull's keep bits
+    unsigned long long* cand_mask = nullptr;  // chunk-0 candidates (k_cull), bit i % 64 of word i / 64
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     FrameCtl* ctl = nullptr;            // zero at a frame's start (k_frame_end clears it)
+    StatShard* stats = nullptr;         // [kStatShards], zero at a frame's start (likewise)
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tvA = nullptr, *tvB = nullptr;  // tile lists: unordered (binning), sorted
@@ -401,12 +400,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
 
     // FrameCtl is zero at a frame's start: k_frame_end of the last frame cleared it, unless that
     // frame never ended (first frame, an error mid-frame)
-    if (!s->meta_clean) HIPCHK(hipMemsetAsync(s->ctl, 0, sizeof(FrameCtl), st));
+    if (!s->meta_clean) {
+        HIPCHK(hipMemsetAsync(s->ctl, 0, sizeof(FrameCtl), st));
+        HIPCHK(hipMemsetAsync(s->stats, 0, kStatShards * sizeof(StatShard), st));
+    }
     s->meta_clean = false;
     ProjParams pp{};
     pp.geo = s->geo;
     pp.cull = s->cull;
-    pp.keep_mask = s->keep_mask;
     pp.n = n_tiles > 0 ? (uint32_t)s->n : 0u;
     std::memcpy(pp.V, uni + 0, 64);
     mat4_mul_ref(uni + 16, uni + 0, pp.PV);
@@ -429,21 +430,18 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.tile_row_begin = tr_begin;
     pp.tile_row_end = tr_end;
     pp.tiles_x = TX;
-    pp.keys_out = s->keysP;
-    pp.rect_out = s->rectP;
     pp.rec = records(s);
     pp.ctl = s->ctl;
+    pp.stats = s->stats;
     pp.thresh = T;
     pp.crec = s->crec;
     pp.skey = s->skey;
     pp.srect = s->srect;
     pp.c0 = s->c0;
     pp.c1 = s->c1;
+    pp.cand_mask = s->cand_mask;
     mark(EV_PROJ0);
-    // two-phase projection (cull planes first) when most Gaussians are outside this frame's
-    // rows: row strips, or a previous frame that saw under half of the scene
-    const bool two_phase = sc > 1 || (s->have_last && s->last.n_vis * 2 < s->n);
-    launch_project(pp, two_phase, st);
+    launch_project(pp, st);
     launch_colour(pp, st);
     mark(EV_PROJ1);
 
@@ -519,7 +517,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     {  // statistics into the slot, FrameCtl zeroed for the next frame
         const uint32_t q = s->seq_next++;
         s->stat_want[slot] = q;
-        launch_frame_end(s->ctl, s->d_ctl_slot + slot, s->d_seq + slot, q, st);
+        launch_frame_end(s->ctl, s->stats, s->d_ctl_slot + slot, s->d_seq + slot, q, st);
     }
     s->meta_clean = true;
     mark(EV_END);
@@ -658,17 +656,17 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->geo, 3 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->shade, (size_t)shade_stride(n_sh) * std::max<uint64_t>(n, 1));
             dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
-            dev_alloc(s->keep_mask, (size_t)(n / 64 + 1));
             dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
-            dev_alloc(s->keysP, n); dev_alloc(s->rectP, n);
             dev_alloc(s->crec, 3 * ((size_t)sort_parts(n) * kSortTile + 1));
             dev_alloc(s->ctl, 1);
+            dev_alloc(s->stats, kStatShards);
             // slots: part * kSortTile + q < sort_parts(n) * kSortTile
             const size_t nslots = (size_t)sort_parts(n) * kSortTile + 1;
             dev_alloc(s->skey, nslots);
             dev_alloc(s->srect, nslots);
             dev_alloc(s->c0, (size_t)sort_parts(n) + 1);
             dev_alloc(s->c1, (size_t)sort_parts(n) + 1);
+            dev_alloc(s->cand_mask, (size_t)sort_parts(n) * (kSortTile / 64) + 1);
             const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hf));
             HIPCHK(hipHostMalloc((void**)&s->h_seq, 64, hf));
@@ -713,15 +711,15 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->geo);
     dev_free(s->shade);
     dev_free(s->cull);
-    dev_free(s->keep_mask);
     dev_free(s->r2);
-    dev_free(s->keysP); dev_free(s->rectP);
     dev_free(s->crec);
     dev_free(s->ctl);
+    dev_free(s->stats);
     dev_free(s->skey);
     dev_free(s->srect);
     dev_free(s->c0);
     dev_free(s->c1);
+    dev_free(s->cand_mask);
     dev_free(s->tvA); dev_free(s->tvB);
     dev_free(s->ranges);
     dev_free(s->bmat);

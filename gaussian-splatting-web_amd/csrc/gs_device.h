@@ -53,6 +53,17 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t sat_tiles[kHistShards];      // per shard: tiles saturated by the end of the frame
 };
 
+// Per-frame counters that many workgroups add to, sharded so that no address takes more than a
+// few hundred device-scope atomics (one address serialises them at ~11 ns each): workgroup b adds
+// to shard b % kStatShards; k_frame_end sums the shards into FrameCtl and zeroes them.
+constexpr int kStatShards = 64;
+struct StatShard {
+    unsigned long long k_total;
+    uint32_t n_vis, key_min_inv, key_max;
+    uint32_t n_chunk[2];
+    uint32_t pad;
+};
+
 // Composite slots.  k_project gives the chunk-0 splats of projection partition `part` (kSortTile
 // Gaussians) the slots part * kSortTile + q, q < c0[part] (in arrival order); k_records gives the
 // chunk-1 splats of that partition part * kSortTile + kSortTile - 1 - q, q < c1[part].  A
@@ -109,19 +120,17 @@ struct ProjParams {
                               // (x 1.0001): the conservative cull bound's camera factor
     int W, H;
     int tile_row_begin, tile_row_end, tiles_x;
-    uint32_t* keys_out;       // [n]: depth key or kSentinel
-    uint32_t* rect_out;       // [n]: packed tile rectangle
     Records rec;              // out: r2 of every visible Gaussian (k_records: r01 too)
     FrameCtl* ctl;
+    StatShard* stats;         // [kStatShards] (n_vis, k_total, key range, n_chunk)
     uint32_t thresh;          // chunk-0 threshold key: chunk 0 = visible splats with key < thresh
     // composite slots (see slot_c0): records, sort keys, rects, per-partition counts
     float4* crec;
     uint2* skey;
     uint32_t* srect;
     uint32_t* c0;             // [parts] chunk-0 splats per projection partition (k_project)
-    uint32_t* c1;             // [parts] chunk-1 splats per projection partition (k_records; zeroed by k_project)
-    // two-phase frames: k_cull's keep bit per Gaussian (bit i%64 of word i/64)
-    unsigned long long* keep_mask;
+    uint32_t* c1;             // [parts] chunk-1 splats per projection partition (k_records; zeroed by k_cull)
+    unsigned long long* cand_mask;  // [n / 64] chunk-0 candidates (k_cull)
     // k_records: unsaturated-tile SAT of chunk 0 (k_sat); rec_all = every visible (debug)
     const uint32_t* sat;
     int rec_all;
@@ -220,13 +229,14 @@ struct CompositeParams {
 // launchers (gs_kernels.hip)
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, float4* shade, float4* cull,
                       hipStream_t s);
-void launch_project(const ProjParams& p, bool two_phase, hipStream_t s);
+void launch_project(const ProjParams& p, hipStream_t s);
 void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 slots (or, rec_all, every record)
 void launch_colour(const ProjParams& p, hipStream_t s);   // colours of the chunk-0 slots
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit, wide rows
 // stats -> host slot + seq; then FrameCtl zeroed for the next frame
-void launch_frame_end(FrameCtl* ctl, FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq, hipStream_t s);
+void launch_frame_end(FrameCtl* ctl, StatShard* stats, FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq,
+                      hipStream_t s);
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s);
 void launch_tile_sort(const TileSortParams& p, hipStream_t s);

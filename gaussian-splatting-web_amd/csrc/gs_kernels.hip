@@ -209,10 +209,10 @@ __device__ __forceinline__ bool pixel_rect(float cx, float cy, float hx, float h
 
 // The same conservative cull from the Gaussian's cull plane (x, y, z, ||R(q) diag(s)||_F^2),
 // written at upload: false = provably invisible in this strip.
-__device__ __forceinline__ bool cull_keep(const ProjParams& p, float4 c, int row_lo, int row_hi) {
+__device__ __forceinline__ bool cull_keep(const ProjParams& p, float4 c, int row_lo, int row_hi, float& vz0) {
 #pragma clang fp contract(off)
     const float x = c.x, y = c.y, z = c.z;
-    const float vz0 = ((p.V[2] * x + p.V[6] * y) + p.V[10] * z) + p.V[14] * 1.0f;
+    vz0 = ((p.V[2] * x + p.V[6] * y) + p.V[10] * z) + p.V[14] * 1.0f;  // = project_footprint's vz
     const float cw = ((p.PV[3] * x + p.PV[7] * y) + p.PV[11] * z) + p.PV[15] * 1.0f;
     const float cz = ((p.PV[2] * x + p.PV[6] * y) + p.PV[10] * z) + p.PV[14] * 1.0f;
     if (!((cw > 0.0f) && (cz >= 0.0f) && (cz <= cw))) return false;  // :230 + near/far (exact)
@@ -406,9 +406,10 @@ __device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, u
 }
 
 // Chunk 1 (after chunk 0 left tiles unsaturated), or every visible Gaussian's per-Gaussian
-// record (rec_all, debug): visible Gaussians with key >= thresh whose rect touches an unsaturated
-// tile (the SAT of k_sat) get a chunk-1 slot (slot_c1) with their record and colour.  Waves
-// cover 64 consecutive Gaussians of one projection partition: one counter add per wave.
+// record (rec_all, debug): from the cull plane, Gaussians at or past thresh that may be visible
+// are projected; the visible ones whose rect touches an unsaturated tile (the SAT of k_sat) get a
+// chunk-1 slot (slot_c1) with their record and colour.  Waves cover 64 consecutive Gaussians of
+// one projection partition: one counter add per wave.
 __global__ __launch_bounds__(256) void k_records(ProjParams p) {
     if (!p.rec_all && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
     const int row_lo = p.tile_row_begin * kTile;
@@ -418,23 +419,21 @@ __global__ __launch_bounds__(256) void k_records(ProjParams p) {
     for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < p.n; i0 += gridDim.x * blockDim.x) {
         const uint32_t i = i0 + lane;
         bool want = false;
-        const uint32_t key = i < p.n ? p.keys_out[i] : kSentinel;
-        if (key != kSentinel) {
-            want = true;
-            if (!p.rec_all) {
-                const uint32_t pr = p.rect_out[i];
-                want = key >= p.thresh && pr != kRectEmpty;
-                if (want && pr != kRectLarge) {
-                    const uint32_t x0 = pr & 0xfffu, y0 = (pr >> 12) & 0xfffu;
-                    const uint32_t x1 = x0 + ((pr >> 24) & 15u), y1 = y0 + (pr >> 28);
-                    const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
-                    const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
-                    want = (b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]) != 0u;
-                }
-            }
-        }
+        float vz;
+        if (i < p.n && cull_keep(p, p.cull[i], row_lo, row_hi, vz)) want = p.rec_all || sortable_key(vz) >= p.thresh;
         Proj o;
         want = want && project_core(p, i, row_lo, row_hi, false, o);
+        if (want && !p.rec_all) {
+            const uint32_t pr = o.prect;
+            want = pr != kRectEmpty;
+            if (want && pr != kRectLarge) {
+                const uint32_t x0 = pr & 0xfffu, y0 = (pr >> 12) & 0xfffu;
+                const uint32_t x1 = x0 + ((pr >> 24) & 15u), y1 = y0 + (pr >> 28);
+                const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
+                const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
+                want = (b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]) != 0u;
+            }
+        }
         if (p.rec_all) {
             if (want) {
                 float4* r = rec_r01(p.rec, i);
@@ -449,10 +448,15 @@ __global__ __launch_bounds__(256) void k_records(ProjParams p) {
         const uint64_t b = __ballot(want);
         if (!b) continue;
         uint32_t base = 0;
+        const uint32_t ntiles = want ? o.ntiles : 0u;
+        unsigned long long kt = ntiles;
+        for (int d = 32; d >= 1; d >>= 1) kt += __shfl_xor(kt, d, 64);
         if (lane == 0) {
             const uint32_t c = (uint32_t)__popcll(b);
             base = atomicAdd(&p.c1[i0 / kSortTile], c);
-            atomicAdd(&p.ctl->n_chunk[1], c);
+            StatShard* st = p.stats + (i0 >> 6) % kStatShards;
+            atomicAdd(&st->n_chunk[1], c);
+            atomicAdd(&st->k_total, kt);
         }
         base = __shfl(base, 0, 64);
         if (want) {
@@ -465,103 +469,120 @@ __global__ __launch_bounds__(256) void k_records(ProjParams p) {
     }
 }
 
-// Two-phase frames, first phase: the conservative cull of every Gaussian from its 16-B cull plane,
-// one Gaussian per thread at full occupancy (a streaming read), as a keep bitmask for k_project.
+// Projection, phase A (a chip-wide grid-stride stream, one Gaussian per thread): every Gaussian's
+// 16-B cull plane gives its depth key (vz rounded exactly as project_footprint rounds it) and
+// the conservative cull (cull_keep: exact near/far, a provable bound on the quad box against this
+// frame's rows).  Survivors nearer than thresh are chunk-0 candidates (bit i % 64 of cand_mask
+// word i / 64); survivors at or past thresh are only counted (n_vis is exact when the frame has
+// one chunk) and enter the depth range.
 __global__ __launch_bounds__(256) void k_cull(ProjParams p) {
+    __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
+    if (threadIdx.x == 0) { s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
+    __syncthreads();
+    uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i - lane < p.n; i += gridDim.x * blockDim.x) {
-        const bool keep = i < p.n && cull_keep(p, p.cull[i], row_lo, row_hi);
-        const unsigned long long b = __ballot(keep);
-        if (lane == 0) p.keep_mask[i >> 6] = b;
+        bool cand = false;
+        float vz;
+        if (i < p.n && cull_keep(p, p.cull[i], row_lo, row_hi, vz)) {
+            const uint32_t key = sortable_key(vz);
+            cand = key < p.thresh;
+            if (!cand) {  // past the threshold: counted, not projected
+                ++my_vis;
+                my_kmin_inv = max(my_kmin_inv, ~key);
+                my_kmax = max(my_kmax, key);
+            }
+        }
+        const unsigned long long b = __ballot(cand);
+        if (lane == 0) p.cand_mask[i >> 6] = b;
+    }
+    if (my_vis) {
+        atomicAdd(&s_vis, my_vis);
+        atomicMax(&s_kmin_inv, my_kmin_inv);
+        atomicMax(&s_kmax, my_kmax);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_vis) {
+        StatShard* st = p.stats + blockIdx.x % kStatShards;
+        atomicAdd(&st->n_vis, s_vis);
+        atomicMax(&st->key_min_inv, s_kmin_inv);
+        atomicMax(&st->key_max, s_kmax);
     }
 }
 
-// Per projection partition (kSortTile Gaussians): project every Gaussian (key and packed rect
-// of each; kSentinel when invisible) and give each chunk-0 splat (visible, key < thresh) a
-// composite slot of the partition (slot_c0, arrival order: the per-tile sort orders them) with
-// its records.  Visible count, tile total, the depth-key range and c0 / c1 are published.
-// TWO_PHASE (row strips, mostly off-screen frames): phase A reads k_cull's keep bits and keeps an
-// order-preserving list of the survivors in LDS; phase B projects the survivors densely, so culled
-// Gaussians cost neither their 48 B nor divergent lanes.
-template <bool TWO_PHASE>
-__global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
+// Projection, phase B (one workgroup per projection partition of kSortTile Gaussians): the
+// partition's candidates (cand_mask, listed in LDS in index order) projected densely (their 48-B
+// geometry records gathered); each visible one gets a composite slot of the partition (slot_c0,
+// arrival order: the per-tile sort orders them) with its records.  Publishes the visible count,
+// their tile total, the depth-key range, c0 and c1 (zeroed for k_records).
+__global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     __shared__ unsigned long long s_k;
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
     __shared__ uint32_t s_cnt;
-    __shared__ unsigned long long s_mask[kSortIPT][kProjThreads / 64];
-    __shared__ uint32_t s_base[kSortIPT][kProjThreads / 64];
-    __shared__ uint32_t s_total;
-    __shared__ uint16_t s_list[TWO_PHASE ? kSortTile : 1];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    __shared__ uint32_t s_wbase[kSortTile / 64 + 1];
+    __shared__ uint16_t s_list[kSortTile];
+    const int tid = threadIdx.x, lane = tid & 63;
     if (tid == 0) { s_k = 0; s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
     uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
     unsigned long long my_k = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = sort_parts(p.n);
+    constexpr uint32_t kWords = kSortTile / 64;  // mask words per partition (= 64)
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
         const uint32_t p0 = part * kSortTile;
-        uint32_t nitems = min((uint32_t)kSortTile, p.n - p0);
         if (tid == 0) s_cnt = 0;
-        if (TWO_PHASE) {
-            for (int it = 0; it < kSortIPT; ++it) {
-                const uint32_t i = p0 + it * kProjThreads + tid;
-                // the wave's 64 Gaussians are one mask word (zero bits past n)
-                const uint64_t b = i - lane < p.n ? p.keep_mask[(i - lane) >> 6] : 0ull;
-                if (i < p.n && !((b >> lane) & 1ull)) {
-                    p.keys_out[i] = kSentinel;
-                    p.rect_out[i] = kRectEmpty;
-                }
-                if (lane == 0) s_mask[it][w] = b;
-            }
-            __syncthreads();
-            if (tid < 64) {  // exclusive prefix of the 16 x 4 (round, wave) ballots: index order
-                const uint32_t c = __popcll(s_mask[tid >> 2][tid & 3]);
-                const uint32_t incl = wave_incl_scan(c);
-                s_base[tid >> 2][tid & 3] = incl - c;
-                if (tid == 63) s_total = incl;
-            }
-            __syncthreads();
-            for (int it = 0; it < kSortIPT; ++it) {
-                const uint64_t b = s_mask[it][w];
-                if ((b >> lane) & 1ull) s_list[s_base[it][w] + __popcll(b & lanemask_lt())] = (uint16_t)(it * kProjThreads + tid);
-            }
-            nitems = s_total;
+        // candidate list: word k of the partition's mask holds Gaussians p0 + 64 k + bit
+        unsigned long long mw = 0;
+        if (tid < (int)kWords) {
+            const uint32_t wi = part * kWords + tid;
+            mw = (uint64_t)wi * 64 < p.n ? p.cand_mask[wi] : 0ull;
+            const uint32_t c = (uint32_t)__popcll(mw);
+            const uint32_t incl = wave_incl_scan(c);
+            s_wbase[tid] = incl - c;
+            if (tid == (int)kWords - 1) s_wbase[kWords] = incl;
         }
         __syncthreads();
-        const uint32_t rounds = (nitems + kProjThreads - 1) / kProjThreads;
-        for (uint32_t r = 0; r < rounds; ++r) {  // block-uniform
-            const uint32_t q = r * kProjThreads + tid;
+        if (tid < (int)kWords) {
+            uint32_t o = s_wbase[tid];
+            while (mw) {
+                const int bit = __ffsll((long long)mw) - 1;
+                mw &= mw - 1;
+                s_list[o++] = (uint16_t)(tid * 64 + bit);
+            }
+        }
+        __syncthreads();
+        const uint32_t nitems = s_wbase[kWords];
+        for (uint32_t q0 = 0; q0 < nitems; q0 += kProjThreads) {  // block-uniform
+            const uint32_t q = q0 + tid;
             Proj o;
-            bool c0 = false;
+            bool vis = false;
             uint32_t i = 0;
             if (q < nitems) {
-                i = p0 + (TWO_PHASE ? (uint32_t)s_list[q] : q);
-                if (project_core(p, i, row_lo, row_hi, !TWO_PHASE, o)) {
+                i = p0 + (uint32_t)s_list[q];
+                vis = project_core(p, i, row_lo, row_hi, false, o);
+                if (vis) {
                     ++my_vis;
                     my_k += o.ntiles;
                     my_kmin_inv = max(my_kmin_inv, ~o.key);
                     my_kmax = max(my_kmax, o.key);
-                    c0 = o.key < p.thresh;
                 }
-                p.keys_out[i] = o.key;
-                p.rect_out[i] = o.prect;
             }
-            const uint64_t b = __ballot(c0);
+            const uint64_t b = __ballot(vis);
             if (b) {
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&s_cnt, (uint32_t)__popcll(b));
                 base = __shfl(base, 0, 64);
-                if (c0) store_slot(p, slot_c0(part, base + (uint32_t)__popcll(b & lanemask_lt())), i, o);
+                if (vis) store_slot(p, slot_c0(part, base + (uint32_t)__popcll(b & lanemask_lt())), i, o);
             }
         }
         __syncthreads();
         if (tid == 0) {
             p.c0[part] = s_cnt;
             p.c1[part] = 0;
-            if (s_cnt) atomicAdd(&p.ctl->n_chunk[0], s_cnt);
+            if (s_cnt) atomicAdd(&p.stats[blockIdx.x % kStatShards].n_chunk[0], s_cnt);
         }
     }
     if (my_vis) {
@@ -572,10 +593,11 @@ __global__ __launch_bounds__(kProjThreads, 6) void k_project(ProjParams p) {
     }
     __syncthreads();
     if (tid == 0 && s_vis) {
-        atomicAdd(&p.ctl->n_vis, s_vis);
-        atomicAdd(&p.ctl->k_total, s_k);
-        atomicMax(&p.ctl->key_min_inv, s_kmin_inv);
-        atomicMax(&p.ctl->key_max, s_kmax);
+        StatShard* st = p.stats + blockIdx.x % kStatShards;
+        atomicAdd(&st->n_vis, s_vis);
+        atomicAdd(&st->k_total, s_k);
+        atomicMax(&st->key_min_inv, s_kmin_inv);
+        atomicMax(&st->key_max, s_kmax);
     }
 }
 
@@ -1216,20 +1238,43 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     }
 }
 
-// End of a frame: the saturation statistic (depth key of the farthest splat a tile saturated
-// at), then FrameCtl stored into the host's pinned slot (mapped, fine-grained) and the sequence
-// number published with a system-scope release; the host reads it a frame or two later.  Then
-// FrameCtl is zeroed for the next frame.
-__global__ __launch_bounds__(64) void k_frame_end(FrameCtl* ctl, FrameCtl* host_ctl, uint32_t* host_seq,
-                                                 uint32_t seq) {
+// End of a frame: the statistic shards summed into FrameCtl (and zeroed), the saturation
+// statistic (depth key of the farthest splat a tile saturated at), then FrameCtl stored into the
+// host's pinned slot (mapped, fine-grained) and the sequence number published with a
+// system-scope release; the host reads it a frame or two later.  Then FrameCtl is zeroed for the
+// next frame.  One wave; lane l sums shard l.
+__global__ __launch_bounds__(64) void k_frame_end(FrameCtl* ctl, StatShard* stats, FrameCtl* host_ctl,
+                                                 uint32_t* host_seq, uint32_t seq) {
     constexpr uint32_t kWords = sizeof(FrameCtl) / 4;
-    static_assert(kWords <= 64, "FrameCtl is copied by one wave");
-    constexpr uint32_t kKeyW = offsetof(FrameCtl, sat_key) / 4;
+    static_assert(kWords <= 64 && kStatShards == 64, "one wave");
     const uint32_t lane = threadIdx.x;
+    StatShard sh = stats[lane];
+    stats[lane] = StatShard{};
+    unsigned long long kt = sh.k_total;
+    uint32_t nv = sh.n_vis, kmi = sh.key_min_inv, kma = sh.key_max, c0 = sh.n_chunk[0], c1 = sh.n_chunk[1];
+    for (int d = 32; d >= 1; d >>= 1) {
+        kt += __shfl_xor(kt, d, 64);
+        nv += __shfl_xor(nv, d, 64);
+        c0 += __shfl_xor(c0, d, 64);
+        c1 += __shfl_xor(c1, d, 64);
+        kmi = max(kmi, (uint32_t)__shfl_xor(kmi, d, 64));
+        kma = max(kma, (uint32_t)__shfl_xor(kma, d, 64));
+    }
     uint32_t key = 0;
     for (int k = 0; k < kHistShards; ++k) key = max(key, ctl->sat_key_shard[k]);
+    if (lane == 0) {
+        ctl->k_total = kt;
+        ctl->n_vis = nv;
+        ctl->key_min_inv = kmi;
+        ctl->key_max = kma;
+        ctl->n_chunk[0] = c0;
+        ctl->n_chunk[1] = c1;
+        ctl->sat_key = key;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
     uint32_t* src = (uint32_t*)ctl;
-    const uint32_t v = lane < kWords ? (lane == kKeyW ? key : src[lane]) : 0u;
+    const uint32_t v = lane < kWords ? src[lane] : 0u;
     if (lane < kWords) ((uint32_t*)host_ctl)[lane] = v;
     __threadfence_system();
     __builtin_amdgcn_wave_barrier();
@@ -1968,15 +2013,11 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, flo
     hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, aos, n, n_sh,
                        geo, shade, cull);
 }
-void launch_project(const ProjParams& p, bool two_phase, hipStream_t s) {
+void launch_project(const ProjParams& p, hipStream_t s) {
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, sort_parts(p.n)));
-    if (two_phase) {
-        const unsigned cgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (p.n + 255) / 256));
-        hipLaunchKernelGGL(k_cull, dim3(cgrid), dim3(256), 0, s, p);
-        hipLaunchKernelGGL(k_project<true>, dim3(grid), dim3(kProjThreads), 0, s, p);
-    } else {
-        hipLaunchKernelGGL(k_project<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
-    }
+    const unsigned cgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (p.n + 255) / 256));
+    hipLaunchKernelGGL(k_cull, dim3(cgrid), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_project, dim3(grid), dim3(kProjThreads), 0, s, p);
 }
 void launch_colour(const ProjParams& p, hipStream_t s) {
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, sort_parts(p.n)));
@@ -2019,8 +2060,9 @@ void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
     hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(kTsThreads), 0, s, p);
 }
-void launch_frame_end(FrameCtl* ctl, FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq, hipStream_t s) {
-    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, ctl, host_ctl, host_seq, seq);
+void launch_frame_end(FrameCtl* ctl, StatShard* stats, FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, ctl, stats, host_ctl, host_seq, seq);
 }
 void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
                 const FrameCtl* ctl, hipStream_t s) {

@@ -9,7 +9,7 @@
                                     MI355X_MICROARCH.md §HBM), write_bytes = WRITE_SIZE x 1024
   profiles/<tag>_pmc.txt            the same as a table
 
-    python tools/profile_summary.py gpurun_out/prof_r01 r01
+    python tools/profile_summary.py gpurun_out/prof_r01 r01 [out_dir (default profiles/)]
 """
 import csv
 import json
@@ -28,8 +28,8 @@ def short(name):
     return re.sub(r"^void ", "", name).replace("gs::", "")
 
 
-def frames_of(rows, key_start="k_project"):
-    """Split dispatches (in order) into frames starting at k_project; label positions."""
+def frames_of(rows, key_start="k_cull"):
+    """Split dispatches (in order) into frames starting at k_cull; label positions."""
     frames, cur = [], None
     for r in rows:
         n = short(r["Kernel_Name"])
@@ -59,7 +59,7 @@ def load_trace(path):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    prof = os.path.join(ROOT, "profiles")
+    prof = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(prof, tag + "_kernel_stats.csv"))
 
