@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <array>
+#include <utility>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -145,7 +146,10 @@ struct gs_scene {
     uint2* skey = nullptr;
     uint32_t* srect = nullptr;
     uint32_t *c0 = nullptr, *c1 = nullptr;  // [parts]: slots per projection partition and chunk
-    unsigned long long* cand_mask = nullptr;  // chunk-0 candidates (k_cull), bit i % 64 of word i / 64
+    uint16_t* cand = nullptr;           // chunk-0 candidates per partition (k_cull): offsets
+    PartBound* bounds = nullptr;        // [parts] partition bounds (upload)
+    uint32_t* orig = nullptr;           // [n] reference index of each storage slot (Morton order)
+    uint32_t* sidx = nullptr;           // [slots] storage index of each composite slot
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     FrameCtl* ctl = nullptr;            // zero at a frame's start (k_frame_end clears it)
     StatShard* stats = nullptr;         // [kStatShards], zero at a frame's start (likewise)
@@ -439,7 +443,10 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.srect = s->srect;
     pp.c0 = s->c0;
     pp.c1 = s->c1;
-    pp.cand_mask = s->cand_mask;
+    pp.cand = s->cand;
+    pp.bounds = s->bounds;
+    pp.orig = s->orig;
+    pp.sidx = s->sidx;
     mark(EV_PROJ0);
     launch_project(pp, st);
     launch_colour(pp, st);
@@ -462,6 +469,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         mark(eb);
         BinParams bp{};
         bp.skey = s->skey;
+        bp.sidx = s->sidx;
         bp.srect = s->srect;
         bp.cnt = chunk == 0 ? s->c0 : s->c1;
         bp.parts = sort_parts(pp.n);
@@ -573,6 +581,46 @@ static void check_frame_errors(gs_scene* s) {
     }
 }
 
+// Stable LSD radix sort of (key, value) pairs on bits [b0, b1) on the device: (ka, va) in, ping-pong
+// with (kb, vb); returns the buffers holding the result.
+static std::pair<uint32_t*, uint32_t*> device_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb,
+                                                         uint64_t n, int b0, int b1, hipStream_t st) {
+    if (n == 0) return {ka, va};
+    const int npass = (b1 - b0 + 7) / 8;
+    uint32_t *hist = nullptr, *offs = nullptr, *gsum = nullptr;
+    const size_t region = 256 * ((sort_parts(n, kDepthSortIpt) + kGroupParts - 1) / kGroupParts + 1);
+    try {
+        dev_alloc(hist, (size_t)npass * kHistWords);
+        dev_alloc(offs, (size_t)256 * sort_parts(n, kDepthSortIpt));
+        dev_alloc(gsum, (size_t)npass * region);
+        HIPCHK(hipMemsetAsync(hist, 0, (size_t)npass * kHistWords * 4, st));
+        HIPCHK(hipMemsetAsync(gsum, 0, (size_t)npass * region * 4, st));
+        for (int ps = 0; ps < npass; ++ps) {
+            SortPass sp{};
+            sp.keys_in = ka; sp.vals_in = va; sp.keys_out = kb; sp.vals_out = vb;
+            sp.n = (uint32_t)n;
+            sp.ipt = kDepthSortIpt;
+            sp.parts_max = sort_parts(n, sp.ipt);
+            sp.shift = b0 + 8 * ps;
+            const int bits = std::min(8, b1 - sp.shift);
+            sp.mask = (1u << bits) - 1u;
+            sp.hist = hist + ps * kHistWords;
+            sp.offsets = offs;
+            sp.gsum = gsum + (size_t)ps * region;
+            launch_sort_pass(sp, st);
+            std::swap(ka, kb);
+            std::swap(va, vb);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(st));
+    } catch (...) {
+        dev_free(hist); dev_free(offs); dev_free(gsum);
+        throw;
+    }
+    dev_free(hist); dev_free(offs); dev_free(gsum);
+    return {ka, va};
+}
+
 extern "C" {
 
 int gs_abi_version(void) { return GS_ABI_VERSION; }
@@ -646,7 +694,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
         *out = nullptr;
         if (n_sh != 1 && n_sh != 4 && n_sh != 9 && n_sh != 16)
             throw GsError(GS_ERR_UNSUPPORTED, "n_sh_coeffs must be 1, 4, 9 or 16");
-        if (n >= 0xFFFFFFF0ull) throw GsError(GS_ERR_UNSUPPORTED, "scene larger than 2^32-16 Gaussians");
+        if (n > (1ull << 28)) throw GsError(GS_ERR_UNSUPPORTED, "scene larger than 2^28 Gaussians");
         HIPCHK(hipSetDevice(c->device));
         gs_scene* s = new gs_scene();
         s->ctx = c;
@@ -666,7 +714,10 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->srect, nslots);
             dev_alloc(s->c0, (size_t)sort_parts(n) + 1);
             dev_alloc(s->c1, (size_t)sort_parts(n) + 1);
-            dev_alloc(s->cand_mask, (size_t)sort_parts(n) * (kSortTile / 64) + 1);
+            dev_alloc(s->cand, nslots);
+            dev_alloc(s->bounds, (size_t)sort_parts(n) + 1);
+            dev_alloc(s->orig, (size_t)n + 1);
+            dev_alloc(s->sidx, nslots);
             const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hf));
             HIPCHK(hipHostMalloc((void**)&s->h_seq, 64, hf));
@@ -674,21 +725,36 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             HIPCHK(hipHostGetDevicePointer((void**)&s->d_ctl_slot, s->h_ctl, 0));
             HIPCHK(hipHostGetDevicePointer((void**)&s->d_seq, s->h_seq, 0));
             ensure_tile_capacity(s, 4 * n + (1u << 20));
-            // AoS -> SoA on device, in chunks of 4M records
+            // AoS -> SoA on device in spatial (Morton) order: codes, stable sort, gather-transpose,
+            // then the partition bounds
             const uint64_t rb = 64 + 16 * (uint64_t)n_sh;
-            const uint64_t chunk = std::min<uint64_t>(n, 1u << 22);
-            uint8_t* tmp = nullptr;
-            if (n) dev_alloc(tmp, chunk * rb);
-            for (uint64_t i0 = 0; i0 < n; i0 += chunk) {
-                const uint64_t m = std::min(chunk, n - i0);
-                HIPCHK(hipMemcpyAsync(tmp, (const uint8_t*)aos + i0 * rb, m * rb, hipMemcpyHostToDevice,
-                                      c->stream));
-                launch_transpose(tmp, m, n_sh, s->geo + 3 * i0, s->shade + i0 * shade_stride(n_sh), s->cull + i0,
-                                 c->stream);
-                HIPCHK(hipGetLastError());
-                HIPCHK(hipStreamSynchronize(c->stream));
+            if (n) {
+                uint8_t* tmp = nullptr;
+                uint32_t *bbox = nullptr, *kA = nullptr, *vA = nullptr, *kB = nullptr, *vB = nullptr;
+                auto free_tmp = [&] {
+                    dev_free(tmp); dev_free(bbox); dev_free(kA); dev_free(vA); dev_free(kB); dev_free(vB);
+                };
+                try {
+                    hipStream_t st = c->stream;
+                    dev_alloc(tmp, n * rb);
+                    dev_alloc(bbox, 6);
+                    dev_alloc(kA, n); dev_alloc(vA, n); dev_alloc(kB, n); dev_alloc(vB, n);
+                    HIPCHK(hipMemcpyAsync(tmp, aos, n * rb, hipMemcpyHostToDevice, st));
+                    const uint32_t b0[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+                    HIPCHK(hipMemcpyAsync(bbox, b0, sizeof(b0), hipMemcpyHostToDevice, st));
+                    launch_bbox(tmp, n, (uint32_t)rb, bbox, st);
+                    launch_morton(tmp, n, (uint32_t)rb, bbox, kA, vA, st);
+                    const auto r = device_sort_pairs(kA, vA, kB, vB, n, 0, 32, st);
+                    launch_transpose(tmp, n, n_sh, r.second, s->geo, s->shade, s->cull, s->orig, st);
+                    launch_part_bounds(s->cull, n, s->bounds, st);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(hipStreamSynchronize(st));
+                } catch (...) {
+                    free_tmp();
+                    throw;
+                }
+                free_tmp();
             }
-            dev_free(tmp);
         } catch (...) {
             gs_scene_free(s);
             throw;
@@ -719,7 +785,10 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->srect);
     dev_free(s->c0);
     dev_free(s->c1);
-    dev_free(s->cand_mask);
+    dev_free(s->cand);
+    dev_free(s->bounds);
+    dev_free(s->orig);
+    dev_free(s->sidx);
     dev_free(s->tvA); dev_free(s->tvB);
     dev_free(s->ranges);
     dev_free(s->bmat);
@@ -879,46 +948,26 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
         if (n >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "n too large");
         if (n == 0) return GS_OK;
         HIPCHK(hipSetDevice(c->device));
-        const int npass = (end_bit - begin_bit + 7) / 8;
-        uint32_t *kA, *vA, *kB, *vB, *hist, *offs, *gsum;
-        dev_alloc(kA, n); dev_alloc(vA, n); dev_alloc(kB, n); dev_alloc(vB, n);
-        dev_alloc(hist, (size_t)npass * kHistWords);
-        dev_alloc(offs, (size_t)256 * sort_parts(n, kDepthSortIpt));
-        const size_t region = 256 * ((sort_parts(n, kDepthSortIpt) + kGroupParts - 1) / kGroupParts + 1);
-        dev_alloc(gsum, (size_t)npass * region);
-        hipStream_t st = c->stream;
-        HIPCHK(hipMemcpyAsync(kA, keys, n * 4, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(vA, vals, n * 4, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemsetAsync(hist, 0, (size_t)npass * kHistWords * 4, st));
-        HIPCHK(hipMemsetAsync(gsum, 0, (size_t)npass * region * 4, st));
-        uint32_t *ki = kA, *vi = vA, *ko = kB, *vo = vB;
-        for (int ps = 0; ps < npass; ++ps) {
-            SortPass sp{};
-            sp.keys_in = ki; sp.vals_in = vi; sp.keys_out = ko; sp.vals_out = vo;
-            sp.n = (uint32_t)n;
-            sp.ipt = kDepthSortIpt;
-            sp.parts_max = sort_parts(n, sp.ipt);
-            sp.shift = begin_bit + 8 * ps;
-            const int bits = std::min(8, end_bit - sp.shift);
-            sp.mask = (1u << bits) - 1u;
-            sp.hist = hist + ps * kHistWords;
-            sp.offsets = offs;
-            sp.gsum = gsum + (size_t)ps * region;
-            launch_sort_pass(sp, st);
-            std::swap(ki, ko);
-            std::swap(vi, vo);
+        uint32_t *kA = nullptr, *vA = nullptr, *kB = nullptr, *vB = nullptr;
+        try {
+            dev_alloc(kA, n); dev_alloc(vA, n); dev_alloc(kB, n); dev_alloc(vB, n);
+            hipStream_t st = c->stream;
+            HIPCHK(hipMemcpyAsync(kA, keys, n * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(vA, vals, n * 4, hipMemcpyHostToDevice, st));
+            const auto r = device_sort_pairs(kA, vA, kB, vB, n, begin_bit, end_bit, st);
+            HIPCHK(hipMemcpy(keys, r.first, n * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(vals, r.second, n * 4, hipMemcpyDeviceToHost));
+        } catch (...) {
+            dev_free(kA); dev_free(vA); dev_free(kB); dev_free(vB);
+            throw;
         }
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(keys, ki, n * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(vals, vi, n * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        dev_free(kA); dev_free(vA); dev_free(kB); dev_free(vB); dev_free(hist); dev_free(offs);
-        dev_free(gsum);
+        dev_free(kA); dev_free(vA); dev_free(kB); dev_free(vB);
         return GS_OK;
     });
 }
 
-// The last frame's composite slots as (slot, depth key, Gaussian index), chunk 0 then chunk 1.
+// The last frame's visible splats' composite slots as (slot, depth key, reference index), chunk 0
+// then chunk 1.
 static std::vector<std::array<uint32_t, 3>> frame_slots(gs_scene* s) {
     collect_stats(s, true);
     const uint32_t parts = sort_parts(s->n);
@@ -926,6 +975,8 @@ static std::vector<std::array<uint32_t, 3>> frame_slots(gs_scene* s) {
     if (!parts) return out;
     std::vector<uint32_t> c0(parts), c1(parts);
     std::vector<uint2> sk((size_t)parts * kSortTile);
+    std::vector<uint32_t> rect((size_t)parts * kSortTile);
+    HIPCHK(hipMemcpy(rect.data(), s->srect, rect.size() * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(c0.data(), s->c0, parts * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(c1.data(), s->c1, parts * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(sk.data(), s->skey, sk.size() * sizeof(uint2), hipMemcpyDeviceToHost));
@@ -934,6 +985,7 @@ static std::vector<std::array<uint32_t, 3>> frame_slots(gs_scene* s) {
         for (uint32_t p = 0; p < parts; ++p)
             for (uint32_t q = 0; q < (ch ? c1[p] : c0[p]); ++q) {
                 const uint32_t g = ch ? slot_c1(p, q) : slot_c0(p, q);
+                if (rect[g] == kRectHole) continue;  // an invisible chunk-0 candidate
                 out.push_back({g, sk[g].x, sk[g].y});
             }
     return out;
@@ -974,13 +1026,18 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
             launch_records(rp, c->stream);
             HIPCHK(hipStreamSynchronize(c->stream));
             const Records rc = records(s);  // r01 lives in the shading blocks' padding
-            std::vector<float> a((size_t)m * 8), b((size_t)m * 4);
-            HIPCHK(hipMemcpy2D(a.data(), 32, rc.r01 + rc.off, (size_t)rc.stride * 16, 32, m, hipMemcpyDeviceToHost));
+            const uint64_t n = s->n;           // storage slot j holds reference record orig[j]
+            std::vector<float> a((size_t)n * 8), b((size_t)n * 4);
+            std::vector<uint32_t> orig(n);
+            HIPCHK(hipMemcpy2D(a.data(), 32, rc.r01 + rc.off, (size_t)rc.stride * 16, 32, n, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(b.data(), s->r2, b.size() * 4, hipMemcpyDeviceToHost));
-            for (uint64_t j = 0; j < m; ++j) {
-                std::memcpy(out16 + 16 * j, &a[8 * j], 32);
-                std::memset(out16 + 16 * j + 8, 0, 16);
-                std::memcpy(out16 + 16 * j + 12, &b[4 * j], 16);
+            HIPCHK(hipMemcpy(orig.data(), s->orig, n * 4, hipMemcpyDeviceToHost));
+            for (uint64_t j = 0; j < n; ++j) {
+                const uint64_t o = orig[j];
+                if (o >= m) continue;
+                std::memcpy(out16 + 16 * o, &a[8 * j], 32);
+                std::memset(out16 + 16 * o + 8, 0, 16);
+                std::memcpy(out16 + 16 * o + 12, &b[4 * j], 16);
             }
         }
         // colour words [8, 11): from the composite record of each slot of the frame

@@ -34,6 +34,7 @@ constexpr uint32_t kGroupParts = 32;    // radix partitions per group sum (the d
 // binning reads the full rectangle from the record); kRectEmpty = visible but binds no tile.
 constexpr uint32_t kRectLarge = 0xFFFFFFFFu;
 constexpr uint32_t kRectEmpty = 0xFFFFFFFEu;
+constexpr uint32_t kRectHole = 0xFFFFFFFDu;   // a composite slot whose candidate was not visible
 
 // Device-side error bits (FrameCtl::err); a nonzero word fails the frame.
 constexpr uint32_t kErrOverflow = 1u;
@@ -62,6 +63,13 @@ struct StatShard {
     uint32_t n_vis, key_min_inv, key_max;
     uint32_t n_chunk[2];
     uint32_t pad;
+};
+
+// Bound of a projection partition (k_part_bounds, at upload): box of its finite positions,
+// largest ||R(q) diag(s)||_F^2, count of finite positions.
+struct PartBound {
+    float lo[3], hi[3], trs;
+    uint32_t nfin;
 };
 
 // Composite slots.  k_project gives the chunk-0 splats of projection partition `part` (kSortTile
@@ -130,7 +138,10 @@ struct ProjParams {
     uint32_t* srect;
     uint32_t* c0;             // [parts] chunk-0 splats per projection partition (k_project)
     uint32_t* c1;             // [parts] chunk-1 splats per projection partition (k_records; zeroed by k_cull)
-    unsigned long long* cand_mask;  // [n / 64] chunk-0 candidates (k_cull)
+    uint16_t* cand;           // [parts * kSortTile] chunk-0 candidates: offsets in the partition (k_cull)
+    const PartBound* bounds;  // [parts] (k_part_bounds)
+    const uint32_t* orig;     // [n] reference index of each storage slot (Morton order)
+    uint32_t* sidx;           // [slots] storage index of each composite slot
     // k_records: unsaturated-tile SAT of chunk 0 (k_sat); rec_all = every visible (debug)
     const uint32_t* sat;
     int rec_all;
@@ -178,7 +189,8 @@ struct SortPass {
 };
 
 struct BinParams {
-    const uint2* skey;            // [slots] (depth key, Gaussian index)
+    const uint2* skey;            // [slots] (depth key, reference index)
+    const uint32_t* sidx;         // [slots] storage index
     const uint32_t* srect;        // [slots] packed tile rectangle
     const uint32_t* cnt;          // [parts] the chunk's splats per projection partition (c0 or c1)
     uint32_t parts;               // projection partitions
@@ -227,8 +239,12 @@ struct CompositeParams {
 };
 
 // launchers (gs_kernels.hip)
-void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, float4* shade, float4* cull,
-                      hipStream_t s);
+void launch_bbox(const uint8_t* aos, uint64_t n, uint32_t rb, uint32_t* bbox, hipStream_t s);
+void launch_morton(const uint8_t* aos, uint64_t n, uint32_t rb, const uint32_t* bbox, uint32_t* keys,
+                   uint32_t* vals, hipStream_t s);
+void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, const uint32_t* perm, float4* geo, float4* shade,
+                      float4* cull, uint32_t* orig, hipStream_t s);
+void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s);
 void launch_project(const ProjParams& p, hipStream_t s);
 void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 slots (or, rec_all, every record)
 void launch_colour(const ProjParams& p, hipStream_t s);   // colours of the chunk-0 slots

@@ -60,14 +60,92 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp
     return base + incl - v;
 }
 
-// ============================================================================ k_transpose
-__global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ aos, uint64_t n,
-                                                   int n_sh, float4* __restrict__ geo,
-                                                   float4* __restrict__ shade,
-                                                   float4* __restrict__ cull) {
+// ============================================================================ scene upload
+// The scene is stored in spatial (Morton) order: k_bbox + k_morton give every record a 30-bit
+// Morton code of its position in the scene's box (non-finite positions last), a stable radix
+// sort orders them, k_transpose writes storage slot s from record perm[s] and keeps orig[s] =
+// perm[s] (the reference's index: ties in depth are broken by it).  k_part_bounds then bounds
+// each projection partition (kSortTile consecutive slots) for the per-partition cull.
+
+// ordered-uint encoding of a float (monotone), for min / max with integer atomics
+__device__ __forceinline__ uint32_t f2ord(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+
+// bbox[0..2] = min, bbox[3..5] = max of the finite positions (ordered uints; bbox[0..2] start at
+// ~0, bbox[3..5] at 0)
+__global__ __launch_bounds__(256) void k_bbox(const uint8_t* __restrict__ aos, uint64_t n, uint32_t rb,
+                                              uint32_t* __restrict__ bbox) {
+    __shared__ uint32_t s[6];
+    if (threadIdx.x < 6) s[threadIdx.x] = threadIdx.x < 3 ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+    uint32_t lo[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, hi[3] = {0u, 0u, 0u};
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const float* r = (const float*)(aos + i * rb);
+        const float x = r[0], y = r[1], z = r[2];
+        if (!(isfinite(x) && isfinite(y) && isfinite(z))) continue;
+        const float v[3] = {x, y, z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = min(lo[k], f2ord(v[k]));
+            hi[k] = max(hi[k], f2ord(v[k]));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        atomicMin(&s[k], lo[k]);
+        atomicMax(&s[3 + k], hi[k]);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) atomicMin(&bbox[threadIdx.x], s[threadIdx.x]);
+    else if (threadIdx.x < 6) atomicMax(&bbox[threadIdx.x], s[threadIdx.x]);
+}
+
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 10 bits -> every third bit
+    v &= 0x3FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_morton(const uint8_t* __restrict__ aos, uint64_t n, uint32_t rb,
+                                                const uint32_t* __restrict__ bbox, uint32_t* __restrict__ keys,
+                                                uint32_t* __restrict__ vals) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const float* r = (const float*)(aos + i * (uint64_t)(64 + 16 * n_sh));
+    const float* r = (const float*)(aos + i * rb);
+    uint32_t code = 0xFFFFFFFFu;  // non-finite positions last (never visible)
+    if (isfinite(r[0]) && isfinite(r[1]) && isfinite(r[2])) {
+        code = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float lo = ord2f(bbox[k]), hi = ord2f(bbox[3 + k]);
+            const float ext = hi - lo;
+            float t = ext > 0.0f ? (r[k] - lo) / ext : 0.0f;
+            t = fminf(fmaxf(t, 0.0f), 1.0f);
+            code |= spread3(min((uint32_t)(t * 1024.0f), 1023u)) << (2 - k);
+        }
+    }
+    keys[i] = code;
+    vals[i] = (uint32_t)i;
+}
+
+// Storage slot i from reference record perm[i] (or i): geometry record, cull plane, shading block.
+__global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ aos, uint64_t n,
+                                                   int n_sh, const uint32_t* __restrict__ perm,
+                                                   float4* __restrict__ geo, float4* __restrict__ shade,
+                                                   float4* __restrict__ cull, uint32_t* __restrict__ orig) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t src = perm ? perm[i] : i;
+    orig[i] = (uint32_t)src;
+    const float* r = (const float*)(aos + src * (uint64_t)(64 + 16 * n_sh));
     // src/ply.ts:249-257 record: pos[0:3] | scale[4:7] | rot[8:12] | opacity[12] | sh[k] at 16+4k
     geo[3 * i + 0] = make_float4(r[0], r[1], r[2], r[12]);  // position, opacity logit
     geo[3 * i + 1] = make_float4(r[4], r[5], r[6], r[8]);   // scale, rot.x
@@ -100,6 +178,50 @@ __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ a
 #pragma unroll
     for (uint32_t t = 0; t < 13; ++t)
         if (t < q) o[t] = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
+}
+
+// Per projection partition (kSortTile consecutive storage slots): the box of its finite
+// positions, the largest ||R(q) diag(s)||_F^2 (NaN counts as infinite) and its count of finite
+// positions (zero: nothing in it can be visible).
+__global__ __launch_bounds__(256) void k_part_bounds(const float4* __restrict__ cull, uint64_t n,
+                                                     PartBound* __restrict__ out) {
+    __shared__ uint32_t s[8];
+    if (threadIdx.x < 8) s[threadIdx.x] = threadIdx.x < 3 ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+    const uint64_t p0 = (uint64_t)blockIdx.x * kSortTile;
+    uint32_t lo[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, hi[3] = {0u, 0u, 0u}, trs = 0u, fin = 0u;
+    for (uint32_t k = threadIdx.x; k < (uint32_t)kSortTile; k += 256) {
+        const uint64_t i = p0 + k;
+        if (i >= n) break;
+        const float4 c = cull[i];
+        if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) continue;
+        const float v[3] = {c.x, c.y, c.z};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = min(lo[d], f2ord(v[d]));
+            hi[d] = max(hi[d], f2ord(v[d]));
+        }
+        trs = max(trs, f2ord(c.w != c.w ? INFINITY : c.w));
+        ++fin;
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        atomicMin(&s[d], lo[d]);
+        atomicMax(&s[3 + d], hi[d]);
+    }
+    atomicMax(&s[6], trs);
+    atomicAdd(&s[7], fin);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        PartBound b;
+        for (int d = 0; d < 3; ++d) {
+            b.lo[d] = ord2f(s[d]);
+            b.hi[d] = ord2f(s[3 + d]);
+        }
+        b.trs = s[7] ? ord2f(s[6]) : 0.0f;
+        b.nfin = s[7];
+        out[blockIdx.x] = b;
+    }
 }
 
 // ============================================================================ k_project
@@ -399,7 +521,8 @@ __device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, u
     float4* r = p.crec + 3 * (uint64_t)slot;
     r[0] = o.r0;
     r[1] = o.r1;
-    p.skey[slot] = make_uint2(o.key, i);
+    p.skey[slot] = make_uint2(o.key, p.orig[i]);
+    p.sidx[slot] = i;
     p.srect[slot] = o.prect;
     p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles), __uint_as_float(o.bbx),
                               __uint_as_float(o.bby));
@@ -469,34 +592,152 @@ __global__ __launch_bounds__(256) void k_records(ProjParams p) {
     }
 }
 
-// Projection, phase A (a chip-wide grid-stride stream, one Gaussian per thread): every Gaussian's
-// 16-B cull plane gives its depth key (vz rounded exactly as project_footprint rounds it) and
-// the conservative cull (cull_keep: exact near/far, a provable bound on the quad box against this
-// frame's rows).  Survivors nearer than thresh are chunk-0 candidates (bit i % 64 of cand_mask
-// word i / 64); survivors at or past thresh are only counted (n_vis is exact when the frame has
-// one chunk) and enter the depth range.
-__global__ __launch_bounds__(256) void k_cull(ProjParams p) {
+// Can a Gaussian of partition b be a chunk-0 candidate of this frame (pass cull_keep with key <
+// thresh)?  The interval form of cull_keep over the partition's box, in double with slack for
+// the per-Gaussian float roundings: clip coordinates are affine (extremes at the 8 corners), the
+// ratios x/w, y/w take their extremes at the corners when every corner has w > 0, the quad bound
+// grows with focal / |vz| and ||R diag(s)||_F^2; key < thresh needs the box's smallest key.
+__device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, int row_hi) {
+    if (!b.nfin) return false;
+    double mn[5], mx[5];  // vz, cx, cy, cz, cw
+    double mag[5];        // sum |coefficient * coordinate|: the scale of the float rounding
+    for (int k = 0; k < 5; ++k) {
+        mn[k] = 1e300;
+        mx[k] = -1e300;
+        mag[k] = 0.0;
+    }
+    for (int c = 0; c < 8; ++c) {
+        const double x = (c & 1) ? b.hi[0] : b.lo[0], y = (c & 2) ? b.hi[1] : b.lo[1], z = (c & 4) ? b.hi[2] : b.lo[2];
+        const double v[5] = {
+            (double)p.V[2] * x + (double)p.V[6] * y + (double)p.V[10] * z + (double)p.V[14],
+            (double)p.PV[0] * x + (double)p.PV[4] * y + (double)p.PV[8] * z + (double)p.PV[12],
+            (double)p.PV[1] * x + (double)p.PV[5] * y + (double)p.PV[9] * z + (double)p.PV[13],
+            (double)p.PV[2] * x + (double)p.PV[6] * y + (double)p.PV[10] * z + (double)p.PV[14],
+            (double)p.PV[3] * x + (double)p.PV[7] * y + (double)p.PV[11] * z + (double)p.PV[15]};
+        const double m[5] = {
+            fabs(p.V[2] * x) + fabs(p.V[6] * y) + fabs(p.V[10] * z) + fabs((double)p.V[14]),
+            fabs(p.PV[0] * x) + fabs(p.PV[4] * y) + fabs(p.PV[8] * z) + fabs((double)p.PV[12]),
+            fabs(p.PV[1] * x) + fabs(p.PV[5] * y) + fabs(p.PV[9] * z) + fabs((double)p.PV[13]),
+            fabs(p.PV[2] * x) + fabs(p.PV[6] * y) + fabs(p.PV[10] * z) + fabs((double)p.PV[14]),
+            fabs(p.PV[3] * x) + fabs(p.PV[7] * y) + fabs(p.PV[11] * z) + fabs((double)p.PV[15])};
+        for (int k = 0; k < 5; ++k) {
+            mn[k] = fmin(mn[k], v[k]);
+            mx[k] = fmax(mx[k], v[k]);
+            mag[k] = fmax(mag[k], m[k]);
+        }
+    }
+    double sl[5];
+    for (int k = 0; k < 5; ++k) sl[k] = 1e-5 * mag[k] + 1e-30;
+    if (!(mx[4] + sl[4] > 0.0)) return false;           // every clip w <= 0
+    if (!(mx[3] + sl[3] >= 0.0)) return false;          // every clip z < 0 (near)
+    if (!(mn[3] - sl[3] - (mx[4] + sl[4]) <= 0.0)) return false;  // every clip z > w (far)
+    if (p.thresh != kSentinel) {  // the smallest depth key in the box
+        uint32_t kmin = 0;
+        if (mx[0] + sl[0] < 0.0) kmin = sortable_key((float)(mx[0] + sl[0]));
+        else if (mn[0] - sl[0] > 0.0) kmin = sortable_key((float)(mn[0] - sl[0]));
+        kmin = kmin > 64u ? kmin - 64u : 0u;
+        if (kmin >= p.thresh) return false;
+    }
+    if (!(mn[4] - sl[4] > 0.0)) return true;            // a corner with w <= 0: no ratio bound
+    if (!(mn[0] - sl[0] > 0.0 || mx[0] + sl[0] < 0.0)) return true;  // vz crosses 0
+    double pxl = 1e300, pxh = -1e300, pyl = 1e300, pyh = -1e300;
+    for (int c = 0; c < 8; ++c) {  // pixel centre of each corner (ratios in double)
+        const double x = (c & 1) ? b.hi[0] : b.lo[0], y = (c & 2) ? b.hi[1] : b.lo[1], z = (c & 4) ? b.hi[2] : b.lo[2];
+        const double cx = (double)p.PV[0] * x + (double)p.PV[4] * y + (double)p.PV[8] * z + (double)p.PV[12];
+        const double cy = (double)p.PV[1] * x + (double)p.PV[5] * y + (double)p.PV[9] * z + (double)p.PV[13];
+        const double cw = (double)p.PV[3] * x + (double)p.PV[7] * y + (double)p.PV[11] * z + (double)p.PV[15];
+        const double px = (cx / cw + 1.0) * p.W * 0.5, py = (1.0 - cy / cw) * p.H * 0.5;
+        pxl = fmin(pxl, px); pxh = fmax(pxh, px);
+        pyl = fmin(pyl, py); pyh = fmax(pyh, py);
+    }
+    const double az = fmin(fabs(mn[0]), fabs(mx[0])) * (1.0 - 1e-5);
+    const double a = (double)p.focal / az;
+    const double trs = (double)b.trs * p.scale_mod * p.scale_mod;
+    const double hb = 4.0 * fmax(sqrt(2.0 * (a * a * p.w01_spec2 * trs + 0.6)), 0.45) * 1.03 + 4.0;
+    if (!(hb < 1e30)) return true;
+    return !(pyh + hb < (double)row_lo - 1.0 || pyl - hb > (double)row_hi + 1.0 || pxh + hb < -1.0 ||
+             pxl - hb > (double)p.W);
+}
+
+// Projection, phase A (one workgroup per projection partition of kSortTile storage slots): a
+// partition whose bound rules it out (part_maybe) costs one 32-B read; otherwise every
+// Gaussian's 16-B cull plane gives its depth key (vz rounded exactly as project_footprint rounds
+// it) and the conservative cull (cull_keep: exact near/far, a provable bound on the quad box
+// against this frame's rows).  Survivors nearer than thresh are the partition's chunk-0
+// candidates (cand: their offsets in index order; c0 = their count, the partition's chunk-0
+// slots); survivors at or past thresh are only counted (n_vis is exact when the frame has one
+// chunk and no partition was ruled out by the threshold) and enter the depth range.
+__global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
-    if (threadIdx.x == 0) { s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
-    __syncthreads();
+    __shared__ unsigned long long s_mask[kSortIPT][kProjThreads / 64];
+    __shared__ uint32_t s_base[kSortIPT][kProjThreads / 64];
+    __shared__ uint32_t s_total;
+    __shared__ int s_maybe;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    if (tid == 0) { s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
     uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i - lane < p.n; i += gridDim.x * blockDim.x) {
-        bool cand = false;
-        float vz;
-        if (i < p.n && cull_keep(p, p.cull[i], row_lo, row_hi, vz)) {
-            const uint32_t key = sortable_key(vz);
-            cand = key < p.thresh;
-            if (!cand) {  // past the threshold: counted, not projected
-                ++my_vis;
-                my_kmin_inv = max(my_kmin_inv, ~key);
-                my_kmax = max(my_kmax, key);
+    const uint32_t parts = sort_parts(p.n);
+    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+        const uint32_t p0 = part * kSortTile;
+        if (tid == 0) s_maybe = part_maybe(p, p.bounds[part], row_lo, row_hi);
+        __syncthreads();
+        if (!s_maybe) {
+            if (tid == 0) {
+                p.c0[part] = 0;
+                p.c1[part] = 0;
+            }
+            __syncthreads();
+            continue;
+        }
+        uint32_t cand = 0;  // bit it: slot p0 + it * kProjThreads + tid is a candidate
+        constexpr int kGroup = 4;  // cull planes in flight per thread
+        for (int g = 0; g < kSortIPT; g += kGroup) {
+            float4 c[kGroup];
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                const uint32_t i = p0 + (g + u) * kProjThreads + tid;
+                c[u] = i < p.n ? p.cull[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                const int it = g + u;
+                const uint32_t i = p0 + it * kProjThreads + tid;
+                bool cd = false;
+                float vz;
+                if (i < p.n && cull_keep(p, c[u], row_lo, row_hi, vz)) {
+                    const uint32_t key = sortable_key(vz);
+                    cd = key < p.thresh;
+                    if (!cd) {  // past the threshold: counted, not projected
+                        ++my_vis;
+                        my_kmin_inv = max(my_kmin_inv, ~key);
+                        my_kmax = max(my_kmax, key);
+                    }
+                }
+                cand |= (cd ? 1u : 0u) << it;
+                const uint64_t bb = __ballot(cd);
+                if (lane == 0) s_mask[it][w] = bb;
             }
         }
-        const unsigned long long b = __ballot(cand);
-        if (lane == 0) p.cand_mask[i >> 6] = b;
+        __syncthreads();
+        if (tid < 64) {  // exclusive prefix of the 16 x 4 (round, wave) ballots: index order
+            const uint32_t cnt = __popcll(s_mask[tid >> 2][tid & 3]);
+            const uint32_t incl = wave_incl_scan(cnt);
+            s_base[tid >> 2][tid & 3] = incl - cnt;
+            if (tid == 63) s_total = incl;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kSortIPT; ++it) {
+            const uint64_t bb = s_mask[it][w];
+            if ((cand >> it) & 1u) p.cand[p0 + s_base[it][w] + __popcll(bb & lanemask_lt())] = (uint16_t)(it * kProjThreads + tid);
+        }
+        if (tid == 0) {
+            p.c0[part] = s_total;
+            p.c1[part] = 0;
+        }
+        __syncthreads();
     }
     if (my_vis) {
         atomicAdd(&s_vis, my_vis);
@@ -504,7 +745,7 @@ __global__ __launch_bounds__(256) void k_cull(ProjParams p) {
         atomicMax(&s_kmax, my_kmax);
     }
     __syncthreads();
-    if (threadIdx.x == 0 && s_vis) {
+    if (tid == 0 && s_vis) {
         StatShard* st = p.stats + blockIdx.x % kStatShards;
         atomicAdd(&st->n_vis, s_vis);
         atomicMax(&st->key_min_inv, s_kmin_inv);
@@ -512,77 +753,38 @@ __global__ __launch_bounds__(256) void k_cull(ProjParams p) {
     }
 }
 
-// Projection, phase B (one workgroup per projection partition of kSortTile Gaussians): the
-// partition's candidates (cand_mask, listed in LDS in index order) projected densely (their 48-B
-// geometry records gathered); each visible one gets a composite slot of the partition (slot_c0,
-// arrival order: the per-tile sort orders them) with its records.  Publishes the visible count,
-// their tile total, the depth-key range, c0 and c1 (zeroed for k_records).
+// Work units of the per-slot passes: (partition, round of kProjThreads slots), so that a
+// partition full of candidates is spread over kSortIPT workgroups.
+__device__ __forceinline__ uint32_t slot_units(const ProjParams& p) { return sort_parts(p.n) * kSortIPT; }
+
+// Projection, phase B: candidate q of a partition (slot slot_c0(part, q)) projected from its
+// 48-B geometry record; a visible one gets its records in its slot, an invisible one leaves the
+// slot a hole (rect kRectHole).  Publishes the visible count, their tile total, the depth range.
 __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     __shared__ unsigned long long s_k;
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
-    __shared__ uint32_t s_cnt;
-    __shared__ uint32_t s_wbase[kSortTile / 64 + 1];
-    __shared__ uint16_t s_list[kSortTile];
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     if (tid == 0) { s_k = 0; s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
+    __syncthreads();
     uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
     unsigned long long my_k = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
-    const uint32_t parts = sort_parts(p.n);
-    constexpr uint32_t kWords = kSortTile / 64;  // mask words per partition (= 64)
-    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        const uint32_t p0 = part * kSortTile;
-        if (tid == 0) s_cnt = 0;
-        // candidate list: word k of the partition's mask holds Gaussians p0 + 64 k + bit
-        unsigned long long mw = 0;
-        if (tid < (int)kWords) {
-            const uint32_t wi = part * kWords + tid;
-            mw = (uint64_t)wi * 64 < p.n ? p.cand_mask[wi] : 0ull;
-            const uint32_t c = (uint32_t)__popcll(mw);
-            const uint32_t incl = wave_incl_scan(c);
-            s_wbase[tid] = incl - c;
-            if (tid == (int)kWords - 1) s_wbase[kWords] = incl;
-        }
-        __syncthreads();
-        if (tid < (int)kWords) {
-            uint32_t o = s_wbase[tid];
-            while (mw) {
-                const int bit = __ffsll((long long)mw) - 1;
-                mw &= mw - 1;
-                s_list[o++] = (uint16_t)(tid * 64 + bit);
-            }
-        }
-        __syncthreads();
-        const uint32_t nitems = s_wbase[kWords];
-        for (uint32_t q0 = 0; q0 < nitems; q0 += kProjThreads) {  // block-uniform
-            const uint32_t q = q0 + tid;
-            Proj o;
-            bool vis = false;
-            uint32_t i = 0;
-            if (q < nitems) {
-                i = p0 + (uint32_t)s_list[q];
-                vis = project_core(p, i, row_lo, row_hi, false, o);
-                if (vis) {
-                    ++my_vis;
-                    my_k += o.ntiles;
-                    my_kmin_inv = max(my_kmin_inv, ~o.key);
-                    my_kmax = max(my_kmax, o.key);
-                }
-            }
-            const uint64_t b = __ballot(vis);
-            if (b) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&s_cnt, (uint32_t)__popcll(b));
-                base = __shfl(base, 0, 64);
-                if (vis) store_slot(p, slot_c0(part, base + (uint32_t)__popcll(b & lanemask_lt())), i, o);
-            }
-        }
-        __syncthreads();
-        if (tid == 0) {
-            p.c0[part] = s_cnt;
-            p.c1[part] = 0;
-            if (s_cnt) atomicAdd(&p.stats[blockIdx.x % kStatShards].n_chunk[0], s_cnt);
+    const uint32_t units = slot_units(p);
+    for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const uint32_t part = u / kSortIPT, q = (u % kSortIPT) * kProjThreads + tid;
+        if (q >= p.c0[part]) continue;
+        const uint32_t p0 = part * kSortTile, slot = slot_c0(part, q);
+        const uint32_t i = p0 + (uint32_t)p.cand[p0 + q];
+        Proj o;
+        if (project_core(p, i, row_lo, row_hi, false, o)) {
+            store_slot(p, slot, i, o);
+            ++my_vis;
+            my_k += o.ntiles;
+            my_kmin_inv = max(my_kmin_inv, ~o.key);
+            my_kmax = max(my_kmax, o.key);
+        } else {
+            p.srect[slot] = kRectHole;
         }
     }
     if (my_vis) {
@@ -595,26 +797,27 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     if (tid == 0 && s_vis) {
         StatShard* st = p.stats + blockIdx.x % kStatShards;
         atomicAdd(&st->n_vis, s_vis);
+        atomicAdd(&st->n_chunk[0], s_vis);
         atomicAdd(&st->k_total, s_k);
         atomicMax(&st->key_min_inv, s_kmin_inv);
         atomicMax(&st->key_max, s_kmax);
     }
 }
 
-// Colours of the chunk-0 slots, one thread per slot, partition by partition (the shading blocks
-// of a partition's splats are read in roughly index order): the SH colour and the depth key
-// (the composite's saturation statistic) into the record's third quad.
+// Colours of the chunk-0 slots, one thread per slot: the SH colour and the depth key (the
+// composite's saturation statistic) into the record's third quad.
 __global__ __launch_bounds__(256) void k_colour(ProjParams p) {
-    const uint32_t parts = sort_parts(p.n);
-    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        const uint32_t cnt = p.c0[part];
-        for (uint32_t q = threadIdx.x; q < cnt; q += 256) {
-            const uint32_t slot = slot_c0(part, q);
-            const uint2 k = p.skey[slot];
-            float4 c = sh_colour(p.rec.r01 + (uint64_t)k.y * p.rec.stride, p.rec.off, p.cam);
-            c.w = __uint_as_float(k.x);
-            p.crec[3 * (uint64_t)slot + 2] = c;
-        }
+    const uint32_t units = slot_units(p);
+    for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const uint32_t part = u / kSortIPT, q = (u % kSortIPT) * kProjThreads + threadIdx.x;
+        if (q >= p.c0[part]) continue;
+        const uint32_t slot = slot_c0(part, q);
+        const uint32_t pr = p.srect[slot];
+        if (pr == kRectHole || pr == kRectEmpty) continue;  // not visible / binds no tile
+        const uint32_t j = p.sidx[slot];
+        float4 c = sh_colour(p.rec.r01 + (uint64_t)j * p.rec.stride, p.rec.off, p.cam);
+        c.w = __uint_as_float(p.skey[slot].x);
+        p.crec[3 * (uint64_t)slot + 2] = c;
     }
 }
 
@@ -883,7 +1086,7 @@ struct TileRect {
 };
 
 __device__ __forceinline__ bool rect_unpack(const BinParams& p, uint32_t pr, uint32_t j, TileRect& r) {
-    if (pr == kRectEmpty) return false;
+    if (pr == kRectEmpty || pr == kRectHole) return false;
     if (pr == kRectLarge) {  // tile box from the pixel box in the record
         const float4 m = p.rec.r2[j];
         const uint32_t bx = __float_as_uint(m.z), by = __float_as_uint(m.w);
@@ -991,10 +1194,11 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
     return true;
 }
 
-// ---- binning into per-tile lists, a two-level counting sort without global atomics.  Binning
-// partition b (of kBinParts) takes the chunk's slots of projection partitions b, b + kBinParts,
-// ... (interleaved: balanced whatever the scene order); the tiles are cut into bands of
-// <= kBandTiles.
+// ---- binning into per-tile lists, a two-level counting sort without global atomics.  The
+// chunk's slots come in units of (projection partition, round of kProjThreads slots); binning
+// partition b (of kBinParts) takes units b, b + kBinParts, ... (interleaved: balanced whatever
+// the scene order, also when a few partitions hold all the splats); the tiles are cut into bands
+// of <= kBandTiles.
 //   k_bin_count    workgroup (partition b, band): LDS counters of its splats' entries per tile
 //                  (ellipse rows; chunk 1: unsaturated tiles only) -> bmat[b][t]
 //   k_bin_colscan  per tile: exclusive prefix of bmat[.][t] over the partitions, tile totals
@@ -1002,19 +1206,29 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
 //   k_bin_emit     workgroup (b, band): LDS cursors tbase[t] + bmat[b][t]; each entry takes a
 //                  position with an LDS atomic (lists are unordered inside a tile: k_tile_sort)
 // Count and emission walk the same ellipse rows, so a tile's count and its entries agree.
-constexpr uint32_t kBinMaxPP = 4096;  // projection partitions per binning partition (2^32 / 4096 / 256)
+constexpr uint32_t kBinMaxUnits = 4096;  // units per binning partition (scenes up to 2^28 Gaussians)
 
-// The slots of binning partition b: s_pref[k] = splats of its first k projection partitions
-// (b + j kBinParts, j < k); returns the total.  Contains barriers.
+__device__ __forceinline__ uint32_t bin_units(const BinParams& p, uint32_t b) {
+    const uint32_t units = p.parts * (uint32_t)kSortIPT;
+    return units > b ? (units - b + kBinParts - 1) / kBinParts : 0u;
+}
+
+// The slots of binning partition b: s_pref[k] = slots of its first k units; returns the total.
+// Contains barriers.
 __device__ uint32_t bin_slots(const BinParams& p, uint32_t b, uint32_t* s_pref, uint32_t* s_tmp) {
-    const uint32_t m = p.parts > b ? (p.parts - b + kBinParts - 1) / kBinParts : 0u;
+    const uint32_t m = min(bin_units(p, b), kBinMaxUnits);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    constexpr int per = kBinMaxPP / kBinThreads;
+    constexpr int per = kBinMaxUnits / kBinThreads;
     uint32_t c[per], sum = 0;
 #pragma unroll
     for (int k = 0; k < per; ++k) {
         const uint32_t j = (uint32_t)tid * per + k;
-        c[k] = j < m ? p.cnt[b + j * kBinParts] : 0u;
+        c[k] = 0;
+        if (j < m) {
+            const uint32_t u = b + j * kBinParts, part = u / kSortIPT, r0 = (u % kSortIPT) * kProjThreads;
+            const uint32_t cn = p.cnt[part];
+            c[k] = cn > r0 ? min(cn - r0, (uint32_t)kProjThreads) : 0u;
+        }
         sum += c[k];
     }
     const uint32_t incl = wave_incl_scan(sum);
@@ -1037,13 +1251,14 @@ __device__ uint32_t bin_slots(const BinParams& p, uint32_t b, uint32_t* s_pref, 
 
 // The r-th slot of binning partition b (r < total of bin_slots).
 __device__ __forceinline__ uint32_t bin_slot(const BinParams& p, uint32_t b, const uint32_t* s_pref, uint32_t r) {
-    const uint32_t m = p.parts > b ? (p.parts - b + kBinParts - 1) / kBinParts : 0u;
+    const uint32_t m = min(bin_units(p, b), kBinMaxUnits);
     uint32_t lo = 0, hi = m;  // largest k < m with s_pref[k] <= r
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (s_pref[mid] <= r) lo = mid; else hi = mid;
     }
-    const uint32_t part = b + lo * kBinParts, q = r - s_pref[lo];
+    const uint32_t u = b + lo * kBinParts, part = u / kSortIPT;
+    const uint32_t q = (u % kSortIPT) * kProjThreads + (r - s_pref[lo]);
     return p.chunk ? slot_c1(part, q) : slot_c0(part, q);
 }
 
@@ -1071,7 +1286,7 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
 
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     __shared__ uint32_t s_cnt[kBandTiles];
-    __shared__ uint32_t s_pref[kBinMaxPP + 1];
+    __shared__ uint32_t s_pref[kBinMaxUnits + 1];
     __shared__ uint32_t s_tmp[kBinThreads / 64];
     if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
     const uint32_t part = blockIdx.x % kBinParts, band = blockIdx.x / kBinParts;
@@ -1081,7 +1296,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     for (uint32_t r = threadIdx.x; r < total; r += kBinThreads) {
         const uint32_t g = bin_slot(p, part, s_pref, r);
         TileRect tr;
-        if (!rect_unpack(p, p.srect[g], p.skey[g].y, tr)) continue;
+        if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
         const float4* q = p.crec + 3 * (uint64_t)g;
         splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
     }
@@ -1181,7 +1396,7 @@ constexpr uint32_t kWideQueue = 512;
 
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_cur[kBandTiles];
-    __shared__ uint32_t s_pref[kBinMaxPP + 1];
+    __shared__ uint32_t s_pref[kBinMaxUnits + 1];
     __shared__ uint32_t s_tmp[kBinThreads / 64];
     __shared__ uint32_t s_wide[kWideQueue];
     __shared__ uint32_t s_nw;
@@ -1196,7 +1411,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     for (uint32_t r = threadIdx.x; r < total; r += kBinThreads) {
         const uint32_t g = bin_slot(p, part, s_pref, r);
         TileRect tr;
-        if (!rect_unpack(p, p.srect[g], p.skey[g].y, tr)) continue;
+        if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
         if (rect_wide(tr)) {
             const uint32_t qi = atomicAdd(&s_nw, 1u);
             if (qi < kWideQueue) {
@@ -1218,7 +1433,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     for (uint32_t qi = wave; qi < nq; qi += kBinThreads / 64) {  // wave-uniform
         const uint32_t g = s_wide[qi];
         TileRect tr;
-        rect_unpack(p, p.srect[g], p.skey[g].y, tr);
+        rect_unpack(p, p.srect[g], p.sidx[g], tr);
         const float4* q = p.crec + 3 * (uint64_t)g;
         const Ellipse e = ellipse_of(q[0], q[1]);
         const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
@@ -2007,21 +2222,37 @@ void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void
     const unsigned grid = (unsigned)std::min<uint64_t>(8192, (npx + 255) / 256);
     hipLaunchKernelGGL(k_present, dim3(grid), dim3(256), 0, s, in, in_f16, W, H, out_kind, out);
 }
-void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, float4* geo, float4* shade, float4* cull,
-                      hipStream_t s) {
+void launch_bbox(const uint8_t* aos, uint64_t n, uint32_t rb, uint32_t* bbox, hipStream_t s) {
     if (!n) return;
-    hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, aos, n, n_sh,
-                       geo, shade, cull);
+    const unsigned grid = (unsigned)std::min<uint64_t>(256, (n + 255) / 256);
+    hipLaunchKernelGGL(k_bbox, dim3(grid), dim3(256), 0, s, aos, n, rb, bbox);
+}
+void launch_morton(const uint8_t* aos, uint64_t n, uint32_t rb, const uint32_t* bbox, uint32_t* keys,
+                   uint32_t* vals, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_morton, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, aos, n, rb, bbox, keys, vals);
+}
+void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, const uint32_t* perm, float4* geo, float4* shade,
+                      float4* cull, uint32_t* orig, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_transpose, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, aos, n, n_sh, perm,
+                       geo, shade, cull, orig);
+}
+void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_part_bounds, dim3(sort_parts(n)), dim3(256), 0, s, cull, n, out);
 }
 void launch_project(const ProjParams& p, hipStream_t s) {
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, sort_parts(p.n)));
-    const unsigned cgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (p.n + 255) / 256));
-    hipLaunchKernelGGL(k_cull, dim3(cgrid), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(k_project, dim3(grid), dim3(kProjThreads), 0, s, p);
+    const uint32_t parts = sort_parts(p.n);
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, parts));
+    hipLaunchKernelGGL(k_cull, dim3(grid), dim3(kProjThreads), 0, s, p);
+    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (uint64_t)parts * kSortIPT));
+    hipLaunchKernelGGL(k_project, dim3(ugrid), dim3(kProjThreads), 0, s, p);
 }
 void launch_colour(const ProjParams& p, hipStream_t s) {
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, sort_parts(p.n)));
-    hipLaunchKernelGGL(k_colour, dim3(grid), dim3(256), 0, s, p);
+    const uint32_t parts = sort_parts(p.n);
+    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (uint64_t)parts * kSortIPT));
+    hipLaunchKernelGGL(k_colour, dim3(ugrid), dim3(256), 0, s, p);
 }
 void launch_records(const ProjParams& p, hipStream_t s) {
     if (!p.n) return;

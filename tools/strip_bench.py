@@ -23,13 +23,14 @@ def main():
     only = int(os.environ["STRIP"]) if "STRIP" in os.environ else None
     for G in gl:
         rows = strip_geometry(H, 0, G)[1]
-        buf = gs.DeviceBuffer(rows * W * 16)
+        buf = gs.DeviceBuffer((rows if G > 1 else H) * W * 16)
         worst = 0.0
         line = []
         for g in range(G):
             if only is not None and g != only:
                 continue
-            o = gs.make_opts(strip_index=g, strip_count=G, timing=1)
+            o = gs.make_opts(strip_index=g, strip_count=G, timing=int(os.environ.get("TIMING", "1")),
+                             out_format=gs.GS_OUT_RGBA_F16)
             for _ in range(5):
                 sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
             ctx.sync()
