@@ -119,6 +119,7 @@ uint32_t scaled_threshold(uint32_t k, float factor) {
 
 struct gs_ctx {
     int device = 0;
+    int num_cus = 256;            // k_chunk1's grid: one workgroup per CU
     hipStream_t stream = nullptr;
     void* d_out = nullptr;
     size_t d_out_bytes = 0;
@@ -153,6 +154,7 @@ struct gs_scene {
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     FrameCtl* ctl = nullptr;            // zero at a frame's start (k_frame_end clears it)
     StatShard* stats = nullptr;         // [kStatShards], zero at a frame's start (likewise)
+    uint32_t* bar = nullptr;            // k_chunk1's grid-barrier counter, zero at a frame's start
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tvA = nullptr, *tvB = nullptr;  // tile lists: unordered (binning), sorted
@@ -407,6 +409,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     if (!s->meta_clean) {
         HIPCHK(hipMemsetAsync(s->ctl, 0, sizeof(FrameCtl), st));
         HIPCHK(hipMemsetAsync(s->stats, 0, kStatShards * sizeof(StatShard), st));
+        HIPCHK(hipMemsetAsync(s->bar, 0, 16, st));
     }
     s->meta_clean = false;
     ProjParams pp{};
@@ -452,80 +455,85 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     launch_colour(pp, st);
     mark(EV_PROJ1);
 
-    // ---- per chunk: bin -> per-tile sort -> composite.  Chunk 1 (the splats at or past T that
-    // touch a tile chunk 0 left unsaturated) is enqueued with chunk 0 and gated on the device:
-    // every kernel of it returns at once when chunk 0 saturated every tile.
-    const size_t sat_words = (size_t)(tr_end - tr_begin + 1) * (TX + 1);
-    unsigned long long* unsat_mask = (unsigned long long*)(s->sat + ((sat_words + 1) & ~(size_t)1));
-    for (int chunk = 0; chunk < (two_chunks ? 2 : 1); ++chunk) {
-        const int eb = chunk == 0 ? EV_DSORT_0 : EV_DSORT_1;
-        if (chunk == 1) {
-            launch_sat(s->done, TX, tr_end - tr_begin, s->sat, unsat_mask, s->ctl, st);
-            ProjParams rp = pp;
-            rp.sat = s->sat;
-            rp.rec_all = 0;
-            launch_records(rp, st);
-        }
-        mark(eb);
-        BinParams bp{};
-        bp.skey = s->skey;
-        bp.sidx = s->sidx;
-        bp.srect = s->srect;
-        bp.cnt = chunk == 0 ? s->c0 : s->c1;
-        bp.parts = sort_parts(pp.n);
-        bp.rec = records(s);
-        bp.crec = s->crec;
-        bp.done = s->done;
-        bp.ctl = s->ctl;
-        bp.chunk = chunk;
-        bp.tile_row_begin = tr_begin;
-        bp.tiles_x = TX;
-        bp.capacity = (uint32_t)s->kcap;
-        bp.ranges = s->ranges;
-        bp.n_tiles = (uint32_t)n_tiles;
-        bp.bmat = s->bmat;
-        bp.tbase = s->tbase;
-        bp.tvals = s->tvA;
-        bp.rows = tr_end - tr_begin;
-        launch_bin(bp, st);
-        mark(eb + 1);
-        TileSortParams tsp{};  // each tile's list into (depth key, index) order
-        tsp.ranges = s->ranges;
-        tsp.in = s->tvA;
-        tsp.out = s->tvB;
-        tsp.skey = s->skey;
-        tsp.done = chunk == 1 ? s->done : nullptr;
-        tsp.n_tiles = n_tiles;
-        launch_tile_sort(tsp, st);
-        mark(eb + 2);
-        mark(eb + 3);
-
-        CompositeParams cp{};
-        cp.ranges = s->ranges;
-        cp.tvals = s->tvB;
-        cp.rec = s->crec;
-        cp.W = W;
-        cp.H = H;
-        cp.tiles_x = TX;
-        cp.tile_row_begin = tr_begin;
-        cp.row0 = sc > 1 ? tr_begin * kTile : 0;
-        cp.n_tiles = n_tiles;
-        cp.t_min = o.t_min;
-        cp.mode = !two_chunks ? kCompSingle : (chunk == 0 ? kCompFirst : kCompSecond);
-        cp.state = s->state;
-        cp.done = s->done;
-        cp.ctl = s->ctl;
-        cp.out = out;
-        cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
-        launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
-        mark(eb + 4);
+    // ---- chunk 0: bin -> per-tile sort -> composite.  Chunk 1 (the splats at or past T that
+    // touch a tile chunk 0 left unsaturated) is one cooperative launch enqueued behind it that
+    // returns at once when chunk 0 saturated every tile (k_chunk1).
+    BinParams bp{};
+    bp.skey = s->skey;
+    bp.sidx = s->sidx;
+    bp.srect = s->srect;
+    bp.cnt = s->c0;
+    bp.parts = sort_parts(pp.n);
+    bp.rec = records(s);
+    bp.crec = s->crec;
+    bp.done = s->done;
+    bp.ctl = s->ctl;
+    bp.chunk = 0;
+    bp.tile_row_begin = tr_begin;
+    bp.tiles_x = TX;
+    bp.capacity = (uint32_t)s->kcap;
+    bp.ranges = s->ranges;
+    bp.n_tiles = (uint32_t)n_tiles;
+    bp.bmat = s->bmat;
+    bp.tbase = s->tbase;
+    bp.tvals = s->tvA;
+    bp.rows = tr_end - tr_begin;
+    TileSortParams tsp{};  // each tile's list into (depth key, index) order
+    tsp.ranges = s->ranges;
+    tsp.in = s->tvA;
+    tsp.out = s->tvB;
+    tsp.skey = s->skey;
+    tsp.done = nullptr;
+    tsp.n_tiles = n_tiles;
+    CompositeParams cp{};
+    cp.ranges = s->ranges;
+    cp.tvals = s->tvB;
+    cp.rec = s->crec;
+    cp.W = W;
+    cp.H = H;
+    cp.tiles_x = TX;
+    cp.tile_row_begin = tr_begin;
+    cp.row0 = sc > 1 ? tr_begin * kTile : 0;
+    cp.n_tiles = n_tiles;
+    cp.t_min = o.t_min;
+    cp.mode = two_chunks ? kCompFirst : kCompSingle;
+    cp.state = s->state;
+    cp.done = s->done;
+    cp.ctl = s->ctl;
+    cp.out = out;
+    cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
+    mark(EV_DSORT_0);
+    launch_bin(bp, st);
+    mark(EV_BIN_0);
+    launch_tile_sort(tsp, st);
+    mark(EV_TSORT_0);
+    mark(EV_RANGES_0);
+    launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
+    mark(EV_COMP_0);
+    if (two_chunks) {
+        Chunk1Params c1{};
+        c1.pp = pp;
+        c1.pp.sat = s->sat;
+        c1.pp.rec_all = 0;
+        c1.bp = bp;
+        c1.bp.cnt = s->c1;
+        c1.bp.chunk = 1;
+        c1.tp = tsp;
+        c1.tp.done = s->done;
+        c1.cp = cp;
+        c1.cp.mode = kCompSecond;
+        c1.sat = s->sat;
+        c1.bar = s->bar;
+        for (int e = 0; e < 4; ++e) mark(EV_DSORT_1 + e);
+        launch_chunk1(c1, c->num_cus, o.accum == GS_ACCUM_FP16_TARGET, st);
+        mark(EV_COMP_1);
     }
     if (!two_chunks && o.timing == 1)
         for (int e = 0; e < 5; ++e) mark(EV_DSORT_1 + e);
     {  // statistics into the slot, FrameCtl zeroed for the next frame
         const uint32_t q = s->seq_next++;
         s->stat_want[slot] = q;
-        launch_frame_end(s->ctl, s->stats, s->d_ctl_slot + slot, s->d_seq + slot, q, st);
+        launch_frame_end(s->ctl, s->stats, s->bar, s->d_ctl_slot + slot, s->d_seq + slot, q, st);
     }
     s->meta_clean = true;
     mark(EV_END);
@@ -574,6 +582,10 @@ static size_t out_bytes_for(int W, int H, const gs_opts& o) {
 // Frame errors surface here: every frame's FrameCtl comes back asynchronously.
 static void check_frame_errors(gs_scene* s) {
     collect_stats(s, true);
+    if (s->have_last && (s->last.err & kErrBarrier)) {
+        s->last.err &= ~kErrBarrier;
+        throw GsError(GS_ERR_DEVICE_FAULT, "chunk-1 grid barrier timed out (workgroups not co-resident)");
+    }
     if (s->have_last && (s->last.err & kErrOverflow)) {
         s->last.err = 0;
         ensure_tile_capacity(s, s->last.k_total);
@@ -663,6 +675,9 @@ int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
         gs_ctx* c = new gs_ctx();
         c->device = dev;
         try {
+            int cus = 0;
+            HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            if (cus > 0) c->num_cus = cus;
             HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             for (auto& f : c->fe)
                 for (auto& e : f.ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -708,6 +723,8 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->crec, 3 * ((size_t)sort_parts(n) * kSortTile + 1));
             dev_alloc(s->ctl, 1);
             dev_alloc(s->stats, kStatShards);
+            dev_alloc(s->bar, 4);
+            HIPCHK(hipMemset(s->bar, 0, 16));
             // slots: part * kSortTile + q < sort_parts(n) * kSortTile
             const size_t nslots = (size_t)sort_parts(n) * kSortTile + 1;
             dev_alloc(s->skey, nslots);
@@ -781,6 +798,7 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->crec);
     dev_free(s->ctl);
     dev_free(s->stats);
+    dev_free(s->bar);
     dev_free(s->skey);
     dev_free(s->srect);
     dev_free(s->c0);
@@ -825,7 +843,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
         if (!out_dev) throw GsError(GS_ERR_INVALID, "null output");
         if (out_bytes < out_bytes_for(W, H, o)) throw GsError(GS_ERR_INVALID, "output buffer too small");
         HIPCHK(hipSetDevice(c->device));
-        if (s->have_last && (s->last.err & kErrOverflow)) check_frame_errors(s);
+        if (s->have_last && (s->last.err & (kErrOverflow | kErrBarrier))) check_frame_errors(s);
         hipStream_t st = stream ? (hipStream_t)stream : c->stream;
         render_frame(c, s, (const float*)uni, W, H, o, out_dev, st);
         return GS_OK;
@@ -869,6 +887,7 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
             render_frame(c, s, (const float*)uni, W, H, o, c->d_out, c->stream);
             HIPCHK(hipStreamSynchronize(c->stream));
             collect_stats(s, true);
+            if (s->last.err & kErrBarrier) check_frame_errors(s);
             if (!(s->last.err & kErrOverflow)) break;
             s->last.err = 0;
             if (attempt >= 2) throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded");

@@ -38,6 +38,7 @@ constexpr uint32_t kRectHole = 0xFFFFFFFDu;   // a composite slot whose candidat
 
 // Device-side error bits (FrameCtl::err); a nonzero word fails the frame.
 constexpr uint32_t kErrOverflow = 1u;
+constexpr uint32_t kErrBarrier = 2u;   // a grid barrier of k_chunk1 timed out
 
 struct FrameCtl {                 // zeroed at the start of every frame
     unsigned long long k_total;   // sum of tile counts over visible splats (project)
@@ -238,6 +239,15 @@ struct CompositeParams {
     int out_f16;
 };
 
+struct Chunk1Params {
+    ProjParams pp;                // records_body: chunk-1 slots (pp.sat = the SAT)
+    BinParams bp;                 // chunk 1
+    TileSortParams tp;
+    CompositeParams cp;           // mode kCompSecond
+    uint32_t* sat;                // SAT of the unsaturated tiles (written by the first phase)
+    uint32_t* bar;                // grid-barrier arrival counter, zero at launch (k_frame_end)
+};
+
 // launchers (gs_kernels.hip)
 void launch_bbox(const uint8_t* aos, uint64_t n, uint32_t rb, uint32_t* bbox, hipStream_t s);
 void launch_morton(const uint8_t* aos, uint64_t n, uint32_t rb, const uint32_t* bbox, uint32_t* keys,
@@ -251,10 +261,11 @@ void launch_colour(const ProjParams& p, hipStream_t s);   // colours of the chun
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit, wide rows
 // stats -> host slot + seq; then FrameCtl zeroed for the next frame
-void launch_frame_end(FrameCtl* ctl, StatShard* stats, FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq,
-                      hipStream_t s);
-void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
-                const FrameCtl* ctl, hipStream_t s);
+void launch_frame_end(FrameCtl* ctl, StatShard* stats, uint32_t* bar, FrameCtl* host_ctl, uint32_t* host_seq,
+                      uint32_t seq, hipStream_t s);
+// chunk 1 in one launch (grid: one workgroup per CU; returns at once when chunk 0 saturated every tile)
+struct Chunk1Params;
+void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t s);
 void launch_tile_sort(const TileSortParams& p, hipStream_t s);
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);
 void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void* out, hipStream_t s);

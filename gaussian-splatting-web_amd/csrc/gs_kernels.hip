@@ -533,13 +533,12 @@ __device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, u
 // are projected; the visible ones whose rect touches an unsaturated tile (the SAT of k_sat) get a
 // chunk-1 slot (slot_c1) with their record and colour.  Waves cover 64 consecutive Gaussians of
 // one projection partition: one counter add per wave.
-__global__ __launch_bounds__(256) void k_records(ProjParams p) {
-    if (!p.rec_all && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
+__device__ void records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
     const uint32_t lane = lane_id();
-    for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < p.n; i0 += gridDim.x * blockDim.x) {
+    for (uint32_t i0 = blk * blockDim.x + (threadIdx.x & ~63u); i0 < p.n; i0 += nblk * blockDim.x) {
         const uint32_t i = i0 + lane;
         bool want = false;
         float vz;
@@ -590,6 +589,11 @@ __global__ __launch_bounds__(256) void k_records(ProjParams p) {
             p.crec[3 * (uint64_t)slot + 2] = c;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_records(ProjParams p) {
+    if (!p.rec_all && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
+    records_body(p, blockIdx.x, gridDim.x);
 }
 
 // Can a Gaussian of partition b be a chunk-0 candidate of this frame (pass cull_keep with key <
@@ -1215,10 +1219,11 @@ __device__ __forceinline__ uint32_t bin_units(const BinParams& p, uint32_t b) {
 
 // The slots of binning partition b: s_pref[k] = slots of its first k units; returns the total.
 // Contains barriers.
+template <int NT>
 __device__ uint32_t bin_slots(const BinParams& p, uint32_t b, uint32_t* s_pref, uint32_t* s_tmp) {
     const uint32_t m = min(bin_units(p, b), kBinMaxUnits);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    constexpr int per = kBinMaxUnits / kBinThreads;
+    constexpr int per = kBinMaxUnits / NT;
     uint32_t c[per], sum = 0;
 #pragma unroll
     for (int k = 0; k < per; ++k) {
@@ -1235,7 +1240,7 @@ __device__ uint32_t bin_slots(const BinParams& p, uint32_t b, uint32_t* s_pref, 
     if (lane == 63) s_tmp[w] = incl;
     __syncthreads();
     uint32_t base = incl - sum, total = 0;
-    for (int i = 0; i < kBinThreads / 64; ++i) {
+    for (int i = 0; i < NT / 64; ++i) {
         if (i < w) base += s_tmp[i];
         total += s_tmp[i];
     }
@@ -1284,16 +1289,14 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
     }
 }
 
-__global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
-    __shared__ uint32_t s_cnt[kBandTiles];
-    __shared__ uint32_t s_pref[kBinMaxUnits + 1];
-    __shared__ uint32_t s_tmp[kBinThreads / 64];
-    if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
-    const uint32_t part = blockIdx.x % kBinParts, band = blockIdx.x / kBinParts;
+// Binning partition / band vb: counts of its splats' entries per tile of the band -> bmat row.
+template <int NT>
+__device__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp) {
+    const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
-    for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += kBinThreads) s_cnt[t] = 0;
-    const uint32_t total = bin_slots(p, part, s_pref, s_tmp);
-    for (uint32_t r = threadIdx.x; r < total; r += kBinThreads) {
+    for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += NT) s_cnt[t] = 0;
+    const uint32_t total = bin_slots<NT>(p, part, s_pref, s_tmp);
+    for (uint32_t r = threadIdx.x; r < total; r += NT) {
         const uint32_t g = bin_slot(p, part, s_pref, r);
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
@@ -1302,7 +1305,16 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     }
     __syncthreads();
     uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
-    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += kBinThreads) row[t] = s_cnt[t - t_lo];
+    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) row[t] = s_cnt[t - t_lo];
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
+    __shared__ uint32_t s_cnt[kBandTiles];
+    __shared__ uint32_t s_pref[kBinMaxUnits + 1];
+    __shared__ uint32_t s_tmp[kBinThreads / 64];
+    if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
+    bin_count_body<kBinThreads>(p, blockIdx.x, s_cnt, s_pref, s_tmp);
 }
 
 // Per tile: exclusive prefix of its column of bmat over the partitions (in place) and the tile's
@@ -1317,11 +1329,9 @@ __device__ __forceinline__ uint32_t colscan_part(uint32_t q) {  // q-th partitio
     return (q % (kBinParts / 8)) * 8 + q / (kBinParts / 8);
 }
 
-__global__ __launch_bounds__(256) void k_bin_colscan(BinParams p) {
-    __shared__ uint32_t s_sum[4][kColTiles];
-    if (p.chunk == 1 && p.ctl->not_done == 0) return;
+__device__ void colscan_body(const BinParams& p, uint32_t vb, uint32_t (*s_sum)[kColTiles]) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t t = blockIdx.x * kColTiles + lane;
+    const uint32_t t = vb * kColTiles + lane;
     const bool ok = t < p.n_tiles;
     uint32_t v[kColRows], sum = 0;
 #pragma unroll
@@ -1333,28 +1343,35 @@ __global__ __launch_bounds__(256) void k_bin_colscan(BinParams p) {
     __syncthreads();
     uint32_t run = 0;
     for (int i = 0; i < w; ++i) run += s_sum[i][lane];
-    if (!ok) return;
+    if (ok) {
 #pragma unroll
-    for (int k = 0; k < kColRows; ++k) {
-        p.bmat[(uint64_t)colscan_part(w * kColRows + k) * p.n_tiles + t] = run;
-        run += v[k];
+        for (int k = 0; k < kColRows; ++k) {
+            p.bmat[(uint64_t)colscan_part(w * kColRows + k) * p.n_tiles + t] = run;
+            run += v[k];
+        }
+        if (w == 3) p.tbase[t] = run;
     }
-    if (w == 3) p.tbase[t] = run;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_bin_colscan(BinParams p) {
+    __shared__ uint32_t s_sum[4][kColTiles];
+    if (p.chunk == 1 && p.ctl->not_done == 0) return;
+    colscan_body(p, blockIdx.x, s_sum);
 }
 
 // One workgroup: exclusive scan of the tile totals in tile order -> ranges [begin, end) and
 // tbase = begin; the chunk's totals.
 constexpr int kScanThreads = 1024;
 
-__global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
-    __shared__ uint32_t s_w[kScanThreads / 64];
-    if (p.chunk == 1 && p.ctl->not_done == 0) return;
+template <int NT>
+__device__ void tile_scan_body(const BinParams& p, uint32_t* s_w) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    constexpr int nw = kScanThreads / 64;
+    constexpr int nw = NT / 64;
     constexpr int ipt = 8;
     const uint32_t cap = p.capacity;
     uint32_t carry = 0;
-    for (uint32_t t0 = 0; t0 < p.n_tiles; t0 += kScanThreads * ipt) {
+    for (uint32_t t0 = 0; t0 < p.n_tiles; t0 += NT * ipt) {
         uint32_t v[ipt], sum = 0;
 #pragma unroll
         for (int k = 0; k < ipt; ++k) {
@@ -1389,26 +1406,29 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
     }
 }
 
+__global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
+    __shared__ uint32_t s_w[kScanThreads / 64];
+    if (p.chunk == 1 && p.ctl->not_done == 0) return;
+    tile_scan_body<kScanThreads>(p, s_w);
+}
+
 // Wide splats (>= kWideTiles box tiles) are queued in LDS by the thread that meets them and
 // emitted row by row by whole waves (lanes over columns); the queue holds kWideQueue splats,
 // beyond that the thread emits its splat itself.
 constexpr uint32_t kWideQueue = 512;
 
-__global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
-    __shared__ uint32_t s_cur[kBandTiles];
-    __shared__ uint32_t s_pref[kBinMaxUnits + 1];
-    __shared__ uint32_t s_tmp[kBinThreads / 64];
-    __shared__ uint32_t s_wide[kWideQueue];
-    __shared__ uint32_t s_nw;
-    if (p.chunk == 1 && p.ctl->not_done == 0) return;
-    const uint32_t part = blockIdx.x % kBinParts, band = blockIdx.x / kBinParts;
+template <int NT>
+__device__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, uint32_t* s_pref, uint32_t* s_tmp,
+                              uint32_t* s_wide, uint32_t* s_nw_p) {
+    uint32_t& s_nw = *s_nw_p;
+    const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
     const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
-    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += kBinThreads) s_cur[t - t_lo] = p.tbase[t] + row[t];
+    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) s_cur[t - t_lo] = p.tbase[t] + row[t];
     if (threadIdx.x == 0) s_nw = 0;
-    const uint32_t total = bin_slots(p, part, s_pref, s_tmp);
+    const uint32_t total = bin_slots<NT>(p, part, s_pref, s_tmp);
     const uint32_t cap = p.capacity;
-    for (uint32_t r = threadIdx.x; r < total; r += kBinThreads) {
+    for (uint32_t r = threadIdx.x; r < total; r += NT) {
         const uint32_t g = bin_slot(p, part, s_pref, r);
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
@@ -1430,7 +1450,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     if (threadIdx.x == 0 && s_nw) atomicAdd(&p.ctl->wide_n[p.chunk], s_nw);  // statistics
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
-    for (uint32_t qi = wave; qi < nq; qi += kBinThreads / 64) {  // wave-uniform
+    for (uint32_t qi = wave; qi < nq; qi += NT / 64) {  // wave-uniform
         const uint32_t g = s_wide[qi];
         TileRect tr;
         rect_unpack(p, p.srect[g], p.sidx[g], tr);
@@ -1451,6 +1471,17 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
             }
         }
     }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
+    __shared__ uint32_t s_cur[kBandTiles];
+    __shared__ uint32_t s_pref[kBinMaxUnits + 1];
+    __shared__ uint32_t s_tmp[kBinThreads / 64];
+    __shared__ uint32_t s_wide[kWideQueue];
+    __shared__ uint32_t s_nw;
+    if (p.chunk == 1 && p.ctl->not_done == 0) return;
+    bin_emit_body<kBinThreads>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, &s_nw);
 }
 
 // End of a frame: the statistic shards summed into FrameCtl (and zeroed), the saturation
@@ -1458,13 +1489,14 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
 // host's pinned slot (mapped, fine-grained) and the sequence number published with a
 // system-scope release; the host reads it a frame or two later.  Then FrameCtl is zeroed for the
 // next frame.  One wave; lane l sums shard l.
-__global__ __launch_bounds__(64) void k_frame_end(FrameCtl* ctl, StatShard* stats, FrameCtl* host_ctl,
+__global__ __launch_bounds__(64) void k_frame_end(FrameCtl* ctl, StatShard* stats, uint32_t* bar, FrameCtl* host_ctl,
                                                  uint32_t* host_seq, uint32_t seq) {
     constexpr uint32_t kWords = sizeof(FrameCtl) / 4;
     static_assert(kWords <= 64 && kStatShards == 64, "one wave");
     const uint32_t lane = threadIdx.x;
     StatShard sh = stats[lane];
     stats[lane] = StatShard{};
+    if (lane == 0) *bar = 0u;  // k_chunk1's barrier counter
     unsigned long long kt = sh.k_total;
     uint32_t nv = sh.n_vis, kmi = sh.key_min_inv, kma = sh.key_max, c0 = sh.n_chunk[0], c1 = sh.n_chunk[1];
     for (int d = 32; d >= 1; d >>= 1) {
@@ -1497,19 +1529,17 @@ __global__ __launch_bounds__(64) void k_frame_end(FrameCtl* ctl, StatShard* stat
     if (lane < kWords) src[lane] = 0u;
 }
 
-// Summed-area table and bitmask of the tiles chunk 0 left unsaturated (done == 0): one
-// workgroup; row prefixes by waves, then column prefixes by threads, in LDS when the table fits.
-__global__ __launch_bounds__(1024) void k_sat(const uint8_t* __restrict__ done, int tiles_x, int rows,
-                                              uint32_t* __restrict__ sat,
-                                              unsigned long long* __restrict__ mask, const FrameCtl* ctl) {
-    __shared__ uint32_t s_sat[kSatMaxWords];
-    if (ctl->not_done == 0) return;  // every tile saturated: chunk 1 is empty and never reads it
+// Summed-area table of the tiles chunk 0 left unsaturated (done == 0): one workgroup of NT
+// threads; row prefixes by waves, then column prefixes by threads, in `lds` when given and the
+// table fits, else in place in `sat`.
+template <int NT>
+__device__ void sat_body(const uint8_t* __restrict__ done, int tiles_x, int rows, uint32_t* __restrict__ sat,
+                         uint32_t* lds) {
     const uint32_t sw = (uint32_t)tiles_x + 1, words = sw * (uint32_t)(rows + 1);
-    const int mw = (tiles_x + 63) / 64;
-    uint32_t* t = words <= (uint32_t)kSatMaxWords ? s_sat : sat;
+    uint32_t* t = (lds && words <= (uint32_t)kSatMaxWords) ? lds : sat;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    for (uint32_t x = tid; x < sw; x += 1024) t[x] = 0;
-    for (int r = w; r < rows; r += 16) {
+    for (uint32_t x = tid; x < sw; x += NT) t[x] = 0;
+    for (int r = w; r < rows; r += NT / 64) {
         uint32_t* row = t + (uint64_t)(r + 1) * sw;
         uint32_t run = 0;
         if (lane == 0) row[0] = 0;
@@ -1517,14 +1547,13 @@ __global__ __launch_bounds__(1024) void k_sat(const uint8_t* __restrict__ done, 
             const int x = x0 + lane;
             const uint32_t v = (x < tiles_x && !done[(uint64_t)r * tiles_x + x]) ? 1u : 0u;
             const uint64_t b = __ballot(v);
-            if (lane == 0) mask[(uint64_t)r * mw + (x0 >> 6)] = b;
             const uint32_t incl = run + __popcll(b & ((lanemask_lt() << 1) | 1ull));
             if (x < tiles_x) row[x + 1] = incl;
             run += __popcll(b);
         }
     }
     __syncthreads();
-    for (uint32_t x = tid; x < sw; x += 1024) {
+    for (uint32_t x = tid; x < sw; x += NT) {
         uint32_t acc = 0;
         for (int r = 1; r <= rows; ++r) {
             acc += t[(uint64_t)r * sw + x];
@@ -1532,11 +1561,10 @@ __global__ __launch_bounds__(1024) void k_sat(const uint8_t* __restrict__ done, 
         }
     }
     __syncthreads();
-    if (t == s_sat)
-        for (uint32_t q = tid; q < words; q += 1024) sat[q] = s_sat[q];
+    if (t != sat)
+        for (uint32_t q = tid; q < words; q += NT) sat[q] = t[q];
 }
 
-// ============================================================================ k_ranges
 // ============================================================================ k_tile_sort
 // One workgroup per tile orders the tile's list by key (the slot itself, or (skey.x, skey.y)),
 // ascending; keys are unique.  Lists of up to kTsCap entries are sorted in one round: 1024
@@ -1671,10 +1699,9 @@ __device__ void ts_segment(TsShared& S, const unsigned long long (&k)[kTsIpt], c
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kTsThreads) void k_tile_sort(TileSortParams p) {
-    __shared__ TsShared S;
+__device__ void tile_sort_body(const TileSortParams& p, uint32_t vb, TsShared& S) {
     const int per = (p.n_tiles + 7) >> 3;  // XCD-banded, as k_composite
-    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    const int tile = (int)(vb & 7) * per + (int)(vb >> 3);
     if (tile >= p.n_tiles) return;
     if (p.done && p.done[tile]) return;
     const uint2 range = p.ranges[tile];
@@ -1785,6 +1812,11 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(TileSortParams p) {
         done_n += nc;
         lo = hi;
     }
+}
+
+__global__ __launch_bounds__(kTsThreads) void k_tile_sort(TileSortParams p) {
+    __shared__ TsShared S;
+    tile_sort_body(p, blockIdx.x, S);
 }
 
 // ============================================================================ k_composite
@@ -2013,15 +2045,22 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
 // slowest tile's chain when there are too few tiles to fill the chip.
 constexpr int kCompBatchQ = 256;
 
+struct CompQShared {
+    float4 sR[2][kCompBatchQ][3];
+    uint8_t sL[2][4][kCompBatchQ];  // per quarter: batch indices, segment = producing wave
+    uint32_t sN[2][4][4];           // per quarter, per producing wave: list length
+    uint32_t s_sat;
+};
+
 template <bool FP16_TARGET>
-__global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
-    __shared__ float4 sR[2][kCompBatchQ][3];
-    __shared__ uint8_t sL[2][4][kCompBatchQ];  // per quarter: batch indices, segment = producing wave
-    __shared__ uint32_t sN[2][4][4];           // per quarter, per producing wave: list length
-    __shared__ uint32_t s_sat;
+__device__ void composite_q_body(const CompositeParams& p, uint32_t vb, CompQShared& S) {
+    auto& sR = S.sR;
+    auto& sL = S.sL;
+    auto& sN = S.sN;
+    uint32_t& s_sat = S.s_sat;
     const int tid = threadIdx.x;
     const int per = (p.n_tiles + 7) >> 3;
-    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    const int tile = (int)(vb & 7) * per + (int)(vb >> 3);
     if (tile >= p.n_tiles) return;
     if (p.mode == kCompSecond && p.done[tile]) return;
     const int qw = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -2178,6 +2217,77 @@ __global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
     }
 }
 
+template <bool FP16_TARGET>
+__global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
+    __shared__ CompQShared S;
+    composite_q_body<FP16_TARGET>(p, blockIdx.x, S);
+}
+
+// ============================================================================ k_chunk1
+// Chunk 1 as ONE launch.  It has work only in frames where chunk 0 left a tile unsaturated, so
+// its usual cost is this launch returning at once (eight gated launches cost ~35 us of floors).
+// When it runs, it is the chunk-0 pipeline's phases in order, separated by grid barriers, on a
+// grid of one 256-thread workgroup per CU (every workgroup co-resident): SAT of the unsaturated
+// tiles -> chunk-1 slots (records_body) -> bin count -> column scan -> tile scan -> emission ->
+// per-tile sort -> composite (kCompSecond) of the unsaturated tiles.
+
+// Grid barrier number k (k = 1, 2, ...): a monotonic arrival counter (zero at launch) reaches
+// k * G.  Release / acquire at agent scope (cdna_hip_programming.md Guideline 16); bounded spin.
+__device__ __forceinline__ void grid_sync(uint32_t* cnt, uint32_t target, FrameCtl* ctl) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t spins = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+            if (++spins > (1u << 26)) {
+                atomicOr(&ctl->err, kErrBarrier);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+constexpr size_t kBinLdsWords = kBandTiles + (kBinMaxUnits + 1) + 4 + kWideQueue + 1;
+constexpr size_t kChunk1Lds = std::max(std::max(kBinLdsWords * 4, sizeof(TsShared)), sizeof(CompQShared));
+
+template <bool FP16_TARGET>
+__global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kChunk1Lds];
+    FrameCtl* ctl = c.cp.ctl;
+    if (ctl->not_done == 0) return;  // chunk 0 saturated every tile
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    uint32_t nb = 0;
+    if (b == 0) sat_body<256>(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat, nullptr);
+    grid_sync(c.bar, ++nb * G, ctl);
+    records_body(c.pp, b, G);
+    grid_sync(c.bar, ++nb * G, ctl);
+    uint32_t* s_a = (uint32_t*)lds;
+    uint32_t* s_pref = s_a + kBandTiles;
+    uint32_t* s_tmp = s_pref + kBinMaxUnits + 1;
+    uint32_t* s_wide = s_tmp + 4;
+    uint32_t* s_nw = s_wide + kWideQueue;
+    const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles);
+    for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256>(c.bp, vb, s_a, s_pref, s_tmp);
+    grid_sync(c.bar, ++nb * G, ctl);
+    const uint32_t ncol = (c.bp.n_tiles + kColTiles - 1) / kColTiles;
+    for (uint32_t vb = b; vb < ncol; vb += G) colscan_body(c.bp, vb, (uint32_t(*)[kColTiles])lds);
+    grid_sync(c.bar, ++nb * G, ctl);
+    if (b == 0) tile_scan_body<256>(c.bp, s_a);
+    grid_sync(c.bar, ++nb * G, ctl);
+    for (uint32_t vb = b; vb < nbin; vb += G) bin_emit_body<256>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
+    grid_sync(c.bar, ++nb * G, ctl);
+    const uint32_t ntb = 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
+    for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body(c.tp, vb, *(TsShared*)lds);
+    grid_sync(c.bar, ++nb * G, ctl);
+    for (uint32_t vb = b; vb < ntb; vb += G) composite_q_body<FP16_TARGET>(c.cp, vb, *(CompQShared*)lds);
+}
+
 // ============================================================================ k_present
 // PostProcessRenderer.fragmentMain (src/post_process_render.ts:62-77) per pixel: the sampler
 // reads texel (x, H-1-y) at its centre (exact), a' = saturate(1.5 a), a' = a'^4 (as (a'^2)^2,
@@ -2291,13 +2401,16 @@ void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
     hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(kTsThreads), 0, s, p);
 }
-void launch_frame_end(FrameCtl* ctl, StatShard* stats, FrameCtl* host_ctl, uint32_t* host_seq, uint32_t seq,
-                      hipStream_t s) {
-    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, ctl, stats, host_ctl, host_seq, seq);
+void launch_frame_end(FrameCtl* ctl, StatShard* stats, uint32_t* bar, FrameCtl* host_ctl, uint32_t* host_seq,
+                      uint32_t seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, ctl, stats, bar, host_ctl, host_seq, seq);
 }
-void launch_sat(const uint8_t* done, int tiles_x, int rows, uint32_t* sat, unsigned long long* mask,
-                const FrameCtl* ctl, hipStream_t s) {
-    hipLaunchKernelGGL(k_sat, dim3(1), dim3(1024), 0, s, done, tiles_x, rows, sat, mask, ctl);
+void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t s) {
+    if (c.cp.n_tiles <= 0) return;
+    if (accum_fp16)
+        hipLaunchKernelGGL(k_chunk1<true>, dim3(grid), dim3(256), 0, s, c);
+    else
+        hipLaunchKernelGGL(k_chunk1<false>, dim3(grid), dim3(256), 0, s, c);
 }
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;
