@@ -148,6 +148,8 @@ struct gs_scene {
     uint32_t* srect = nullptr;
     uint32_t *c0 = nullptr, *c1 = nullptr;  // [parts]: slots per projection partition and chunk
     uint16_t* cand = nullptr;           // chunk-0 candidates per partition (k_cull): offsets
+    uint32_t* units = nullptr;          // the frame's non-empty chunk-0 work units (k_cull)
+    uint32_t* plist = nullptr;          // the frame's surviving projection partitions (k_part_cull)
     PartBound* bounds = nullptr;        // [parts] partition bounds (upload)
     uint32_t* orig = nullptr;           // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx = nullptr;           // [slots] storage index of each composite slot
@@ -447,12 +449,13 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.c0 = s->c0;
     pp.c1 = s->c1;
     pp.cand = s->cand;
+    pp.units = s->units;
+    pp.plist = s->plist;
     pp.bounds = s->bounds;
     pp.orig = s->orig;
     pp.sidx = s->sidx;
     mark(EV_PROJ0);
     launch_project(pp, st);
-    launch_colour(pp, st);
     mark(EV_PROJ1);
 
     // ---- chunk 0: bin -> per-tile sort -> composite.  Chunk 1 (the splats at or past T that
@@ -463,7 +466,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     bp.sidx = s->sidx;
     bp.srect = s->srect;
     bp.cnt = s->c0;
-    bp.parts = sort_parts(pp.n);
+    bp.parts = proj_parts(pp.n);
+    bp.units = s->units;
     bp.rec = records(s);
     bp.crec = s->crec;
     bp.done = s->done;
@@ -517,6 +521,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.pp.rec_all = 0;
         c1.bp = bp;
         c1.bp.cnt = s->c1;
+        c1.bp.units = nullptr;  // chunk 1: every unit
         c1.bp.chunk = 1;
         c1.tp = tsp;
         c1.tp.done = s->done;
@@ -720,19 +725,21 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->shade, (size_t)shade_stride(n_sh) * std::max<uint64_t>(n, 1));
             dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
-            dev_alloc(s->crec, 3 * ((size_t)sort_parts(n) * kSortTile + 1));
+            dev_alloc(s->crec, 3 * ((size_t)proj_parts(n) * kProjTile + 1));
             dev_alloc(s->ctl, 1);
             dev_alloc(s->stats, kStatShards);
             dev_alloc(s->bar, 4);
             HIPCHK(hipMemset(s->bar, 0, 16));
-            // slots: part * kSortTile + q < sort_parts(n) * kSortTile
-            const size_t nslots = (size_t)sort_parts(n) * kSortTile + 1;
+            // slots: part * kProjTile + q < proj_parts(n) * kProjTile
+            const size_t nslots = (size_t)proj_parts(n) * kProjTile + 1;
             dev_alloc(s->skey, nslots);
             dev_alloc(s->srect, nslots);
-            dev_alloc(s->c0, (size_t)sort_parts(n) + 1);
-            dev_alloc(s->c1, (size_t)sort_parts(n) + 1);
+            dev_alloc(s->c0, (size_t)proj_parts(n) + 1);
+            dev_alloc(s->c1, (size_t)proj_parts(n) + 1);
+            dev_alloc(s->units, (size_t)kUnitShards * unit_shard_cap(proj_parts(n)) + 1);
+            dev_alloc(s->plist, (size_t)proj_parts(n) + kUnitShards + 1);
             dev_alloc(s->cand, nslots);
-            dev_alloc(s->bounds, (size_t)sort_parts(n) + 1);
+            dev_alloc(s->bounds, (size_t)proj_parts(n) + 1);
             dev_alloc(s->orig, (size_t)n + 1);
             dev_alloc(s->sidx, nslots);
             const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
@@ -804,6 +811,8 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->c0);
     dev_free(s->c1);
     dev_free(s->cand);
+    dev_free(s->units);
+    dev_free(s->plist);
     dev_free(s->bounds);
     dev_free(s->orig);
     dev_free(s->sidx);
@@ -989,12 +998,12 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
 // then chunk 1.
 static std::vector<std::array<uint32_t, 3>> frame_slots(gs_scene* s) {
     collect_stats(s, true);
-    const uint32_t parts = sort_parts(s->n);
+    const uint32_t parts = proj_parts(s->n);
     std::vector<std::array<uint32_t, 3>> out;
     if (!parts) return out;
     std::vector<uint32_t> c0(parts), c1(parts);
-    std::vector<uint2> sk((size_t)parts * kSortTile);
-    std::vector<uint32_t> rect((size_t)parts * kSortTile);
+    std::vector<uint2> sk((size_t)parts * kProjTile);
+    std::vector<uint32_t> rect((size_t)parts * kProjTile);
     HIPCHK(hipMemcpy(rect.data(), s->srect, rect.size() * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(c0.data(), s->c0, parts * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(c1.data(), s->c1, parts * 4, hipMemcpyDeviceToHost));
@@ -1061,7 +1070,7 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
         }
         // colour words [8, 11): from the composite record of each slot of the frame
         if (!sl.empty()) {
-            const size_t ns = (size_t)sort_parts(s->n) * kSortTile;
+            const size_t ns = (size_t)proj_parts(s->n) * kProjTile;
             std::vector<float> cr(ns * 12);
             HIPCHK(hipMemcpy(cr.data(), s->crec, ns * 48, hipMemcpyDeviceToHost));
             for (const auto& e : sl)

@@ -16,6 +16,9 @@ constexpr int kTile = 16;             // 16x16-pixel composite tile
 constexpr int kProjThreads = 256;  // = kSortThreads: k_project works on radix partitions
 constexpr int kSortThreads = 256;     // 4 waves
 constexpr int kSortIPT = 16;          // items per thread
+constexpr int kProjTile = 1024;       // projection partition: bounds, candidates, slot block
+constexpr int kProjRounds = kProjTile / kProjThreads;  // work units (rounds of kProjThreads) per partition
+constexpr int kUnitShards = 8;        // the frame's work-unit list, sharded (FrameCtl::unit_n)
 constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per radix partition
 constexpr int kBinThreads = 1024;     // binning workgroup (one partition of the chunk's ranks)
 constexpr int kBinParts = 256;        // binning partitions per chunk (rows of BinParams::bmat)
@@ -51,6 +54,8 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t key_min_inv;         // ~(smallest depth key of a visible splat) (project)
     uint32_t key_max;             // largest depth key of a visible splat (project)
     uint32_t sat_key;             // depth key of the farthest splat a tile saturated at (k_frame_end)
+    uint32_t unit_n[kUnitShards]; // chunk-0 work units per shard (k_cull; see ProjParams::units)
+    uint32_t part_n[kUnitShards]; // surviving projection partitions per shard (k_part_cull)
     uint32_t sat_key_shard[kHistShards];  // per shard: the same, max over the shard's tiles
     uint32_t sat_tiles[kHistShards];      // per shard: tiles saturated by the end of the frame
 };
@@ -73,33 +78,36 @@ struct PartBound {
     uint32_t nfin;
 };
 
-// Composite slots.  k_project gives the chunk-0 splats of projection partition `part` (kSortTile
-// Gaussians) the slots part * kSortTile + q, q < c0[part] (in arrival order); k_records gives the
-// chunk-1 splats of that partition part * kSortTile + kSortTile - 1 - q, q < c1[part].  A
-// Gaussian is in at most one chunk, so the two never meet.  Per slot: the composite record
-// (3 float4), skey = (depth key, Gaussian index) (the per-tile sort key: ties in depth fall back
-// to the index, as the reference's stable sort over index-ordered slots) and the packed rect.
-__host__ __device__ inline uint32_t slot_c0(uint32_t part, uint32_t q) { return part * (uint32_t)kSortTile + q; }
+// Composite slots.  k_project gives the chunk-0 splats of projection partition `part` (kProjTile
+// storage slots) the slots part * kProjTile + q, q < c0[part] (q = the candidate's position in
+// the partition's list; an invisible candidate leaves a hole); k_records gives the chunk-1
+// splats of that partition part * kProjTile + kProjTile - 1 - q, q < c1[part].  A Gaussian is in
+// at most one chunk, so the two never meet.  Per slot: the composite record (3 float4),
+// skey = (depth key, reference index) (the per-tile sort key: ties in depth fall back to the
+// index, as the reference's stable sort over index-ordered slots), the storage index and the
+// packed rect.  Work unit u = part * kProjRounds + round covers slots round * kProjThreads ..
+// (+ kProjThreads) of the partition.
+__host__ __device__ inline uint32_t proj_parts(uint64_t n) { return (uint32_t)((n + kProjTile - 1) / kProjTile); }
+__host__ __device__ inline uint32_t slot_c0(uint32_t part, uint32_t q) { return part * (uint32_t)kProjTile + q; }
 __host__ __device__ inline uint32_t slot_c1(uint32_t part, uint32_t q) {
-    return part * (uint32_t)kSortTile + (uint32_t)kSortTile - 1u - q;
+    return part * (uint32_t)kProjTile + (uint32_t)kProjTile - 1u - q;
+}
+__host__ __device__ inline uint32_t unit_shard_cap(uint32_t parts) {
+    return (parts + kUnitShards - 1) / kUnitShards * kProjRounds;
 }
 
-// Scene layout in HBM: a 48-B geometry record per Gaussian (3 float4: x, y, z, opacity logit |
-// scale xyz, rot.x | rot.y, rot.z, rot.w, 0) read by k_project (streamed, or gathered for the
-// survivors of the cull), a 16-B cull plane (x, y, z, ||R(q) diag(s)||_F^2), and one
-// shading block per Gaussian [x, y, z, sh[k][c] at 3 + 3k + c] of shade_stride float4 (a power
-// of two, so a block never straddles more 128-B lines than it must; 256 B at SH degree 3).
-// The frame's projected record of Gaussian j (k_project stores it for the chunk-0 splats,
-// k_records for the chunk-1 splats it needs):
+// Scene layout in HBM (storage slots in Morton order, orig[] = reference index): a 48-B
+// geometry record per Gaussian (3 float4: x, y, z, opacity logit | scale xyz, rot.x | rot.y,
+// rot.z, rot.w, 0) gathered by k_project for the chunk-0 candidates, a 16-B cull plane (x, y, z,
+// ||R(q) diag(s)||_F^2) streamed by k_cull, and one shading block per Gaussian [x, y, z,
+// sh[k][c] at 3 + 3k + c] of shade_stride float4 (a power of two, so a block never straddles more
+// 128-B lines than it must; 256 B at SH degree 3), read by k_colour.
+// The per-Gaussian record of Gaussian j (debug dump and chunk-1 bookkeeping):
 //   r01 = quads shade_quads(n_sh), +1 of j's shading block (its padding): cx, cy, e1x', e1y' |
 //         e2x', e2y', log2(op), pixel box x (centre in pixels; quad axes e/|e|^2 * sqrt(log2 e);
-//         box x0 | x1 << 16, u32 bits)
-//   colour = quad shade_quads(n_sh) + 2: r, g, b, 0 (SH at the frame's view direction), stored
-//         with r01, so k_shade gathers one 48-B record per splat
+//         box x0 | x1 << 16, u32 bits); colour at quad shade_quads(n_sh) + 2 (rec_all only)
 //   r2[j] = depth key, tile count, pixel box x, pixel box y (u32 bits), dense
-// Composite record, 3 float4 per depth rank of the chunk at slot g = chunk base + rank (written
-// by k_shade before the binning, which reads it; the tile lists hold g):
-//   [0], [1], [2] = the r01 quads and the colour
+// Composite record, 3 float4 per slot: [0], [1] = the r01 quads, [2] = r, g, b, depth key bits.
 __host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
 __host__ __device__ inline uint32_t shade_stride(int n_sh) {  // block + 3 record quads, power of 2
     const uint32_t q = shade_quads(n_sh) + 3;
@@ -139,7 +147,9 @@ struct ProjParams {
     uint32_t* srect;
     uint32_t* c0;             // [parts] chunk-0 splats per projection partition (k_project)
     uint32_t* c1;             // [parts] chunk-1 splats per projection partition (k_records; zeroed by k_cull)
-    uint16_t* cand;           // [parts * kSortTile] chunk-0 candidates: offsets in the partition (k_cull)
+    uint16_t* cand;           // [parts * kProjTile] chunk-0 candidates: offsets in the partition (k_cull)
+    uint32_t* units;          // [kUnitShards][unit_shard_cap] the non-empty chunk-0 work units (k_cull)
+    uint32_t* plist;          // [kUnitShards][ceil(parts / kUnitShards)] surviving partitions (k_part_cull)
     const PartBound* bounds;  // [parts] (k_part_bounds)
     const uint32_t* orig;     // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx;           // [slots] storage index of each composite slot
@@ -195,6 +205,8 @@ struct BinParams {
     const uint32_t* srect;        // [slots] packed tile rectangle
     const uint32_t* cnt;          // [parts] the chunk's splats per projection partition (c0 or c1)
     uint32_t parts;               // projection partitions
+    const uint32_t* units;        // chunk 0: the frame's work-unit list (ProjParams::units); chunk 1:
+                                  // null (every unit of every partition)
     Records rec;                  // r2 (wide rects)
     const float4* crec;           // composite records, 3 float4 per slot
     const uint8_t* done;          // chunk 1: per-tile "saturated after chunk 0"
@@ -257,7 +269,6 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, const uint32_t* 
 void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s);
 void launch_project(const ProjParams& p, hipStream_t s);
 void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 slots (or, rec_all, every record)
-void launch_colour(const ProjParams& p, hipStream_t s);   // colours of the chunk-0 slots
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit, wide rows
 // stats -> host slot + seq; then FrameCtl zeroed for the next frame

@@ -65,7 +65,7 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp
 // Morton code of its position in the scene's box (non-finite positions last), a stable radix
 // sort orders them, k_transpose writes storage slot s from record perm[s] and keeps orig[s] =
 // perm[s] (the reference's index: ties in depth are broken by it).  k_part_bounds then bounds
-// each projection partition (kSortTile consecutive slots) for the per-partition cull.
+// each projection partition (kProjTile consecutive slots) for the per-partition cull.
 
 // ordered-uint encoding of a float (monotone), for min / max with integer atomics
 __device__ __forceinline__ uint32_t f2ord(float f) {
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ a
         if (t < q) o[t] = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
 }
 
-// Per projection partition (kSortTile consecutive storage slots): the box of its finite
+// Per projection partition (kProjTile consecutive storage slots): the box of its finite
 // positions, the largest ||R(q) diag(s)||_F^2 (NaN counts as infinite) and its count of finite
 // positions (zero: nothing in it can be visible).
 __global__ __launch_bounds__(256) void k_part_bounds(const float4* __restrict__ cull, uint64_t n,
@@ -188,9 +188,9 @@ __global__ __launch_bounds__(256) void k_part_bounds(const float4* __restrict__ 
     __shared__ uint32_t s[8];
     if (threadIdx.x < 8) s[threadIdx.x] = threadIdx.x < 3 ? 0xFFFFFFFFu : 0u;
     __syncthreads();
-    const uint64_t p0 = (uint64_t)blockIdx.x * kSortTile;
+    const uint64_t p0 = (uint64_t)blockIdx.x * kProjTile;
     uint32_t lo[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, hi[3] = {0u, 0u, 0u}, trs = 0u, fin = 0u;
-    for (uint32_t k = threadIdx.x; k < (uint32_t)kSortTile; k += 256) {
+    for (uint32_t k = threadIdx.x; k < (uint32_t)kProjTile; k += 256) {
         const uint64_t i = p0 + k;
         if (i >= n) break;
         const float4 c = cull[i];
@@ -575,14 +575,14 @@ __device__ void records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
         for (int d = 32; d >= 1; d >>= 1) kt += __shfl_xor(kt, d, 64);
         if (lane == 0) {
             const uint32_t c = (uint32_t)__popcll(b);
-            base = atomicAdd(&p.c1[i0 / kSortTile], c);
+            base = atomicAdd(&p.c1[i0 / kProjTile], c);
             StatShard* st = p.stats + (i0 >> 6) % kStatShards;
             atomicAdd(&st->n_chunk[1], c);
             atomicAdd(&st->k_total, kt);
         }
         base = __shfl(base, 0, 64);
         if (want) {
-            const uint32_t slot = slot_c1(i0 / kSortTile, base + (uint32_t)__popcll(b & lanemask_lt()));
+            const uint32_t slot = slot_c1(i0 / kProjTile, base + (uint32_t)__popcll(b & lanemask_lt()));
             store_slot(p, slot, i, o);
             float4 c = sh_colour(p.rec.r01 + (uint64_t)i * p.rec.stride, p.rec.off, p.cam);
             c.w = __uint_as_float(o.key);
@@ -597,149 +597,197 @@ __global__ __launch_bounds__(256) void k_records(ProjParams p) {
 }
 
 // Can a Gaussian of partition b be a chunk-0 candidate of this frame (pass cull_keep with key <
-// thresh)?  The interval form of cull_keep over the partition's box, in double with slack for
-// the per-Gaussian float roundings: clip coordinates are affine (extremes at the 8 corners), the
-// ratios x/w, y/w take their extremes at the corners when every corner has w > 0, the quad bound
-// grows with focal / |vz| and ||R diag(s)||_F^2; key < thresh needs the box's smallest key.
+// thresh)?  The interval form of cull_keep over the partition's box, in float with slack far
+// above the roundings of both this bound and the per-Gaussian test (1e-4 of each term's
+// magnitude, 4 px on the quad bound): clip coordinates are affine (extremes at the 8 corners),
+// the ratios x/w, y/w take their extremes at the corners when every corner has w > 0, the quad
+// bound grows with focal / |vz| and ||R diag(s)||_F^2; key < thresh needs the box's smallest key.
 __device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, int row_hi) {
     if (!b.nfin) return false;
-    double mn[5], mx[5];  // vz, cx, cy, cz, cw
-    double mag[5];        // sum |coefficient * coordinate|: the scale of the float rounding
-    for (int k = 0; k < 5; ++k) {
-        mn[k] = 1e300;
-        mx[k] = -1e300;
-        mag[k] = 0.0;
-    }
-    for (int c = 0; c < 8; ++c) {
-        const double x = (c & 1) ? b.hi[0] : b.lo[0], y = (c & 2) ? b.hi[1] : b.lo[1], z = (c & 4) ? b.hi[2] : b.lo[2];
-        const double v[5] = {
-            (double)p.V[2] * x + (double)p.V[6] * y + (double)p.V[10] * z + (double)p.V[14],
-            (double)p.PV[0] * x + (double)p.PV[4] * y + (double)p.PV[8] * z + (double)p.PV[12],
-            (double)p.PV[1] * x + (double)p.PV[5] * y + (double)p.PV[9] * z + (double)p.PV[13],
-            (double)p.PV[2] * x + (double)p.PV[6] * y + (double)p.PV[10] * z + (double)p.PV[14],
-            (double)p.PV[3] * x + (double)p.PV[7] * y + (double)p.PV[11] * z + (double)p.PV[15]};
-        const double m[5] = {
-            fabs(p.V[2] * x) + fabs(p.V[6] * y) + fabs(p.V[10] * z) + fabs((double)p.V[14]),
-            fabs(p.PV[0] * x) + fabs(p.PV[4] * y) + fabs(p.PV[8] * z) + fabs((double)p.PV[12]),
-            fabs(p.PV[1] * x) + fabs(p.PV[5] * y) + fabs(p.PV[9] * z) + fabs((double)p.PV[13]),
-            fabs(p.PV[2] * x) + fabs(p.PV[6] * y) + fabs(p.PV[10] * z) + fabs((double)p.PV[14]),
-            fabs(p.PV[3] * x) + fabs(p.PV[7] * y) + fabs(p.PV[11] * z) + fabs((double)p.PV[15])};
-        for (int k = 0; k < 5; ++k) {
-            mn[k] = fmin(mn[k], v[k]);
-            mx[k] = fmax(mx[k], v[k]);
-            mag[k] = fmax(mag[k], m[k]);
+    // coefficient rows: vz (V row 2), clip x, y, z, w (PV rows 0-3), column-major matrices
+    const float C[5][4] = {{p.V[2], p.V[6], p.V[10], p.V[14]},
+                           {p.PV[0], p.PV[4], p.PV[8], p.PV[12]},
+                           {p.PV[1], p.PV[5], p.PV[9], p.PV[13]},
+                           {p.PV[2], p.PV[6], p.PV[10], p.PV[14]},
+                           {p.PV[3], p.PV[7], p.PV[11], p.PV[15]}};
+    float mn[5], mx[5], sl[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {  // the affine form's range over the box (per-axis extremes)
+        float lo = C[k][3], hi = C[k][3], mag = fabsf(C[k][3]);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float a0 = C[k][d] * b.lo[d], a1 = C[k][d] * b.hi[d];
+            lo += fminf(a0, a1);
+            hi += fmaxf(a0, a1);
+            mag += fmaxf(fabsf(a0), fabsf(a1));
         }
+        sl[k] = 1e-4f * mag + 1e-30f;
+        mn[k] = lo - sl[k];
+        mx[k] = hi + sl[k];
     }
-    double sl[5];
-    for (int k = 0; k < 5; ++k) sl[k] = 1e-5 * mag[k] + 1e-30;
-    if (!(mx[4] + sl[4] > 0.0)) return false;           // every clip w <= 0
-    if (!(mx[3] + sl[3] >= 0.0)) return false;          // every clip z < 0 (near)
-    if (!(mn[3] - sl[3] - (mx[4] + sl[4]) <= 0.0)) return false;  // every clip z > w (far)
-    if (p.thresh != kSentinel) {  // the smallest depth key in the box
+    if (!(mx[4] > 0.0f)) return false;        // every clip w <= 0
+    if (!(mx[3] >= 0.0f)) return false;       // every clip z < 0 (near)
+    if (!(mn[3] <= mx[4])) return false;      // every clip z > w (far)
+    if (p.thresh != kSentinel) {              // the smallest depth key in the box
         uint32_t kmin = 0;
-        if (mx[0] + sl[0] < 0.0) kmin = sortable_key((float)(mx[0] + sl[0]));
-        else if (mn[0] - sl[0] > 0.0) kmin = sortable_key((float)(mn[0] - sl[0]));
+        if (mx[0] < 0.0f) kmin = sortable_key(mx[0]);
+        else if (mn[0] > 0.0f) kmin = sortable_key(mn[0]);
         kmin = kmin > 64u ? kmin - 64u : 0u;
         if (kmin >= p.thresh) return false;
     }
-    if (!(mn[4] - sl[4] > 0.0)) return true;            // a corner with w <= 0: no ratio bound
-    if (!(mn[0] - sl[0] > 0.0 || mx[0] + sl[0] < 0.0)) return true;  // vz crosses 0
-    double pxl = 1e300, pxh = -1e300, pyl = 1e300, pyh = -1e300;
-    for (int c = 0; c < 8; ++c) {  // pixel centre of each corner (ratios in double)
-        const double x = (c & 1) ? b.hi[0] : b.lo[0], y = (c & 2) ? b.hi[1] : b.lo[1], z = (c & 4) ? b.hi[2] : b.lo[2];
-        const double cx = (double)p.PV[0] * x + (double)p.PV[4] * y + (double)p.PV[8] * z + (double)p.PV[12];
-        const double cy = (double)p.PV[1] * x + (double)p.PV[5] * y + (double)p.PV[9] * z + (double)p.PV[13];
-        const double cw = (double)p.PV[3] * x + (double)p.PV[7] * y + (double)p.PV[11] * z + (double)p.PV[15];
-        const double px = (cx / cw + 1.0) * p.W * 0.5, py = (1.0 - cy / cw) * p.H * 0.5;
-        pxl = fmin(pxl, px); pxh = fmax(pxh, px);
-        pyl = fmin(pyl, py); pyh = fmax(pyh, py);
+    if (!(mn[4] > 0.0f)) return true;         // a corner with w <= 0: no ratio bound
+    if (!(mn[0] > 0.0f || mx[0] < 0.0f)) return true;  // vz crosses 0
+    float pxl = INFINITY, pxh = -INFINITY, pyl = INFINITY, pyh = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {  // pixel centre of each corner
+        const float x = (c & 1) ? b.hi[0] : b.lo[0], y = (c & 2) ? b.hi[1] : b.lo[1], z = (c & 4) ? b.hi[2] : b.lo[2];
+        const float cx = C[1][0] * x + C[1][1] * y + C[1][2] * z + C[1][3];
+        const float cy = C[2][0] * x + C[2][1] * y + C[2][2] * z + C[2][3];
+        const float cw = C[4][0] * x + C[4][1] * y + C[4][2] * z + C[4][3];
+        const float px = (cx / cw + 1.0f) * (float)p.W * 0.5f, py = (1.0f - cy / cw) * (float)p.H * 0.5f;
+        pxl = fminf(pxl, px); pxh = fmaxf(pxh, px);
+        pyl = fminf(pyl, py); pyh = fmaxf(pyh, py);
     }
-    const double az = fmin(fabs(mn[0]), fabs(mx[0])) * (1.0 - 1e-5);
-    const double a = (double)p.focal / az;
-    const double trs = (double)b.trs * p.scale_mod * p.scale_mod;
-    const double hb = 4.0 * fmax(sqrt(2.0 * (a * a * p.w01_spec2 * trs + 0.6)), 0.45) * 1.03 + 4.0;
-    if (!(hb < 1e30)) return true;
-    return !(pyh + hb < (double)row_lo - 1.0 || pyl - hb > (double)row_hi + 1.0 || pxh + hb < -1.0 ||
-             pxl - hb > (double)p.W);
+    const float az = fminf(fabsf(mn[0]), fabsf(mx[0]));
+    const float a = p.focal / az;
+    const float trs = b.trs * p.scale_mod * p.scale_mod;
+    // the corner ratios' own error: relative slack on the pixel extent plus 4 px
+    const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w01_spec2 * trs + 0.6f)), 0.45f) * 1.03f + 4.0f +
+                     1e-3f * (float)max(p.W, p.H);
+    if (!(hb < 1e30f)) return true;
+    return !(pyh + hb < (float)row_lo - 1.0f || pyl - hb > (float)row_hi + 1.0f || pxh + hb < -1.0f ||
+             pxl - hb > (float)p.W);
 }
 
-// Projection, phase A (one workgroup per projection partition of kSortTile storage slots): a
-// partition whose bound rules it out (part_maybe) costs one 32-B read; otherwise every
+// Per projection partition (one thread each): the partition test (part_maybe), the surviving
+// partitions appended to the frame's partition list (kUnitShards shards, part % kUnitShards), and
+// the partition's chunk counts zeroed (c0 for the ruled-out ones, c1 for every one: k_records
+// adds to it).
+__global__ __launch_bounds__(256) void k_part_cull(ProjParams p) {
+    const int row_lo = p.tile_row_begin * kTile;
+    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+    const uint32_t parts = proj_parts(p.n), pcap = (parts + kUnitShards - 1) / kUnitShards;
+    const uint32_t part = blockIdx.x * 256 + threadIdx.x;
+    const bool maybe = part < parts && part_maybe(p, p.bounds[part], row_lo, row_hi);
+    if (part < parts) {
+        p.c1[part] = 0;
+        if (!maybe) p.c0[part] = 0;
+    }
+    // lanes of a wave hold consecutive partitions: one add per (wave, shard)
+    const uint32_t sh = part % kUnitShards;
+    for (uint32_t k = 0; k < kUnitShards; ++k) {
+        const uint64_t b = __ballot(maybe && sh == k);
+        if (!b) continue;
+        uint32_t base = 0;
+        if (lane_id() == (uint32_t)(__ffsll((long long)b) - 1)) base = atomicAdd(&p.ctl->part_n[k], (uint32_t)__popcll(b));
+        base = __shfl(base, __ffsll((long long)b) - 1, 64);
+        if (maybe && sh == k) p.plist[(uint64_t)k * pcap + base + __popcll(b & lanemask_lt())] = part;
+    }
+}
+
+// The frame's list of non-empty chunk-0 work units (k_cull appends them, kUnitShards shards).
+struct UnitList {
+    const uint32_t* units;  // null: unit j is j
+    uint32_t cap;
+    uint32_t pre[kUnitShards + 1];
+    uint32_t total;
+};
+__device__ __forceinline__ UnitList load_units(const uint32_t* units, const FrameCtl* ctl, uint32_t parts) {
+    UnitList L;
+    L.units = units;
+    L.cap = unit_shard_cap(parts);
+    L.pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < kUnitShards; ++k) L.pre[k + 1] = L.pre[k] + ctl->unit_n[k];
+    L.total = L.pre[kUnitShards];
+    return L;
+}
+__device__ __forceinline__ uint32_t unit_at(const UnitList& L, uint32_t j) {
+    if (!L.units) return j;
+    int k = 0;
+#pragma unroll
+    for (int t = 1; t < kUnitShards; ++t) k += j >= L.pre[t] ? 1 : 0;
+    return L.units[(uint64_t)k * L.cap + (j - L.pre[k])];
+}
+
+// Projection, phase A (one workgroup per surviving projection partition of kProjTile storage
+// slots, from k_part_cull's list; a ruled-out partition costs nothing here): every
 // Gaussian's 16-B cull plane gives its depth key (vz rounded exactly as project_footprint rounds
 // it) and the conservative cull (cull_keep: exact near/far, a provable bound on the quad box
 // against this frame's rows).  Survivors nearer than thresh are the partition's chunk-0
 // candidates (cand: their offsets in index order; c0 = their count, the partition's chunk-0
-// slots); survivors at or past thresh are only counted (n_vis is exact when the frame has one
-// chunk and no partition was ruled out by the threshold) and enter the depth range.
+// slots; its non-empty work units are appended to the frame's list); survivors at or past thresh
+// are only counted (n_vis is exact when the frame has one chunk and no partition was ruled out
+// by the threshold) and enter the depth range.
 __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
-    __shared__ unsigned long long s_mask[kSortIPT][kProjThreads / 64];
-    __shared__ uint32_t s_base[kSortIPT][kProjThreads / 64];
+    __shared__ unsigned long long s_mask[kProjRounds][kProjThreads / 64];
+    __shared__ uint32_t s_base[kProjRounds][kProjThreads / 64];
     __shared__ uint32_t s_total;
-    __shared__ int s_maybe;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     if (tid == 0) { s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
     uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
-    const uint32_t parts = sort_parts(p.n);
-    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        const uint32_t p0 = part * kSortTile;
-        if (tid == 0) s_maybe = part_maybe(p, p.bounds[part], row_lo, row_hi);
-        __syncthreads();
-        if (!s_maybe) {
-            if (tid == 0) {
-                p.c0[part] = 0;
-                p.c1[part] = 0;
-            }
-            __syncthreads();
-            continue;
+    const uint32_t parts = proj_parts(p.n), ucap = unit_shard_cap(parts);
+    const uint32_t pcap = (parts + kUnitShards - 1) / kUnitShards;
+    uint32_t ppre[kUnitShards + 1];
+    ppre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < kUnitShards; ++k) ppre[k + 1] = ppre[k] + p.ctl->part_n[k];
+    for (uint32_t jp = blockIdx.x; jp < ppre[kUnitShards]; jp += gridDim.x) {
+        int sh = 0;
+#pragma unroll
+        for (int t = 1; t < kUnitShards; ++t) sh += jp >= ppre[t] ? 1 : 0;
+        const uint32_t part = p.plist[(uint64_t)sh * pcap + (jp - ppre[sh])];
+        const uint32_t p0 = part * kProjTile;
+        float4 c[kProjRounds];
+#pragma unroll
+        for (int it = 0; it < kProjRounds; ++it) {
+            const uint32_t i = p0 + it * kProjThreads + tid;
+            c[it] = i < p.n ? p.cull[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         uint32_t cand = 0;  // bit it: slot p0 + it * kProjThreads + tid is a candidate
-        constexpr int kGroup = 4;  // cull planes in flight per thread
-        for (int g = 0; g < kSortIPT; g += kGroup) {
-            float4 c[kGroup];
 #pragma unroll
-            for (int u = 0; u < kGroup; ++u) {
-                const uint32_t i = p0 + (g + u) * kProjThreads + tid;
-                c[u] = i < p.n ? p.cull[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < kGroup; ++u) {
-                const int it = g + u;
-                const uint32_t i = p0 + it * kProjThreads + tid;
-                bool cd = false;
-                float vz;
-                if (i < p.n && cull_keep(p, c[u], row_lo, row_hi, vz)) {
-                    const uint32_t key = sortable_key(vz);
-                    cd = key < p.thresh;
-                    if (!cd) {  // past the threshold: counted, not projected
-                        ++my_vis;
-                        my_kmin_inv = max(my_kmin_inv, ~key);
-                        my_kmax = max(my_kmax, key);
-                    }
+        for (int it = 0; it < kProjRounds; ++it) {
+            const uint32_t i = p0 + it * kProjThreads + tid;
+            bool cd = false;
+            float vz;
+            if (i < p.n && cull_keep(p, c[it], row_lo, row_hi, vz)) {
+                const uint32_t key = sortable_key(vz);
+                cd = key < p.thresh;
+                if (!cd) {  // past the threshold: counted, not projected
+                    ++my_vis;
+                    my_kmin_inv = max(my_kmin_inv, ~key);
+                    my_kmax = max(my_kmax, key);
                 }
-                cand |= (cd ? 1u : 0u) << it;
-                const uint64_t bb = __ballot(cd);
-                if (lane == 0) s_mask[it][w] = bb;
             }
+            cand |= (cd ? 1u : 0u) << it;
+            const uint64_t bb = __ballot(cd);
+            if (lane == 0) s_mask[it][w] = bb;
         }
         __syncthreads();
-        if (tid < 64) {  // exclusive prefix of the 16 x 4 (round, wave) ballots: index order
-            const uint32_t cnt = __popcll(s_mask[tid >> 2][tid & 3]);
+        if (tid < 64) {  // exclusive prefix of the (round, wave) ballots: index order
+            constexpr int nb = kProjRounds * (kProjThreads / 64);
+            const uint32_t cnt = tid < nb ? __popcll(s_mask[tid / (kProjThreads / 64)][tid % (kProjThreads / 64)]) : 0u;
             const uint32_t incl = wave_incl_scan(cnt);
-            s_base[tid >> 2][tid & 3] = incl - cnt;
+            if (tid < nb) s_base[tid / (kProjThreads / 64)][tid % (kProjThreads / 64)] = incl - cnt;
             if (tid == 63) s_total = incl;
         }
         __syncthreads();
 #pragma unroll
-        for (int it = 0; it < kSortIPT; ++it) {
+        for (int it = 0; it < kProjRounds; ++it) {
             const uint64_t bb = s_mask[it][w];
             if ((cand >> it) & 1u) p.cand[p0 + s_base[it][w] + __popcll(bb & lanemask_lt())] = (uint16_t)(it * kProjThreads + tid);
         }
         if (tid == 0) {
-            p.c0[part] = s_total;
-            p.c1[part] = 0;
+            const uint32_t tot = s_total;
+            p.c0[part] = tot;
+            if (tot) {  // the partition's work units into the frame's list (shard by partition)
+                const uint32_t nu = (tot + kProjThreads - 1) / kProjThreads, sh = part % kUnitShards;
+                const uint32_t pos = atomicAdd(&p.ctl->unit_n[sh], nu);
+                for (uint32_t r = 0; r < nu; ++r) p.units[(uint64_t)sh * ucap + pos + r] = part * kProjRounds + r;
+            }
         }
         __syncthreads();
     }
@@ -757,13 +805,11 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     }
 }
 
-// Work units of the per-slot passes: (partition, round of kProjThreads slots), so that a
-// partition full of candidates is spread over kSortIPT workgroups.
-__device__ __forceinline__ uint32_t slot_units(const ProjParams& p) { return sort_parts(p.n) * kSortIPT; }
-
 // Projection, phase B: candidate q of a partition (slot slot_c0(part, q)) projected from its
-// 48-B geometry record; a visible one gets its records in its slot, an invisible one leaves the
-// slot a hole (rect kRectHole).  Publishes the visible count, their tile total, the depth range.
+// 48-B geometry record, one work unit (kProjThreads candidates) per workgroup iteration over the
+// frame's unit list; a visible one gets its records and (from its shading block, one thread per
+// splat in the reference's expression order: sh_colour) its colour in its slot, an invisible one
+// leaves the slot a hole (rect kRectHole).  Publishes the visible count, their tile total, the depth range.
 __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     __shared__ unsigned long long s_k;
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
@@ -774,15 +820,21 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     unsigned long long my_k = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
-    const uint32_t units = slot_units(p);
-    for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
-        const uint32_t part = u / kSortIPT, q = (u % kSortIPT) * kProjThreads + tid;
+    const UnitList L = load_units(p.units, p.ctl, proj_parts(p.n));
+    for (uint32_t j = blockIdx.x; j < L.total; j += gridDim.x) {
+        const uint32_t u = unit_at(L, j);
+        const uint32_t part = u / kProjRounds, q = (u % kProjRounds) * kProjThreads + tid;
         if (q >= p.c0[part]) continue;
-        const uint32_t p0 = part * kSortTile, slot = slot_c0(part, q);
+        const uint32_t p0 = part * kProjTile, slot = slot_c0(part, q);
         const uint32_t i = p0 + (uint32_t)p.cand[p0 + q];
         Proj o;
         if (project_core(p, i, row_lo, row_hi, false, o)) {
             store_slot(p, slot, i, o);
+            if (o.prect != kRectEmpty) {  // the SH colour of a splat that binds a tile
+                float4 col = sh_colour(p.rec.r01 + (uint64_t)i * p.rec.stride, p.rec.off, p.cam);
+                col.w = __uint_as_float(o.key);
+                p.crec[3 * (uint64_t)slot + 2] = col;
+            }
             ++my_vis;
             my_k += o.ntiles;
             my_kmin_inv = max(my_kmin_inv, ~o.key);
@@ -805,23 +857,6 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
         atomicAdd(&st->k_total, s_k);
         atomicMax(&st->key_min_inv, s_kmin_inv);
         atomicMax(&st->key_max, s_kmax);
-    }
-}
-
-// Colours of the chunk-0 slots, one thread per slot: the SH colour and the depth key (the
-// composite's saturation statistic) into the record's third quad.
-__global__ __launch_bounds__(256) void k_colour(ProjParams p) {
-    const uint32_t units = slot_units(p);
-    for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
-        const uint32_t part = u / kSortIPT, q = (u % kSortIPT) * kProjThreads + threadIdx.x;
-        if (q >= p.c0[part]) continue;
-        const uint32_t slot = slot_c0(part, q);
-        const uint32_t pr = p.srect[slot];
-        if (pr == kRectHole || pr == kRectEmpty) continue;  // not visible / binds no tile
-        const uint32_t j = p.sidx[slot];
-        float4 c = sh_colour(p.rec.r01 + (uint64_t)j * p.rec.stride, p.rec.off, p.cam);
-        c.w = __uint_as_float(p.skey[slot].x);
-        p.crec[3 * (uint64_t)slot + 2] = c;
     }
 }
 
@@ -1212,16 +1247,24 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
 // Count and emission walk the same ellipse rows, so a tile's count and its entries agree.
 constexpr uint32_t kBinMaxUnits = 4096;  // units per binning partition (scenes up to 2^28 Gaussians)
 
-__device__ __forceinline__ uint32_t bin_units(const BinParams& p, uint32_t b) {
-    const uint32_t units = p.parts * (uint32_t)kSortIPT;
-    return units > b ? (units - b + kBinParts - 1) / kBinParts : 0u;
+// The chunk's work units: chunk 0 the frame's list (k_cull), chunk 1 every unit of every partition.
+__device__ __forceinline__ UnitList bin_unit_list(const BinParams& p) {
+    if (p.units) return load_units(p.units, p.ctl, p.parts);
+    UnitList L;
+    L.units = nullptr;
+    L.total = p.parts * (uint32_t)kProjRounds;
+    return L;
 }
 
-// The slots of binning partition b: s_pref[k] = slots of its first k units; returns the total.
-// Contains barriers.
+__device__ __forceinline__ uint32_t bin_units(const UnitList& L, uint32_t b) {
+    return L.total > b ? (L.total - b + kBinParts - 1) / kBinParts : 0u;
+}
+
+// The slots of binning partition b (units b, b + kBinParts, ... of the chunk's list):
+// s_pref[k] = slots of its first k units; returns the total.  Contains barriers.
 template <int NT>
-__device__ uint32_t bin_slots(const BinParams& p, uint32_t b, uint32_t* s_pref, uint32_t* s_tmp) {
-    const uint32_t m = min(bin_units(p, b), kBinMaxUnits);
+__device__ uint32_t bin_slots(const BinParams& p, const UnitList& L, uint32_t b, uint32_t* s_pref, uint32_t* s_tmp) {
+    const uint32_t m = min(bin_units(L, b), kBinMaxUnits);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     constexpr int per = kBinMaxUnits / NT;
     uint32_t c[per], sum = 0;
@@ -1230,7 +1273,8 @@ __device__ uint32_t bin_slots(const BinParams& p, uint32_t b, uint32_t* s_pref, 
         const uint32_t j = (uint32_t)tid * per + k;
         c[k] = 0;
         if (j < m) {
-            const uint32_t u = b + j * kBinParts, part = u / kSortIPT, r0 = (u % kSortIPT) * kProjThreads;
+            const uint32_t u = unit_at(L, b + j * kBinParts);
+            const uint32_t part = u / kProjRounds, r0 = (u % kProjRounds) * kProjThreads;
             const uint32_t cn = p.cnt[part];
             c[k] = cn > r0 ? min(cn - r0, (uint32_t)kProjThreads) : 0u;
         }
@@ -1255,15 +1299,16 @@ __device__ uint32_t bin_slots(const BinParams& p, uint32_t b, uint32_t* s_pref, 
 }
 
 // The r-th slot of binning partition b (r < total of bin_slots).
-__device__ __forceinline__ uint32_t bin_slot(const BinParams& p, uint32_t b, const uint32_t* s_pref, uint32_t r) {
-    const uint32_t m = min(bin_units(p, b), kBinMaxUnits);
+__device__ __forceinline__ uint32_t bin_slot(const BinParams& p, const UnitList& L, uint32_t b,
+                                             const uint32_t* s_pref, uint32_t r) {
+    const uint32_t m = min(bin_units(L, b), kBinMaxUnits);
     uint32_t lo = 0, hi = m;  // largest k < m with s_pref[k] <= r
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (s_pref[mid] <= r) lo = mid; else hi = mid;
     }
-    const uint32_t u = b + lo * kBinParts, part = u / kSortIPT;
-    const uint32_t q = (u % kSortIPT) * kProjThreads + (r - s_pref[lo]);
+    const uint32_t u = unit_at(L, b + lo * kBinParts), part = u / kProjRounds;
+    const uint32_t q = (u % kProjRounds) * kProjThreads + (r - s_pref[lo]);
     return p.chunk ? slot_c1(part, q) : slot_c0(part, q);
 }
 
@@ -1295,9 +1340,10 @@ __device__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt,
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
     for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += NT) s_cnt[t] = 0;
-    const uint32_t total = bin_slots<NT>(p, part, s_pref, s_tmp);
+    const UnitList L = bin_unit_list(p);
+    const uint32_t total = bin_slots<NT>(p, L, part, s_pref, s_tmp);
     for (uint32_t r = threadIdx.x; r < total; r += NT) {
-        const uint32_t g = bin_slot(p, part, s_pref, r);
+        const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
         const float4* q = p.crec + 3 * (uint64_t)g;
@@ -1426,10 +1472,11 @@ __device__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, 
     const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) s_cur[t - t_lo] = p.tbase[t] + row[t];
     if (threadIdx.x == 0) s_nw = 0;
-    const uint32_t total = bin_slots<NT>(p, part, s_pref, s_tmp);
+    const UnitList L = bin_unit_list(p);
+    const uint32_t total = bin_slots<NT>(p, L, part, s_pref, s_tmp);
     const uint32_t cap = p.capacity;
     for (uint32_t r = threadIdx.x; r < total; r += NT) {
-        const uint32_t g = bin_slot(p, part, s_pref, r);
+        const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
         if (rect_wide(tr)) {
@@ -2350,19 +2397,16 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, const uint32_t* 
 }
 void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s) {
     if (!n) return;
-    hipLaunchKernelGGL(k_part_bounds, dim3(sort_parts(n)), dim3(256), 0, s, cull, n, out);
+    hipLaunchKernelGGL(k_part_bounds, dim3(proj_parts(n)), dim3(256), 0, s, cull, n, out);
 }
 void launch_project(const ProjParams& p, hipStream_t s) {
-    const uint32_t parts = sort_parts(p.n);
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kMaxGrid, parts));
+    const uint32_t parts = proj_parts(p.n);
+    if (!parts) return;
+    hipLaunchKernelGGL(k_part_cull, dim3((parts + 255) / 256), dim3(256), 0, s, p);
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, parts));
     hipLaunchKernelGGL(k_cull, dim3(grid), dim3(kProjThreads), 0, s, p);
-    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (uint64_t)parts * kSortIPT));
+    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (uint64_t)parts * kProjRounds));
     hipLaunchKernelGGL(k_project, dim3(ugrid), dim3(kProjThreads), 0, s, p);
-}
-void launch_colour(const ProjParams& p, hipStream_t s) {
-    const uint32_t parts = sort_parts(p.n);
-    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (uint64_t)parts * kSortIPT));
-    hipLaunchKernelGGL(k_colour, dim3(ugrid), dim3(256), 0, s, p);
 }
 void launch_records(const ProjParams& p, hipStream_t s) {
     if (!p.n) return;
