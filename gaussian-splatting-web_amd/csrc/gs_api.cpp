@@ -139,7 +139,8 @@ struct gs_scene {
     uint64_t n = 0;
     int n_sh = 0;
     float4* geo = nullptr;              // geometry records (3 float4 per Gaussian)
-    float4* shade = nullptr;            // shading blocks (shade_stride float4 per Gaussian)
+    float4* shade = nullptr;            // packed SH coefficients (sh_quads float4 per Gaussian)
+    float4* dbg = nullptr;              // per-Gaussian debug records (3 float4), allocated on demand
     float4* cull = nullptr;             // cull planes (two-phase projection)
     float4* r2 = nullptr;
     // composite slots (slot_c0 / slot_c1): records (3 float4), (depth key, index), packed rect
@@ -202,7 +203,7 @@ static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
 static Records records(gs_scene* s) {
-    return Records{s->shade, s->r2, shade_stride(s->n_sh), shade_quads(s->n_sh)};
+    return Records{s->dbg, s->r2, 3u, 0u};
 }
 
 static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
@@ -440,6 +441,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.tile_row_end = tr_end;
     pp.tiles_x = TX;
     pp.rec = records(s);
+    pp.sh = s->shade;
+    pp.shq = sh_quads(s->n_sh);
     pp.ctl = s->ctl;
     pp.stats = s->stats;
     pp.thresh = T;
@@ -722,7 +725,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
         s->n_sh = n_sh;
         try {
             dev_alloc(s->geo, 3 * (size_t)std::max<uint64_t>(n, 1));
-            dev_alloc(s->shade, (size_t)shade_stride(n_sh) * std::max<uint64_t>(n, 1));
+            dev_alloc(s->shade, (size_t)sh_quads(n_sh) * std::max<uint64_t>(n, 1));
             dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->crec, 3 * ((size_t)proj_parts(n) * kProjTile + 1));
@@ -800,6 +803,7 @@ void gs_scene_free(gs_scene* s) {
     }
     dev_free(s->geo);
     dev_free(s->shade);
+    dev_free(s->dbg);
     dev_free(s->cull);
     dev_free(s->r2);
     dev_free(s->crec);
@@ -1049,15 +1053,17 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
         const uint64_t m = std::min(cap, s->n);
         const auto sl = frame_slots(s);
         if (m) {  // r01 -> words [0, 8); r2 -> words [12, 16); colour below
+            if (!s->dbg) dev_alloc(s->dbg, 3 * (size_t)std::max<uint64_t>(s->n, 1));
             ProjParams rp = s->last_pp;  // records of every visible Gaussian (a frame stores fewer)
+            rp.rec = records(s);
             rp.rec_all = 1;
             launch_records(rp, c->stream);
             HIPCHK(hipStreamSynchronize(c->stream));
-            const Records rc = records(s);  // r01 lives in the shading blocks' padding
+            const Records rc = records(s);
             const uint64_t n = s->n;           // storage slot j holds reference record orig[j]
             std::vector<float> a((size_t)n * 8), b((size_t)n * 4);
             std::vector<uint32_t> orig(n);
-            HIPCHK(hipMemcpy2D(a.data(), 32, rc.r01 + rc.off, (size_t)rc.stride * 16, 32, n, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy2D(a.data(), 32, rc.r01, (size_t)rc.stride * 16, 32, n, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(b.data(), s->r2, b.size() * 4, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(orig.data(), s->orig, n * 4, hipMemcpyDeviceToHost));
             for (uint64_t j = 0; j < n; ++j) {

@@ -99,26 +99,21 @@ __host__ __device__ inline uint32_t unit_shard_cap(uint32_t parts) {
 // Scene layout in HBM (storage slots in Morton order, orig[] = reference index): a 48-B
 // geometry record per Gaussian (3 float4: x, y, z, opacity logit | scale xyz, rot.x | rot.y,
 // rot.z, rot.w, 0) gathered by k_project for the chunk-0 candidates, a 16-B cull plane (x, y, z,
-// ||R(q) diag(s)||_F^2) streamed by k_cull, and one shading block per Gaussian [x, y, z,
-// sh[k][c] at 3 + 3k + c] of shade_stride float4 (a power of two, so a block never straddles more
-// 128-B lines than it must; 256 B at SH degree 3), read by k_colour.
-// The per-Gaussian record of Gaussian j (debug dump and chunk-1 bookkeeping):
-//   r01 = quads shade_quads(n_sh), +1 of j's shading block (its padding): cx, cy, e1x', e1y' |
-//         e2x', e2y', log2(op), pixel box x (centre in pixels; quad axes e/|e|^2 * sqrt(log2 e);
-//         box x0 | x1 << 16, u32 bits); colour at quad shade_quads(n_sh) + 2 (rec_all only)
-//   r2[j] = depth key, tile count, pixel box x, pixel box y (u32 bits), dense
+// ||R(q) diag(s)||_F^2) streamed by k_cull, and the packed SH coefficients, sh_quads(n_sh) float4
+// per Gaussian (coefficient k channel c at 3k + c; 192 B at degree 3), read by k_project for
+// the splats it keeps (Morton order makes those reads nearly dense).
+// Per-Gaussian records (the debug dump; rec_all): Records::r01 = 3 quads per Gaussian: cx, cy,
+// e1x', e1y' | e2x', e2y', log2(op), pixel box x (centre in pixels; quad axes e/|e|^2 *
+// sqrt(log2 e); box x0 | x1 << 16, u32 bits) | colour; r2[j] = depth key, tile count, pixel box
+// x, pixel box y (u32 bits), written for every visible splat of a frame.
 // Composite record, 3 float4 per slot: [0], [1] = the r01 quads, [2] = r, g, b, depth key bits.
-__host__ __device__ inline uint32_t shade_quads(int n_sh) { return (uint32_t)(3 + 3 * n_sh + 3) / 4; }
-__host__ __device__ inline uint32_t shade_stride(int n_sh) {  // block + 3 record quads, power of 2
-    const uint32_t q = shade_quads(n_sh) + 3;
-    return q <= 4 ? 4 : q <= 8 ? 8 : 16;
-}
+__host__ __device__ inline uint32_t sh_quads(int n_sh) { return (uint32_t)(3 * n_sh + 3) / 4; }
 
 struct Records {
-    float4* r01;      // the shading blocks (records at quad `off` of each block)
+    float4* r01;      // debug records, stride quads per Gaussian (null outside the debug dump)
     float4* r2;
-    uint32_t stride;  // float4 per block (shade_stride)
-    uint32_t off;     // shade_quads(n_sh)
+    uint32_t stride;  // 3
+    uint32_t off;     // 0
 };
 __host__ __device__ inline float4* rec_r01(const Records& r, uint64_t j) {
     return r.r01 + j * r.stride + r.off;
@@ -157,6 +152,8 @@ struct ProjParams {
     const uint32_t* sat;
     int rec_all;
     float cam[3];             // camera position (SH view direction)
+    const float4* sh;         // [n][shq] packed SH coefficients
+    uint32_t shq;             // sh_quads(n_sh)
 };
 
 // Element filter of a radix pass (the first pass of a depth chunk decides chunk membership).

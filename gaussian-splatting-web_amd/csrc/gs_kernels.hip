@@ -162,21 +162,18 @@ __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ a
                         (r02 * r02 + r12 * r12 + r22 * r22) * r[6] * r[6];
         cull[i] = make_float4(r[0], r[1], r[2], t * 1.0001f);
     }
-    const uint32_t q = shade_quads(n_sh);
-    float v[4 * 13];
+    const uint32_t q = sh_quads(n_sh);  // SH coefficients sh[k][c] at 3k + c, packed
+    float v[4 * 12];
 #pragma unroll
-    for (int t = 0; t < 4 * 13; ++t) v[t] = 0.0f;
-    v[0] = r[0];
-    v[1] = r[1];
-    v[2] = r[2];
+    for (int t = 0; t < 4 * 12; ++t) v[t] = 0.0f;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
         if (k < n_sh)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) v[3 + 3 * k + c] = r[16 + 4 * k + c];
-    float4* o = shade + i * shade_stride(n_sh);
+            for (int c = 0; c < 3; ++c) v[3 * k + c] = r[16 + 4 * k + c];
+    float4* o = shade + i * q;
 #pragma unroll
-    for (uint32_t t = 0; t < 13; ++t)
+    for (uint32_t t = 0; t < 12; ++t)
         if (t < q) o[t] = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
 }
 
@@ -468,21 +465,22 @@ __device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, in
         return true;
 }
 
-// SH colour of a Gaussian from its shading block blk (nq quads: position, coefficients),
-// src/simple_render.ts:5-67, :321: one thread, the reference's expression order with contraction
-// off (bit-identical to the oracle).
-__device__ __forceinline__ float4 sh_colour(const float4* __restrict__ blk, uint32_t nq, const float* cam) {
+// SH colour of a Gaussian at (px, py, pz) from its packed coefficients sh (nq quads,
+// coefficient k channel c at 3k + c), src/simple_render.ts:5-67, :321: one thread, the
+// reference's expression order with contraction off (bit-identical to the oracle).
+__device__ __forceinline__ float4 sh_colour(const float4* __restrict__ shq, uint32_t nq, float px, float py, float pz,
+                                            const float* cam) {
 #pragma clang fp contract(off)
-    float f[52];
+    float f[48];
 #pragma unroll
-    for (uint32_t t = 0; t < 13; ++t) {
-        const float4 q = t < nq ? blk[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (uint32_t t = 0; t < 12; ++t) {
+        const float4 q = t < nq ? shq[t] : make_float4(0.f, 0.f, 0.f, 0.f);
         f[4 * t] = q.x;
         f[4 * t + 1] = q.y;
         f[4 * t + 2] = q.z;
         f[4 * t + 3] = q.w;
     }
-    const float dx = f[0] - cam[0], dy = f[1] - cam[1], dz = f[2] - cam[2];
+    const float dx = px - cam[0], dy = py - cam[1], dz = pz - cam[2];
     const float l = sqrtf(dx * dx + dy * dy + dz * dz);
     const float X = dx / l, Y = dy / l, Z = dz / l;
     const float xx = X * X, yy = Y * Y, zz = Z * Z, xy = X * Y, xz = X * Z, yz = Y * Z;
@@ -495,7 +493,7 @@ __device__ __forceinline__ float4 sh_colour(const float4* __restrict__ blk, uint
     float col[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float* sh = f + 3 + c;  // sh[3 k] = coefficient k, channel c
+        const float* sh = f + c;  // sh[3 k] = coefficient k, channel c
         float r = C0 * sh[0];
         r = r + C1 * (-Y * sh[3] + Z * sh[6] - X * sh[9]);
         r = r + C20 * xy * sh[12] + C21 * yz * sh[15] + C22 * (2.0f * zz - xx - yy) * sh[18] +
@@ -510,9 +508,15 @@ __device__ __forceinline__ float4 sh_colour(const float4* __restrict__ blk, uint
     return make_float4(col[0], col[1], col[2], 0.0f);
 }
 
-// Gaussian j's colour, stored after its record quads (k_colour, k_records).
+// SH colour of storage slot j (its position from the geometry record).
+__device__ __forceinline__ float4 colour_of(const ProjParams& p, uint32_t j) {
+    const float4 g0 = p.geo[3 * (uint64_t)j];
+    return sh_colour(p.sh + (uint64_t)j * p.shq, p.shq, g0.x, g0.y, g0.z, p.cam);
+}
+
+// Gaussian j's colour after its per-Gaussian record quads (debug dump, rec_all).
 __device__ __forceinline__ void store_colour(const ProjParams& p, uint32_t j) {
-    rec_r01(p.rec, j)[2] = sh_colour(p.rec.r01 + (uint64_t)j * p.rec.stride, p.rec.off, p.cam);
+    rec_r01(p.rec, j)[2] = colour_of(p, j);
 }
 
 // A visible splat's composite slot: records r0, r1 (the colour quad follows: k_colour or
@@ -584,7 +588,7 @@ __device__ void records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
         if (want) {
             const uint32_t slot = slot_c1(i0 / kProjTile, base + (uint32_t)__popcll(b & lanemask_lt()));
             store_slot(p, slot, i, o);
-            float4 c = sh_colour(p.rec.r01 + (uint64_t)i * p.rec.stride, p.rec.off, p.cam);
+            float4 c = colour_of(p, i);
             c.w = __uint_as_float(o.key);
             p.crec[3 * (uint64_t)slot + 2] = c;
         }
@@ -831,7 +835,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
         if (project_core(p, i, row_lo, row_hi, false, o)) {
             store_slot(p, slot, i, o);
             if (o.prect != kRectEmpty) {  // the SH colour of a splat that binds a tile
-                float4 col = sh_colour(p.rec.r01 + (uint64_t)i * p.rec.stride, p.rec.off, p.cam);
+                float4 col = colour_of(p, i);
                 col.w = __uint_as_float(o.key);
                 p.crec[3 * (uint64_t)slot + 2] = col;
             }
