@@ -430,3 +430,66 @@ def test_skewed_tile_keys(gpu_ctx):
     ref, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=0.0)
     r = image_close_fp32(img, ref, name="skewed_keys")
     assert r[2], r
+
+
+def _plus_z_uniforms(W, H, fovy=1.0):
+    """A +z-forward camera (the reference's JSON-camera convention, src/camera.ts:467-492): view
+    flips y and z, projection = 3DGS getProjectionMatrix (src/camera.ts:19-42), column-major."""
+    view = np.diag([1.0, -1.0, -1.0, 1.0]).astype(np.float32)
+    n, f = 0.2, 100.0
+    th = np.tan(fovy / 2)
+    tw = th * W / H
+    P = np.zeros((4, 4), np.float64)
+    P[0, 0] = 1.0 / tw
+    P[1, 1] = 1.0 / th
+    P[2, 2] = f / (f - n)
+    P[2, 3] = -(f * n) / (f - n)
+    P[3, 2] = 1.0
+    return gs.pack_uniforms(view.T.reshape(-1), P.T.reshape(-1).astype(np.float32))
+
+
+@pytest.mark.parametrize("cam", ["oblique", "plus_z"])
+def test_other_cameras_strips_and_oracle(gpu_ctx, cam):
+    """Partition bounds and the per-partition cull under an oblique -z camera and a +z camera:
+    the full frame against the fp32 oracle, row strips bit-identical to it."""
+    W, H = 640, 480
+    n = 200_000
+    aos = gs.synth_aos(n, 47, W, H)
+    if cam == "oblique":
+        view = gs.look_at((3.0, 2.0, 4.0), (0.0, 0.0, -11.0))
+        u = gs.pack_uniforms(view, gs.perspective(1.04719755, W / H, 0.03, 1000.0))
+    else:
+        u = _plus_z_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    full = sc.render(u, W, H, gs.make_opts(chunk_fraction=1.0, timing=1))
+    assert gpu_ctx.timings()["n_vis"] > 1000
+    ref, st = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=1e-4)
+    r = image_close_fp32(full, ref, name="cam_" + cam)
+    assert r[2], r
+    for G in (3, 8):
+        parts = [sc.render(u, W, H, gs.make_opts(strip_index=g, strip_count=G, chunk_fraction=1.0))
+                 for g in range(G)]
+        assert np.array_equal(np.concatenate(parts, axis=0)[:H], full), G
+
+
+def test_non_finite_gaussians(gpu_ctx):
+    """NaN / infinite positions, scales and rotations (stored last in Morton order, outside the
+    partition bounds): never drawn, the rest of the image unchanged (fp32 oracle)."""
+    W, H = 320, 240
+    n = 50_000
+    aos = gs.synth_aos(n, 53, W, H).reshape(n, 80)
+    rng = np.random.default_rng(53)
+    bad = rng.choice(n, 600, replace=False)
+    aos[bad[:200], 0] = np.nan
+    aos[bad[200:300], 1] = np.inf
+    aos[bad[300:400], 4:7] = np.inf
+    aos[bad[400:500], 8:12] = np.nan
+    aos[bad[500:], 12] = np.nan
+    aos = aos.reshape(-1)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    img = sc.render(u, W, H)
+    ref, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=1e-4)
+    assert np.isfinite(img).all()
+    r = image_close_fp32(img, ref, name="non_finite")
+    assert r[2], r
