@@ -33,18 +33,15 @@ VALU_PEAK = 256 * 4 * 2.4e9 / 4  # wave instructions / s
 
 
 def algorithmic_bytes(stage, n, n_vis, k, W, H, n_chunk0=None):
-    """Bytes a kernel must move per launch."""
+    """Bytes a kernel group must move per launch."""
     if stage == "project":
-        # read the 48-B geometry record and write key + packed tile rect (8 B) of every Gaussian;
-        # write the 48-B projected record and the 12-B compacted sort element of every chunk-0 splat
-        return 56 * n + 60 * (n_vis if n_chunk0 is None else n_chunk0)
+        # k_cull reads the 16-B cull plane of every Gaussian of a surviving partition (<= N);
+        # each chunk-0 splat: its 48-B geometry record and 192-B SH read, 80 B of slot records
+        # (composite record 48, sort key 8, storage index 4, rect 4, per-Gaussian r2 16) written
+        return 16 * n + 320 * (n_vis if n_chunk0 is None else n_chunk0)
     if stage == "composite":
         # per (tile, splat) entry: the 4-B slot and the 48-B composite record; RGBA f16 out
         return 52 * k + 8 * W * H
-    if stage == "sort":
-        # 4 LSD passes: upsweep reads the key (4 B), downsweep reads key+index+rect and writes
-        # them (24 B); pass 0 runs over all N keys
-        return 28 * n + 3 * 28 * n_vis
     raise KeyError(stage)
 
 
@@ -52,7 +49,7 @@ def pmc_traffic(kernel):
     """HBM bytes per frame of `kernel` from the committed PMC profile of this bench command
     (profiles/<round>_pmc.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE, summed over the kernel's
     launches in a frame); None when no profile is committed."""
-    names = {"composite": "k_composite<false>", "project": "k_project", "sort": "k_radix_"}
+    names = {"composite": "k_composite<false>", "project": "k_project"}
     prof = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc.json")) \
         if os.path.isdir(os.path.join(ROOT, "profiles")) else []
     if not prof:
@@ -60,24 +57,20 @@ def pmc_traffic(kernel):
     d = json.load(open(os.path.join(ROOT, "profiles", prof[-1])))
     tot = 0.0
     for lab, e in d.items():
-        if lab.startswith(names[kernel]) and "traffic_bytes" in e:
-            base = re.sub(r"<[^>]*>", "", lab)  # k_radix_downsweep<8>#2 -> k_radix_downsweep#2
-            if kernel == "sort" and not any(base == "k_radix_%s#%d" % (k, i) for k in
-                                            ("upsweep", "scan", "downsweep") for i in range(4)):
-                continue  # depth passes only
+        if lab.startswith(names[kernel] + "#") and "traffic_bytes" in e:
             tot += e["traffic_bytes"]
     return (tot if tot else None), prof[-1]
 
 
 def pmc_valu(kernel):
     """VALU wave instructions per frame of `kernel` from the committed PMC profile (SQ_INSTS_VALU)."""
-    names = {"composite": "k_composite<false>", "project": "k_project", "sort": "k_radix_"}
+    names = {"composite": "k_composite<false>", "project": "k_project"}
     prof = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc.json")) \
         if os.path.isdir(os.path.join(ROOT, "profiles")) else []
     if not prof:
         return None
     d = json.load(open(os.path.join(ROOT, "profiles", prof[-1])))
-    tot = sum(e.get("SQ_INSTS_VALU", 0.0) for lab, e in d.items() if lab.startswith(names[kernel]))
+    tot = sum(e.get("SQ_INSTS_VALU", 0.0) for lab, e in d.items() if lab.startswith(names[kernel] + "#"))
     return tot or None
 
 
@@ -185,16 +178,23 @@ def main():
     st = ctx.timings()
     st["ms_composite_stage_pass"] = st["ms_composite"]
     st["ms_composite"] = ms_composite_live
+    # one untimed one-chunk frame for the exact visible count and K of SURVEY 8d's byte model
+    # (with a chunk split the pipeline never projects the splats past it)
+    cur["opts"] = gs.make_opts(strip_index=rank, strip_count=world, chunk_fraction=1.0,
+                               out_format=gs.GS_OUT_RGBA_F16)
+    frame()
+    sync()
+    ex = ctx.timings()
     if launched:
         import torch
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        tot = torch.tensor([st["n_vis"], st["k_total"], st["k_entries"]], dtype=torch.float64, device="cuda")
+        tot = torch.tensor([ex["n_vis"], ex["k_total"], st["k_entries"]], dtype=torch.float64, device="cuda")
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         n_vis_all, k_all, k_binned = (int(x) for x in tot.tolist())
     else:
-        n_vis_all, k_all, k_binned = st["n_vis"], st["k_total"], st["k_entries"]
+        n_vis_all, k_all, k_binned = ex["n_vis"], ex["k_total"], st["k_entries"]
 
     ms = elapsed / args.steps * 1e3
     fps = args.steps / elapsed
@@ -202,10 +202,10 @@ def main():
 
     # roofline of the dominant kernel (this rank's per-launch event time, HIP events on the
     # stream the kernel runs on; algorithmic bytes per launch of this rank)
-    stages = {"project": st["ms_project"], "composite": st["ms_composite"], "sort": st["ms_sort"]}
+    stages = {"project": st["ms_project"], "composite": st["ms_composite"]}
     dom = max(stages, key=stages.get)
     rows_here = max(0, min(t1 * 16, H) - row0)
-    a_bytes = algorithmic_bytes(dom, N, st["n_vis"], st["k_entries"], W, rows_here,
+    a_bytes = algorithmic_bytes(dom, N, ex["n_vis"], st["k_entries"], W, rows_here,
                                 n_chunk0=int(round(st["chunk_fraction"] * st["n_vis"])))
     achieved = a_bytes / (stages[dom] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dom)
@@ -233,14 +233,19 @@ def main():
                        "n_gaussians": N, "width": W, "height": H,
                        "parallelism": "row-strips x%d + all-gather" % world if world > 1 else "single GPU"},
             # per-stage HIP-event times from the separate timing=1 loop (events between stages add
-            # ~35 us to its frame), except ms_composite, timed live in the headline loop
-            "stages_ms": {k: round(st[k], 4) for k in ("ms_total", "ms_project", "ms_sort", "ms_bin",
-                                                          "ms_tile_sort", "ms_ranges", "ms_composite",
-                                                          "ms_other")},
-            "n_vis": n_vis_all,
-            "k_total": k_all,
-            "k_binned": k_binned,
-            "chunk_fraction": round(st["chunk_fraction"], 4),
+            # ~20 us to its frame), except ms_composite, timed live in the headline loop:
+            # project = partition cull + cull + projection/colour, bin = count + scans + emission,
+            # tile_sort = per-tile sort, chunk1 = the chunk-1 launch (returns at once when chunk 0
+            # saturated every tile)
+            "stages_ms": {"ms_total": round(st["ms_total"], 4), "ms_project": round(st["ms_project"], 4),
+                          "ms_bin": round(st["ms_bin"], 4), "ms_tile_sort": round(st["ms_tile_sort"], 4),
+                          "ms_composite": round(st["ms_composite"], 4), "ms_chunk1": round(st["ms_sort"], 4),
+                          "ms_other": round(st["ms_other"], 4)},
+            "n_vis": n_vis_all,         # exact, from the one-chunk frame
+            "k_total": k_all,           # SURVEY's K (box tiles of the visible splats), same frame
+            "k_binned": k_binned,       # (tile, splat) entries a timed frame binned (chunk 0)
+            # chunk-0 splats of a timed frame over the exact visible count
+            "chunk_fraction": round(st["chunk_fraction"] * st["n_vis"] / max(1, ex["n_vis"]), 4),
             "tiles_unsaturated": st["tiles_unsaturated"],
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4),

@@ -274,8 +274,8 @@ static void harvest(gs_ctx* c, FrameEvents& f) {
         HIPCHK(hipEventElapsedTime(&ms, f.ev[a], f.ev[b]));
         return (double)ms;
     };
-    HIPCHK(hipEventSynchronize(f.ev[f.level == 1 ? EV_END : f.chunk1 ? EV_COMP_1 : EV_COMP_0]));
-    c->acc_comp_ms += el(EV_RANGES_0, EV_COMP_0) + (f.chunk1 ? el(EV_RANGES_1, EV_COMP_1) : 0.0);
+    HIPCHK(hipEventSynchronize(f.ev[f.level == 1 ? EV_END : EV_COMP_0]));
+    c->acc_comp_ms += el(EV_RANGES_0, EV_COMP_0);
     c->comp_frames++;
     if (f.level != 1) {
         f.pending = false;
@@ -283,10 +283,10 @@ static void harvest(gs_ctx* c, FrameEvents& f) {
     }
     c->acc_ms[ST_TOTAL] += el(EV_BEGIN, EV_END);
     c->acc_ms[ST_PROJECT] += el(EV_PROJ0, EV_PROJ1);
-    c->acc_ms[ST_SORT] += el(EV_PROJ1, EV_DSORT_0) + el(EV_COMP_0, EV_DSORT_1);
-    c->acc_ms[ST_BIN] += el(EV_DSORT_0, EV_BIN_0) + el(EV_DSORT_1, EV_BIN_1);
-    c->acc_ms[ST_TSORT] += el(EV_BIN_0, EV_TSORT_0) + el(EV_BIN_1, EV_TSORT_1);
-    c->acc_ms[ST_RANGES] += el(EV_TSORT_0, EV_RANGES_0) + el(EV_TSORT_1, EV_RANGES_1);
+    c->acc_ms[ST_SORT] += f.chunk1 ? el(EV_COMP_0, EV_COMP_1) : 0.0;  // chunk 1 (k_chunk1)
+    c->acc_ms[ST_BIN] += el(EV_DSORT_0, EV_BIN_0);
+    c->acc_ms[ST_TSORT] += el(EV_BIN_0, EV_TSORT_0);
+    c->acc_ms[ST_RANGES] += el(EV_TSORT_0, EV_RANGES_0);
     c->acc_frames++;
     f.pending = false;
 }
@@ -532,12 +532,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.cp.mode = kCompSecond;
         c1.sat = s->sat;
         c1.bar = s->bar;
-        for (int e = 0; e < 4; ++e) mark(EV_DSORT_1 + e);
         launch_chunk1(c1, c->num_cus, o.accum == GS_ACCUM_FP16_TARGET, st);
-        mark(EV_COMP_1);
+        if (o.timing == 1) mark(EV_COMP_1);
     }
-    if (!two_chunks && o.timing == 1)
-        for (int e = 0; e < 5; ++e) mark(EV_DSORT_1 + e);
     {  // statistics into the slot, FrameCtl zeroed for the next frame
         const uint32_t q = s->seq_next++;
         s->stat_want[slot] = q;

@@ -81,24 +81,31 @@ typedef struct gs_opts {
                              (each event costs the stream a few microseconds) */
     float chunk_fraction; /* depth split between the two chunks (the image never depends on it):
                              0 = adaptive (from the depth at which tiles saturated last frame),
-                             >= 1 = one chunk, (0,1) = fixed split at the depth-rank quantile
-                             2^-t <= chunk_fraction of the last one-chunk frame (tests/diagnostics) */
+                             >= 1 = one chunk, (0,1) = fixed split at the depth 2^-t <=
+                             chunk_fraction of the way from the last frame's nearest to its
+                             farthest visible splat (tests/diagnostics) */
 } gs_opts;
 
 typedef struct gs_stats {
     uint64_t n;           /* Gaussians in the scene */
-    uint64_t n_vis;       /* splats that reach the sort (visible in this strip) */
+    uint64_t n_vis;       /* visible splats in this strip; exact for a one-chunk frame (with a chunk
+                             split, Gaussians past the split that survive the conservative cull
+                             are counted, and partitions wholly past it are skipped) */
     uint64_t k_entries;   /* (tile, splat) pairs binned (both chunks) */
-    uint64_t k_total;     /* pairs a single-chunk frame would bin (sum of tile counts, SURVEY's K) */
+    uint64_t k_total;     /* sum of the box tile counts of the binned splats (SURVEY's K for a
+                             one-chunk frame) */
     uint32_t tiles_unsaturated;  /* tiles chunk 0 left unsaturated */
     float chunk_fraction; /* fraction of the visible splats sorted in chunk 0 (last frame) */
     int32_t tile_row_begin, tile_row_end;  /* tile rows rendered by the last call */
     int32_t tiles_x;
     int32_t frames;       /* timed frames since gs_timings_reset; ms_composite averages all of them, the
                              other stage times the frames timed with opts.timing = 1 */
-    float ms_total;       /* mean HIP-event times per timed frame: whole frame and per stage; */
+    float ms_total;       /* mean HIP-event times per timed frame: whole frame and per stage: */
     float ms_project, ms_sort, ms_bin, ms_tile_sort, ms_ranges, ms_composite, ms_other;
-                          /* project / composite are single kernels, the others kernel groups */
+                          /* project = partition cull + cull + projection/colour; ms_sort = chunk 1
+                             (one launch; ~0 when chunk 0 saturated every tile); bin = count,
+                             column scan, tile scan, emission; tile_sort = per-tile sort; ranges
+                             = 0 (kept for the ABI); composite = chunk 0's composite */
     uint32_t k_chunk0, k_chunk1;  /* pairs binned per chunk (last frame) */
     uint32_t wide_chunk0, wide_chunk1;  /* splats of >= 32 tiles emitted row-wise, per chunk */
 } gs_stats;
