@@ -28,8 +28,8 @@ def short(name):
     return re.sub(r"^void ", "", name).replace("gs::", "")
 
 
-def frames_of(rows, key_start="k_cull"):
-    """Split dispatches (in order) into frames starting at k_cull; label positions."""
+def frames_of(rows, key_start="k_part_cull"):
+    """Split dispatches (in order) into frames starting at k_part_cull; label positions."""
     frames, cur = [], None
     for r in rows:
         n = short(r["Kernel_Name"])
@@ -63,15 +63,16 @@ def main():
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(prof, tag + "_kernel_stats.csv"))
 
-    # durations by frame position (skip warm-up: use the last 20 frames)
+    # durations by frame position (skip warm-up: the 20 frames before the last, which is
+    # bench.py's untimed one-chunk statistics frame)
     trace = frames_of(load_trace(os.path.join(src, "stats", "run_kernel_trace.csv")))
-    timed = trace[-20:]
+    timed = trace[-21:-1]
     dur = defaultdict(list)
     for f in timed:
         for lab, r in f:
             dur[lab].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    f = trace[-2]
-    lines = ["one steady-state frame (second to last), %d launches" % len(f),
+    f = trace[-3]
+    lines = ["one steady-state frame (third to last), %d launches" % len(f),
              "(gaps inside the stream are host launch latency under the tracer; untraced frames",
              " keep the queue full: compare span with bench ms_per_step)"]
     prev = None
@@ -99,7 +100,7 @@ def main():
                                                    "Start_Timestamp": r["Start_Timestamp"], "c": defaultdict(float)})
             d["c"][r["Counter_Name"]] += float(r["Counter_Value"])
         order = sorted(disp.values(), key=lambda d: int(d["Start_Timestamp"]))
-        for fr in frames_of(order)[-5:]:
+        for fr in frames_of(order)[-6:-1]:
             for lab, d in fr:
                 for c, v in d["c"].items():
                     pmc[lab][c].append(v)
