@@ -1888,6 +1888,15 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(TileSortParams p) {
 // Chunked frames: mode kCompFirst marks saturated tiles done (and writes them out) and parks the
 // per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
 constexpr int kCompBatch = 128;
+#if defined(GS_COMP_STATS) || defined(GS_COMP_TIME)
+#define GS_COMP_DIAG 1
+#endif
+#ifdef GS_COMP_DIAG
+// diagnostics builds only (make diag): counters of k_composite's per-wave blends (GS_COMP_STATS),
+// per-tile wall-clock spans (GS_COMP_TIME or GS_COMP_STATS)
+__device__ unsigned long long g_comp_cnt[16384][2][8];  // per tile and wave (plain stores: no atomics)
+__device__ unsigned long long g_comp_time[16384][3];  // per tile: start | n << 40, end | blends << 40, hw ids
+#endif
 #ifndef GS_QUARTER_TILES
 #define GS_QUARTER_TILES 1536
 #endif
@@ -1895,21 +1904,20 @@ constexpr int kQuarterTiles = GS_QUARTER_TILES;  // at most this many tiles: k_c
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <bool FP16_TARGET>
-__global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
+__device__ __forceinline__ void composite_tile(const CompositeParams& p, const int tile) {
     // staged record per batch entry: [0] c0u, c0v, a, b  [1] c, d, log2(op), slot (bits)
     // [2] r, g, b, -   with u = a lx + b ly + c0u, v = c lx + d ly + c0v in tile-local pixels
     __shared__ float4 sR[2][kCompBatch][3];
-    __shared__ uint8_t sL[2][2][kCompBatch];   // per half: batch indices, segment = producing wave
+    __shared__ uint16_t sL[2][2][kCompBatch];  // per half: LDS byte offsets of the staged records in sR
+                                               // (no multiply when a wave walks its list), segment =
+                                               // producing wave
     __shared__ uint32_t sN[2][2][2];           // per half, per producing wave: list length
     __shared__ uint32_t s_sat;                 // depth key of the splat that saturated the last wave
     const int tid = threadIdx.x;
-    // XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch), so XCD b % 8 gets
-    // the contiguous band of tiles [(b % 8) * per, (b % 8 + 1) * per): a splat's neighbouring
-    // tiles then read its record through one L2
-    const int per = (p.n_tiles + 7) >> 3;
-    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (tile >= p.n_tiles) return;
     if (p.mode == kCompSecond && p.done[tile]) return;
+#ifdef GS_COMP_DIAG
+    const unsigned long long t_begin = wall_clock64();
+#endif
     const int h = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
     const int tx0 = tx * kTile, ty0 = ty * kTile;
@@ -1925,6 +1933,9 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     f2 cr = {0.0f, 0.0f}, cg = {0.0f, 0.0f}, cb = {0.0f, 0.0f};
     f2 T = {1.0f, 1.0f};   // FP32: transmittance
     f2 ca = {0.0f, 0.0f};  // FP16_TARGET: dst.a
+#ifdef GS_COMP_DIAG
+    unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     if (p.mode == kCompSecond) {
         if (in0) {
             const float4 st = p.state[pix0];
@@ -1946,24 +1957,34 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
     float4 ga, gb, gc;
     uint32_t gs_ = 0;
     bool gv = false;
+    // the batch's slot ids are loaded one batch ahead of its records, so the record loads of batch
+    // b + 1 do not wait for a tile-list load first
+    uint32_t sl_next = 0;
+    auto load_slots = [&](uint32_t batch) {
+        const uint32_t e = range.x + batch * kCompBatch + tid;
+        if (e < range.y) sl_next = tvals[e];
+    };
     auto gather = [&](uint32_t batch) {
         const uint32_t e = range.x + batch * kCompBatch + tid;
         gv = e < range.y;
         if (gv) {
-            gs_ = tvals[e];
+            gs_ = sl_next;
             const float4* r = rec + 3 * (uint64_t)gs_;
             ga = r[0];
             gb = r[1];
             gc = r[2];
         }
+        if (batch + 1 < nb) load_slots(batch + 1);
     };
     auto park = [&](int buf) {
         // offsets of the axes' linear forms at the tile origin (explicit roundings, see blend)
         const float cxr = ga.x - (float)tx0, cyr = ga.y - (float)ty0;
         const float c0u = -__builtin_fmaf(cxr, ga.z, cyr * ga.w);
         const float c0v = -__builtin_fmaf(cxr, gb.x, cyr * gb.y);
-        sR[buf][tid][0] = make_float4(c0u, c0v, ga.z, ga.w);
-        sR[buf][tid][1] = make_float4(gb.x, gb.y, gb.z, __uint_as_float(gs_));  // box x: used below only
+        // staged as [b, a, d, c] [c0u, slot, c0v, log2 op] [r, g, b, key]: every value a packed
+        // op broadcasts sits in the low half of an aligned register pair (no moves in the blend)
+        sR[buf][tid][0] = make_float4(ga.w, ga.z, gb.y, gb.x);
+        sR[buf][tid][1] = make_float4(c0u, __uint_as_float(gs_), c0v, gb.z);
         sR[buf][tid][2] = gc;
         // the splat's pixel columns within this tile's rows (ellipse; the binning's margins)
         uint32_t ul = 0u, uh = 0u;
@@ -1974,23 +1995,37 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
             const int qx = tx0 + q * 8;
             const bool hit = cols && x0 <= qx + 7 && x1 >= qx;
             const uint64_t b = __ballot(hit);
-            if (hit) sL[buf][q][h * 64 + __popcll(b & lanemask_lt())] = (uint8_t)tid;
+            if (hit) sL[buf][q][h * 64 + __popcll(b & lanemask_lt())] = (uint16_t)(((buf * kCompBatch + tid) * 3) * 16);
             if (lane == 0) sN[buf][q][h] = (uint32_t)__popcll(b);
         }
     };
-    auto blend = [&](int k, int cur) {
-        const float4 A = sR[cur][k][0];
-        const float4 B = sR[cur][k][1];
-        const float4 C = sR[cur][k][2];
+    const char* const sRb = (const char*)&sR[0][0][0];
+    auto blend = [&](uint32_t off) {
+        const float4 A = *(const float4*)(sRb + off);
+        const float4 B = *(const float4*)(sRb + off + 16);
+        const float4 C = *(const float4*)(sRb + off + 32);
         // every rounding is spelled out (explicit fma or contraction off), so each inlined copy of
         // this blend rounds identically and the image cannot depend on where batches split
-        const f2 u = __builtin_elementwise_fma(ly, (f2)A.w, (f2)__builtin_fmaf(lx, A.z, A.x));
-        const f2 v = __builtin_elementwise_fma(ly, (f2)B.y, (f2)__builtin_fmaf(lx, B.x, A.y));
+        const f2 u = __builtin_elementwise_fma(ly, (f2)A.x, (f2)__builtin_fmaf(lx, A.y, B.x));
+        const f2 v = __builtin_elementwise_fma(ly, (f2)A.z, (f2)__builtin_fmaf(lx, A.w, B.z));
         const f2 qd = __builtin_elementwise_fma(u, u, v * v);
-        const f2 e = (f2)B.z - qd;
+        const f2 e = (f2)B.w - qd;
         const float a0 = __builtin_amdgcn_exp2f(e.x), a1 = __builtin_amdgcn_exp2f(e.y);
         const bool hit0 = live0 && fmaxf(fabsf(u.x), fabsf(v.x)) <= L && a0 >= amin;
         const bool hit1 = live1 && fmaxf(fabsf(u.y), fabsf(v.y)) <= L && a1 >= amin;
+#ifdef GS_COMP_STATS
+        {
+            const uint64_t b0 = __ballot(hit0), b1 = __ballot(hit1);
+            dg[0] += 1;
+            dg[1] += __popcll(__ballot(live0)) + __popcll(__ballot(live1));
+            dg[2] += __popcll(b0) + __popcll(b1);
+            dg[3] += (b0 | b1) == 0;
+            dg[4] += b0 != 0 && b1 == 0;
+            dg[5] += b0 == 0 && b1 != 0;
+            const float r = e.x > e.y ? e.x : e.y;  // best of the pair, ignoring the quad box
+            dg[6] += __popcll(__ballot(r >= -7.99f));
+        }
+#endif
         if (FP16_TARGET) {
 #pragma clang fp contract(off)
             // the blend unit: src * (1 - dst.a) + dst, stored as fp16 (as the oracle does it)
@@ -2011,7 +2046,10 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
                 live1 = ca.y < 1.0f;
             }
         } else {
-            const f2 s2 = {hit0 ? a0 * T.x : 0.0f, hit1 ? a1 * T.y : 0.0f};
+#pragma clang fp contract(off)
+            // (no contraction: T - am T must not become one fma, k_composite_q rounds it twice)
+            const f2 am = {hit0 ? a0 : 0.0f, hit1 ? a1 : 0.0f};
+            const f2 s2 = am * T;  // = hit ? a T : 0 (T is finite and >= 0)
             cr = __builtin_elementwise_fma((f2)C.x, s2, cr);
             cg = __builtin_elementwise_fma((f2)C.y, s2, cg);
             cb = __builtin_elementwise_fma((f2)C.z, s2, cb);
@@ -2020,8 +2058,12 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
             live1 = live1 && T.y >= t_min;
         }
     };
+#ifdef GS_COMP_DIAG
+    if (tid == 0) dg[7] = n;
+#endif
     if (tid == 0) s_sat = 0;
     if (nb > 0) {
+        load_slots(0);
         gather(0);
         park(0);
     }
@@ -2032,26 +2074,26 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
         if (wave_live) {
             for (int seg = 0; seg < 2 && wave_live; ++seg) {
                 const int cnt = (int)sN[cur][h][seg];
-                const uint8_t* list = &sL[cur][h][seg * 64];
+                const uint16_t* list = &sL[cur][h][seg * 64];
                 int k = 0;
                 for (; k + 3 < cnt; k += 4) {  // saturation checked every 4 splats
-                    const int i3 = list[k + 3];
-                    blend(list[k], cur);
-                    blend(list[k + 1], cur);
-                    blend(list[k + 2], cur);
-                    blend(i3, cur);
+                    const uint32_t o3 = list[k + 3];
+                    blend(list[k]);
+                    blend(list[k + 1]);
+                    blend(list[k + 2]);
+                    blend(o3);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][i3][2].w));
+                        if (lane == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + o3 + 44));
                         break;
                     }
                 }
                 for (; wave_live && k < cnt; ++k) {
-                    const int ik = list[k];
-                    blend(ik, cur);
+                    const uint32_t ok = list[k];
+                    blend(ok);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][ik][2].w));
+                        if (lane == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + ok + 44));
                     }
                 }
             }
@@ -2059,6 +2101,24 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
         if (b + 1 < nb) park(cur ^ 1);
         if (__syncthreads_count(wave_live) == 0) break;
     }
+#ifdef GS_COMP_DIAG
+    if (lane == 0 && tile < 16384)
+        for (int i = 0; i < 8; ++i) g_comp_cnt[tile][h][i] = dg[i];
+    __shared__ uint32_t s_blends;
+    if (tid == 0) s_blends = 0;
+    __syncthreads();
+    if (lane == 0) atomicAdd(&s_blends, (uint32_t)dg[0]);
+    __syncthreads();
+    if (tid == 0 && tile < 16384) {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_comp_time[tile][0] = (t_begin & 0xffffffffffull) | ((unsigned long long)min(n, 0xffffffu) << 40);
+        g_comp_time[tile][1] = (wall_clock64() & 0xffffffffffull) | ((unsigned long long)min(s_blends, 0xffffffu) << 40);
+        g_comp_time[tile][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    }
+#endif
     const bool tile_done = __syncthreads_count(live0 || live1) == 0;
     if (tile_done && tid == 0 && n > 0) {  // saturation statistics for the chunk controller
         atomicAdd(&p.ctl->sat_tiles[tile % kHistShards], 1u);
@@ -2089,6 +2149,19 @@ __global__ __launch_bounds__(128) void k_composite(CompositeParams p) {
 }
 
 
+// One tile per workgroup.  XCD-aware order: blocks b and b + 8 share an XCD (round-robin
+// dispatch), so XCD b % 8 gets the contiguous band of tiles [(b % 8) per, (b % 8 + 1) per): a
+// splat's neighbouring tiles then read its record through one L2.  Measured alternatives (8160
+// tiles, 2560 resident workgroups; the last partly filled round costs ~25 % of the span): a
+// resident grid with per-band ticket counters (278 us), an equal static share per workgroup
+// (285 us) and one ticket counter for all bands (352 us) were all slower than this (230 us).
+template <bool FP16_TARGET>
+__global__ __launch_bounds__(128, 5) void k_composite(CompositeParams p) {
+    const int per = (p.n_tiles + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile < p.n_tiles) composite_tile<FP16_TARGET>(p, tile);
+}
+
 // Quarter variant for frames with few tiles (row strips): 4 waves per tile, wave q owns the 8x8
 // quarter (q & 1, q >> 1) at one pixel per lane, and each splat is listed only for the quarters
 // its ellipse reaches (columns within the quarter's rows).  Per pixel it performs the same
@@ -2098,7 +2171,7 @@ constexpr int kCompBatchQ = 256;
 
 struct CompQShared {
     float4 sR[2][kCompBatchQ][3];
-    uint8_t sL[2][4][kCompBatchQ];  // per quarter: batch indices, segment = producing wave
+    uint16_t sL[2][4][kCompBatchQ];  // per quarter: LDS byte offsets of the records in sR, segment = producing wave
     uint32_t sN[2][4][4];           // per quarter, per producing wave: list length
     uint32_t s_sat;
 };
@@ -2139,23 +2212,31 @@ __device__ void composite_q_body(const CompositeParams& p, uint32_t vb, CompQSha
     float4 ga, gb, gc;
     uint32_t gs_ = 0;
     bool gv = false;
+    // the batch's slot ids are loaded one batch ahead of its records, so the record loads of batch
+    // b + 1 do not wait for a tile-list load first
+    uint32_t sl_next = 0;
+    auto load_slots = [&](uint32_t batch) {
+        const uint32_t e = range.x + batch * kCompBatchQ + tid;
+        if (e < range.y) sl_next = tvals[e];
+    };
     auto gather = [&](uint32_t batch) {
         const uint32_t e = range.x + batch * kCompBatchQ + tid;
         gv = e < range.y;
         if (gv) {
-            gs_ = tvals[e];
+            gs_ = sl_next;
             const float4* r = rec + 3 * (uint64_t)gs_;
             ga = r[0];
             gb = r[1];
             gc = r[2];
         }
+        if (batch + 1 < nb) load_slots(batch + 1);
     };
     auto park = [&](int buf) {
         const float cxr = ga.x - (float)tx0, cyr = ga.y - (float)ty0;
         const float c0u = -__builtin_fmaf(cxr, ga.z, cyr * ga.w);
         const float c0v = -__builtin_fmaf(cxr, gb.x, cyr * gb.y);
-        sR[buf][tid][0] = make_float4(c0u, c0v, ga.z, ga.w);
-        sR[buf][tid][1] = make_float4(gb.x, gb.y, gb.z, __uint_as_float(gs_));
+        sR[buf][tid][0] = make_float4(ga.w, ga.z, gb.y, gb.x);  // as k_composite
+        sR[buf][tid][1] = make_float4(c0u, __uint_as_float(gs_), c0v, gb.z);
         sR[buf][tid][2] = gc;
         const Ellipse el = ellipse_of(ga, gb);
 #pragma unroll
@@ -2167,20 +2248,21 @@ __device__ void composite_q_body(const CompositeParams& p, uint32_t vb, CompQSha
                 const int q = hy * 2 + hx, qx = tx0 + hx * 8;
                 const bool hit = cols && (int)ul <= qx + 7 && (int)uh >= qx;
                 const uint64_t b = __ballot(hit);
-                if (hit) sL[buf][q][qw * 64 + __popcll(b & lanemask_lt())] = (uint8_t)tid;
+                if (hit) sL[buf][q][qw * 64 + __popcll(b & lanemask_lt())] = (uint16_t)(((buf * kCompBatchQ + tid) * 3) * 16);
                 if (lane == 0) sN[buf][q][qw] = (uint32_t)__popcll(b);
             }
         }
     };
-    auto blend = [&](int k, int cur) {
-        const float4 A = sR[cur][k][0];
-        const float4 B = sR[cur][k][1];
-        const float4 C = sR[cur][k][2];
+    const char* const sRb = (const char*)&sR[0][0][0];
+    auto blend = [&](uint32_t off) {
+        const float4 A = *(const float4*)(sRb + off);
+        const float4 B = *(const float4*)(sRb + off + 16);
+        const float4 C = *(const float4*)(sRb + off + 32);
         // the same roundings as k_composite's packed pair
-        const float u = __builtin_fmaf(ly, A.w, __builtin_fmaf(lx, A.z, A.x));
-        const float v = __builtin_fmaf(ly, B.y, __builtin_fmaf(lx, B.x, A.y));
+        const float u = __builtin_fmaf(ly, A.x, __builtin_fmaf(lx, A.y, B.x));
+        const float v = __builtin_fmaf(ly, A.z, __builtin_fmaf(lx, A.w, B.z));
         const float qd = __builtin_fmaf(u, u, v * v);
-        const float e = B.z - qd;
+        const float e = B.w - qd;
         const float a = __builtin_amdgcn_exp2f(e);
         const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && a >= amin;
         if (FP16_TARGET) {
@@ -2204,6 +2286,7 @@ __device__ void composite_q_body(const CompositeParams& p, uint32_t vb, CompQSha
     };
     if (tid == 0) s_sat = 0;
     if (nb > 0) {
+        load_slots(0);
         gather(0);
         park(0);
     }
@@ -2214,26 +2297,26 @@ __device__ void composite_q_body(const CompositeParams& p, uint32_t vb, CompQSha
         if (wave_live) {
             for (int seg = 0; seg < 4 && wave_live; ++seg) {
                 const int cnt = (int)sN[cur][qw][seg];
-                const uint8_t* list = &sL[cur][qw][seg * 64];
+                const uint16_t* list = &sL[cur][qw][seg * 64];
                 int k = 0;
                 for (; k + 3 < cnt; k += 4) {
-                    const int i3 = list[k + 3];
-                    blend(list[k], cur);
-                    blend(list[k + 1], cur);
-                    blend(list[k + 2], cur);
-                    blend(i3, cur);
+                    const uint32_t o3 = list[k + 3];
+                    blend(list[k]);
+                    blend(list[k + 1]);
+                    blend(list[k + 2]);
+                    blend(o3);
                     if (!__any(live)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][i3][2].w));
+                        if (lane == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + o3 + 44));
                         break;
                     }
                 }
                 for (; wave_live && k < cnt; ++k) {
-                    const int ik = list[k];
-                    blend(ik, cur);
+                    const uint32_t ok = list[k];
+                    blend(ok);
                     if (!__any(live)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, __float_as_uint(sR[cur][ik][2].w));
+                        if (lane == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + ok + 44));
                     }
                 }
             }
@@ -2468,11 +2551,21 @@ void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
             hipLaunchKernelGGL(k_composite_q<true>, dim3(grid), dim3(256), 0, s, p);
         else
             hipLaunchKernelGGL(k_composite_q<false>, dim3(grid), dim3(256), 0, s, p);
-    } else if (accum_fp16) {
-        hipLaunchKernelGGL(k_composite<true>, dim3(grid), dim3(128), 0, s, p);
     } else {
-        hipLaunchKernelGGL(k_composite<false>, dim3(grid), dim3(128), 0, s, p);
+        if (accum_fp16)
+            hipLaunchKernelGGL(k_composite<true>, dim3(grid), dim3(128), 0, s, p);
+        else
+            hipLaunchKernelGGL(k_composite<false>, dim3(grid), dim3(128), 0, s, p);
     }
 }
 
 }  // namespace gs
+
+#ifdef GS_COMP_DIAG
+extern "C" int gs_diag_comp_times(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_comp_time), (size_t)n * 24) == hipSuccess ? 0 : -1;
+}
+extern "C" int gs_diag_comp_counters(unsigned long long* out, int n_tiles) {  // out: n_tiles x 2 x 8
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_comp_cnt), (size_t)n_tiles * 128) == hipSuccess ? 0 : -1;
+}
+#endif
