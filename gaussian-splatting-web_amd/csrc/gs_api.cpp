@@ -517,7 +517,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     mark(EV_RANGES_0);
     launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
     mark(EV_COMP_0);
-    if (two_chunks) {
+    {  // chunk 1 (when chunk 0 left tiles unsaturated), then the frame's end: statistics into the
+       // slot, FrameCtl zeroed for the next frame; one launch
         Chunk1Params c1{};
         c1.pp = pp;
         c1.pp.sat = s->sat;
@@ -532,13 +533,15 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.cp.mode = kCompSecond;
         c1.sat = s->sat;
         c1.bar = s->bar;
-        launch_chunk1(c1, c->num_cus, o.accum == GS_ACCUM_FP16_TARGET, st);
-        if (o.timing == 1) mark(EV_COMP_1);
-    }
-    {  // statistics into the slot, FrameCtl zeroed for the next frame
+        c1.two_chunks = two_chunks ? 1 : 0;
         const uint32_t q = s->seq_next++;
         s->stat_want[slot] = q;
-        launch_frame_end(s->ctl, s->stats, s->bar, s->d_ctl_slot + slot, s->d_seq + slot, q, st);
+        c1.stats = s->stats;
+        c1.host_ctl = s->d_ctl_slot + slot;
+        c1.host_seq = s->d_seq + slot;
+        c1.seq = q;
+        launch_chunk1(c1, c->num_cus, o.accum == GS_ACCUM_FP16_TARGET, st);
+        if (two_chunks && o.timing == 1) mark(EV_COMP_1);
     }
     s->meta_clean = true;
     mark(EV_END);

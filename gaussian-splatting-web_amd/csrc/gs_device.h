@@ -254,7 +254,13 @@ struct Chunk1Params {
     TileSortParams tp;
     CompositeParams cp;           // mode kCompSecond
     uint32_t* sat;                // SAT of the unsaturated tiles (written by the first phase)
-    uint32_t* bar;                // grid-barrier arrival counter, zero at launch (k_frame_end)
+    uint32_t* bar;                // grid-barrier arrival counter, zero at launch (the frame's end zeroes it)
+    int two_chunks;               // chunk 1 may have work (else only the frame's end runs)
+    // the frame's end (frame_end_body): statistics shards, pinned-slot copy, sequence number
+    StatShard* stats;
+    FrameCtl* host_ctl;
+    uint32_t* host_seq;
+    uint32_t seq;
 };
 
 // launchers (gs_kernels.hip)
@@ -269,8 +275,6 @@ void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 slots (or, 
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit, wide rows
 // stats -> host slot + seq; then FrameCtl zeroed for the next frame
-void launch_frame_end(FrameCtl* ctl, StatShard* stats, uint32_t* bar, FrameCtl* host_ctl, uint32_t* host_seq,
-                      uint32_t seq, hipStream_t s);
 // chunk 1 in one launch (grid: one workgroup per CU; returns at once when chunk 0 saturated every tile)
 struct Chunk1Params;
 void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t s);

@@ -354,11 +354,10 @@ struct Proj {
 
 // Cull, footprint, depth key, tile rect and projected record of Gaussian i; false (key =
 // kSentinel) when invisible.  Deterministic: k_records recomputes the same record bit for bit.
-__device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, int row_lo, int row_hi,
-                                             bool cull, Proj& o) {
+__device__ __forceinline__ bool project_core_g(const ProjParams& p, uint32_t i, const float4 g0, const float4 g1,
+                                               const float4 g2, int row_lo, int row_hi, bool cull, Proj& o) {
     o.key = kSentinel;
     o.prect = kRectEmpty;
-    const float4 g0 = p.geo[3 * (uint64_t)i], g1 = p.geo[3 * (uint64_t)i + 1], g2 = p.geo[3 * (uint64_t)i + 2];
         const float x = g0.x, y = g0.y, z = g0.z;
         const float sx = g1.x, sy = g1.y, sz = g1.z;
         const float qx = g1.w, qy = g2.x, qz = g2.y, qw = g2.z;
@@ -465,16 +464,25 @@ __device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, in
         return true;
 }
 
+// project_core_g with Gaussian i's geometry record loaded here.
+__device__ __forceinline__ bool project_core(const ProjParams& p, uint32_t i, int row_lo, int row_hi,
+                                             bool cull, Proj& o) {
+    const float4 g0 = p.geo[3 * (uint64_t)i], g1 = p.geo[3 * (uint64_t)i + 1], g2 = p.geo[3 * (uint64_t)i + 2];
+    return project_core_g(p, i, g0, g1, g2, row_lo, row_hi, cull, o);
+}
+
 // SH colour of a Gaussian at (px, py, pz) from its packed coefficients sh (nq quads,
 // coefficient k channel c at 3k + c), src/simple_render.ts:5-67, :321: one thread, the
 // reference's expression order with contraction off (bit-identical to the oracle).
+// shq[STRIDE t] = quad t of the packed coefficients (STRIDE 64: a wave's LDS staging, k_project)
+template <int STRIDE = 1>
 __device__ __forceinline__ float4 sh_colour(const float4* __restrict__ shq, uint32_t nq, float px, float py, float pz,
                                             const float* cam) {
 #pragma clang fp contract(off)
     float f[48];
 #pragma unroll
     for (uint32_t t = 0; t < 12; ++t) {
-        const float4 q = t < nq ? shq[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 q = t < nq ? shq[STRIDE * t] : make_float4(0.f, 0.f, 0.f, 0.f);
         f[4 * t] = q.x;
         f[4 * t + 1] = q.y;
         f[4 * t + 2] = q.z;
@@ -521,15 +529,16 @@ __device__ __forceinline__ void store_colour(const ProjParams& p, uint32_t j) {
 
 // A visible splat's composite slot: records r0, r1 (the colour quad follows: k_colour or
 // k_records), its sort key (depth key, index) and packed rect; and its per-Gaussian r2.
-__device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, uint32_t i, const Proj& o) {
+__device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, uint32_t i, uint32_t oi, const Proj& o) {
     float4* r = p.crec + 3 * (uint64_t)slot;
     r[0] = o.r0;
     r[1] = o.r1;
-    p.skey[slot] = make_uint2(o.key, p.orig[i]);
+    p.skey[slot] = make_uint2(o.key, oi);
     p.sidx[slot] = i;
     p.srect[slot] = o.prect;
-    p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles), __uint_as_float(o.bbx),
-                              __uint_as_float(o.bby));
+    if (o.prect == kRectLarge)  // binning reads the pixel box of a rect wider or taller than 16 tiles
+        p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles), __uint_as_float(o.bbx),
+                                  __uint_as_float(o.bby));
 }
 
 // Chunk 1 (after chunk 0 left tiles unsaturated), or every visible Gaussian's per-Gaussian
@@ -587,7 +596,7 @@ __device__ void records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
         base = __shfl(base, 0, 64);
         if (want) {
             const uint32_t slot = slot_c1(i0 / kProjTile, base + (uint32_t)__popcll(b & lanemask_lt()));
-            store_slot(p, slot, i, o);
+            store_slot(p, slot, i, p.orig[i], o);
             float4 c = colour_of(p, i);
             c.w = __uint_as_float(o.key);
             p.crec[3 * (uint64_t)slot + 2] = c;
@@ -708,10 +717,14 @@ __device__ __forceinline__ UnitList load_units(const uint32_t* units, const Fram
 }
 __device__ __forceinline__ uint32_t unit_at(const UnitList& L, uint32_t j) {
     if (!L.units) return j;
-    int k = 0;
+    uint32_t k = 0, base = 0;  // selects, not an indexed array: no scratch round trip
 #pragma unroll
-    for (int t = 1; t < kUnitShards; ++t) k += j >= L.pre[t] ? 1 : 0;
-    return L.units[(uint64_t)k * L.cap + (j - L.pre[k])];
+    for (int t = 1; t < kUnitShards; ++t)
+        if (j >= L.pre[t]) {
+            k = (uint32_t)t;
+            base = L.pre[t];
+        }
+    return L.units[(uint64_t)k * L.cap + (j - base)];
 }
 
 // Projection, phase A (one workgroup per surviving projection partition of kProjTile storage
@@ -814,10 +827,15 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
 // frame's unit list; a visible one gets its records and (from its shading block, one thread per
 // splat in the reference's expression order: sh_colour) its colour in its slot, an invisible one
 // leaves the slot a hole (rect kRectHole).  Publishes the visible count, their tile total, the depth range.
+template <bool SH12>  // SH12: degree-3 scenes (12 coefficient quads), staged through LDS
 __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     __shared__ unsigned long long s_k;
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
+    // per wave: the SH quads of its 64 candidates, [quad][lane], loaded straight into LDS
+    // (global_load_lds: no registers held, in flight while the footprint is computed)
+    __shared__ float4 s_sh[SH12 ? kProjThreads / 64 : 1][SH12 ? 12 : 1][64];
     const int tid = threadIdx.x;
+    const int wv = tid >> 6, lane = tid & 63;
     if (tid == 0) { s_k = 0; s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
     __syncthreads();
     uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
@@ -828,14 +846,68 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     for (uint32_t j = blockIdx.x; j < L.total; j += gridDim.x) {
         const uint32_t u = unit_at(L, j);
         const uint32_t part = u / kProjRounds, q = (u % kProjRounds) * kProjThreads + tid;
-        if (q >= p.c0[part]) continue;
-        const uint32_t p0 = part * kProjTile, slot = slot_c0(part, q);
-        const uint32_t i = p0 + (uint32_t)p.cand[p0 + q];
+        const uint32_t p0 = part * kProjTile;
+        const uint32_t cq = p.cand[p0 + q];  // in flight with the count (always inside the buffer)
+        const uint32_t c0n = p.c0[part];
+        asm volatile("" ::"v"(cq));          // keeps the candidate load ahead of the branch
+        if (q >= c0n) continue;
+        const uint32_t slot = slot_c0(part, q);
+        const uint32_t i = p0 + cq;
+        uint32_t oi;
+        float4 g0, g1, g2;
+        if (SH12) {
+            // one asm block: the geometry record into registers, then the 12 SH quads straight
+            // into this wave's LDS staging (global_load_lds: lane l lands at M0 + the
+            // instruction's offset + 16 l, so M0 steps by 1024 - 16 per quad),
+            // then a wait for the geometry alone (vmcnt counts in issue order: 12 still in
+            // flight).  The compiler does not see these loads, so it cannot drain them early.
+            const float4* gp = p.geo + 3 * (uint64_t)i;
+            const float4* sp = p.sh + 12 * (uint64_t)i;
+            const uint32_t* op = p.orig + i;
+            uint32_t m0save;
+            const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)&s_sh[wv][0][0]);
+            asm volatile(
+                "s_mov_b32 %[msave], m0\n"
+                "global_load_dword %[oi], %[op], off\n"
+                "global_load_dwordx4 %[g0], %[gp], off\n"
+                "global_load_dwordx4 %[g1], %[gp], off offset:16\n"
+                "global_load_dwordx4 %[g2], %[gp], off offset:32\n"
+                "s_mov_b32 m0, %[lds]\n s_nop 0\n"
+                "global_load_lds_dwordx4 %[sp], off\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:16\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:32\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:48\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:64\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:80\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:96\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:112\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:128\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:144\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:160\n"
+                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:176\n"
+                "s_waitcnt vmcnt(12)\n"
+                "s_mov_b32 m0, %[msave]\n"  // M0 restored (the compiler's value, if it holds one)
+                : [g0] "=&v"(g0), [g1] "=&v"(g1), [g2] "=&v"(g2), [oi] "=&v"(oi), [msave] "=&s"(m0save)
+                : [gp] "v"(gp), [sp] "v"(sp), [op] "v"(op), [lds] "s"(lds)
+                : "memory");
+        } else {
+            oi = p.orig[i];
+            const float4* gi = p.geo + 3 * (uint64_t)i;
+            g0 = gi[0];
+            g1 = gi[1];
+            g2 = gi[2];
+        }
         Proj o;
-        if (project_core(p, i, row_lo, row_hi, false, o)) {
-            store_slot(p, slot, i, o);
+        if (project_core_g(p, i, g0, g1, g2, row_lo, row_hi, false, o)) {
+            store_slot(p, slot, i, oi, o);
             if (o.prect != kRectEmpty) {  // the SH colour of a splat that binds a tile
-                float4 col = colour_of(p, i);
+                float4 col;
+                if (SH12) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    col = sh_colour<64>(&s_sh[wv][0][lane], 12, g0.x, g0.y, g0.z, p.cam);
+                } else {
+                    col = sh_colour(p.sh + (uint64_t)i * p.shq, p.shq, g0.x, g0.y, g0.z, p.cam);
+                }
                 col.w = __uint_as_float(o.key);
                 p.crec[3 * (uint64_t)slot + 2] = col;
             }
@@ -1540,8 +1612,8 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
 // host's pinned slot (mapped, fine-grained) and the sequence number published with a
 // system-scope release; the host reads it a frame or two later.  Then FrameCtl is zeroed for the
 // next frame.  One wave; lane l sums shard l.
-__global__ __launch_bounds__(64) void k_frame_end(FrameCtl* ctl, StatShard* stats, uint32_t* bar, FrameCtl* host_ctl,
-                                                 uint32_t* host_seq, uint32_t seq) {
+__device__ void frame_end_body(FrameCtl* ctl, StatShard* stats, uint32_t* bar, FrameCtl* host_ctl, uint32_t* host_seq,
+                               uint32_t seq) {
     constexpr uint32_t kWords = sizeof(FrameCtl) / 4;
     static_assert(kWords <= 64 && kStatShards == 64, "one wave");
     const uint32_t lane = threadIdx.x;
@@ -2391,10 +2463,8 @@ constexpr size_t kBinLdsWords = kBandTiles + (kBinMaxUnits + 1) + 4 + kWideQueue
 constexpr size_t kChunk1Lds = std::max(std::max(kBinLdsWords * 4, sizeof(TsShared)), sizeof(CompQShared));
 
 template <bool FP16_TARGET>
-__global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kChunk1Lds];
+__device__ void chunk1_phases(const Chunk1Params& c, uint8_t* lds) {
     FrameCtl* ctl = c.cp.ctl;
-    if (ctl->not_done == 0) return;  // chunk 0 saturated every tile
     const uint32_t G = gridDim.x, b = blockIdx.x;
     uint32_t nb = 0;
     if (b == 0) sat_body<256>(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat, nullptr);
@@ -2420,7 +2490,20 @@ __global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
     for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body(c.tp, vb, *(TsShared*)lds);
     grid_sync(c.bar, ++nb * G, ctl);
     for (uint32_t vb = b; vb < ntb; vb += G) composite_q_body<FP16_TARGET>(c.cp, vb, *(CompQShared*)lds);
+    grid_sync(c.bar, ++nb * G, ctl);  // every phase done before the frame's end reads FrameCtl
 }
+
+template <bool FP16_TARGET>
+__global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kChunk1Lds];
+    FrameCtl* ctl = c.cp.ctl;
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    if (c.two_chunks && ctl->not_done != 0) chunk1_phases<FP16_TARGET>(c, lds);  // else: chunk 0 saturated every tile
+    // the frame's end (one wave): FrameCtl is read by no workgroup after this point
+    if (b == 0 && threadIdx.x < 64) frame_end_body(ctl, c.stats, c.bar, c.host_ctl, c.host_seq, c.seq);
+    (void)G;
+}
+
 
 // ============================================================================ k_present
 // PostProcessRenderer.fragmentMain (src/post_process_render.ts:62-77) per pixel: the sampler
@@ -2493,7 +2576,10 @@ void launch_project(const ProjParams& p, hipStream_t s) {
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, parts));
     hipLaunchKernelGGL(k_cull, dim3(grid), dim3(kProjThreads), 0, s, p);
     const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (uint64_t)parts * kProjRounds));
-    hipLaunchKernelGGL(k_project, dim3(ugrid), dim3(kProjThreads), 0, s, p);
+    if (p.shq == 12)
+        hipLaunchKernelGGL(k_project<true>, dim3(ugrid), dim3(kProjThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_project<false>, dim3(ugrid), dim3(kProjThreads), 0, s, p);
 }
 void launch_records(const ProjParams& p, hipStream_t s) {
     if (!p.n) return;
@@ -2532,12 +2618,8 @@ void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
     hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(kTsThreads), 0, s, p);
 }
-void launch_frame_end(FrameCtl* ctl, StatShard* stats, uint32_t* bar, FrameCtl* host_ctl, uint32_t* host_seq,
-                      uint32_t seq, hipStream_t s) {
-    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, ctl, stats, bar, host_ctl, host_seq, seq);
-}
 void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t s) {
-    if (c.cp.n_tiles <= 0) return;
+    if (!c.two_chunks || c.cp.n_tiles <= 0) grid = 1;  // the frame's end only
     if (accum_fp16)
         hipLaunchKernelGGL(k_chunk1<true>, dim3(grid), dim3(256), 0, s, c);
     else
