@@ -1539,18 +1539,61 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
 // beyond that the thread emits its splat itself.
 constexpr uint32_t kWideQueue = 512;
 
-template <int NT>
+// SCAN: tbase holds the tile totals (colscan) and every workgroup scans them itself up to its
+// band's end (k_tile_scan's work, repeated per workgroup from L2 instead of one more launch on
+// the frame's critical path); the workgroups of partition 0 write the band's ranges, the one of
+// the last band the chunk's total.  Otherwise tbase holds the list begins (tile_scan_body).
+template <int NT, bool SCAN = false>
 __device__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, uint32_t* s_pref, uint32_t* s_tmp,
                               uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
     const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
-    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) s_cur[t - t_lo] = p.tbase[t] + row[t];
+    const uint32_t cap = p.capacity;
+    if (SCAN) {
+        constexpr int nw = NT / 64, ipt = 8;
+        const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+        uint32_t carry = 0;
+        for (uint32_t t0 = 0; t0 < t_hi; t0 += NT * ipt) {
+            uint32_t v[ipt], sum = 0;
+#pragma unroll
+            for (int k = 0; k < ipt; ++k) {
+                const uint32_t t = t0 + (uint32_t)tid * ipt + k;
+                v[k] = t < t_hi ? p.tbase[t] : 0u;
+                sum += v[k];
+            }
+            const uint32_t incl = wave_incl_scan(sum);
+            if (lane == 63) s_tmp[w] = incl;
+            __syncthreads();
+            uint32_t base = carry + incl - sum, tot = 0;
+            for (int i = 0; i < nw; ++i) {
+                if (i < w) base += s_tmp[i];
+                tot += s_tmp[i];
+            }
+#pragma unroll
+            for (int k = 0; k < ipt; ++k) {
+                const uint32_t t = t0 + (uint32_t)tid * ipt + k;
+                if (t >= t_lo && t < t_hi) {
+                    const uint32_t bb = min(base, cap);
+                    s_cur[t - t_lo] = bb + row[t];
+                    if (part == 0) p.ranges[t] = make_uint2(bb, min(base + v[k], cap));
+                }
+                base += v[k];
+            }
+            carry += tot;
+            __syncthreads();
+        }
+        if (part == 0 && t_hi == p.n_tiles && threadIdx.x == 0) {
+            p.ctl->k_chunk[p.chunk] = min(carry, cap);
+            if (carry > cap) atomicOr(&p.ctl->err, kErrOverflow);
+        }
+    } else {
+        for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) s_cur[t - t_lo] = p.tbase[t] + row[t];
+    }
     if (threadIdx.x == 0) s_nw = 0;
     const UnitList L = bin_unit_list(p);
     const uint32_t total = bin_slots<NT>(p, L, part, s_pref, s_tmp);
-    const uint32_t cap = p.capacity;
     for (uint32_t r = threadIdx.x; r < total; r += NT) {
         const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
@@ -1604,7 +1647,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_wide[kWideQueue];
     __shared__ uint32_t s_nw;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;
-    bin_emit_body<kBinThreads>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, &s_nw);
+    bin_emit_body<kBinThreads, true>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, &s_nw);
 }
 
 // End of a frame: the statistic shards summed into FrameCtl (and zeroed), the saturation
@@ -2610,8 +2653,7 @@ void launch_bin(const BinParams& p, hipStream_t s) {
     const unsigned grid = kBinParts * bin_bands(p.n_tiles);
     hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(kBinThreads), 0, s, p);
     hipLaunchKernelGGL(k_bin_colscan, dim3((p.n_tiles + kColTiles - 1) / kColTiles), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, s, p);
-    hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);
+    hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);  // scans the tile totals itself
 }
 void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return;
