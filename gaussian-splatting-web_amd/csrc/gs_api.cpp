@@ -150,7 +150,6 @@ struct gs_scene {
     uint32_t *c0 = nullptr, *c1 = nullptr;  // [parts]: slots per projection partition and chunk
     uint16_t* cand = nullptr;           // chunk-0 candidates per partition (k_cull): offsets
     uint32_t* units = nullptr;          // the frame's non-empty chunk-0 work units (k_cull)
-    uint32_t* plist = nullptr;          // the frame's surviving projection partitions (k_part_cull)
     PartBound* bounds = nullptr;        // [parts] partition bounds (upload)
     uint32_t* orig = nullptr;           // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx = nullptr;           // [slots] storage index of each composite slot
@@ -453,7 +452,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.c1 = s->c1;
     pp.cand = s->cand;
     pp.units = s->units;
-    pp.plist = s->plist;
     pp.bounds = s->bounds;
     pp.orig = s->orig;
     pp.sidx = s->sidx;
@@ -740,7 +738,6 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->c0, (size_t)proj_parts(n) + 1);
             dev_alloc(s->c1, (size_t)proj_parts(n) + 1);
             dev_alloc(s->units, (size_t)kUnitShards * unit_shard_cap(proj_parts(n)) + 1);
-            dev_alloc(s->plist, (size_t)proj_parts(n) + kUnitShards + 1);
             dev_alloc(s->cand, nslots);
             dev_alloc(s->bounds, (size_t)proj_parts(n) + 1);
             dev_alloc(s->orig, (size_t)n + 1);
@@ -816,7 +813,6 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->c1);
     dev_free(s->cand);
     dev_free(s->units);
-    dev_free(s->plist);
     dev_free(s->bounds);
     dev_free(s->orig);
     dev_free(s->sidx);

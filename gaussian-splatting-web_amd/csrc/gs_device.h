@@ -55,7 +55,6 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t key_max;             // largest depth key of a visible splat (project)
     uint32_t sat_key;             // depth key of the farthest splat a tile saturated at (k_frame_end)
     uint32_t unit_n[kUnitShards]; // chunk-0 work units per shard (k_cull; see ProjParams::units)
-    uint32_t part_n[kUnitShards]; // surviving projection partitions per shard (k_part_cull)
     uint32_t sat_key_shard[kHistShards];  // per shard: the same, max over the shard's tiles
     uint32_t sat_tiles[kHistShards];      // per shard: tiles saturated by the end of the frame
 };
@@ -144,7 +143,6 @@ struct ProjParams {
     uint32_t* c1;             // [parts] chunk-1 splats per projection partition (k_records; zeroed by k_cull)
     uint16_t* cand;           // [parts * kProjTile] chunk-0 candidates: offsets in the partition (k_cull)
     uint32_t* units;          // [kUnitShards][unit_shard_cap] the non-empty chunk-0 work units (k_cull)
-    uint32_t* plist;          // [kUnitShards][ceil(parts / kUnitShards)] surviving partitions (k_part_cull)
     const PartBound* bounds;  // [parts] (k_part_bounds)
     const uint32_t* orig;     // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx;           // [slots] storage index of each composite slot

@@ -672,32 +672,6 @@ __device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, 
              pxl - hb > (float)p.W);
 }
 
-// Per projection partition (one thread each): the partition test (part_maybe), the surviving
-// partitions appended to the frame's partition list (kUnitShards shards, part % kUnitShards), and
-// the partition's chunk counts zeroed (c0 for the ruled-out ones, c1 for every one: k_records
-// adds to it).
-__global__ __launch_bounds__(256) void k_part_cull(ProjParams p) {
-    const int row_lo = p.tile_row_begin * kTile;
-    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
-    const uint32_t parts = proj_parts(p.n), pcap = (parts + kUnitShards - 1) / kUnitShards;
-    const uint32_t part = blockIdx.x * 256 + threadIdx.x;
-    const bool maybe = part < parts && part_maybe(p, p.bounds[part], row_lo, row_hi);
-    if (part < parts) {
-        p.c1[part] = 0;
-        if (!maybe) p.c0[part] = 0;
-    }
-    // lanes of a wave hold consecutive partitions: one add per (wave, shard)
-    const uint32_t sh = part % kUnitShards;
-    for (uint32_t k = 0; k < kUnitShards; ++k) {
-        const uint64_t b = __ballot(maybe && sh == k);
-        if (!b) continue;
-        uint32_t base = 0;
-        if (lane_id() == (uint32_t)(__ffsll((long long)b) - 1)) base = atomicAdd(&p.ctl->part_n[k], (uint32_t)__popcll(b));
-        base = __shfl(base, __ffsll((long long)b) - 1, 64);
-        if (maybe && sh == k) p.plist[(uint64_t)k * pcap + base + __popcll(b & lanemask_lt())] = part;
-    }
-}
-
 // The frame's list of non-empty chunk-0 work units (k_cull appends them, kUnitShards shards).
 struct UnitList {
     const uint32_t* units;  // null: unit j is j
@@ -727,8 +701,8 @@ __device__ __forceinline__ uint32_t unit_at(const UnitList& L, uint32_t j) {
     return L.units[(uint64_t)k * L.cap + (j - base)];
 }
 
-// Projection, phase A (one workgroup per surviving projection partition of kProjTile storage
-// slots, from k_part_cull's list; a ruled-out partition costs nothing here): every
+// Projection, phase A (one workgroup per projection partition of kProjTile storage slots; the
+// partition's bound is tested first (part_maybe), a ruled-out partition costs one read): every
 // Gaussian's 16-B cull plane gives its depth key (vz rounded exactly as project_footprint rounds
 // it) and the conservative cull (cull_keep: exact near/far, a provable bound on the quad box
 // against this frame's rows).  Survivors nearer than thresh are the partition's chunk-0
@@ -747,16 +721,15 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = proj_parts(p.n), ucap = unit_shard_cap(parts);
-    const uint32_t pcap = (parts + kUnitShards - 1) / kUnitShards;
-    uint32_t ppre[kUnitShards + 1];
-    ppre[0] = 0;
-#pragma unroll
-    for (int k = 0; k < kUnitShards; ++k) ppre[k + 1] = ppre[k] + p.ctl->part_n[k];
-    for (uint32_t jp = blockIdx.x; jp < ppre[kUnitShards]; jp += gridDim.x) {
-        int sh = 0;
-#pragma unroll
-        for (int t = 1; t < kUnitShards; ++t) sh += jp >= ppre[t] ? 1 : 0;
-        const uint32_t part = p.plist[(uint64_t)sh * pcap + (jp - ppre[sh])];
+    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
+        // the partition test first (part_maybe on its bound, uniform): a ruled-out partition
+        // costs one 32-B read; the chunk counts are zeroed here (c1: k_records adds to it)
+        const bool maybe = part_maybe(p, p.bounds[part], row_lo, row_hi);
+        if (tid == 0) {
+            p.c1[part] = 0;
+            if (!maybe) p.c0[part] = 0;
+        }
+        if (!maybe) continue;
         const uint32_t p0 = part * kProjTile;
         float4 c[kProjRounds];
 #pragma unroll
@@ -2615,7 +2588,6 @@ void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStrea
 void launch_project(const ProjParams& p, hipStream_t s) {
     const uint32_t parts = proj_parts(p.n);
     if (!parts) return;
-    hipLaunchKernelGGL(k_part_cull, dim3((parts + 255) / 256), dim3(256), 0, s, p);
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, parts));
     hipLaunchKernelGGL(k_cull, dim3(grid), dim3(kProjThreads), 0, s, p);
     const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (uint64_t)parts * kProjRounds));

@@ -28,8 +28,8 @@ def short(name):
     return re.sub(r"^void ", "", name).replace("gs::", "")
 
 
-def frames_of(rows, key_start="k_part_cull"):
-    """Split dispatches (in order) into frames starting at k_part_cull; label positions."""
+def frames_of(rows, key_start="k_cull"):
+    """Split dispatches (in order) into frames starting at k_cull; label positions."""
     frames, cur = [], None
     for r in rows:
         n = short(r["Kernel_Name"])
