@@ -134,15 +134,14 @@ struct gs_ctx {
     std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
 };
 
-struct gs_scene {
-    gs_ctx* ctx = nullptr;
-    uint64_t n = 0;
-    int n_sh = 0;
-    float4* geo = nullptr;              // geometry records (3 float4 per Gaussian)
-    float4* shade = nullptr;            // packed SH coefficients (sh_quads float4 per Gaussian)
-    float4* dbg = nullptr;              // per-Gaussian debug records (3 float4), allocated on demand
-    float4* cull = nullptr;             // cull planes (two-phase projection)
-    float4* r2 = nullptr;
+// Everything one frame writes.  Two sets, used by alternate frames, each with its own stream: the
+// next frame's culling, projection, binning and per-tile sort run while this frame composites
+// (only the composite, which writes the caller's buffer, waits for the caller's stream).
+struct FrameSet {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_in = nullptr;         // the caller's stream at the frame's call
+    hipEvent_t ev_out = nullptr;        // the frame's end
+    float4* r2 = nullptr;               // per-Gaussian box of rects wider than 16 tiles
     // composite slots (slot_c0 / slot_c1): records (3 float4), (depth key, index), packed rect
     float4* crec = nullptr;
     uint2* skey = nullptr;
@@ -150,13 +149,11 @@ struct gs_scene {
     uint32_t *c0 = nullptr, *c1 = nullptr;  // [parts]: slots per projection partition and chunk
     uint16_t* cand = nullptr;           // chunk-0 candidates per partition (k_cull): offsets
     uint32_t* units = nullptr;          // the frame's non-empty chunk-0 work units (k_cull)
-    PartBound* bounds = nullptr;        // [parts] partition bounds (upload)
-    uint32_t* orig = nullptr;           // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx = nullptr;           // [slots] storage index of each composite slot
-    ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
-    FrameCtl* ctl = nullptr;            // zero at a frame's start (k_frame_end clears it)
+    FrameCtl* ctl = nullptr;            // zero at a frame's start (the frame's end clears it)
     StatShard* stats = nullptr;         // [kStatShards], zero at a frame's start (likewise)
     uint32_t* bar = nullptr;            // k_chunk1's grid-barrier counter, zero at a frame's start
+    bool meta_clean = false;            // the set's last frame zeroed FrameCtl (see render_frame)
     // tile lists
     uint64_t kcap = 0;
     uint32_t *tvA = nullptr, *tvB = nullptr;  // tile lists: unordered (binning), sorted
@@ -169,6 +166,23 @@ struct gs_scene {
     int tiles_cap = 0;
     float4* state = nullptr;
     uint64_t state_cap = 0;
+};
+
+struct gs_scene {
+    gs_ctx* ctx = nullptr;
+    uint64_t n = 0;
+    int n_sh = 0;
+    float4* geo = nullptr;              // geometry records (3 float4 per Gaussian)
+    float4* shade = nullptr;            // packed SH coefficients (sh_quads float4 per Gaussian)
+    float4* dbg = nullptr;              // per-Gaussian debug records (3 float4), allocated on demand
+    float4* cull = nullptr;             // cull planes (two-phase projection)
+    FrameSet fs[2];                     // per-frame buffers, alternating frame to frame
+    int cur_fs = 0;                     // the set the next frame uses
+    int last_fs = 0;                    // the set of the last frame
+    uint32_t* orig = nullptr;           // [n] reference index of each storage slot (Morton order)
+    PartBound* bounds = nullptr;        // [parts] partition bounds (upload)
+    ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
+    int last_tiles = 0;                 // tiles of the last frame's strip
     // asynchronous frame statistics (chunk controller, capacity): k_frame_end stores FrameCtl into
     // a pinned slot and then publishes a sequence number there; two slots (two frames in flight)
     FrameCtl* h_ctl = nullptr;    // pinned, coherent, device-mapped (d_ctl_slot): 2 slots
@@ -176,7 +190,6 @@ struct gs_scene {
     FrameCtl* d_ctl_slot = nullptr;
     uint32_t* d_seq = nullptr;
     uint32_t seq_next = 1;
-    bool meta_clean = false;      // the last frame's k_frame_end zeroed FrameCtl (see render_frame)
     uint32_t stat_want[2] = {};   // sequence number that completes the slot's frame
     bool stat_pending[2] = {};
     int stat_cur = 0;
@@ -185,7 +198,6 @@ struct gs_scene {
     uint32_t chunk_T = kNoSplit;        // adaptive chunk threshold for the next frame
     uint32_t key_lo = 0, key_hi = 0;    // depth-key range of the last frame's visible splats
     bool have_krange = false;
-    int last_tiles = 0;                 // tiles of the last frame's strip
     bool have_frame = false;
 };
 
@@ -201,44 +213,44 @@ static constexpr int kDepthSortIpt = 8;
 static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
-static Records records(gs_scene* s) {
-    return Records{s->dbg, s->r2, 3u, 0u};
+static Records records(gs_scene* s, const FrameSet& F) {
+    return Records{s->dbg, F.r2, 3u, 0u};
 }
 
-static void ensure_tile_capacity(gs_scene* s, uint64_t k) {
-    if (k <= s->kcap && s->tvA) return;
+static void ensure_tile_capacity(FrameSet& F, uint64_t k) {
+    if (k <= F.kcap && F.tvA) return;
     if (k >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "more than 2^32 tile entries");
     const uint64_t cap = std::min<uint64_t>(0xFFFFFFFEull, std::max<uint64_t>(k + k / 2, 1u << 20));
-    dev_free(s->tvA); dev_free(s->tvB);
-    dev_alloc(s->tvA, cap); dev_alloc(s->tvB, cap);
-    s->kcap = cap;
+    dev_free(F.tvA); dev_free(F.tvB);
+    dev_alloc(F.tvA, cap); dev_alloc(F.tvB, cap);
+    F.kcap = cap;
 }
 
-static void ensure_tiles(gs_scene* s, int n_tiles) {
-    if (n_tiles <= s->tiles_cap && s->ranges) return;
-    dev_free(s->ranges);
-    dev_free(s->done);
-    dev_free(s->bmat);
-    dev_free(s->tbase);
-    dev_alloc(s->ranges, (size_t)n_tiles);
-    dev_alloc(s->done, (size_t)n_tiles);
-    dev_alloc(s->bmat, (size_t)kBinParts * n_tiles);
-    dev_alloc(s->tbase, (size_t)n_tiles);
-    s->tiles_cap = n_tiles;
+static void ensure_tiles(FrameSet& F, int n_tiles) {
+    if (n_tiles <= F.tiles_cap && F.ranges) return;
+    dev_free(F.ranges);
+    dev_free(F.done);
+    dev_free(F.bmat);
+    dev_free(F.tbase);
+    dev_alloc(F.ranges, (size_t)n_tiles);
+    dev_alloc(F.done, (size_t)n_tiles);
+    dev_alloc(F.bmat, (size_t)kBinParts * n_tiles);
+    dev_alloc(F.tbase, (size_t)n_tiles);
+    F.tiles_cap = n_tiles;
 }
 
-static void ensure_sat(gs_scene* s, size_t words) {
-    if (words <= s->sat_cap && s->sat) return;
-    dev_free(s->sat);
-    dev_alloc(s->sat, words);
-    s->sat_cap = words;
+static void ensure_sat(FrameSet& F, size_t words) {
+    if (words <= F.sat_cap && F.sat) return;
+    dev_free(F.sat);
+    dev_alloc(F.sat, words);
+    F.sat_cap = words;
 }
 
-static void ensure_state(gs_scene* s, uint64_t pixels) {
-    if (pixels <= s->state_cap && s->state) return;
-    dev_free(s->state);
-    dev_alloc(s->state, pixels);
-    s->state_cap = pixels;
+static void ensure_state(FrameSet& F, uint64_t pixels) {
+    if (pixels <= F.state_cap && F.state) return;
+    dev_free(F.state);
+    dev_alloc(F.state, pixels);
+    F.state_cap = pixels;
 }
 
 static void ensure_out(gs_ctx* c, size_t bytes) {
@@ -358,6 +370,13 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     strip_geometry(H, o.strip_index, sc, tr_begin, tr_end, rows_padded);
     const int TX = (W + kTile - 1) / kTile;
     const int n_tiles = TX * (tr_end - tr_begin);
+    FrameSet& F = s->fs[s->cur_fs];
+    // the frame's kernels run on its set's stream; the caller's stream `st` orders only the
+    // composite (the caller's buffer) and waits for the frame's end.  Stage timing (level 1)
+    // serialises the frames so that each stage's events measure that stage alone.
+    const hipStream_t cst = st;
+    st = F.stream;
+    if (o.timing == 1) HIPCHK(hipStreamWaitEvent(st, s->fs[s->cur_fs ^ 1].ev_out, 0));
     collect_stats(s, false);
     const int slot = s->stat_cur;  // this frame's statistics slot
     if (s->stat_pending[slot]) {  // two frames in flight: the older one's statistics first
@@ -365,8 +384,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         collect_stats(s, false);
         s->stat_pending[slot] = false;
     }
-    if (s->have_last && s->last.k_total > s->kcap) ensure_tile_capacity(s, s->last.k_total);
-    ensure_tiles(s, std::max(n_tiles, 1));
+    if (s->have_last && s->last.k_total > F.kcap) ensure_tile_capacity(F, s->last.k_total);
+    ensure_tiles(F, std::max(n_tiles, 1));
     s->last_tiles = n_tiles;
     // chunk threshold: adaptive, one chunk (chunk_fraction >= 1), or a fixed split for tests and
     // diagnostics (chunk_fraction in (0,1): the depth 2^-t <= chunk_fraction of the way from the
@@ -386,8 +405,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     }
     const bool two_chunks = T != kNoSplit;
     if (two_chunks) {
-        ensure_state(s, (uint64_t)W * H);
-        ensure_sat(s, (size_t)(tr_end - tr_begin + 1) * (TX + 1) + 2 + (size_t)(tr_end - tr_begin) * ((TX + 63) / 64) * 2);
+        ensure_state(F, (uint64_t)W * H);
+        ensure_sat(F, (size_t)(tr_end - tr_begin + 1) * (TX + 1) + 2 + (size_t)(tr_end - tr_begin) * ((TX + 63) / 64) * 2);
     }
 
     // timing 1: events between every stage; 2: around the composite only (each event record costs
@@ -408,12 +427,12 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
 
     // FrameCtl is zero at a frame's start: k_frame_end of the last frame cleared it, unless that
     // frame never ended (first frame, an error mid-frame)
-    if (!s->meta_clean) {
-        HIPCHK(hipMemsetAsync(s->ctl, 0, sizeof(FrameCtl), st));
-        HIPCHK(hipMemsetAsync(s->stats, 0, kStatShards * sizeof(StatShard), st));
-        HIPCHK(hipMemsetAsync(s->bar, 0, 16, st));
+    if (!F.meta_clean) {
+        HIPCHK(hipMemsetAsync(F.ctl, 0, sizeof(FrameCtl), st));
+        HIPCHK(hipMemsetAsync(F.stats, 0, kStatShards * sizeof(StatShard), st));
+        HIPCHK(hipMemsetAsync(F.bar, 0, 16, st));
     }
-    s->meta_clean = false;
+    F.meta_clean = false;
     ProjParams pp{};
     pp.geo = s->geo;
     pp.cull = s->cull;
@@ -439,22 +458,22 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.tile_row_begin = tr_begin;
     pp.tile_row_end = tr_end;
     pp.tiles_x = TX;
-    pp.rec = records(s);
+    pp.rec = records(s, F);
     pp.sh = s->shade;
     pp.shq = sh_quads(s->n_sh);
-    pp.ctl = s->ctl;
-    pp.stats = s->stats;
+    pp.ctl = F.ctl;
+    pp.stats = F.stats;
     pp.thresh = T;
-    pp.crec = s->crec;
-    pp.skey = s->skey;
-    pp.srect = s->srect;
-    pp.c0 = s->c0;
-    pp.c1 = s->c1;
-    pp.cand = s->cand;
-    pp.units = s->units;
+    pp.crec = F.crec;
+    pp.skey = F.skey;
+    pp.srect = F.srect;
+    pp.c0 = F.c0;
+    pp.c1 = F.c1;
+    pp.cand = F.cand;
+    pp.units = F.units;
     pp.bounds = s->bounds;
     pp.orig = s->orig;
-    pp.sidx = s->sidx;
+    pp.sidx = F.sidx;
     mark(EV_PROJ0);
     launch_project(pp, st);
     mark(EV_PROJ1);
@@ -463,37 +482,37 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     // touch a tile chunk 0 left unsaturated) is one cooperative launch enqueued behind it that
     // returns at once when chunk 0 saturated every tile (k_chunk1).
     BinParams bp{};
-    bp.skey = s->skey;
-    bp.sidx = s->sidx;
-    bp.srect = s->srect;
-    bp.cnt = s->c0;
+    bp.skey = F.skey;
+    bp.sidx = F.sidx;
+    bp.srect = F.srect;
+    bp.cnt = F.c0;
     bp.parts = proj_parts(pp.n);
-    bp.units = s->units;
-    bp.rec = records(s);
-    bp.crec = s->crec;
-    bp.done = s->done;
-    bp.ctl = s->ctl;
+    bp.units = F.units;
+    bp.rec = records(s, F);
+    bp.crec = F.crec;
+    bp.done = F.done;
+    bp.ctl = F.ctl;
     bp.chunk = 0;
     bp.tile_row_begin = tr_begin;
     bp.tiles_x = TX;
-    bp.capacity = (uint32_t)s->kcap;
-    bp.ranges = s->ranges;
+    bp.capacity = (uint32_t)F.kcap;
+    bp.ranges = F.ranges;
     bp.n_tiles = (uint32_t)n_tiles;
-    bp.bmat = s->bmat;
-    bp.tbase = s->tbase;
-    bp.tvals = s->tvA;
+    bp.bmat = F.bmat;
+    bp.tbase = F.tbase;
+    bp.tvals = F.tvA;
     bp.rows = tr_end - tr_begin;
     TileSortParams tsp{};  // each tile's list into (depth key, index) order
-    tsp.ranges = s->ranges;
-    tsp.in = s->tvA;
-    tsp.out = s->tvB;
-    tsp.skey = s->skey;
+    tsp.ranges = F.ranges;
+    tsp.in = F.tvA;
+    tsp.out = F.tvB;
+    tsp.skey = F.skey;
     tsp.done = nullptr;
     tsp.n_tiles = n_tiles;
     CompositeParams cp{};
-    cp.ranges = s->ranges;
-    cp.tvals = s->tvB;
-    cp.rec = s->crec;
+    cp.ranges = F.ranges;
+    cp.tvals = F.tvB;
+    cp.rec = F.crec;
     cp.W = W;
     cp.H = H;
     cp.tiles_x = TX;
@@ -502,9 +521,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     cp.n_tiles = n_tiles;
     cp.t_min = o.t_min;
     cp.mode = two_chunks ? kCompFirst : kCompSingle;
-    cp.state = s->state;
-    cp.done = s->done;
-    cp.ctl = s->ctl;
+    cp.state = F.state;
+    cp.done = F.done;
+    cp.ctl = F.ctl;
     cp.out = out;
     cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
     mark(EV_DSORT_0);
@@ -512,6 +531,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     mark(EV_BIN_0);
     launch_tile_sort(tsp, st);
     mark(EV_TSORT_0);
+    HIPCHK(hipEventRecord(F.ev_in, cst));  // the caller's buffer: after the caller's earlier work
+    HIPCHK(hipStreamWaitEvent(st, F.ev_in, 0));
     mark(EV_RANGES_0);
     launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
     mark(EV_COMP_0);
@@ -519,30 +540,34 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
        // slot, FrameCtl zeroed for the next frame; one launch
         Chunk1Params c1{};
         c1.pp = pp;
-        c1.pp.sat = s->sat;
+        c1.pp.sat = F.sat;
         c1.pp.rec_all = 0;
         c1.bp = bp;
-        c1.bp.cnt = s->c1;
+        c1.bp.cnt = F.c1;
         c1.bp.units = nullptr;  // chunk 1: every unit
         c1.bp.chunk = 1;
         c1.tp = tsp;
-        c1.tp.done = s->done;
+        c1.tp.done = F.done;
         c1.cp = cp;
         c1.cp.mode = kCompSecond;
-        c1.sat = s->sat;
-        c1.bar = s->bar;
+        c1.sat = F.sat;
+        c1.bar = F.bar;
         c1.two_chunks = two_chunks ? 1 : 0;
         const uint32_t q = s->seq_next++;
         s->stat_want[slot] = q;
-        c1.stats = s->stats;
+        c1.stats = F.stats;
         c1.host_ctl = s->d_ctl_slot + slot;
         c1.host_seq = s->d_seq + slot;
         c1.seq = q;
         launch_chunk1(c1, c->num_cus, o.accum == GS_ACCUM_FP16_TARGET, st);
         if (two_chunks && o.timing == 1) mark(EV_COMP_1);
     }
-    s->meta_clean = true;
+    F.meta_clean = true;
     mark(EV_END);
+    HIPCHK(hipEventRecord(F.ev_out, st));
+    HIPCHK(hipStreamWaitEvent(cst, F.ev_out, 0));  // the caller's later work sees the frame
+    s->last_fs = s->cur_fs;
+    s->cur_fs ^= 1;
     s->last_pp = pp;
     HIPCHK(hipGetLastError());
     if (timed) {
@@ -594,7 +619,7 @@ static void check_frame_errors(gs_scene* s) {
     }
     if (s->have_last && (s->last.err & kErrOverflow)) {
         s->last.err = 0;
-        ensure_tile_capacity(s, s->last.k_total);
+        for (FrameSet& F : s->fs) ensure_tile_capacity(F, s->last.k_total);
         throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded; capacity grown, render again");
     }
 }
@@ -725,30 +750,36 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->geo, 3 * (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->shade, (size_t)sh_quads(n_sh) * std::max<uint64_t>(n, 1));
             dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
-            dev_alloc(s->r2, (size_t)std::max<uint64_t>(n, 1));
-            dev_alloc(s->crec, 3 * ((size_t)proj_parts(n) * kProjTile + 1));
-            dev_alloc(s->ctl, 1);
-            dev_alloc(s->stats, kStatShards);
-            dev_alloc(s->bar, 4);
-            HIPCHK(hipMemset(s->bar, 0, 16));
-            // slots: part * kProjTile + q < proj_parts(n) * kProjTile
-            const size_t nslots = (size_t)proj_parts(n) * kProjTile + 1;
-            dev_alloc(s->skey, nslots);
-            dev_alloc(s->srect, nslots);
-            dev_alloc(s->c0, (size_t)proj_parts(n) + 1);
-            dev_alloc(s->c1, (size_t)proj_parts(n) + 1);
-            dev_alloc(s->units, (size_t)kUnitShards * unit_shard_cap(proj_parts(n)) + 1);
-            dev_alloc(s->cand, nslots);
             dev_alloc(s->bounds, (size_t)proj_parts(n) + 1);
             dev_alloc(s->orig, (size_t)n + 1);
-            dev_alloc(s->sidx, nslots);
+            for (FrameSet& F : s->fs) {
+                HIPCHK(hipStreamCreateWithFlags(&F.stream, hipStreamNonBlocking));
+                HIPCHK(hipEventCreateWithFlags(&F.ev_in, hipEventDisableTiming));
+                HIPCHK(hipEventCreateWithFlags(&F.ev_out, hipEventDisableTiming));
+                HIPCHK(hipEventRecord(F.ev_out, F.stream));  // "the last frame on this set ended"
+                dev_alloc(F.r2, (size_t)std::max<uint64_t>(n, 1));
+                dev_alloc(F.crec, 3 * ((size_t)proj_parts(n) * kProjTile + 1));
+                dev_alloc(F.ctl, 1);
+                dev_alloc(F.stats, kStatShards);
+                dev_alloc(F.bar, 4);
+                HIPCHK(hipMemset(F.bar, 0, 16));
+                // slots: part * kProjTile + q < proj_parts(n) * kProjTile
+                const size_t nslots = (size_t)proj_parts(n) * kProjTile + 1;
+                dev_alloc(F.skey, nslots);
+                dev_alloc(F.srect, nslots);
+                dev_alloc(F.c0, (size_t)proj_parts(n) + 1);
+                dev_alloc(F.c1, (size_t)proj_parts(n) + 1);
+                dev_alloc(F.units, (size_t)kUnitShards * unit_shard_cap(proj_parts(n)) + 1);
+                dev_alloc(F.cand, nslots);
+                dev_alloc(F.sidx, nslots);
+                ensure_tile_capacity(F, 4 * n + (1u << 20));
+            }
             const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
             HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hf));
             HIPCHK(hipHostMalloc((void**)&s->h_seq, 64, hf));
             std::memset(s->h_seq, 0, 64);
             HIPCHK(hipHostGetDevicePointer((void**)&s->d_ctl_slot, s->h_ctl, 0));
             HIPCHK(hipHostGetDevicePointer((void**)&s->d_seq, s->h_seq, 0));
-            ensure_tile_capacity(s, 4 * n + (1u << 20));
             // AoS -> SoA on device in spatial (Morton) order: codes, stable sort, gather-transpose,
             // then the partition bounds
             const uint64_t rb = 64 + 16 * (uint64_t)n_sh;
@@ -794,6 +825,8 @@ void gs_scene_free(gs_scene* s) {
     if (s->ctx) {
         (void)hipSetDevice(s->ctx->device);
         (void)hipStreamSynchronize(s->ctx->stream);
+        for (FrameSet& F : s->fs)
+            if (F.stream) (void)hipStreamSynchronize(F.stream);
         auto& v = s->ctx->scenes;
         v.erase(std::remove(v.begin(), v.end(), s), v.end());
         if (s->ctx->last_scene == s) s->ctx->last_scene = nullptr;
@@ -802,27 +835,33 @@ void gs_scene_free(gs_scene* s) {
     dev_free(s->shade);
     dev_free(s->dbg);
     dev_free(s->cull);
-    dev_free(s->r2);
-    dev_free(s->crec);
-    dev_free(s->ctl);
-    dev_free(s->stats);
-    dev_free(s->bar);
-    dev_free(s->skey);
-    dev_free(s->srect);
-    dev_free(s->c0);
-    dev_free(s->c1);
-    dev_free(s->cand);
-    dev_free(s->units);
+    for (FrameSet& F : s->fs) {
+        if (F.stream) (void)hipStreamSynchronize(F.stream);
+        dev_free(F.r2);
+        dev_free(F.crec);
+        dev_free(F.ctl);
+        dev_free(F.stats);
+        dev_free(F.bar);
+        dev_free(F.skey);
+        dev_free(F.srect);
+        dev_free(F.c0);
+        dev_free(F.c1);
+        dev_free(F.cand);
+        dev_free(F.units);
+        dev_free(F.sidx);
+        dev_free(F.tvA); dev_free(F.tvB);
+        dev_free(F.ranges);
+        dev_free(F.bmat);
+        dev_free(F.tbase);
+        dev_free(F.done);
+        dev_free(F.sat);
+        dev_free(F.state);
+        if (F.ev_in) (void)hipEventDestroy(F.ev_in);
+        if (F.ev_out) (void)hipEventDestroy(F.ev_out);
+        if (F.stream) (void)hipStreamDestroy(F.stream);
+    }
     dev_free(s->bounds);
     dev_free(s->orig);
-    dev_free(s->sidx);
-    dev_free(s->tvA); dev_free(s->tvB);
-    dev_free(s->ranges);
-    dev_free(s->bmat);
-    dev_free(s->tbase);
-    dev_free(s->done);
-    dev_free(s->sat);
-    dev_free(s->state);
     if (s->h_ctl) (void)hipHostFree(s->h_ctl);
     if (s->h_seq) (void)hipHostFree(s->h_seq);
     delete s;
@@ -900,7 +939,7 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
             if (!(s->last.err & kErrOverflow)) break;
             s->last.err = 0;
             if (attempt >= 2) throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded");
-            ensure_tile_capacity(s, s->last.k_total);  // grow and render the frame again
+            for (FrameSet& F : s->fs) ensure_tile_capacity(F, s->last.k_total);  // grow, render again
         }
         if (out_host) HIPCHK(hipMemcpy(out_host, c->d_out, bytes, hipMemcpyDeviceToHost));
         return GS_OK;
@@ -998,16 +1037,17 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
 // then chunk 1.
 static std::vector<std::array<uint32_t, 3>> frame_slots(gs_scene* s) {
     collect_stats(s, true);
+    const FrameSet& F = s->fs[s->last_fs];
     const uint32_t parts = proj_parts(s->n);
     std::vector<std::array<uint32_t, 3>> out;
     if (!parts) return out;
     std::vector<uint32_t> c0(parts), c1(parts);
     std::vector<uint2> sk((size_t)parts * kProjTile);
     std::vector<uint32_t> rect((size_t)parts * kProjTile);
-    HIPCHK(hipMemcpy(rect.data(), s->srect, rect.size() * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(c0.data(), s->c0, parts * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(c1.data(), s->c1, parts * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(sk.data(), s->skey, sk.size() * sizeof(uint2), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(rect.data(), F.srect, rect.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c0.data(), F.c0, parts * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c1.data(), F.c1, parts * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(sk.data(), F.skey, sk.size() * sizeof(uint2), hipMemcpyDeviceToHost));
     const bool chunk1 = s->last.n_chunk[1] > 0;
     for (int ch = 0; ch < (chunk1 ? 2 : 1); ++ch)
         for (uint32_t p = 0; p < parts; ++p)
@@ -1025,7 +1065,7 @@ int gs_debug_last_order(gs_ctx* c, gs_scene* s, uint32_t* out_keys, uint32_t* ou
         if (!c || !s || !out_n) throw GsError(GS_ERR_INVALID, "null argument");
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         HIPCHK(hipSetDevice(c->device));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipDeviceSynchronize());  // both frame sets' streams
         auto sl = frame_slots(s);  // every composite slot, in the composite's (key, index) order
         std::sort(sl.begin(), sl.end(), [](const std::array<uint32_t, 3>& a, const std::array<uint32_t, 3>& b) {
             return a[1] != b[1] ? a[1] < b[1] : a[2] < b[2];
@@ -1045,22 +1085,23 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
         if (!c || !s || !out16) throw GsError(GS_ERR_INVALID, "null argument");
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         HIPCHK(hipSetDevice(c->device));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipDeviceSynchronize());  // both frame sets' streams
         const uint64_t m = std::min(cap, s->n);
         const auto sl = frame_slots(s);
+        const FrameSet& F = s->fs[s->last_fs];
         if (m) {  // r01 -> words [0, 8); r2 -> words [12, 16); colour below
             if (!s->dbg) dev_alloc(s->dbg, 3 * (size_t)std::max<uint64_t>(s->n, 1));
             ProjParams rp = s->last_pp;  // records of every visible Gaussian (a frame stores fewer)
-            rp.rec = records(s);
+            rp.rec = records(s, F);
             rp.rec_all = 1;
             launch_records(rp, c->stream);
-            HIPCHK(hipStreamSynchronize(c->stream));
-            const Records rc = records(s);
+            HIPCHK(hipDeviceSynchronize());  // both frame sets' streams
+            const Records rc = records(s, F);
             const uint64_t n = s->n;           // storage slot j holds reference record orig[j]
             std::vector<float> a((size_t)n * 8), b((size_t)n * 4);
             std::vector<uint32_t> orig(n);
             HIPCHK(hipMemcpy2D(a.data(), 32, rc.r01, (size_t)rc.stride * 16, 32, n, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(b.data(), s->r2, b.size() * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(b.data(), F.r2, b.size() * 4, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(orig.data(), s->orig, n * 4, hipMemcpyDeviceToHost));
             for (uint64_t j = 0; j < n; ++j) {
                 const uint64_t o = orig[j];
@@ -1074,7 +1115,7 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
         if (!sl.empty()) {
             const size_t ns = (size_t)proj_parts(s->n) * kProjTile;
             std::vector<float> cr(ns * 12);
-            HIPCHK(hipMemcpy(cr.data(), s->crec, ns * 48, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(cr.data(), F.crec, ns * 48, hipMemcpyDeviceToHost));
             for (const auto& e : sl)
                 if (e[2] < m) std::memcpy(out16 + 16 * (uint64_t)e[2] + 8, &cr[12 * (size_t)e[0] + 8], 12);
         }

@@ -11,7 +11,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 $OUT/tests.log
 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
 python3 -c "import json;d=json.loads(open('$OUT/bench.log').read().strip().splitlines()[-1]);print('fps',d['fps'],'ms',d['ms_per_step'],d['stages_ms'])"
-GS=1,8 timeout -k 10 200 python3 tools/strip_bench.py > $OUT/strips.log 2>&1 || { tail -30 $OUT/strips.log; exit 1; }
+GS=1,8 TIMING=2 timeout -k 10 200 python3 tools/strip_bench.py > $OUT/strips.log 2>&1 || { tail -30 $OUT/strips.log; exit 1; }
 cat $OUT/strips.log
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; }
 python3 tools/kstats.py $OUT/prof/run_kernel_stats.csv || true
