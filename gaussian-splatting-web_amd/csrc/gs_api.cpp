@@ -559,7 +559,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.host_ctl = s->d_ctl_slot + slot;
         c1.host_seq = s->d_seq + slot;
         c1.seq = q;
-        launch_chunk1(c1, c->num_cus, o.accum == GS_ACCUM_FP16_TARGET, st);
+        // 64 workgroups: chunk 1 is small when it has work at all, and a frame whose chunk 0
+        // saturated every tile pays only for these launching (LDS-heavy, beside the next frame)
+        launch_chunk1(c1, std::min(c->num_cus, 64), o.accum == GS_ACCUM_FP16_TARGET, st);
         if (two_chunks && o.timing == 1) mark(EV_COMP_1);
     }
     F.meta_clean = true;

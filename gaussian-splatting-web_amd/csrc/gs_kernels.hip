@@ -689,6 +689,12 @@ __device__ __forceinline__ UnitList load_units(const uint32_t* units, const Fram
     L.total = L.pre[kUnitShards];
     return L;
 }
+// A listed unit: bits [0, 20) = partition * kProjRounds + round, bits [20, 28) = its candidate
+// count - 1 (so k_project and binning need no count load).  Unlisted units (chunk 1: every unit
+// j of every partition) are the bare number j.
+__device__ __forceinline__ uint32_t unit_id(uint32_t u) { return u & 0xFFFFFu; }
+__device__ __forceinline__ uint32_t unit_count(uint32_t u) { return ((u >> 20) & 0xFFu) + 1u; }
+
 __device__ __forceinline__ uint32_t unit_at(const UnitList& L, uint32_t j) {
     if (!L.units) return j;
     uint32_t k = 0, base = 0;  // selects, not an indexed array: no scratch round trip
@@ -776,7 +782,9 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
             if (tot) {  // the partition's work units into the frame's list (shard by partition)
                 const uint32_t nu = (tot + kProjThreads - 1) / kProjThreads, sh = part % kUnitShards;
                 const uint32_t pos = atomicAdd(&p.ctl->unit_n[sh], nu);
-                for (uint32_t r = 0; r < nu; ++r) p.units[(uint64_t)sh * ucap + pos + r] = part * kProjRounds + r;
+                for (uint32_t r = 0; r < nu; ++r)
+                    p.units[(uint64_t)sh * ucap + pos + r] =
+                        (part * kProjRounds + r) | ((min(tot - r * kProjThreads, (uint32_t)kProjThreads) - 1u) << 20);
             }
         }
         __syncthreads();
@@ -817,13 +825,11 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const UnitList L = load_units(p.units, p.ctl, proj_parts(p.n));
     for (uint32_t j = blockIdx.x; j < L.total; j += gridDim.x) {
-        const uint32_t u = unit_at(L, j);
-        const uint32_t part = u / kProjRounds, q = (u % kProjRounds) * kProjThreads + tid;
+        const uint32_t u = unit_at(L, j), id = unit_id(u);
+        const uint32_t part = id / kProjRounds, q = (id % kProjRounds) * kProjThreads + tid;
         const uint32_t p0 = part * kProjTile;
-        const uint32_t cq = p.cand[p0 + q];  // in flight with the count (always inside the buffer)
-        const uint32_t c0n = p.c0[part];
-        asm volatile("" ::"v"(cq));          // keeps the candidate load ahead of the branch
-        if (q >= c0n) continue;
+        if ((uint32_t)tid >= unit_count(u)) continue;
+        const uint32_t cq = p.cand[p0 + q];
         const uint32_t slot = slot_c0(part, q);
         const uint32_t i = p0 + cq;
         uint32_t oi;
@@ -1311,7 +1317,9 @@ __device__ __forceinline__ uint32_t bin_units(const UnitList& L, uint32_t b) {
 
 // The slots of binning partition b (units b, b + kBinParts, ... of the chunk's list):
 // s_pref[k] = slots of its first k units; returns the total.  Contains barriers.
-template <int NT>
+// LISTED: the chunk's units come from k_cull's list, counts packed in the entries (chunk 0);
+// otherwise every unit of every partition, counts from p.cnt (chunk 1)
+template <int NT, bool LISTED>
 __device__ uint32_t bin_slots(const BinParams& p, const UnitList& L, uint32_t b, uint32_t* s_pref, uint32_t* s_tmp) {
     const uint32_t m = min(bin_units(L, b), kBinMaxUnits);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -1323,9 +1331,13 @@ __device__ uint32_t bin_slots(const BinParams& p, const UnitList& L, uint32_t b,
         c[k] = 0;
         if (j < m) {
             const uint32_t u = unit_at(L, b + j * kBinParts);
-            const uint32_t part = u / kProjRounds, r0 = (u % kProjRounds) * kProjThreads;
-            const uint32_t cn = p.cnt[part];
-            c[k] = cn > r0 ? min(cn - r0, (uint32_t)kProjThreads) : 0u;
+            if (LISTED) {
+                c[k] = unit_count(u);
+            } else {
+                const uint32_t part = u / kProjRounds, r0 = (u % kProjRounds) * kProjThreads;
+                const uint32_t cn = p.cnt[part];
+                c[k] = cn > r0 ? min(cn - r0, (uint32_t)kProjThreads) : 0u;
+            }
         }
         sum += c[k];
     }
@@ -1356,7 +1368,7 @@ __device__ __forceinline__ uint32_t bin_slot(const BinParams& p, const UnitList&
         const uint32_t mid = (lo + hi) >> 1;
         if (s_pref[mid] <= r) lo = mid; else hi = mid;
     }
-    const uint32_t u = unit_at(L, b + lo * kBinParts), part = u / kProjRounds;
+    const uint32_t u = unit_id(unit_at(L, b + lo * kBinParts)), part = u / kProjRounds;
     const uint32_t q = (u % kProjRounds) * kProjThreads + (r - s_pref[lo]);
     return p.chunk ? slot_c1(part, q) : slot_c0(part, q);
 }
@@ -1384,13 +1396,13 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
 }
 
 // Binning partition / band vb: counts of its splats' entries per tile of the band -> bmat row.
-template <int NT>
+template <int NT, bool LISTED>
 __device__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp) {
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
     for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += NT) s_cnt[t] = 0;
     const UnitList L = bin_unit_list(p);
-    const uint32_t total = bin_slots<NT>(p, L, part, s_pref, s_tmp);
+    const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
     for (uint32_t r = threadIdx.x; r < total; r += NT) {
         const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
@@ -1409,7 +1421,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     __shared__ uint32_t s_pref[kBinMaxUnits + 1];
     __shared__ uint32_t s_tmp[kBinThreads / 64];
     if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
-    bin_count_body<kBinThreads>(p, blockIdx.x, s_cnt, s_pref, s_tmp);
+    bin_count_body<kBinThreads, true>(p, blockIdx.x, s_cnt, s_pref, s_tmp);
 }
 
 // Per tile: exclusive prefix of its column of bmat over the partitions (in place) and the tile's
@@ -1516,7 +1528,7 @@ constexpr uint32_t kWideQueue = 512;
 // band's end (k_tile_scan's work, repeated per workgroup from L2 instead of one more launch on
 // the frame's critical path); the workgroups of partition 0 write the band's ranges, the one of
 // the last band the chunk's total.  Otherwise tbase holds the list begins (tile_scan_body).
-template <int NT, bool SCAN = false>
+template <int NT, bool SCAN, bool LISTED>
 __device__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, uint32_t* s_pref, uint32_t* s_tmp,
                               uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
@@ -1566,7 +1578,7 @@ __device__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, 
     }
     if (threadIdx.x == 0) s_nw = 0;
     const UnitList L = bin_unit_list(p);
-    const uint32_t total = bin_slots<NT>(p, L, part, s_pref, s_tmp);
+    const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
     for (uint32_t r = threadIdx.x; r < total; r += NT) {
         const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
@@ -1620,7 +1632,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_wide[kWideQueue];
     __shared__ uint32_t s_nw;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;
-    bin_emit_body<kBinThreads, true>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, &s_nw);
+    bin_emit_body<kBinThreads, true, true>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, &s_nw);
 }
 
 // End of a frame: the statistic shards summed into FrameCtl (and zeroed), the saturation
@@ -2493,14 +2505,14 @@ __device__ void chunk1_phases(const Chunk1Params& c, uint8_t* lds) {
     uint32_t* s_wide = s_tmp + 4;
     uint32_t* s_nw = s_wide + kWideQueue;
     const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles);
-    for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256>(c.bp, vb, s_a, s_pref, s_tmp);
+    for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256, false>(c.bp, vb, s_a, s_pref, s_tmp);
     grid_sync(c.bar, ++nb * G, ctl);
     const uint32_t ncol = (c.bp.n_tiles + kColTiles - 1) / kColTiles;
     for (uint32_t vb = b; vb < ncol; vb += G) colscan_body(c.bp, vb, (uint32_t(*)[kColTiles])lds);
     grid_sync(c.bar, ++nb * G, ctl);
     if (b == 0) tile_scan_body<256>(c.bp, s_a);
     grid_sync(c.bar, ++nb * G, ctl);
-    for (uint32_t vb = b; vb < nbin; vb += G) bin_emit_body<256>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
+    for (uint32_t vb = b; vb < nbin; vb += G) bin_emit_body<256, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
     grid_sync(c.bar, ++nb * G, ctl);
     const uint32_t ntb = 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
     for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body(c.tp, vb, *(TsShared*)lds);
