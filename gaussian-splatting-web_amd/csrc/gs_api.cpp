@@ -85,6 +85,14 @@ enum {
 };
 enum { ST_TOTAL, ST_PROJECT, ST_SORT, ST_BIN, ST_TSORT, ST_RANGES, ST_COMPOSITE, ST_COUNT };
 
+#ifndef GS_FRAME_SETS
+#define GS_FRAME_SETS 3
+#endif
+// Frames in flight: per-frame buffers (FrameSet), statistics slots and timing events rotate over
+// this many frames; frame f reuses frame f - kFrameSets's set once that frame has ended.
+constexpr int kFrameSets = GS_FRAME_SETS;
+constexpr int kDeepTiles = 1536;  // frames of at most this many tiles keep kFrameSets in flight
+
 struct FrameEvents {
     hipEvent_t ev[EV_COUNT] = {};
     bool pending = false;
@@ -123,7 +131,7 @@ struct gs_ctx {
     hipStream_t stream = nullptr;
     void* d_out = nullptr;
     size_t d_out_bytes = 0;
-    FrameEvents fe[2];  // ping-pong: frame t's events are read once frame t+1 needs the slot
+    FrameEvents fe[kFrameSets];  // rotating: frame t's events are read once frame t + kFrameSets needs the slot
     int fe_cur = 0;
     double acc_ms[ST_COUNT] = {};
     uint32_t acc_frames = 0;    // frames timed at level 1 (every stage)
@@ -176,7 +184,7 @@ struct gs_scene {
     float4* shade = nullptr;            // packed SH coefficients (sh_quads float4 per Gaussian)
     float4* dbg = nullptr;              // per-Gaussian debug records (3 float4), allocated on demand
     float4* cull = nullptr;             // cull planes (two-phase projection)
-    FrameSet fs[2];                     // per-frame buffers, alternating frame to frame
+    FrameSet fs[kFrameSets];            // per-frame buffers, rotating frame to frame
     int cur_fs = 0;                     // the set the next frame uses
     int last_fs = 0;                    // the set of the last frame
     uint32_t* orig = nullptr;           // [n] reference index of each storage slot (Morton order)
@@ -184,14 +192,14 @@ struct gs_scene {
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     int last_tiles = 0;                 // tiles of the last frame's strip
     // asynchronous frame statistics (chunk controller, capacity): k_frame_end stores FrameCtl into
-    // a pinned slot and then publishes a sequence number there; two slots (two frames in flight)
-    FrameCtl* h_ctl = nullptr;    // pinned, coherent, device-mapped (d_ctl_slot): 2 slots
+    // a pinned slot and then publishes a sequence number there; kFrameSets slots (frames in flight)
+    FrameCtl* h_ctl = nullptr;    // pinned, coherent, device-mapped (d_ctl_slot): kFrameSets slots
     uint32_t* h_seq = nullptr;    // pinned, coherent, device-mapped (d_seq): per slot
     FrameCtl* d_ctl_slot = nullptr;
     uint32_t* d_seq = nullptr;
     uint32_t seq_next = 1;
-    uint32_t stat_want[2] = {};   // sequence number that completes the slot's frame
-    bool stat_pending[2] = {};
+    uint32_t stat_want[kFrameSets] = {};   // sequence number that completes the slot's frame
+    bool stat_pending[kFrameSets] = {};
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
     bool have_last = false;
@@ -328,8 +336,8 @@ static bool wait_slot(gs_scene* s, int slot, hipStream_t st) {
 
 // Latest frame statistics that have arrived on the host; `wait` blocks for the newest frame.
 static void collect_stats(gs_scene* s, bool wait) {
-    for (int k = 0; k < 2; ++k) {
-        const int slot = (s->stat_cur + k) & 1;  // older slot first
+    for (int k = 0; k < kFrameSets; ++k) {
+        const int slot = (s->stat_cur + k) % kFrameSets;  // oldest slot first
         if (!s->stat_pending[slot]) continue;
         if (!seq_arrived(s, slot)) {
             if (!wait) continue;
@@ -371,15 +379,21 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     const int TX = (W + kTile - 1) / kTile;
     const int n_tiles = TX * (tr_end - tr_begin);
     FrameSet& F = s->fs[s->cur_fs];
+    {  // frames in flight: three for small frames (row strips: latency-bound kernels, so a third
+       // frame's early kernels fill the GPU; measured G=8 strip 0.156 -> 0.144 ms), two for large
+       // ones (a third only adds contention: 448 -> 461 us at the bench configuration)
+        const int depth = n_tiles <= kDeepTiles ? kFrameSets : 2;
+        if (depth < kFrameSets) HIPCHK(hipEventSynchronize(s->fs[(s->cur_fs + kFrameSets - depth) % kFrameSets].ev_out));
+    }
     // the frame's kernels run on its set's stream; the caller's stream `st` orders only the
     // composite (the caller's buffer) and waits for the frame's end.  Stage timing (level 1)
     // serialises the frames so that each stage's events measure that stage alone.
     const hipStream_t cst = st;
     st = F.stream;
-    if (o.timing == 1) HIPCHK(hipStreamWaitEvent(st, s->fs[s->cur_fs ^ 1].ev_out, 0));
+    if (o.timing == 1) HIPCHK(hipStreamWaitEvent(st, s->fs[s->last_fs].ev_out, 0));
     collect_stats(s, false);
     const int slot = s->stat_cur;  // this frame's statistics slot
-    if (s->stat_pending[slot]) {  // two frames in flight: the older one's statistics first
+    if (s->stat_pending[slot]) {  // the slot's last frame (kFrameSets ago): its statistics first
         wait_slot(s, slot, nullptr);
         collect_stats(s, false);
         s->stat_pending[slot] = false;
@@ -569,15 +583,15 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     HIPCHK(hipEventRecord(F.ev_out, st));
     HIPCHK(hipStreamWaitEvent(cst, F.ev_out, 0));  // the caller's later work sees the frame
     s->last_fs = s->cur_fs;
-    s->cur_fs ^= 1;
+    s->cur_fs = (s->cur_fs + 1) % kFrameSets;
     s->last_pp = pp;
     HIPCHK(hipGetLastError());
     if (timed) {
         fe.pending = true;
-        c->fe_cur ^= 1;
+        c->fe_cur = (c->fe_cur + 1) % kFrameSets;
     }
     s->stat_pending[slot] = true;  // frame statistics arrive asynchronously (k_frame_end)
-    s->stat_cur ^= 1;
+    s->stat_cur = (s->stat_cur + 1) % kFrameSets;
     s->have_frame = true;
     c->last_scene = s;
     c->stats.n = s->n;
@@ -777,7 +791,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 ensure_tile_capacity(F, 4 * n + (1u << 20));
             }
             const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
-            HIPCHK(hipHostMalloc((void**)&s->h_ctl, 2 * sizeof(FrameCtl), hf));
+            HIPCHK(hipHostMalloc((void**)&s->h_ctl, kFrameSets * sizeof(FrameCtl), hf));
             HIPCHK(hipHostMalloc((void**)&s->h_seq, 64, hf));
             std::memset(s->h_seq, 0, 64);
             HIPCHK(hipHostGetDevicePointer((void**)&s->d_ctl_slot, s->h_ctl, 0));
@@ -963,8 +977,7 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
     return guarded([&] {
         if (!c || !out) throw GsError(GS_ERR_INVALID, "null argument");
         HIPCHK(hipSetDevice(c->device));
-        harvest(c, c->fe[c->fe_cur ^ 1]);
-        harvest(c, c->fe[c->fe_cur]);
+        for (int k = 1; k <= kFrameSets; ++k) harvest(c, c->fe[(c->fe_cur + k) % kFrameSets]);  // oldest first
         gs_stats st = c->stats;
         if (c->last_scene) {
             collect_stats(c->last_scene, true);
