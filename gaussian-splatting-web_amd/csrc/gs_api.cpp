@@ -1,13 +1,13 @@
 // gs_api.cpp — C ABI (include/gsplat.h): contexts, scenes and the per-frame pipeline.
 //
-// A frame (render_frame) is a fixed sequence of launches on one HIP stream with no host round
-// trip; data-dependent sizes live in FrameCtl on the device:
-//   memset(FrameCtl, histograms) -> k_project -> 4 radix passes (depth key; carries the Gaussian
-//   index and its packed tile rectangle) -> per chunk: bin (count/scan/emit) -> 1-2 radix passes
-//   (tile id) -> k_ranges -> k_composite
-// Chunk 0 = the front ceil(f * n_vis) depth ranks; chunk 1 = the rest, binned only into tiles
-// chunk 0 left unsaturated.  f adapts from earlier frames' statistics (read back asynchronously);
-// the image does not depend on f.
+// A frame (render_frame) is a fixed sequence of 8 launches with no host round trip; data-
+// dependent sizes live in FrameCtl on the device:
+//   k_cull -> k_project -> k_bin_count -> k_bin_colscan -> k_bin_emit -> k_tile_sort ->
+//   k_composite -> k_chunk1 (chunk 1 when chunk 0 left tiles unsaturated, then the frame's end)
+// Chunk 0 = the visible splats nearer than a depth key T; chunk 1 = the rest, binned only into
+// tiles chunk 0 left unsaturated.  T adapts from earlier frames' statistics (read back
+// asynchronously); the image does not depend on T.  Frames rotate over kFrameSets sets of
+// per-frame buffers, each with its own stream, so consecutive frames overlap on the GPU.
 // Reference call stack replaced: Renderer.animate/draw (src/renderer.ts:332-387, :301-330).
 #include <hip/hip_runtime.h>
 
@@ -191,7 +191,7 @@ struct gs_scene {
     PartBound* bounds = nullptr;        // [parts] partition bounds (upload)
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     int last_tiles = 0;                 // tiles of the last frame's strip
-    // asynchronous frame statistics (chunk controller, capacity): k_frame_end stores FrameCtl into
+    // asynchronous frame statistics (chunk controller, capacity): the frame's end (k_chunk1) stores FrameCtl into
     // a pinned slot and then publishes a sequence number there; kFrameSets slots (frames in flight)
     FrameCtl* h_ctl = nullptr;    // pinned, coherent, device-mapped (d_ctl_slot): kFrameSets slots
     uint32_t* h_seq = nullptr;    // pinned, coherent, device-mapped (d_seq): per slot
@@ -314,7 +314,7 @@ static bool seq_arrived(const gs_scene* s, int slot) {
     return __atomic_load_n(&s->h_seq[slot], __ATOMIC_ACQUIRE) == s->stat_want[slot];
 }
 
-// Spin until k_frame_end published `slot`'s sequence number.  `st` (nullable) is a stream the
+// Spin until the frame's end (k_chunk1) published `slot`'s sequence number.  `st` (nullable) is a stream the
 // signal is queued on: polled now and then, so a fault surfaces as an error, not a hang.
 // Without a stream: a device synchronize if the signal is late.  False: it never came.
 static bool wait_slot(gs_scene* s, int slot, hipStream_t st) {
@@ -439,7 +439,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     }
     mark(EV_BEGIN);
 
-    // FrameCtl is zero at a frame's start: k_frame_end of the last frame cleared it, unless that
+    // FrameCtl is zero at a frame's start: the end of the set's last frame cleared it, unless that
     // frame never ended (first frame, an error mid-frame)
     if (!F.meta_clean) {
         HIPCHK(hipMemsetAsync(F.ctl, 0, sizeof(FrameCtl), st));
@@ -590,7 +590,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         fe.pending = true;
         c->fe_cur = (c->fe_cur + 1) % kFrameSets;
     }
-    s->stat_pending[slot] = true;  // frame statistics arrive asynchronously (k_frame_end)
+    s->stat_pending[slot] = true;  // frame statistics arrive asynchronously (k_chunk1)
     s->stat_cur = (s->stat_cur + 1) % kFrameSets;
     s->have_frame = true;
     c->last_scene = s;

@@ -53,7 +53,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t n_chunk[2];          // splats (composite slots) per chunk
     uint32_t key_min_inv;         // ~(smallest depth key of a visible splat) (project)
     uint32_t key_max;             // largest depth key of a visible splat (project)
-    uint32_t sat_key;             // depth key of the farthest splat a tile saturated at (k_frame_end)
+    uint32_t sat_key;             // depth key of the farthest splat a tile saturated at (the frame's end, k_chunk1)
     uint32_t unit_n[kUnitShards]; // chunk-0 work units per shard (k_cull; see ProjParams::units)
     uint32_t sat_key_shard[kHistShards];  // per shard: the same, max over the shard's tiles
     uint32_t sat_tiles[kHistShards];      // per shard: tiles saturated by the end of the frame
@@ -61,7 +61,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
 
 // Per-frame counters that many workgroups add to, sharded so that no address takes more than a
 // few hundred device-scope atomics (one address serialises them at ~11 ns each): workgroup b adds
-// to shard b % kStatShards; k_frame_end sums the shards into FrameCtl and zeroes them.
+// to shard b % kStatShards; the frame's end (k_chunk1) sums the shards into FrameCtl and zeroes them.
 constexpr int kStatShards = 64;
 struct StatShard {
     unsigned long long k_total;
@@ -191,7 +191,7 @@ struct SortPass {
                               // upsweep accumulates it, the downsweep scans it into digit bases)
     uint32_t* offsets;        // [parts][256] scratch: partition counts (upsweep)
     uint32_t* gsum;           // [parts / kGroupParts][256] group sums of the counts (zeroed; reset
-                              // by k_ranges after the chunk's passes)
+                              // by the chunk's tile scan)
 };
 
 struct BinParams {
@@ -209,11 +209,11 @@ struct BinParams {
     int chunk;                    // 0 or 1
     int tile_row_begin, tiles_x;
     uint32_t capacity;            // entry capacity of the tile-list arrays
-    uint2* ranges;                // [n_tiles] out (k_tile_scan): [begin, end) of each tile's list
+    uint2* ranges;                // [n_tiles] out (k_bin_emit / the tile scan): [begin, end) of each tile's list
     uint32_t n_tiles;
     uint32_t* bmat;               // [kBinParts][n_tiles] entries of binning partition p in tile t,
                                   // then (k_bin_colscan) the entries of the earlier partitions
-    uint32_t* tbase;              // [n_tiles] entries per tile, then (k_tile_scan) the tile's begin
+    uint32_t* tbase;              // [n_tiles] entries per tile, then (chunk 1's tile scan) the tile's begin
     uint32_t* tvals;              // out: composite slots, grouped by tile, unordered in a tile
     int rows;                     // tile rows of the strip
 };

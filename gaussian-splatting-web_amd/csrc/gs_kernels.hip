@@ -1,20 +1,23 @@
 // gs_kernels.hip — CDNA4 (gfx950) kernels of the splat forward path.
 //
-//   k_transpose   scene upload: reference AoS record (src/ply.ts:249-257) -> geometry records,
-//                 shading blocks and cull planes
-//   k_project     per Gaussian: depth key (src/shaders.ts:36-68) + vs_points projection
-//                 (src/simple_render.ts:217-332) + tile rectangle; one streaming pass over the
-//                 geometry planes (colour is deferred to the binning).
-//   k_radix_*     one stable 8-bit LSD radix pass (upsweep / scan / downsweep); replaces
-//                 webgpu-radix-sort's 16 x 2-bit passes (RS:621-654).
-//   k_bin         per depth-sorted splat: (tile, splat) pairs emitted in depth order (count,
-//                 scan, emit); SH colour (:26-66) of every splat that receives an entry.
-//   k_ranges      per tile: [begin, end) of its list after the stable tile-id sort.
-//   k_composite   16x16 tile workgroup: front-to-back "under" blending of fs_main's alpha
-//                 (src/simple_render.ts:169-200, blend state :455-471), splat batches staged in LDS.
+// Upload (once per scene): k_bbox, k_morton, a device radix sort (k_radix_*), k_transpose (the
+// reference AoS record, src/ply.ts:249-257 -> geometry records, packed SH, cull planes, Morton
+// storage order), k_part_bounds.
+// Per frame (8 launches, no host round trip):
+//   k_cull        per 1024-Gaussian partition: bound test, then per Gaussian the depth key
+//                 (src/shaders.ts:36-68) and a conservative cull; chunk-0 candidates + work units
+//   k_project     per candidate: vs_points (src/simple_render.ts:217-332) and the SH colour
+//                 (:26-66), the composite slot record, sort key and packed tile rectangle
+//   k_bin_count / k_bin_colscan / k_bin_emit   two-level counting sort of (tile, slot) entries
+//   k_tile_sort   per tile: its slots by (depth key, reference index) = the reference's stable
+//                 depth sort (src/renderer.ts:175-183) restricted to the tile
+//   k_composite   16x16 tile: front-to-back "under" blending of fs_main's alpha
+//                 (src/simple_render.ts:169-200, blend state :455-471), batches staged in LDS
+//   k_chunk1      chunk 1 (tiles chunk 0 left unsaturated) as one cooperative launch, then the
+//                 frame's end (statistics shards -> FrameCtl -> pinned host slot)
 //
-// Inter-workgroup hand-offs (look-back words) follow cdna_hip_programming.md Guideline 16 R2:
-// the data word is the flag (one relaxed agent-scope store / load), state re-zeroed every call.
+// Inter-workgroup hand-offs (the grid barrier) follow cdna_hip_programming.md Guideline 16:
+// agent-scope release / acquire, bounded spins, counters zeroed by the frame's end.
 #include <algorithm>
 
 #include "gs_device.h"
@@ -353,7 +356,7 @@ struct Proj {
 };
 
 // Cull, footprint, depth key, tile rect and projected record of Gaussian i; false (key =
-// kSentinel) when invisible.  Deterministic: k_records recomputes the same record bit for bit.
+// kSentinel) when invisible.  Deterministic: records_body recomputes the same record bit for bit.
 __device__ __forceinline__ bool project_core_g(const ProjParams& p, uint32_t i, const float4 g0, const float4 g1,
                                                const float4 g2, int row_lo, int row_hi, bool cull, Proj& o) {
     o.key = kSentinel;
@@ -1296,7 +1299,8 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
 //   k_bin_count    workgroup (partition b, band): LDS counters of its splats' entries per tile
 //                  (ellipse rows; chunk 1: unsaturated tiles only) -> bmat[b][t]
 //   k_bin_colscan  per tile: exclusive prefix of bmat[.][t] over the partitions, tile totals
-//   k_tile_scan    one workgroup: exclusive scan of the totals in tile order -> ranges, tbase
+//   (tile scan)    exclusive scan of the totals in tile order -> ranges (k_bin_emit does it per
+//                  workgroup; k_chunk1 runs tile_scan_body once)
 //   k_bin_emit     workgroup (b, band): LDS cursors tbase[t] + bmat[b][t]; each entry takes a
 //                  position with an LDS atomic (lists are unordered inside a tile: k_tile_sort)
 // Count and emission walk the same ellipse rows, so a tile's count and its entries agree.
@@ -1468,8 +1472,7 @@ __global__ __launch_bounds__(256) void k_bin_colscan(BinParams p) {
 }
 
 // One workgroup: exclusive scan of the tile totals in tile order -> ranges [begin, end) and
-// tbase = begin; the chunk's totals.
-constexpr int kScanThreads = 1024;
+// tbase = begin; the chunk's totals (chunk 1, in k_chunk1).
 
 template <int NT>
 __device__ void tile_scan_body(const BinParams& p, uint32_t* s_w) {
@@ -1513,11 +1516,6 @@ __device__ void tile_scan_body(const BinParams& p, uint32_t* s_w) {
     }
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
-    __shared__ uint32_t s_w[kScanThreads / 64];
-    if (p.chunk == 1 && p.ctl->not_done == 0) return;
-    tile_scan_body<kScanThreads>(p, s_w);
-}
 
 // Wide splats (>= kWideTiles box tiles) are queued in LDS by the thread that meets them and
 // emitted row by row by whole waves (lanes over columns); the queue holds kWideQueue splats,
@@ -1525,7 +1523,7 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(BinParams p) {
 constexpr uint32_t kWideQueue = 512;
 
 // SCAN: tbase holds the tile totals (colscan) and every workgroup scans them itself up to its
-// band's end (k_tile_scan's work, repeated per workgroup from L2 instead of one more launch on
+// band's end (the tile scan, repeated per workgroup from L2 instead of one more launch on
 // the frame's critical path); the workgroups of partition 0 write the band's ranges, the one of
 // the last band the chunk's total.  Otherwise tbase holds the list begins (tile_scan_body).
 template <int NT, bool SCAN, bool LISTED>
