@@ -142,13 +142,14 @@ struct gs_ctx {
     std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
 };
 
-// Everything one frame writes.  Two sets, used by alternate frames, each with its own stream: the
-// next frame's culling, projection, binning and per-tile sort run while this frame composites
-// (only the composite, which writes the caller's buffer, waits for the caller's stream).
+// Everything one frame writes.  kFrameSets sets, used by frames in turn, each with its own stream
+// for the frame's culling, projection, binning and per-tile sort; the composite and the frame's
+// end run on the caller's stream (its buffer, in call order) once those are done.  So the next
+// frames' early kernels run while this frame composites, with one cross-stream wait per frame.
 struct FrameSet {
     hipStream_t stream = nullptr;
-    hipEvent_t ev_in = nullptr;         // the caller's stream at the frame's call
-    hipEvent_t ev_out = nullptr;        // the frame's end
+    hipEvent_t ev_early = nullptr;      // the frame's culling .. per-tile sort done (set stream)
+    hipEvent_t ev_out = nullptr;        // the frame's end (on the caller's stream)
     float4* r2 = nullptr;               // per-Gaussian box of rects wider than 16 tiles
     // composite slots (slot_c0 / slot_c1): records (3 float4), (depth key, index), packed rect
     float4* crec = nullptr;
@@ -385,11 +386,12 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         const int depth = n_tiles <= kDeepTiles ? kFrameSets : 2;
         if (depth < kFrameSets) HIPCHK(hipEventSynchronize(s->fs[(s->cur_fs + kFrameSets - depth) % kFrameSets].ev_out));
     }
-    // the frame's kernels run on its set's stream; the caller's stream `st` orders only the
-    // composite (the caller's buffer) and waits for the frame's end.  Stage timing (level 1)
-    // serialises the frames so that each stage's events measure that stage alone.
+    // culling .. per-tile sort run on the set's stream, the composite and the frame's end on the
+    // caller's stream `st`.  Stage timing (level 1) serialises the frames so that each stage's
+    // events measure that stage alone.
     const hipStream_t cst = st;
     st = F.stream;
+    HIPCHK(hipStreamWaitEvent(st, F.ev_out, 0));  // the set's last frame ended (normally long ago)
     if (o.timing == 1) HIPCHK(hipStreamWaitEvent(st, s->fs[s->last_fs].ev_out, 0));
     collect_stats(s, false);
     const int slot = s->stat_cur;  // this frame's statistics slot
@@ -545,8 +547,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     mark(EV_BIN_0);
     launch_tile_sort(tsp, st);
     mark(EV_TSORT_0);
-    HIPCHK(hipEventRecord(F.ev_in, cst));  // the caller's buffer: after the caller's earlier work
-    HIPCHK(hipStreamWaitEvent(st, F.ev_in, 0));
+    HIPCHK(hipEventRecord(F.ev_early, st));
+    HIPCHK(hipStreamWaitEvent(cst, F.ev_early, 0));
+    st = cst;  // the composite (the caller's buffer) and the frame's end, in call order
     mark(EV_RANGES_0);
     launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
     mark(EV_COMP_0);
@@ -581,7 +584,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     F.meta_clean = true;
     mark(EV_END);
     HIPCHK(hipEventRecord(F.ev_out, st));
-    HIPCHK(hipStreamWaitEvent(cst, F.ev_out, 0));  // the caller's later work sees the frame
     s->last_fs = s->cur_fs;
     s->cur_fs = (s->cur_fs + 1) % kFrameSets;
     s->last_pp = pp;
@@ -770,7 +772,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->orig, (size_t)n + 1);
             for (FrameSet& F : s->fs) {
                 HIPCHK(hipStreamCreateWithFlags(&F.stream, hipStreamNonBlocking));
-                HIPCHK(hipEventCreateWithFlags(&F.ev_in, hipEventDisableTiming));
+                HIPCHK(hipEventCreateWithFlags(&F.ev_early, hipEventDisableTiming));
                 HIPCHK(hipEventCreateWithFlags(&F.ev_out, hipEventDisableTiming));
                 HIPCHK(hipEventRecord(F.ev_out, F.stream));  // "the last frame on this set ended"
                 dev_alloc(F.r2, (size_t)std::max<uint64_t>(n, 1));
@@ -872,7 +874,7 @@ void gs_scene_free(gs_scene* s) {
         dev_free(F.done);
         dev_free(F.sat);
         dev_free(F.state);
-        if (F.ev_in) (void)hipEventDestroy(F.ev_in);
+        if (F.ev_early) (void)hipEventDestroy(F.ev_early);
         if (F.ev_out) (void)hipEventDestroy(F.ev_out);
         if (F.stream) (void)hipStreamDestroy(F.stream);
     }
