@@ -495,11 +495,13 @@ def test_non_finite_gaussians(gpu_ctx):
     assert r[2], r
 
 
-def test_pipelined_frames_match_single_frames(gpu_ctx):
-    """Consecutive frames overlap on the GPU (two frame sets, each on its own stream): a burst of
-    frames with alternating cameras, strips, chunk splits and two scenes, enqueued without any
-    host wait, must reproduce each frame rendered alone, bit for bit."""
-    W, H = 640, 480
+@pytest.mark.parametrize("size", [(640, 480), (1920, 1080)])
+def test_pipelined_frames_match_single_frames(gpu_ctx, size):
+    """Consecutive frames overlap on the GPU (frame sets with their own streams; three frames in
+    flight below 1536 tiles, two above): a burst of frames with alternating cameras, strips, chunk
+    splits and two scenes, enqueued without any host wait, must reproduce each frame rendered
+    alone, bit for bit."""
+    W, H = size
     n = 200_000
     sa = gs.Scene(gpu_ctx, gs.synth_aos(n, 5, W, H), n, 16)
     sb = gs.Scene(gpu_ctx, gs.synth_aos(n // 2, 6, W, H), n // 2, 16)
@@ -521,10 +523,15 @@ def test_pipelined_frames_match_single_frames(gpu_ctx):
         for (sc, u, o), b in zip(seq, bufs):
             sc.render_device(u, W, H, b.ptr.value, b.nbytes, None, o)
         gpu_ctx.sync()
-        for (sc, u, o), b, ref in zip(seq, bufs, refs):
+        for j, ((sc, u, o), b, ref) in enumerate(zip(seq, bufs, refs)):
             got = np.empty(ref.shape, np.float16)
             b.to_host(got)
-            assert np.array_equal(got.view(np.uint16), ref.view(np.uint16))
+            # a strip's rows past the image (padding to whole tiles) are never written
+            row0 = gs.strip_rows(H, o.strip_index, o.strip_count)[0] if o.strip_count > 1 else 0
+            valid = min(ref.shape[0], H - row0)
+            bad = (got[:valid].view(np.uint16) != ref[:valid].view(np.uint16)).any(axis=2)
+            rows = np.nonzero(bad.any(axis=1))[0]
+            assert not bad.any(), (j, int(bad.sum()), rows[:3].tolist(), rows[-3:].tolist(), o.strip_count)
     for b in bufs:
         b.free()
     sa.close()
