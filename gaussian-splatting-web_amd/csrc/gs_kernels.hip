@@ -2489,7 +2489,8 @@ constexpr size_t kBinLdsWords = kBandTiles + (kBinMaxUnits + 1) + 4 + kWideQueue
 constexpr size_t kChunk1Lds = std::max(std::max(kBinLdsWords * 4, sizeof(TsShared)), sizeof(CompQShared));
 
 template <bool FP16_TARGET>
-__device__ void chunk1_phases(const Chunk1Params& c, uint8_t* lds) {
+__device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* lds) {  // inlined: a
+// reference to the kernel argument must not force a copy of it into scratch
     FrameCtl* ctl = c.cp.ctl;
     const uint32_t G = gridDim.x, b = blockIdx.x;
     uint32_t nb = 0;
