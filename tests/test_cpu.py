@@ -3,6 +3,7 @@ import hashlib
 import json
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -253,3 +254,24 @@ def test_abi_rejects_without_device():
     with pytest.raises(gs.GsError) as e:
         gs.Context(0)
     assert e.value.code == -2
+
+
+def test_kernel_resources_no_scratch():
+    """Per-frame kernels in the built library use no scratch memory (a spill or a copied kernel
+    argument costs a scratch setup per launch, measured +7-10 us on k_chunk1), and the composite
+    keeps the register budget of 5 waves per SIMD it was tuned for."""
+    import shutil
+    lib = os.path.join(ROOT, "gaussian-splatting-web_amd", "lib", "libgsplat.so")
+    if not os.path.exists(lib) or not shutil.which("objcopy") or \
+            not os.path.exists("/opt/rocm/lib/llvm/bin/clang-offload-bundler"):
+        pytest.skip("library or ROCm binutils not present")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_resources import kernel_resources
+    res = kernel_resources(lib)
+    frame = ["k_cull", "k_project<true>", "k_project<false>", "k_bin_count", "k_bin_colscan", "k_bin_emit",
+             "k_tile_sort", "k_composite<false>", "k_composite<true>", "k_composite_q<false>",
+             "k_composite_q<true>", "k_chunk1<false>", "k_chunk1<true>"]
+    for k in frame:
+        assert k in res, (k, sorted(res))
+        assert res[k]["scratch"] == 0, (k, res[k])
+    assert res["k_composite<false>"]["vgpr"] <= 96, res["k_composite<false>"]
