@@ -32,8 +32,10 @@ def kernel_resources(lib):
     """{kernel: {"vgpr": n, "sgpr": n, "lds": bytes, "scratch": bytes}} from the library's code object."""
     with tempfile.TemporaryDirectory() as td:
         fat, co = os.path.join(td, "fat.bin"), os.path.join(td, "co.elf")
-        subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, lib], check=True,
-                       capture_output=True)
+        # an explicit output file: objcopy with one file argument rewrites it in place, which
+        # corrupts any process that has the library mapped
+        subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, lib, os.path.join(td, "copy.so")],
+                       check=True, capture_output=True)
         subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + fat,
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True,
                        capture_output=True)
