@@ -140,7 +140,10 @@ int gs_render(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int W, int 
               const gs_opts* opts, void* out_host_or_null);
 
 /* Same, writing into device memory `out_dev` (>= out_bytes) on `hip_stream` (NULL = the ctx's
- * stream).  Returns when the work is enqueued; the caller synchronises the stream. */
+ * stream).  Returns when the work is enqueued; the caller synchronises the stream.  The frame's
+ * culling, projection, binning and per-tile sort run on the scene's own streams (up to three
+ * frames in flight); the composite (which writes out_dev) and the frame's end run on
+ * `hip_stream` in call order, so work enqueued on it afterwards sees the finished frame. */
 int gs_render_device(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int W, int H,
                      const gs_opts* opts, void* out_dev, uint64_t out_bytes, void* hip_stream);
 
