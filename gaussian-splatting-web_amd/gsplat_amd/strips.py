@@ -45,8 +45,10 @@ class StripPipeline:
         dtype = dtype or torch.float16
         device = torch.device(device or "cuda")
         self.strips = [torch.zeros((rows_padded, W, channels), dtype=dtype, device=device) for _ in range(depth)]
-        self.fulls = [torch.zeros((world * rows_padded, W, channels), dtype=dtype, device=device)
-                      for _ in range(depth)]
+        # one rank: the strip is the whole image, nothing to gather
+        self.single = world == 1
+        self.fulls = self.strips if self.single else \
+            [torch.zeros((world * rows_padded, W, channels), dtype=dtype, device=device) for _ in range(depth)]
         self.cuda = device.type == "cuda"
         if self.cuda:
             self.side = torch.cuda.Stream(device=device)
@@ -58,7 +60,7 @@ class StripPipeline:
         """The buffer to render the next frame into (after its previous gather has finished)."""
         import torch
         b = self.k % len(self.strips)
-        if self.cuda and self.k >= len(self.strips):
+        if self.cuda and not self.single and self.k >= len(self.strips):
             torch.cuda.current_stream().wait_event(self.gathered[b])
         return self.strips[b]
 
@@ -66,7 +68,9 @@ class StripPipeline:
         """All-gather the strip just rendered into the current frame's full buffer; returns it."""
         import torch
         b = self.k % len(self.strips)
-        if self.cuda:
+        if self.single:
+            pass
+        elif self.cuda:
             self.rendered[b].record(torch.cuda.current_stream())
             with torch.cuda.stream(self.side):
                 self.side.wait_event(self.rendered[b])

@@ -55,7 +55,7 @@ def _worker(rank, world, port, W, H, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,size", [(2, (160, 120)), (3, (100, 37))])
+@pytest.mark.parametrize("world,size", [(1, (96, 50)), (2, (160, 120)), (3, (100, 37))])
 def test_strip_allgather_gloo(world, size):
     W, H = size
     ctx = mp.get_context("spawn")
