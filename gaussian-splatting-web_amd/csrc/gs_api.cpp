@@ -161,7 +161,7 @@ struct FrameSet {
     uint32_t* sidx = nullptr;           // [slots] storage index of each composite slot
     FrameCtl* ctl = nullptr;            // zero at a frame's start (the frame's end clears it)
     StatShard* stats = nullptr;         // [kStatShards], zero at a frame's start (likewise)
-    uint32_t* bar = nullptr;            // k_chunk1's grid-barrier counter, zero at a frame's start
+    uint32_t* bar = nullptr;            // k_chunk1's grid barrier: arrival count (zero between barriers), generation
     bool meta_clean = false;            // the set's last frame zeroed FrameCtl (see render_frame)
     // tile lists
     uint64_t kcap = 0;
@@ -203,6 +203,7 @@ struct gs_scene {
     bool stat_pending[kFrameSets] = {};
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
+    uint32_t pending_err = 0;   // error bits of every harvested frame not yet reported (sticky)
     bool have_last = false;
     uint32_t chunk_T = kNoSplit;        // adaptive chunk threshold for the next frame
     uint32_t key_lo = 0, key_hi = 0;    // depth-key range of the last frame's visible splats
@@ -348,6 +349,7 @@ static void collect_stats(gs_scene* s, bool wait) {
             }
         }
         s->last = s->h_ctl[slot];
+        s->pending_err |= s->last.err;  // an older frame's error is not overwritten by a newer clean frame
         s->have_last = true;
         s->stat_pending[slot] = false;
         // chunk controller: chunk 0 = the splats nearer than 1.15x the depth at which the last
@@ -628,15 +630,19 @@ static size_t out_bytes_for(int W, int H, const gs_opts& o) {
     return rows * (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
 }
 
-// Frame errors surface here: every frame's FrameCtl comes back asynchronously.
+// Frame errors surface here: every frame's FrameCtl comes back asynchronously, so an error of a
+// frame rendered with gs_render_device is reported by a later call (gsplat.h).  The error bits of
+// every harvested frame accumulate in pending_err until reported.
 static void check_frame_errors(gs_scene* s) {
     collect_stats(s, true);
-    if (s->have_last && (s->last.err & kErrBarrier)) {
-        s->last.err &= ~kErrBarrier;
+    const uint32_t e = s->pending_err;
+    s->pending_err = 0;
+    if (e & kErrBarrier) {  // a timed-out barrier leaves its arrival count behind: zero every set's
+        HIPCHK(hipDeviceSynchronize());
+        for (FrameSet& F : s->fs) HIPCHK(hipMemset(F.bar, 0, 16));
         throw GsError(GS_ERR_DEVICE_FAULT, "chunk-1 grid barrier timed out (workgroups not co-resident)");
     }
-    if (s->have_last && (s->last.err & kErrOverflow)) {
-        s->last.err = 0;
+    if (e & kErrOverflow) {
         for (FrameSet& F : s->fs) ensure_tile_capacity(F, s->last.k_total);
         throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded; capacity grown, render again");
     }
@@ -909,7 +915,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
         if (!out_dev) throw GsError(GS_ERR_INVALID, "null output");
         if (out_bytes < out_bytes_for(W, H, o)) throw GsError(GS_ERR_INVALID, "output buffer too small");
         HIPCHK(hipSetDevice(c->device));
-        if (s->have_last && (s->last.err & (kErrOverflow | kErrBarrier))) check_frame_errors(s);
+        if (s->pending_err & (kErrOverflow | kErrBarrier)) check_frame_errors(s);
         hipStream_t st = stream ? (hipStream_t)stream : c->stream;
         render_frame(c, s, (const float*)uni, W, H, o, out_dev, st);
         return GS_OK;
@@ -953,9 +959,9 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
             render_frame(c, s, (const float*)uni, W, H, o, c->d_out, c->stream);
             HIPCHK(hipStreamSynchronize(c->stream));
             collect_stats(s, true);
-            if (s->last.err & kErrBarrier) check_frame_errors(s);
-            if (!(s->last.err & kErrOverflow)) break;
-            s->last.err = 0;
+            if (s->pending_err & kErrBarrier) check_frame_errors(s);
+            if (!(s->pending_err & kErrOverflow)) break;
+            s->pending_err = 0;
             if (attempt >= 2) throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded");
             for (FrameSet& F : s->fs) ensure_tile_capacity(F, s->last.k_total);  // grow, render again
         }

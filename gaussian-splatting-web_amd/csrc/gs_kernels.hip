@@ -549,7 +549,7 @@ __device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, u
 // are projected; the visible ones whose rect touches an unsaturated tile (the SAT of k_sat) get a
 // chunk-1 slot (slot_c1) with their record and colour.  Waves cover 64 consecutive Gaussians of
 // one projection partition: one counter add per wave.
-__device__ void records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
+__device__ __forceinline__ void records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
@@ -1401,7 +1401,7 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
 
 // Binning partition / band vb: counts of its splats' entries per tile of the band -> bmat row.
 template <int NT, bool LISTED>
-__device__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp) {
+__device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp) {
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
     for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += NT) s_cnt[t] = 0;
@@ -1440,7 +1440,7 @@ __device__ __forceinline__ uint32_t colscan_part(uint32_t q) {  // q-th partitio
     return (q % (kBinParts / 8)) * 8 + q / (kBinParts / 8);
 }
 
-__device__ void colscan_body(const BinParams& p, uint32_t vb, uint32_t (*s_sum)[kColTiles]) {
+__device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, uint32_t (*s_sum)[kColTiles]) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t = vb * kColTiles + lane;
     const bool ok = t < p.n_tiles;
@@ -1475,7 +1475,7 @@ __global__ __launch_bounds__(256) void k_bin_colscan(BinParams p) {
 // tbase = begin; the chunk's totals (chunk 1, in k_chunk1).
 
 template <int NT>
-__device__ void tile_scan_body(const BinParams& p, uint32_t* s_w) {
+__device__ __forceinline__ void tile_scan_body(const BinParams& p, uint32_t* s_w) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     constexpr int nw = NT / 64;
     constexpr int ipt = 8;
@@ -1527,7 +1527,7 @@ constexpr uint32_t kWideQueue = 512;
 // the frame's critical path); the workgroups of partition 0 write the band's ranges, the one of
 // the last band the chunk's total.  Otherwise tbase holds the list begins (tile_scan_body).
 template <int NT, bool SCAN, bool LISTED>
-__device__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, uint32_t* s_pref, uint32_t* s_tmp,
+__device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, uint32_t* s_pref, uint32_t* s_tmp,
                               uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
@@ -1638,14 +1638,13 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
 // host's pinned slot (mapped, fine-grained) and the sequence number published with a
 // system-scope release; the host reads it a frame or two later.  Then FrameCtl is zeroed for the
 // next frame.  One wave; lane l sums shard l.
-__device__ void frame_end_body(FrameCtl* ctl, StatShard* stats, uint32_t* bar, FrameCtl* host_ctl, uint32_t* host_seq,
+__device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, FrameCtl* host_ctl, uint32_t* host_seq,
                                uint32_t seq) {
     constexpr uint32_t kWords = sizeof(FrameCtl) / 4;
     static_assert(kWords <= 64 && kStatShards == 64, "one wave");
     const uint32_t lane = threadIdx.x;
     StatShard sh = stats[lane];
     stats[lane] = StatShard{};
-    if (lane == 0) *bar = 0u;  // k_chunk1's barrier counter
     unsigned long long kt = sh.k_total;
     uint32_t nv = sh.n_vis, kmi = sh.key_min_inv, kma = sh.key_max, c0 = sh.n_chunk[0], c1 = sh.n_chunk[1];
     for (int d = 32; d >= 1; d >>= 1) {
@@ -1682,7 +1681,7 @@ __device__ void frame_end_body(FrameCtl* ctl, StatShard* stats, uint32_t* bar, F
 // threads; row prefixes by waves, then column prefixes by threads, in `lds` when given and the
 // table fits, else in place in `sat`.
 template <int NT>
-__device__ void sat_body(const uint8_t* __restrict__ done, int tiles_x, int rows, uint32_t* __restrict__ sat,
+__device__ __forceinline__ void sat_body(const uint8_t* __restrict__ done, int tiles_x, int rows, uint32_t* __restrict__ sat,
                          uint32_t* lds) {
     const uint32_t sw = (uint32_t)tiles_x + 1, words = sw * (uint32_t)(rows + 1);
     uint32_t* t = (lds && words <= (uint32_t)kSatMaxWords) ? lds : sat;
@@ -1848,7 +1847,7 @@ __device__ void ts_segment(TsShared& S, const unsigned long long (&k)[kTsIpt], c
     __syncthreads();
 }
 
-__device__ void tile_sort_body(const TileSortParams& p, uint32_t vb, TsShared& S) {
+__device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t vb, TsShared& S) {
     const int per = (p.n_tiles + 7) >> 3;  // XCD-banded, as k_composite
     const int tile = (int)(vb & 7) * per + (int)(vb >> 3);
     if (tile >= p.n_tiles) return;
@@ -2275,7 +2274,7 @@ struct CompQShared {
 };
 
 template <bool FP16_TARGET>
-__device__ void composite_q_body(const CompositeParams& p, uint32_t vb, CompQShared& S) {
+__device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint32_t vb, CompQShared& S) {
     auto& sR = S.sR;
     auto& sL = S.sL;
     auto& sN = S.sN;
@@ -2463,16 +2462,25 @@ __global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
 // tiles -> chunk-1 slots (records_body) -> bin count -> column scan -> tile scan -> emission ->
 // per-tile sort -> composite (kCompSecond) of the unsaturated tiles.
 
-// Grid barrier number k (k = 1, 2, ...): a monotonic arrival counter (zero at launch) reaches
-// k * G.  Release / acquire at agent scope (cdna_hip_programming.md Guideline 16); bounded spin.
-__device__ __forceinline__ void grid_sync(uint32_t* cnt, uint32_t target, FrameCtl* ctl) {
+// Grid barrier: bar[0] counts arrivals, bar[1] is a generation word that is never reset.  A
+// workgroup reads the generation, arrives; the last arriver zeroes the count and then bumps the
+// generation (release), the others spin until the generation moves (acquire).  The count is zero
+// again whenever every workgroup has left a barrier, so no one resets it while another workgroup may
+// still be polling (a reset at the frame's end raced with the last barrier's stragglers).  Agent
+// scope (cdna_hip_programming.md Guideline 16); bounded spin: a timeout sets kErrBarrier, and the
+// host zeroes bar[] before the next launch of the set.
+__device__ __forceinline__ void grid_sync(uint32_t* bar, FrameCtl* ctl) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its stores
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t spins = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+        const uint32_t gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gridDim.x - 1) {
+            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (uint32_t spins = 0; __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen;) {
             if (++spins > (1u << 26)) {
                 atomicOr(&ctl->err, kErrBarrier);
                 break;
@@ -2493,11 +2501,10 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
 // reference to the kernel argument must not force a copy of it into scratch
     FrameCtl* ctl = c.cp.ctl;
     const uint32_t G = gridDim.x, b = blockIdx.x;
-    uint32_t nb = 0;
     if (b == 0) sat_body<256>(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat, nullptr);
-    grid_sync(c.bar, ++nb * G, ctl);
+    grid_sync(c.bar, ctl);
     records_body(c.pp, b, G);
-    grid_sync(c.bar, ++nb * G, ctl);
+    grid_sync(c.bar, ctl);
     uint32_t* s_a = (uint32_t*)lds;
     uint32_t* s_pref = s_a + kBandTiles;
     uint32_t* s_tmp = s_pref + kBinMaxUnits + 1;
@@ -2505,19 +2512,19 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     uint32_t* s_nw = s_wide + kWideQueue;
     const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles);
     for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256, false>(c.bp, vb, s_a, s_pref, s_tmp);
-    grid_sync(c.bar, ++nb * G, ctl);
+    grid_sync(c.bar, ctl);
     const uint32_t ncol = (c.bp.n_tiles + kColTiles - 1) / kColTiles;
     for (uint32_t vb = b; vb < ncol; vb += G) colscan_body(c.bp, vb, (uint32_t(*)[kColTiles])lds);
-    grid_sync(c.bar, ++nb * G, ctl);
+    grid_sync(c.bar, ctl);
     if (b == 0) tile_scan_body<256>(c.bp, s_a);
-    grid_sync(c.bar, ++nb * G, ctl);
+    grid_sync(c.bar, ctl);
     for (uint32_t vb = b; vb < nbin; vb += G) bin_emit_body<256, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
-    grid_sync(c.bar, ++nb * G, ctl);
+    grid_sync(c.bar, ctl);
     const uint32_t ntb = 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
     for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body(c.tp, vb, *(TsShared*)lds);
-    grid_sync(c.bar, ++nb * G, ctl);
+    grid_sync(c.bar, ctl);
     for (uint32_t vb = b; vb < ntb; vb += G) composite_q_body<FP16_TARGET>(c.cp, vb, *(CompQShared*)lds);
-    grid_sync(c.bar, ++nb * G, ctl);  // every phase done before the frame's end reads FrameCtl
+    grid_sync(c.bar, ctl);  // every phase done before the frame's end reads FrameCtl
 }
 
 template <bool FP16_TARGET>
@@ -2527,7 +2534,7 @@ __global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
     const uint32_t G = gridDim.x, b = blockIdx.x;
     if (c.two_chunks && ctl->not_done != 0) chunk1_phases<FP16_TARGET>(c, lds);  // else: chunk 0 saturated every tile
     // the frame's end (one wave): FrameCtl is read by no workgroup after this point
-    if (b == 0 && threadIdx.x < 64) frame_end_body(ctl, c.stats, c.bar, c.host_ctl, c.host_seq, c.seq);
+    if (b == 0 && threadIdx.x < 64) frame_end_body(ctl, c.stats, c.host_ctl, c.host_seq, c.seq);
     (void)G;
 }
 

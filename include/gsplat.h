@@ -143,7 +143,11 @@ int gs_render(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int W, int 
  * stream).  Returns when the work is enqueued; the caller synchronises the stream.  The frame's
  * culling, projection, binning and per-tile sort run on the scene's own streams (up to three
  * frames in flight); the composite (which writes out_dev) and the frame's end run on
- * `hip_stream` in call order, so work enqueued on it afterwards sees the finished frame. */
+ * `hip_stream` in call order, so work enqueued on it afterwards sees the finished frame.
+ * Device-side frame errors (tile-entry overflow, a chunk-1 barrier timeout) come back with the
+ * frame's statistics, asynchronously: an error of frame t is reported (GS_ERR_DEVICE_FAULT) by a
+ * later gs_render_device or gs_sync call, never lost (the bits of every frame are kept
+ * until reported).  gs_render, being synchronous, reports its own frame's errors. */
 int gs_render_device(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int W, int H,
                      const gs_opts* opts, void* out_dev, uint64_t out_bytes, void* hip_stream);
 
