@@ -209,9 +209,22 @@ struct gs_scene {
     uint32_t key_lo = 0, key_hi = 0;    // depth-key range of the last frame's visible splats
     bool have_krange = false;
     bool have_frame = false;
+    // ref_quirks (src/renderer.ts:306): the init-sort slots' state and the draw-ordered copy,
+    // allocated by the first ref_quirks frame (quirk_prepare)
+    uint32_t *qk = nullptr, *qv = nullptr;        // [n] state: (key, value) of slots >= nk after the last sort
+    uint32_t *qK = nullptr, *qV = nullptr, *qK2 = nullptr, *qV2 = nullptr;  // [n] slots, sort ping-pong
+    uint32_t* qinv = nullptr;                     // [n] storage slot of each reference index
+    float4 *qgeo = nullptr, *qshade = nullptr, *qcull = nullptr;  // the scene in draw order
+    uint32_t* qorig = nullptr;                    // [n] = draw rank
+    PartBound* qbounds = nullptr;
+    const uint32_t* qdraw = nullptr;              // [n] Gaussian of each draw rank, last ref_quirks frame
+    bool last_quirk = false;                      // the last frame ran with ref_quirks
 };
 
 static constexpr size_t kHistWords = kHistShards * 256;
+// Largest scene for which the reference's init-sort dispatch is valid: max(N/8, 8) workgroups
+// <= 65535 (src/renderer.ts:306; beyond it WebGPU rejects the dispatch and no key is written).
+static constexpr uint64_t kQuirkMaxN = 65535ull * 8;
 // radix partition sizes (items per thread x 256): small partitions keep every CU busy on the
 // short depth sorts; the tile-id sort is long enough for 4096-element partitions
 // radix partition size of gs_debug_sort_pairs (items per thread x 256)
@@ -373,6 +386,8 @@ static void collect_stats(gs_scene* s, bool wait) {
     }
 }
 
+static void quirk_prepare(gs_scene* s, const float* uni, hipStream_t st);
+
 // The per-frame pipeline.  `out` is device memory of rows_padded*W (strip) or H*W pixels.
 static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o,
                          void* out, hipStream_t st) {
@@ -421,6 +436,12 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
             if (std::isfinite(v) && k < kNoSplit - 1) T = k + 1;
         }
     }
+    const bool quirk = o.ref_quirks != 0;
+    if (quirk) {
+        T = kNoSplit;  // one chunk: the slot keys are draw ranks
+        quirk_prepare(s, uni, F.stream);
+    }
+    s->last_quirk = quirk;
     const bool two_chunks = T != kNoSplit;
     if (two_chunks) {
         ensure_state(F, (uint64_t)W * H);
@@ -492,6 +513,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.bounds = s->bounds;
     pp.orig = s->orig;
     pp.sidx = F.sidx;
+    if (quirk) {  // the frame runs on the draw-ordered copy; each slot's sort key = (0, draw rank)
+        pp.geo = s->qgeo;
+        pp.cull = s->qcull;
+        pp.sh = s->qshade;
+        pp.bounds = s->qbounds;
+        pp.orig = s->qorig;
+        pp.key_zero = 1;
+    }
     mark(EV_PROJ0);
     launch_project(pp, st);
     mark(EV_PROJ1);
@@ -619,7 +648,9 @@ static void validate_render_args(gs_ctx* c, gs_scene* s, const void* uni, int W,
         if (!(o->t_min >= 0.0f && o->t_min < 1.0f)) throw GsError(GS_ERR_INVALID, "t_min must be in [0,1)");
         if (o->timing < 0 || o->timing > 2) throw GsError(GS_ERR_INVALID, "timing must be 0, 1 or 2");
         if (!(o->chunk_fraction >= 0.0f)) throw GsError(GS_ERR_INVALID, "chunk_fraction must be >= 0");
-        if (o->ref_quirks) throw GsError(GS_ERR_UNSUPPORTED, "ref_quirks not built in this version");
+        if (o->ref_quirks && s->n > kQuirkMaxN)
+            throw GsError(GS_ERR_UNSUPPORTED, "ref_quirks: the reference's init-sort dispatch is invalid above 524280 "
+                                              "Gaussians (max(N/8,8) > 65535 workgroups)");
     }
 }
 
@@ -686,6 +717,45 @@ static std::pair<uint32_t*, uint32_t*> device_sort_pairs(uint32_t* ka, uint32_t*
     }
     dev_free(hist); dev_free(offs); dev_free(gsum);
     return {ka, va};
+}
+
+// Slots the reference's init-sort pass keys: trunc(max(N/8, 8)) * 8 (WebIDL [EnforceRange]
+// truncation of dispatchWorkgroups' argument; the shader skips idx >= N).
+static uint64_t quirk_keyed_slots(uint64_t n) {
+    const uint64_t keyed = (uint64_t)std::trunc(std::max((double)n / 8.0, 8.0)) * 8;
+    return std::min(keyed, n);
+}
+
+// ref_quirks: this frame's N init-sort slots -> stable sort -> the draw-ordered copy of the scene
+// (and the next frame's state).  Runs on `st` ahead of the frame's culling; waits for every frame
+// in flight first (they read the copy).
+static void quirk_prepare(gs_scene* s, const float* uni, hipStream_t st) {
+    const uint32_t n = (uint32_t)s->n;
+    HIPCHK(hipDeviceSynchronize());
+    if (!s->qk) {
+        const size_t m = std::max<size_t>(n, 1);
+        dev_alloc(s->qk, m); dev_alloc(s->qv, m);
+        dev_alloc(s->qK, m); dev_alloc(s->qV, m); dev_alloc(s->qK2, m); dev_alloc(s->qV2, m);
+        dev_alloc(s->qinv, m);
+        dev_alloc(s->qgeo, 3 * m);
+        dev_alloc(s->qshade, (size_t)sh_quads(s->n_sh) * m);
+        dev_alloc(s->qcull, m);
+        dev_alloc(s->qorig, m);
+        dev_alloc(s->qbounds, (size_t)proj_parts(n) + 1);
+        HIPCHK(hipMemsetAsync(s->qk, 0, m * 4, st));  // WebGPU buffers start zeroed
+        HIPCHK(hipMemsetAsync(s->qv, 0, m * 4, st));
+        launch_inverse(s->orig, n, s->qinv, st);
+    }
+    if (!n) return;
+    const uint32_t nk = (uint32_t)quirk_keyed_slots(n);
+    const float4 vrow = make_float4(uni[2], uni[6], uni[10], uni[14]);  // view row 2 (column-major)
+    launch_quirk_keys(s->cull, s->orig, n, nk, vrow, s->qk, s->qv, s->qK, s->qV, st);
+    const auto r = device_sort_pairs(s->qK, s->qV, s->qK2, s->qV2, n, 0, 32, st);
+    launch_quirk_gather(r.first, r.second, s->qinv, n, nk, sh_quads(s->n_sh), s->geo, s->shade, s->cull, s->qgeo,
+                        s->qshade, s->qcull, s->qorig, s->qk, s->qv, st);
+    launch_part_bounds(s->qcull, n, s->qbounds, st);
+    HIPCHK(hipGetLastError());
+    s->qdraw = r.second;
 }
 
 extern "C" {
@@ -886,6 +956,9 @@ void gs_scene_free(gs_scene* s) {
     }
     dev_free(s->bounds);
     dev_free(s->orig);
+    dev_free(s->qk); dev_free(s->qv); dev_free(s->qK); dev_free(s->qV); dev_free(s->qK2); dev_free(s->qV2);
+    dev_free(s->qinv); dev_free(s->qgeo); dev_free(s->qshade); dev_free(s->qcull); dev_free(s->qorig);
+    dev_free(s->qbounds);
     if (s->h_ctl) (void)hipHostFree(s->h_ctl);
     if (s->h_seq) (void)hipHostFree(s->h_seq);
     delete s;
@@ -1056,14 +1129,25 @@ int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, i
     });
 }
 
-// The last frame's visible splats' composite slots as (slot, depth key, reference index), chunk 0
-// then chunk 1.
-static std::vector<std::array<uint32_t, 3>> frame_slots(gs_scene* s) {
+// Reference index of each draw rank of the last ref_quirks frame (empty otherwise).
+static std::vector<uint32_t> quirk_draw(gs_scene* s) {
+    std::vector<uint32_t> d;
+    if (!s->last_quirk || !s->qdraw) return d;
+    d.resize(s->n);
+    HIPCHK(hipMemcpy(d.data(), s->qdraw, s->n * 4, hipMemcpyDeviceToHost));
+    return d;
+}
+
+// The last frame's visible splats' composite slots as (slot, depth key, reference index, chunk),
+// chunk 0 then chunk 1.  Under ref_quirks the slot key is (0, draw rank): reported as (draw rank,
+// the Gaussian drawn at that rank).
+static std::vector<std::array<uint32_t, 4>> frame_slots(gs_scene* s) {
     collect_stats(s, true);
     const FrameSet& F = s->fs[s->last_fs];
     const uint32_t parts = proj_parts(s->n);
-    std::vector<std::array<uint32_t, 3>> out;
+    std::vector<std::array<uint32_t, 4>> out;
     if (!parts) return out;
+    const std::vector<uint32_t> qd = quirk_draw(s);
     std::vector<uint32_t> c0(parts), c1(parts);
     std::vector<uint2> sk((size_t)parts * kProjTile);
     std::vector<uint32_t> rect((size_t)parts * kProjTile);
@@ -1077,7 +1161,7 @@ static std::vector<std::array<uint32_t, 3>> frame_slots(gs_scene* s) {
             for (uint32_t q = 0; q < (ch ? c1[p] : c0[p]); ++q) {
                 const uint32_t g = ch ? slot_c1(p, q) : slot_c0(p, q);
                 if (rect[g] == kRectHole) continue;  // an invisible chunk-0 candidate
-                out.push_back({g, sk[g].x, sk[g].y});
+                out.push_back({g, qd.empty() ? sk[g].x : sk[g].y, qd.empty() ? sk[g].y : qd[sk[g].y], (uint32_t)ch});
             }
     return out;
 }
@@ -1089,8 +1173,8 @@ int gs_debug_last_order(gs_ctx* c, gs_scene* s, uint32_t* out_keys, uint32_t* ou
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipDeviceSynchronize());  // both frame sets' streams
-        auto sl = frame_slots(s);  // every composite slot, in the composite's (key, index) order
-        std::sort(sl.begin(), sl.end(), [](const std::array<uint32_t, 3>& a, const std::array<uint32_t, 3>& b) {
+        auto sl = frame_slots(s);  // every composite slot, sorted here by (key, index): the visible set
+        std::sort(sl.begin(), sl.end(), [](const std::array<uint32_t, 4>& a, const std::array<uint32_t, 4>& b) {
             return a[1] != b[1] ? a[1] < b[1] : a[2] < b[2];
         });
         *out_n = sl.size();
@@ -1107,6 +1191,8 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
     return guarded([&] {
         if (!c || !s || !out16) throw GsError(GS_ERR_INVALID, "null argument");
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
+        if (s->last_quirk) throw GsError(GS_ERR_UNSUPPORTED, "per-Gaussian records of a ref_quirks frame "
+                                                             "(a Gaussian may be drawn twice): use gs_debug_last_slots");
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipDeviceSynchronize());  // both frame sets' streams
         const uint64_t m = std::min(cap, s->n);
@@ -1141,6 +1227,75 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
             HIPCHK(hipMemcpy(cr.data(), F.crec, ns * 48, hipMemcpyDeviceToHost));
             for (const auto& e : sl)
                 if (e[2] < m) std::memcpy(out16 + 16 * (uint64_t)e[2] + 8, &cr[12 * (size_t)e[0] + 8], 12);
+        }
+        return GS_OK;
+    });
+}
+
+int gs_debug_last_slots(gs_ctx* c, gs_scene* s, uint32_t* out16, uint64_t cap, uint64_t* out_n) {
+    return guarded([&] {
+        if (!c || !s || !out_n) throw GsError(GS_ERR_INVALID, "null argument");
+        if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipDeviceSynchronize());
+        const auto sl = frame_slots(s);
+        *out_n = sl.size();
+        const uint64_t m = out16 ? std::min<uint64_t>(cap, sl.size()) : 0;
+        if (!m) return GS_OK;
+        const FrameSet& F = s->fs[s->last_fs];
+        const size_t ns = (size_t)proj_parts(s->n) * kProjTile;
+        std::vector<uint32_t> cr(ns * 12), rect(ns);
+        HIPCHK(hipMemcpy(cr.data(), F.crec, ns * 48, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(rect.data(), F.srect, ns * 4, hipMemcpyDeviceToHost));
+        for (uint64_t k = 0; k < m; ++k) {
+            const auto& e = sl[k];
+            uint32_t* o = out16 + 16 * k;
+            o[0] = e[1];
+            o[1] = e[2];
+            o[2] = e[3];
+            o[3] = rect[e[0]];
+            std::memcpy(o + 4, &cr[12 * (size_t)e[0]], 48);
+        }
+        return GS_OK;
+    });
+}
+
+int gs_debug_tile_lists(gs_ctx* c, gs_scene* s, uint32_t* out_ranges, uint64_t ranges_cap, uint32_t* out_entries,
+                        uint64_t entries_cap, uint64_t* out_tiles, uint64_t* out_entries_n) {
+    return guarded([&] {
+        if (!c || !s || !out_tiles || !out_entries_n) throw GsError(GS_ERR_INVALID, "null argument");
+        if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipDeviceSynchronize());
+        collect_stats(s, true);
+        if (s->last.n_chunk[1] > 0)
+            throw GsError(GS_ERR_UNSUPPORTED, "tile lists of a two-chunk frame (render with chunk_fraction >= 1)");
+        const FrameSet& F = s->fs[s->last_fs];
+        const int nt = s->last_tiles;
+        *out_tiles = (uint64_t)std::max(nt, 0);
+        std::vector<uint2> rg((size_t)std::max(nt, 1));
+        if (nt > 0) HIPCHK(hipMemcpy(rg.data(), F.ranges, (size_t)nt * sizeof(uint2), hipMemcpyDeviceToHost));
+        uint64_t total = 0;
+        for (int t = 0; t < nt; ++t) total = std::max<uint64_t>(total, rg[t].y);
+        *out_entries_n = total;
+        if (out_ranges)
+            for (int t = 0; t < nt && (uint64_t)t < ranges_cap; ++t) {
+                out_ranges[2 * t] = rg[t].x;
+                out_ranges[2 * t + 1] = rg[t].y;
+            }
+        const uint64_t m = out_entries ? std::min(entries_cap, total) : 0;
+        if (!m) return GS_OK;
+        std::vector<uint32_t> tv(m);
+        HIPCHK(hipMemcpy(tv.data(), F.tvB, m * 4, hipMemcpyDeviceToHost));
+        const size_t ns = (size_t)proj_parts(s->n) * kProjTile;
+        std::vector<uint2> sk(ns);
+        HIPCHK(hipMemcpy(sk.data(), F.skey, ns * sizeof(uint2), hipMemcpyDeviceToHost));
+        const std::vector<uint32_t> qd = quirk_draw(s);
+        for (uint64_t e = 0; e < m; ++e) {
+            const uint32_t g = tv[e];
+            if (g >= ns) throw GsError(GS_ERR_INTERNAL, "tile list entry out of range");
+            out_entries[2 * e] = qd.empty() ? sk[g].x : sk[g].y;
+            out_entries[2 * e + 1] = qd.empty() ? sk[g].y : qd[sk[g].y];
         }
         return GS_OK;
     });

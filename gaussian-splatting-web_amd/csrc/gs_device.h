@@ -152,6 +152,7 @@ struct ProjParams {
     float cam[3];             // camera position (SH view direction)
     const float4* sh;         // [n][shq] packed SH coefficients
     uint32_t shq;             // sh_quads(n_sh)
+    uint32_t key_zero;        // ref_quirks: slot sort key (0, draw rank) -- orig holds the rank
 };
 
 // Element filter of a radix pass (the first pass of a depth chunk decides chunk membership).
@@ -268,6 +269,14 @@ void launch_morton(const uint8_t* aos, uint64_t n, uint32_t rb, const uint32_t* 
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, const uint32_t* perm, float4* geo, float4* shade,
                       float4* cull, uint32_t* orig, hipStream_t s);
 void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s);
+// ref_quirks (src/renderer.ts:306): the init-sort pass's (key, value) slots and the draw-ordered
+// scene copy (see k_quirk_keys / k_quirk_gather)
+void launch_inverse(const uint32_t* orig, uint64_t n, uint32_t* inv, hipStream_t s);
+void launch_quirk_keys(const float4* cull, const uint32_t* orig, uint32_t n, uint32_t nk, float4 vrow,
+                       const uint32_t* qk, const uint32_t* qv, uint32_t* keys, uint32_t* vals, hipStream_t s);
+void launch_quirk_gather(const uint32_t* skeys, const uint32_t* svals, const uint32_t* inv, uint32_t n, uint32_t nk,
+                         uint32_t shq, const float4* geo, const float4* shade, const float4* cull, float4* dgeo,
+                         float4* dshade, float4* dcull, uint32_t* dorig, uint32_t* qk, uint32_t* qv, hipStream_t s);
 void launch_project(const ProjParams& p, hipStream_t s);
 void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 slots (or, rec_all, every record)
 void launch_sort_pass(const SortPass& p, hipStream_t s);

@@ -536,7 +536,7 @@ __device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, u
     float4* r = p.crec + 3 * (uint64_t)slot;
     r[0] = o.r0;
     r[1] = o.r1;
-    p.skey[slot] = make_uint2(o.key, oi);
+    p.skey[slot] = make_uint2(p.key_zero ? 0u : o.key, oi);
     p.sidx[slot] = i;
     p.srect[slot] = o.prect;
     if (o.prect == kRectLarge)  // binning reads the pixel box of a rect wider or taller than 16 tiles
@@ -2539,6 +2539,70 @@ __global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
 }
 
 
+// ============================================================================ ref_quirks
+// The reference's init-sort pass runs dispatchWorkgroups(max(N/8, 8)) workgroups of 8 threads
+// (src/renderer.ts:306; src/shaders.ts:42-73): with WebIDL truncation only the first
+// nk = trunc(max(N/8, 8)) * 8 slots get (depth key, index); slots nk..N-1 keep the (key, value)
+// the previous frame's in-place radix sort left there (zero on the first frame).  The sort then
+// orders all N slots (stable: ties by slot) and instance i draws Gaussian value[i], so a
+// Gaussian can be drawn twice (or not at all).  Here: the N slots are keyed (k_quirk_keys),
+// sorted by the device radix sort, and the draw list is gathered into a scene copy in draw order
+// (k_quirk_gather) whose "reference index" is the draw rank; the frame then runs on that copy
+// with every slot's depth key set to 0, so each tile's list is in draw-rank order.
+
+// inv[orig[j]] = j: storage slot of each reference index.
+__global__ __launch_bounds__(256) void k_inverse(const uint32_t* __restrict__ orig, uint64_t n,
+                                                 uint32_t* __restrict__ inv) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < n) inv[orig[j]] = (uint32_t)j;
+}
+
+// Slots of the init-sort pass: slot g < nk = (sortable((V [p,1]).z), g) of Gaussian g (stored at
+// storage slot j, orig[j] = g; the key bit-identical to k_cull's), slot s >= nk = the state.
+__global__ __launch_bounds__(256) void k_quirk_keys(const float4* __restrict__ cull, const uint32_t* __restrict__ orig,
+                                                    uint32_t n, uint32_t nk, float4 vrow,
+                                                    const uint32_t* __restrict__ qk, const uint32_t* __restrict__ qv,
+                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+#pragma clang fp contract(off)
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t g = orig[j];
+    if (g < nk) {
+        const float4 c = cull[j];
+        const float vz = ((vrow.x * c.x + vrow.y * c.y) + vrow.z * c.z) + vrow.w * 1.0f;  // src/shaders.ts:66-68
+        keys[g] = sortable_key(vz);
+        vals[g] = g;
+    }
+    if (j >= nk) {
+        keys[j] = qk[j];
+        vals[j] = qv[j];
+    }
+}
+
+// Draw entry i = Gaussian svals[i]: its geometry, cull plane and SH copied to row i of the
+// draw-ordered copy, dorig[i] = i; the sorted slots >= nk become the next frame's state.
+__global__ __launch_bounds__(256) void k_quirk_gather(const uint32_t* __restrict__ skeys,
+                                                      const uint32_t* __restrict__ svals,
+                                                      const uint32_t* __restrict__ inv, uint32_t n, uint32_t nk,
+                                                      uint32_t shq, const float4* __restrict__ geo,
+                                                      const float4* __restrict__ shade, const float4* __restrict__ cull,
+                                                      float4* __restrict__ dgeo, float4* __restrict__ dshade,
+                                                      float4* __restrict__ dcull, uint32_t* __restrict__ dorig,
+                                                      uint32_t* __restrict__ qk, uint32_t* __restrict__ qv) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t g = svals[i];
+    const uint64_t j = inv[g < n ? g : 0];
+    for (int k = 0; k < 3; ++k) dgeo[3 * (uint64_t)i + k] = geo[3 * j + k];
+    for (uint32_t k = 0; k < shq; ++k) dshade[(uint64_t)i * shq + k] = shade[j * shq + k];
+    dcull[i] = cull[j];
+    dorig[i] = i;
+    if (i >= nk) {
+        qk[i] = skeys[i];
+        qv[i] = g;
+    }
+}
+
 // ============================================================================ k_present
 // PostProcessRenderer.fragmentMain (src/post_process_render.ts:62-77) per pixel: the sampler
 // reads texel (x, H-1-y) at its centre (exact), a' = saturate(1.5 a), a' = a'^4 (as (a'^2)^2,
@@ -2602,6 +2666,23 @@ void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, const uint32_t* 
 void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_part_bounds, dim3(proj_parts(n)), dim3(256), 0, s, cull, n, out);
+}
+void launch_inverse(const uint32_t* orig, uint64_t n, uint32_t* inv, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_inverse, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, orig, n, inv);
+}
+void launch_quirk_keys(const float4* cull, const uint32_t* orig, uint32_t n, uint32_t nk, float4 vrow,
+                       const uint32_t* qk, const uint32_t* qv, uint32_t* keys, uint32_t* vals, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_quirk_keys, dim3((n + 255) / 256), dim3(256), 0, s, cull, orig, n, nk, vrow, qk, qv, keys,
+                       vals);
+}
+void launch_quirk_gather(const uint32_t* skeys, const uint32_t* svals, const uint32_t* inv, uint32_t n, uint32_t nk,
+                         uint32_t shq, const float4* geo, const float4* shade, const float4* cull, float4* dgeo,
+                         float4* dshade, float4* dcull, uint32_t* dorig, uint32_t* qk, uint32_t* qv, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_quirk_gather, dim3((n + 255) / 256), dim3(256), 0, s, skeys, svals, inv, n, nk, shq, geo,
+                       shade, cull, dgeo, dshade, dcull, dorig, qk, qv);
 }
 void launch_project(const ProjParams& p, hipStream_t s) {
     const uint32_t parts = proj_parts(p.n);

@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = (
     "gs_render", "gs_render_device", "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
     "gs_present_device", "gs_encode_png", "gs_look_at",
     "gs_perspective", "gs_camera_position", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
-    "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records",
+    "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records", "gs_debug_last_slots",
+    "gs_debug_tile_lists",
 )
 
 
@@ -65,6 +66,11 @@ class GsStats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# gs_debug_last_slots row (16 words)
+SLOT_DTYPE = np.dtype([("key", "<u4"), ("index", "<u4"), ("chunk", "<u4"), ("rect", "<u4"),
+                       ("r0", "<f4", 4), ("r1", "<f4", 4), ("col", "<f4", 3), ("keybits", "<u4")])
 
 
 class GsError(RuntimeError):
@@ -119,6 +125,8 @@ def lib():
         L.gs_debug_sort_pairs.argtypes = [P, P, P, U64, I, I]
         L.gs_debug_last_order.argtypes = [P, P, P, P, U64, ctypes.POINTER(U64)]
         L.gs_debug_last_records.argtypes = [P, P, P, U64]
+        L.gs_debug_last_slots.argtypes = [P, P, P, U64, ctypes.POINTER(U64)]
+        L.gs_debug_tile_lists.argtypes = [P, P, P, U64, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]
         _lib = L
     return _lib
 
@@ -333,6 +341,25 @@ class Scene:
         _check(lib().gs_debug_last_order(self.ctx.handle, self.handle, _ptr(keys), _ptr(idx), n.value,
                                          ctypes.byref(n)))
         return keys, idx
+
+    def last_slots(self):
+        """Composite slots of the last frame (gs_debug_last_slots): structured array."""
+        n = ctypes.c_uint64()
+        _check(lib().gs_debug_last_slots(self.ctx.handle, self.handle, None, 0, ctypes.byref(n)))
+        out = np.zeros((n.value, 16), np.uint32)
+        _check(lib().gs_debug_last_slots(self.ctx.handle, self.handle, _ptr(out), n.value, ctypes.byref(n)))
+        return out.view(SLOT_DTYPE).reshape(-1)
+
+    def tile_lists(self):
+        """(ranges [n_tiles, 2], entries [n, 2] = (key, reference index)) the composite consumed."""
+        nt, ne = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().gs_debug_tile_lists(self.ctx.handle, self.handle, None, 0, None, 0, ctypes.byref(nt),
+                                         ctypes.byref(ne)))
+        rg = np.zeros((nt.value, 2), np.uint32)
+        en = np.zeros((ne.value, 2), np.uint32)
+        _check(lib().gs_debug_tile_lists(self.ctx.handle, self.handle, _ptr(rg), nt.value, _ptr(en), ne.value,
+                                         ctypes.byref(nt), ctypes.byref(ne)))
+        return rg, en
 
     def last_records(self):
         out = np.empty((self.n, 16), np.float32)

@@ -74,7 +74,11 @@ typedef struct gs_opts {
     float t_min;          /* a pixel stops compositing once (1 - alpha) < t_min; 0 = never (default 1e-4) */
     int32_t ref_quirks;   /* 1: reproduce the reference's init-sort grid truncation (src/renderer.ts:306):
                              only trunc(max(N/8,8))*8 slots are keyed per frame, the rest keep the previous
-                             frame's sorted (key,value) (zero on the first frame).  State lives in the scene. */
+                             frame's sorted (key,value) (zero on the first frame), so a Gaussian may be drawn
+                             twice or not at all.  The state lives in the scene and advances once per call
+                             (one call = one reference frame; strips of one frame belong on separate scenes,
+                             one per rank).  N <= 524280 (above it the reference's dispatch is invalid:
+                             GS_ERR_UNSUPPORTED).  Waits for the frames in flight (a compatibility mode). */
     int32_t strip_index;  /* row strip rendered by this call, 0 <= strip_index < strip_count */
     int32_t strip_count;  /* number of equal row strips (16-px tile rows, see gs_strip_rows); 1 = whole image */
     int32_t timing;       /* 1: record per-stage hipEvent timings (gs_timings); 2: the composite's only
@@ -211,7 +215,9 @@ int gs_ply_parse(const void* ply, uint64_t bytes, gs_ply_info* info, void* out_a
 /* Stable ascending GPU radix sort of (key,value) on bits [begin_bit,end_bit): host in/out. */
 int gs_debug_sort_pairs(gs_ctx* ctx, uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit,
                         int end_bit);
-/* Sorted depth keys and original Gaussian indices of the last frame (visible splats only). */
+/* The last frame's visible set: depth key and reference index of every composite slot, sorted on
+ * the host by (key, index) (under ref_quirks: (draw rank, Gaussian)).  The order the composite
+ * used is what gs_debug_tile_lists exports. */
 int gs_debug_last_order(gs_ctx* ctx, gs_scene* scene, uint32_t* out_keys, uint32_t* out_index,
                         uint64_t capacity, uint64_t* out_n);
 /* Projected record of every Gaussian in the last frame, 16 floats each: centre cx, cy (pixels);
@@ -220,6 +226,18 @@ int gs_debug_last_order(gs_ctx* ctx, gs_scene* scene, uint32_t* out_keys, uint32
  * (u32 bits).  The colour is evaluated only for splats that received a tile entry this frame;
  * rows of culled Gaussians and the colour of unbinned splats are undefined. */
 int gs_debug_last_records(gs_ctx* ctx, gs_scene* scene, float* out16, uint64_t capacity);
+/* Every composite slot of the last frame, as k_project (chunk 0) / k_chunk1 (chunk 1) wrote it:
+ * 16 words per slot: depth key, reference index (ref_quirks: draw rank, Gaussian), chunk, packed
+ * tile rect, record r0 (4 f32: centre x, y, axis 1 / |e1|^2 * sqrt(log2 e)), r1 (4 f32: axis 2 likewise,
+ * log2 opacity, pixel box x bits), colour r, g, b (f32) and the depth key bits.  out16 NULL: count only. */
+int gs_debug_last_slots(gs_ctx* ctx, gs_scene* scene, uint32_t* out16, uint64_t capacity, uint64_t* out_n);
+/* The per-tile lists the last frame's composite consumed (one-chunk frames only; else
+ * GS_ERR_UNSUPPORTED): out_ranges[2t], [2t+1] = [begin, end) of tile t (row-major in the frame's
+ * strip) in out_entries, whose entries are (depth key, reference index) pairs -- (draw rank,
+ * Gaussian) under ref_quirks -- in composite order.  NULL outputs: counts only. */
+int gs_debug_tile_lists(gs_ctx* ctx, gs_scene* scene, uint32_t* out_ranges, uint64_t ranges_capacity,
+                        uint32_t* out_entries, uint64_t entries_capacity, uint64_t* out_tiles,
+                        uint64_t* out_entries_n);
 
 #ifdef __cplusplus
 }

@@ -32,6 +32,7 @@
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
+#include <parallel/algorithm>
 #endif
 
 namespace {
@@ -337,13 +338,24 @@ int or_project(const void* aos, uint64_t n, int n_sh, const void* uni160, int W,
 
 // Oracle of webgpu-radix-sort (RS:541-654): stable ascending sort of u32 keys carrying u32
 // values.
+// A stable sort by key is a sort by (key, position): positions are distinct, so sorting the
+// packed 64-bit (key << 32 | position) with any (parallel) sort gives exactly the stable order.
 void or_stable_sort_pairs(uint32_t* keys, uint32_t* vals, uint64_t n) {
-    std::vector<uint64_t> idx(n);
-    std::iota(idx.begin(), idx.end(), 0);
-    std::stable_sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return keys[a] < keys[b]; });
-    std::vector<uint32_t> k2(n), v2(n);
-    for (uint64_t i = 0; i < n; ++i) { k2[i] = keys[idx[i]]; v2[i] = vals[idx[i]]; }
-    std::memcpy(keys, k2.data(), n * 4);
+    if (n > 0xFFFFFFFFull) return;
+    std::vector<uint64_t> kp(n);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) kp[i] = ((uint64_t)keys[i] << 32) | (uint64_t)i;
+#ifdef _OPENMP
+    __gnu_parallel::sort(kp.begin(), kp.end());
+#else
+    std::sort(kp.begin(), kp.end());
+#endif
+    std::vector<uint32_t> v2(n);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        keys[i] = (uint32_t)(kp[i] >> 32);
+        v2[i] = vals[kp[i] & 0xFFFFFFFFull];
+    }
     std::memcpy(vals, v2.data(), n * 4);
 }
 
@@ -375,6 +387,14 @@ int or_draw_order(const or_splat* sp, uint64_t n, int quirk, uint32_t* state_key
     return 0;
 }
 
+static int or_num_threads_internal() {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
 // Fragment + blend (src/simple_render.ts:169-200, :455-471) over the draw order.
 // accum_mode 0: fp32 dst; 1: dst rounded to fp16 after every blend (rgba16float target).
 // t_min: a pixel stops accepting splats once (1 - dst.a) < t_min (0 = never).
@@ -383,13 +403,30 @@ int or_composite(const or_splat* sp, const uint32_t* order, uint64_t n_order, in
                  int accum_mode, float t_min, float* out, uint64_t* blends_out) {
     std::memset(out, 0, sizeof(float) * 4 * (size_t)W * H);
     const int TR = (H + 15) / 16;
+    // per 16-row band: the draw positions whose pixel rect reaches it, in draw order (a band's
+    // pixels see exactly the splats in this list, in the same order as a walk over all of them)
+    std::vector<std::vector<uint32_t>> band_list(TR);
+    {
+        const int nth = or_num_threads_internal();
+        std::vector<std::vector<std::vector<uint32_t>>> part(nth, std::vector<std::vector<uint32_t>>(TR));
+        const uint64_t per = (n_order + nth - 1) / std::max(nth, 1);
+#pragma omp parallel for schedule(static, 1)
+        for (int t = 0; t < nth; ++t)
+            for (uint64_t o = t * per; o < std::min<uint64_t>(n_order, (t + 1) * per); ++o) {
+                const or_splat& s = sp[order[o]];
+                if (!s.visible) continue;
+                for (int b = s.rect[1] / 16; b <= std::min(s.rect[3] / 16, TR - 1); ++b) part[t][b].push_back((uint32_t)o);
+            }
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int b = 0; b < TR; ++b)
+            for (int t = 0; t < nth; ++t) band_list[b].insert(band_list[b].end(), part[t][b].begin(), part[t][b].end());
+    }
     uint64_t blends = 0;
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : blends)
     for (int band = 0; band < TR; ++band) {
         const int by0 = band * 16, by1 = std::min(by0 + 15, H - 1);
-        for (uint64_t o = 0; o < n_order; ++o) {
+        for (const uint32_t o : band_list[band]) {
             const or_splat& s = sp[order[o]];
-            if (!s.visible) continue;
             const int y0 = std::max(s.rect[1], by0), y1 = std::min(s.rect[3], by1);
             if (y0 > y1) continue;
             const float e1n = s.e1[0] * s.e1[0] + s.e1[1] * s.e1[1];

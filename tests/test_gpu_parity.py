@@ -1,7 +1,7 @@
 """GPU parity tests: the HIP renderer (through the C ABI) against the CPU oracle.
 
 Tolerances:
-  * depth keys and the sorted draw order: bit-exact;
+  * depth keys and the visible set: bit-exact (per-tile draw order: test_gpu_order.py);
   * projected floats: <= 1e-5 relative (colour/opacity) and <= 1e-3 px absolute (centre);
   * image vs the fp32 oracle: MSE < 1e-8 and max-abs <= 1e-3 outside <= 0.01 % pixels
     (pixels whose quad-edge / alpha-threshold test flips under last-ulp differences);
@@ -97,7 +97,8 @@ def test_projection_and_order(gpu_ctx, scene, cam):
     sp = orc.project(aos, n, nsh, u, W, H)
     vis = sp["visible"] == 1
     keys, idx = sc.last_order()
-    # visible set and draw order are bit-exact
+    # visible set and keys are bit-exact (last_order sorts the slots on the host; the order the
+    # composite used is checked per tile in test_gpu_order.py, and the slot records there too)
     ok_, ov_ = orc.stable_sort_pairs(sp["key"][vis], np.nonzero(vis)[0].astype(np.uint32))
     assert np.array_equal(idx, ov_)
     assert np.array_equal(keys, ok_)
@@ -179,8 +180,6 @@ def test_synthetic_1m_1080p(gpu_ctx):
     assert 0.4 * st["k_tiles"] <= st_gpu["k_entries"] <= st["k_tiles"]
     mse, bad, ok = image_close_fp32(img, ref, name="synth1m")
     assert ok, (mse, bad)
-    keys, idx = sc.last_order()
-    assert np.all(keys[1:] >= keys[:-1])
 
 
 def test_strips_match_full_image(gpu_ctx):
