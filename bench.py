@@ -8,14 +8,17 @@ bicycle PLY is not in this image, so the workload is the seeded synthetic stand-
 
 A step = one frame: uniform upload -> project/key -> depth sort -> bin -> tile sort -> composite
 (-> all-gather of the row strips at N > 1).  The scene is uploaded before timing (inputs resident
-in HBM).  Launch:  python bench.py [--gpus 1 --steps 50 --warmup 5]
+in HBM).  Launch:  python bench.py [--gpus N --steps 50 --warmup 5] [--config 4]
                    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Without torch.distributed.run, --gpus N > 1 starts the N ranks itself (one process per GPU, the
+same environment torch.distributed.run gives them) before anything touches a GPU.
 Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
-import re
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,8 +31,15 @@ import gsplat_amd as gs  # noqa: E402
 from gsplat_amd.strips import strip_geometry  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 4 cycles at 2.4 GHz
-VALU_PEAK = 256 * 4 * 2.4e9 / 4  # wave instructions / s
+# VALU issue peak: 256 CUs x 4 SIMD-32s, one wave64 VALU instruction per SIMD every 2 cycles at
+# 2.4 GHz once two or more waves share a SIMD (MI355X_MICROARCH.md "Wave scheduling", v_fma_f32 row);
+# transcendentals (v_exp_f32) issue at a quarter of that rate
+VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave instructions / s
+
+CONFIGS = {  # BASELINE.json configs the bench can run (index: N, W, H, seed)
+    3: (6_100_000, 1920, 1080, 6),   # the headline: bicycle ~6 M stand-in at 1080p
+    4: (50_000_000, 3840, 2160, 50),  # synthetic 50 M at 4K (the HBM-roofline configuration)
+}
 
 
 def algorithmic_bytes(stage, n, n_vis, k, W, H, n_chunk0=None):
@@ -79,16 +89,51 @@ def frame_bytes(n, n_vis, k, W, H):
     return 236 * n + 148 * n_vis + 48 * k + 16 * W * H
 
 
-def cpu_baseline(aos, n, W, H, u):
-    """The oracle (CPU restatement of the reference semantics) on the same frame, host cores."""
+def cpu_baseline(aos, n, W, H, u, budget_s=10.0, max_frames=10):
+    """The oracle (CPU restatement of the reference semantics) on the same frame, host cores:
+    full frames until about `budget_s` of CPU wall time (at most max_frames), the median frame."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as orc
-    t0 = time.perf_counter()
-    _, st = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=1e-4)
-    dt = time.perf_counter() - t0
+    times = []
+    t_all = time.perf_counter()
+    while len(times) < max_frames and (not times or time.perf_counter() - t_all < budget_s):
+        t0 = time.perf_counter()
+        orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=1e-4)
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
     return {"value": n / dt / 1e6, "unit": "Msplats/s", "cores": orc.num_threads(), "kind": "port",
-            "sample": "1 full frame of the same %d-Gaussian %dx%d workload (project, std::stable_sort, "
-                      "composite; %.1f s wall)" % (n, W, H, dt)}
+            "sample": "median of %d full frames of the same %d-Gaussian %dx%d workload (project, stable sort, "
+                      "composite; %.2f s per frame, %.1f s total)" % (len(times), n, W, H, dt,
+                                                                       time.perf_counter() - t_all)}
+
+
+def orbit_uniforms(W, H, k, period=60):
+    """A moving camera for the orbit loop: at the origin, yaw swinging +-25 deg and pitch +-8 deg
+    around the bench view (-z), a new view every frame; part of the screen leaves the scene's
+    frustum, so tiles go unsaturated and the chunk split moves."""
+    a = 2 * np.pi * k / period
+    yaw, pitch = np.radians(25.0) * np.sin(a), np.radians(8.0) * np.sin(2 * a)
+    target = (np.sin(yaw) * np.cos(pitch), np.sin(pitch), -np.cos(yaw) * np.cos(pitch))
+    view = gs.look_at((0.0, 0.0, 0.0), target)
+    return gs.pack_uniforms(view, gs.perspective(1.04719755, W / H, 0.03, 1000.0), focal=(W, H))
+
+
+def spawn_ranks(n, cmd=None):
+    """torch.distributed.run's job, for `python bench.py --gpus N`: N rank processes on this node
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), started before this process touches a GPU; rank
+    0's JSON line is the output.  Returns the exit status (the worst rank's)."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def main():
@@ -96,22 +141,31 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=6_100_000)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--seed", type=int, default=6)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i]: 3 = 6.1 M at 1080p (default), 4 = 50 M at 4K")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the latency / orbit / stage loops")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (args.gpus, args.gpus))
-    W, H, N = args.width, args.height, args.n
+        sys.exit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    N0, W0, H0, S0 = CONFIGS[args.config]
+    N = args.n or N0
+    W, H = args.width or W0, args.height or H0
+    seed = args.seed if args.seed is not None else S0
 
-    launched = "WORLD_SIZE" in os.environ  # torch.distributed.run: the RCCL path, even at N = 1
+    # torch.distributed.run (or spawn_ranks): RCCL all-gather of the strips at N > 1; a single rank
+    # renders the whole image, and gathers nothing
+    launched = "WORLD_SIZE" in os.environ
     dist = None
     if launched:
         import torch
@@ -119,7 +173,7 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    aos = gs.synth_aos(N, args.seed, W, H)
+    aos = gs.synth_aos(N, seed, W, H)
     u = gs.bench_uniforms(W, H)
     ctx = gs.Context(local_rank)
     scene = gs.Scene(ctx, aos, N, 16)
@@ -140,10 +194,13 @@ def main():
         stream = torch.cuda.current_stream()
         pipe = StripPipeline(rows_padded, W, dtype=torch.float16)  # gather t beside render t+1
 
-        def frame():
+        def frame_u(uu):
             strip = pipe.next_strip()
-            scene.render_device(u, W, H, strip.data_ptr(), strip_bytes, stream.cuda_stream, cur["opts"])
+            scene.render_device(uu, W, H, strip.data_ptr(), strip_bytes, stream.cuda_stream, cur["opts"])
             pipe.submit()
+
+        def frame():
+            frame_u(u)
 
         def sync():
             pipe.finish()
@@ -152,8 +209,11 @@ def main():
     else:
         buf = gs.DeviceBuffer(H * W * 8)
 
+        def frame_u(uu):
+            scene.render_device(uu, W, H, buf.ptr.value, buf.nbytes, None, cur["opts"])
+
         def frame():
-            scene.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, cur["opts"])
+            frame_u(u)
 
         def sync():
             ctx.sync()
@@ -169,6 +229,7 @@ def main():
     sync()
     elapsed = time.perf_counter() - t_start
     ms_composite_live = ctx.timings()["ms_composite"]  # HIP events over the timed region
+
     # stage breakdown (not timed for `value`)
     cur["opts"] = opts_stage
     ctx.timings_reset()
@@ -178,6 +239,37 @@ def main():
     st = ctx.timings()
     st["ms_composite_stage_pass"] = st["ms_composite"]
     st["ms_composite"] = ms_composite_live
+    extra = {}
+    if not args.no_extra:
+        # median single-frame time of 50 frames (each frame waited for, no overlap)
+        cur["opts"] = gs.make_opts(strip_index=rank, strip_count=world, out_format=gs.GS_OUT_RGBA_F16)
+        lat = []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            frame()
+            sync()
+            lat.append(time.perf_counter() - t0)
+        extra["latency_ms_median"] = round(float(np.median(lat)) * 1e3, 4)
+        # a moving camera: a new view every frame (frames in flight, like the headline loop)
+        uo = [orbit_uniforms(W, H, k) for k in range(args.steps)]
+        for k in range(args.warmup):
+            frame_u(uo[k % len(uo)])
+        sync()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            frame_u(uo[k])
+        sync()
+        el = time.perf_counter() - t0
+        st_o = ctx.timings()
+        if launched and world > 1:  # the slowest rank's times
+            import torch
+            tt = torch.tensor([el, extra["latency_ms_median"]], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el, extra["latency_ms_median"] = float(tt[0]), round(float(tt[1]), 4)
+        extra["orbit"] = {"fps": round(args.steps / el, 2), "ms_per_step": round(el / args.steps * 1e3, 4),
+                          "value_msplats": round(N * args.steps / el / 1e6, 3),
+                          "tiles_unsaturated_last": st_o["tiles_unsaturated"], "k_chunk1_last": st_o["k_chunk1"],
+                          "camera": "origin, yaw +-25 deg, pitch +-8 deg, period 60 frames"}
     # one untimed one-chunk frame for the exact visible count and K of SURVEY 8d's byte model
     # (with a chunk split the pipeline never projects the splats past it)
     cur["opts"] = gs.make_opts(strip_index=rank, strip_count=world, chunk_fraction=1.0,
@@ -214,7 +306,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "Msplats/s at 1920x1080, 6.1 M Gaussians (synthetic bicycle stand-in)",
+            "metric": "Msplats/s at %dx%d, %s Gaussians (%s)" % (
+                W, H, "%.1f M" % (N / 1e6), "synthetic bicycle stand-in" if args.config == 3 else "synthetic"),
             "value": round(value, 3),
             "unit": "Msplats/s",
             "n_gpus": world,
@@ -226,10 +319,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY §8d generator, splitmix64 seed %d; bicycle PLY absent); "
-                    "output RGBA f16 (the reference's rgba16float framebuffer)" % args.seed,
-            "config": {"workload": "configs[3]: %d Gaussians (SH deg 3) at %dx%d, lookAt([0,0,0],[0,0,-1]) "
-                                   "perspective(60deg,W/H,0.03,1000)" % (N, W, H),
+            "data": "synthetic (SURVEY §8d generator, splitmix64 seed %d%s); "
+                    "output RGBA f16 (the reference's rgba16float framebuffer)" % (
+                        seed, "; bicycle PLY absent" if args.config == 3 else ""),
+            "config": {"workload": "configs[%d]: %d Gaussians (SH deg 3) at %dx%d, lookAt([0,0,0],[0,0,-1]) "
+                                   "perspective(60deg,W/H,0.03,1000)" % (args.config, N, W, H),
                        "n_gaussians": N, "width": W, "height": H,
                        "parallelism": "row-strips x%d + all-gather" % world if world > 1 else "single GPU"},
             # per-stage HIP-event times from the separate timing=1 loop (events between stages add
@@ -265,6 +359,7 @@ def main():
                                "formula": "236N + 148N_vis + 48K + 16WH (SURVEY 8d)"},
             "cpu_baseline": None,
         }
+        out.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(aos, N, W, H, u)
         print(json.dumps(out), flush=True)

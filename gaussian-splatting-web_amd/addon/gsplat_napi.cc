@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/gsplat.h"
 
@@ -139,12 +140,28 @@ napi_value DeviceCount(napi_env env, napi_callback_info) {
     return r;
 }
 
+// ctxCreate(deviceIndex | [device, ...]): one device, or a device group (row strips on each, one
+// RCCL all-gather; gs_ctx_create)
 napi_value CtxCreate(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     get_args(env, info, 1, argv);
-    const int dev = (int)num(env, argv[0], 0);
+    std::vector<int> devs;
+    bool is_array = false;
+    NAPI_OK(napi_is_array(env, argv[0], &is_array));
+    if (is_array) {
+        uint32_t len = 0;
+        NAPI_OK(napi_get_array_length(env, argv[0], &len));
+        for (uint32_t k = 0; k < len; ++k) {
+            napi_value e;
+            NAPI_OK(napi_get_element(env, argv[0], k, &e));
+            devs.push_back((int)num(env, e, -1));
+        }
+        if (devs.empty()) return throw_gs(env, GS_ERR_INVALID, "ctxCreate: empty device list");
+    } else {
+        devs.push_back((int)num(env, argv[0], 0));
+    }
     gs_ctx* c = nullptr;
-    const int rc = gs_ctx_create(&dev, 1, &c);
+    const int rc = gs_ctx_create(devs.data(), (int)devs.size(), &c);
     if (rc) return throw_gs(env, rc, "gs_ctx_create");
     napi_value r;
     NAPI_OK(napi_create_external(env, c, nullptr, nullptr, &r));

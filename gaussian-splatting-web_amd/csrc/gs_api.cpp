@@ -10,6 +10,7 @@
 // per-frame buffers, each with its own stream, so consecutive frames overlap on the GPU.
 // Reference call stack replaced: Renderer.animate/draw (src/renderer.ts:332-387, :301-330).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <array>
@@ -20,6 +21,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gsplat.h"
@@ -140,6 +142,15 @@ struct gs_ctx {
     gs_stats stats{};
     gs_scene* last_scene = nullptr;
     std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
+    // A device group (gs_ctx_create with ndev > 1): one single-device member context per entry;
+    // member g renders row strip g of G into its slice of a G-strip buffer on its device, then one
+    // RCCL all-gather (ncclCommInitAll over distinct devices; in place) fills every member's
+    // buffer.  A device list with repeats (tests on one GPU) gathers with peer copies instead.
+    std::vector<gs_ctx*> members;
+    std::vector<ncclComm_t> comms;
+    std::vector<void*> gfull;          // [member] the gathered image buffer (G strips, padded)
+    std::vector<size_t> gfull_bytes;
+    std::vector<hipEvent_t> gev;       // [member] strip rendered (peer-copy gather)
 };
 
 // Everything one frame writes.  kFrameSets sets, used by frames in turn, each with its own stream
@@ -219,12 +230,14 @@ struct gs_scene {
     PartBound* qbounds = nullptr;
     const uint32_t* qdraw = nullptr;              // [n] Gaussian of each draw rank, last ref_quirks frame
     bool last_quirk = false;                      // the last frame ran with ref_quirks
+    std::vector<gs_scene*> members;               // a device group's scene: one replica per member
 };
 
 static constexpr size_t kHistWords = kHistShards * 256;
 // Largest scene for which the reference's init-sort dispatch is valid: max(N/8, 8) workgroups
 // <= 65535 (src/renderer.ts:306; beyond it WebGPU rejects the dispatch and no key is written).
 static constexpr uint64_t kQuirkMaxN = 65535ull * 8;
+static constexpr int kMaxGroup = 64;  // devices per context
 // radix partition sizes (items per thread x 256): small partitions keep every CU busy on the
 // short depth sorts; the tile-id sort is long enough for 4096-element partitions
 // radix partition size of gs_debug_sort_pairs (items per thread x 256)
@@ -637,6 +650,8 @@ static void validate_render_args(gs_ctx* c, gs_scene* s, const void* uni, int W,
                                  const gs_opts* o) {
     if (!c || !s || !uni) throw GsError(GS_ERR_INVALID, "null ctx/scene/uniforms");
     if (s->ctx != c) throw GsError(GS_ERR_INVALID, "scene belongs to another context");
+    if (!c->members.empty() && o && o->strip_count != 1)
+        throw GsError(GS_ERR_INVALID, "a device group renders its row strips itself (strip_count must be 1)");
     if (W <= 0 || H <= 0 || W > 65535 || H > 65535) throw GsError(GS_ERR_INVALID, "bad image size");
     if (o) {
         if (o->strip_count < 1 || o->strip_index < 0 || o->strip_index >= o->strip_count)
@@ -758,6 +773,65 @@ static void quirk_prepare(gs_scene* s, const float* uni, hipStream_t st) {
     s->qdraw = r.second;
 }
 
+// A device group's frame (gs_ctx::members): member g renders row strip g of G into slice g of its
+// G-strip buffer, then the gather fills member 0's buffer (RCCL: one in-place all-gather, every
+// member's buffer; repeated devices: peer copies into member 0's).  Enqueue only: the image is on
+// member 0, ordered on st0 (the caller's stream there, or member 0's own).  Returns that buffer.
+static void* render_group(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o, hipStream_t st0) {
+    const int G = (int)c->members.size();
+    int tb, te, rp;
+    strip_geometry(H, 0, G, tb, te, rp);
+    const size_t bpp = o.out_format == GS_OUT_RGBA_F16 ? 8 : 16;
+    const size_t strip_bytes = (size_t)rp * W * bpp, full_bytes = strip_bytes * G;
+    auto stream_of = [&](int g) { return g == 0 ? st0 : c->members[g]->stream; };
+    for (int g = 0; g < G; ++g) {
+        gs_ctx* m = c->members[g];
+        HIPCHK(hipSetDevice(m->device));
+        if (c->gfull_bytes[g] < full_bytes) {
+            if (c->gfull[g]) {
+                HIPCHK(hipDeviceSynchronize());
+                HIPCHK(hipFree(c->gfull[g]));
+                c->gfull[g] = nullptr;
+                c->gfull_bytes[g] = 0;
+            }
+            HIPCHK(hipMalloc(&c->gfull[g], full_bytes));
+            c->gfull_bytes[g] = full_bytes;
+        }
+        gs_opts og = o;
+        og.strip_index = g;
+        og.strip_count = G;
+        render_frame(m, s->members[g], uni, W, H, og, (char*)c->gfull[g] + g * strip_bytes, stream_of(g));
+    }
+    if (!c->comms.empty()) {
+        ncclResult_t r = ncclGroupStart();
+        for (int g = 0; g < G && r == ncclSuccess; ++g)
+            r = ncclAllGather((char*)c->gfull[g] + g * strip_bytes, c->gfull[g], strip_bytes, ncclUint8, c->comms[g],
+                              stream_of(g));
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess || r2 != ncclSuccess)
+            throw GsError(GS_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    } else {
+        for (int g = 1; g < G; ++g) {
+            HIPCHK(hipSetDevice(c->members[g]->device));
+            HIPCHK(hipEventRecord(c->gev[g], stream_of(g)));
+            HIPCHK(hipSetDevice(c->members[0]->device));
+            HIPCHK(hipStreamWaitEvent(st0, c->gev[g], 0));
+            HIPCHK(hipMemcpyPeerAsync((char*)c->gfull[0] + g * strip_bytes, c->members[0]->device,
+                                      (char*)c->gfull[g] + g * strip_bytes, c->members[g]->device, strip_bytes, st0));
+        }
+        // member g's next frame rewrites its slice only after this frame's copy of it
+        HIPCHK(hipSetDevice(c->members[0]->device));
+        HIPCHK(hipEventRecord(c->gev[0], st0));
+        for (int g = 1; g < G; ++g) {
+            HIPCHK(hipSetDevice(c->members[g]->device));
+            HIPCHK(hipStreamWaitEvent(stream_of(g), c->gev[0], 0));
+        }
+    }
+    HIPCHK(hipSetDevice(c->members[0]->device));
+    c->last_scene = s;
+    return c->gfull[0];
+}
+
 extern "C" {
 
 int gs_abi_version(void) { return GS_ABI_VERSION; }
@@ -785,27 +859,46 @@ void gs_opts_default(gs_opts* o) {
     o->chunk_fraction = 0.0f;
 }
 
+static gs_ctx* create_single(int dev);
+
 int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
     return guarded([&] {
         if (!out) throw GsError(GS_ERR_INVALID, "null out");
         *out = nullptr;
-        if (ndev != 1 && !(ndev == 0 && devices == nullptr))
-            throw GsError(GS_ERR_UNSUPPORTED, "one device per context (use one process per GPU)");
+        if (ndev < 0 || ndev > kMaxGroup || (ndev > 0 && !devices) || (ndev == 0 && devices))
+            throw GsError(GS_ERR_INVALID, "bad device list");
         int count = 0;
         if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
             throw GsError(GS_ERR_NO_DEVICE, "no HIP device available");
-        const int dev = devices ? devices[0] : 0;
-        if (dev < 0 || dev >= count) throw GsError(GS_ERR_INVALID, "device index out of range");
-        HIPCHK(hipSetDevice(dev));
+        for (int g = 0; g < std::max(ndev, 1); ++g) {
+            const int dev = devices ? devices[g] : 0;
+            if (dev < 0 || dev >= count) throw GsError(GS_ERR_INVALID, "device index out of range");
+        }
+        if (ndev <= 1) {
+            *out = create_single(devices ? devices[0] : 0);
+            return GS_OK;
+        }
         gs_ctx* c = new gs_ctx();
-        c->device = dev;
+        c->device = devices[0];
         try {
-            int cus = 0;
-            HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            if (cus > 0) c->num_cus = cus;
-            HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-            for (auto& f : c->fe)
-                for (auto& e : f.ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+            for (int g = 0; g < ndev; ++g) c->members.push_back(create_single(devices[g]));
+            std::vector<int> d(devices, devices + ndev);
+            std::sort(d.begin(), d.end());
+            if (std::adjacent_find(d.begin(), d.end()) == d.end()) {  // distinct devices: RCCL
+                c->comms.assign(ndev, nullptr);
+                const ncclResult_t r = ncclCommInitAll(c->comms.data(), ndev, devices);
+                if (r != ncclSuccess) {
+                    c->comms.clear();
+                    throw GsError(GS_ERR_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+                }
+            }
+            c->gfull.assign(ndev, nullptr);
+            c->gfull_bytes.assign(ndev, 0);
+            c->gev.assign(ndev, nullptr);
+            for (int g = 0; g < ndev; ++g) {
+                HIPCHK(hipSetDevice(devices[g]));
+                HIPCHK(hipEventCreateWithFlags(&c->gev[g], hipEventDisableTiming));
+            }
         } catch (...) {
             gs_ctx_destroy(c);
             throw;
@@ -815,8 +908,40 @@ int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
     });
 }
 
+static gs_ctx* create_single(int dev) {
+    HIPCHK(hipSetDevice(dev));
+    gs_ctx* c = new gs_ctx();
+    c->device = dev;
+    try {
+        int cus = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        if (cus > 0) c->num_cus = cus;
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        for (auto& f : c->fe)
+            for (auto& e : f.ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    } catch (...) {
+        gs_ctx_destroy(c);
+        throw;
+    }
+    return c;
+}
+
 void gs_ctx_destroy(gs_ctx* c) {
     if (!c) return;
+    if (!c->members.empty()) {
+        while (!c->scenes.empty()) gs_scene_free(c->scenes.back());
+        for (size_t g = 0; g < c->members.size(); ++g) {
+            (void)hipSetDevice(c->members[g]->device);
+            (void)hipDeviceSynchronize();
+            if (g < c->gfull.size() && c->gfull[g]) (void)hipFree(c->gfull[g]);
+            if (g < c->gev.size() && c->gev[g]) (void)hipEventDestroy(c->gev[g]);
+        }
+        for (ncclComm_t m : c->comms)
+            if (m) (void)ncclCommDestroy(m);
+        for (gs_ctx* m : c->members) gs_ctx_destroy(m);
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     while (!c->scenes.empty()) gs_scene_free(c->scenes.back());
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -835,6 +960,31 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
         if (n_sh != 1 && n_sh != 4 && n_sh != 9 && n_sh != 16)
             throw GsError(GS_ERR_UNSUPPORTED, "n_sh_coeffs must be 1, 4, 9 or 16");
         if (n > (1ull << 28)) throw GsError(GS_ERR_UNSUPPORTED, "scene larger than 2^28 Gaussians");
+        if (!c->members.empty()) {  // a device group: one replica per member, uploaded concurrently
+            const size_t G = c->members.size();
+            gs_scene* s = new gs_scene();
+            s->ctx = c;
+            s->n = n;
+            s->n_sh = n_sh;
+            s->members.assign(G, nullptr);
+            std::vector<int> rc(G, GS_OK);
+            std::vector<std::string> msg(G);
+            std::vector<std::thread> th;
+            for (size_t g = 0; g < G; ++g)
+                th.emplace_back([&, g] {
+                    rc[g] = gs_scene_upload(c->members[g], aos, n, n_sh, &s->members[g]);
+                    if (rc[g] != GS_OK) msg[g] = gs_last_error();
+                });
+            for (auto& t : th) t.join();
+            for (size_t g = 0; g < G; ++g)
+                if (rc[g] != GS_OK) {
+                    gs_scene_free(s);
+                    throw GsError(rc[g], "device " + std::to_string(c->members[g]->device) + ": " + msg[g]);
+                }
+            c->scenes.push_back(s);
+            *out = s;
+            return GS_OK;
+        }
         HIPCHK(hipSetDevice(c->device));
         gs_scene* s = new gs_scene();
         s->ctx = c;
@@ -916,6 +1066,17 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
 
 void gs_scene_free(gs_scene* s) {
     if (!s) return;
+    if (!s->members.empty()) {
+        for (gs_scene* m : s->members)
+            if (m) gs_scene_free(m);
+        if (s->ctx) {
+            auto& v = s->ctx->scenes;
+            v.erase(std::remove(v.begin(), v.end(), s), v.end());
+            if (s->ctx->last_scene == s) s->ctx->last_scene = nullptr;
+        }
+        delete s;
+        return;
+    }
     if (s->ctx) {
         (void)hipSetDevice(s->ctx->device);
         (void)hipStreamSynchronize(s->ctx->stream);
@@ -966,6 +1127,15 @@ void gs_scene_free(gs_scene* s) {
 
 uint64_t gs_scene_count(const gs_scene* s) { return s ? s->n : 0; }
 
+int gs_ctx_info(const gs_ctx* c, int* out_ndev, int* out_gather) {
+    return guarded([&] {
+        if (!c) throw GsError(GS_ERR_INVALID, "null ctx");
+        if (out_ndev) *out_ndev = c->members.empty() ? 1 : (int)c->members.size();
+        if (out_gather) *out_gather = c->members.empty() ? GS_GATHER_NONE : !c->comms.empty() ? GS_GATHER_RCCL : GS_GATHER_PEER_COPY;
+        return GS_OK;
+    });
+}
+
 int gs_strip_rows(int H, int si, int sc, int* row0, int* rows_padded) {
     return guarded([&] {
         if (H <= 0 || sc < 1 || si < 0 || si >= sc || !row0 || !rows_padded)
@@ -987,6 +1157,15 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
         if (opts) o = *opts;
         if (!out_dev) throw GsError(GS_ERR_INVALID, "null output");
         if (out_bytes < out_bytes_for(W, H, o)) throw GsError(GS_ERR_INVALID, "output buffer too small");
+        if (!c->members.empty()) {  // the image (H rows) into out_dev on the first device
+            for (gs_scene* m : s->members)
+                if (m->pending_err & (kErrOverflow | kErrBarrier)) check_frame_errors(m);
+            gs_ctx* m0 = c->members[0];
+            hipStream_t st0 = stream ? (hipStream_t)stream : m0->stream;
+            void* full = render_group(c, s, (const float*)uni, W, H, o, st0);
+            HIPCHK(hipMemcpyAsync(out_dev, full, out_bytes_for(W, H, o), hipMemcpyDeviceToDevice, st0));
+            return GS_OK;
+        }
         HIPCHK(hipSetDevice(c->device));
         if (s->pending_err & (kErrOverflow | kErrBarrier)) check_frame_errors(s);
         hipStream_t st = stream ? (hipStream_t)stream : c->stream;
@@ -1011,6 +1190,7 @@ int gs_present_device(gs_ctx* c, const void* fb_dev, int fb_format, int W, int H
         }
         if (out_bytes < px_bytes * (uint64_t)W * (uint64_t)H) throw GsError(GS_ERR_INVALID, "output buffer too small");
         if (fb_dev == out_dev) throw GsError(GS_ERR_INVALID, "present cannot run in place");
+        if (!c->members.empty()) c = c->members[0];  // a group's image lives on its first device
         HIPCHK(hipSetDevice(c->device));
         launch_present(fb_dev, fb_format == GS_OUT_RGBA_F16, W, H, out_format, out_dev,
                        stream ? (hipStream_t)stream : c->stream);
@@ -1025,8 +1205,32 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
         gs_opts o;
         gs_opts_default(&o);
         if (opts) o = *opts;
-        HIPCHK(hipSetDevice(c->device));
         const size_t bytes = out_bytes_for(W, H, o);
+        if (!c->members.empty()) {
+            for (int attempt = 0;; ++attempt) {
+                void* full = render_group(c, s, (const float*)uni, W, H, o, c->members[0]->stream);
+                bool overflow = false;
+                for (size_t g = 0; g < c->members.size(); ++g) {
+                    HIPCHK(hipSetDevice(c->members[g]->device));
+                    HIPCHK(hipDeviceSynchronize());
+                    gs_scene* m = s->members[g];
+                    collect_stats(m, true);
+                    if (m->pending_err & kErrBarrier) check_frame_errors(m);
+                    if (m->pending_err & kErrOverflow) {
+                        overflow = true;
+                        m->pending_err = 0;
+                        for (FrameSet& F : m->fs) ensure_tile_capacity(F, m->last.k_total);
+                    }
+                }
+                HIPCHK(hipSetDevice(c->members[0]->device));
+                if (!overflow) {
+                    if (out_host) HIPCHK(hipMemcpy(out_host, full, bytes, hipMemcpyDeviceToHost));
+                    return GS_OK;
+                }
+                if (attempt >= 2) throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded");
+            }
+        }
+        HIPCHK(hipSetDevice(c->device));
         ensure_out(c, bytes);
         for (int attempt = 0;; ++attempt) {
             render_frame(c, s, (const float*)uni, W, H, o, c->d_out, c->stream);
@@ -1046,6 +1250,13 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
 int gs_sync(gs_ctx* c) {
     return guarded([&] {
         if (!c) throw GsError(GS_ERR_INVALID, "null ctx");
+        if (!c->members.empty()) {
+            for (gs_ctx* m : c->members) {
+                const int rc = gs_sync(m);
+                if (rc != GS_OK) throw GsError(rc, gs_last_error());
+            }
+            return GS_OK;
+        }
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipDeviceSynchronize());
@@ -1057,6 +1268,35 @@ int gs_sync(gs_ctx* c) {
 int gs_timings(gs_ctx* c, gs_stats* out) {
     return guarded([&] {
         if (!c || !out) throw GsError(GS_ERR_INVALID, "null argument");
+        if (!c->members.empty()) {  // counts summed over the strips, stage times the slowest strip's
+            gs_stats a{};
+            for (size_t g = 0; g < c->members.size(); ++g) {
+                gs_stats m{};
+                const int rc = gs_timings(c->members[g], &m);
+                if (rc != GS_OK) throw GsError(rc, gs_last_error());
+                if (g == 0) {
+                    a = m;
+                    continue;
+                }
+                a.n_vis += m.n_vis;
+                a.k_entries += m.k_entries;
+                a.k_total += m.k_total;
+                a.tiles_unsaturated += m.tiles_unsaturated;
+                a.k_chunk0 += m.k_chunk0;
+                a.k_chunk1 += m.k_chunk1;
+                a.wide_chunk0 += m.wide_chunk0;
+                a.wide_chunk1 += m.wide_chunk1;
+                a.tile_row_end = std::max(a.tile_row_end, m.tile_row_end);
+                for (float* f : {&a.ms_total, &a.ms_project, &a.ms_sort, &a.ms_bin, &a.ms_tile_sort, &a.ms_ranges,
+                                 &a.ms_composite, &a.ms_other}) {
+                    const float v = *(const float*)((const char*)&m + ((const char*)f - (const char*)&a));
+                    *f = std::max(*f, v);
+                }
+            }
+            a.tile_row_begin = 0;
+            *out = a;
+            return GS_OK;
+        }
         HIPCHK(hipSetDevice(c->device));
         for (int k = 1; k <= kFrameSets; ++k) harvest(c, c->fe[(c->fe_cur + k) % kFrameSets]);  // oldest first
         gs_stats st = c->stats;
@@ -1093,6 +1333,11 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
 int gs_timings_reset(gs_ctx* c) {
     return guarded([&] {
         if (!c) throw GsError(GS_ERR_INVALID, "null ctx");
+        for (gs_ctx* m : c->members) {
+            const int rc = gs_timings_reset(m);
+            if (rc != GS_OK) throw GsError(rc, gs_last_error());
+        }
+        if (!c->members.empty()) return GS_OK;
         HIPCHK(hipSetDevice(c->device));
         harvest(c, c->fe[0]);
         harvest(c, c->fe[1]);
@@ -1106,6 +1351,7 @@ int gs_timings_reset(gs_ctx* c) {
 
 int gs_debug_sort_pairs(gs_ctx* c, uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit, int end_bit) {
     return guarded([&] {
+        if (c && !c->members.empty()) throw GsError(GS_ERR_UNSUPPORTED, "debug exports take a single-device context");
         if (!c || (!keys && n) || (!vals && n)) throw GsError(GS_ERR_INVALID, "null argument");
         if (begin_bit < 0 || end_bit > 32 || begin_bit >= end_bit) throw GsError(GS_ERR_INVALID, "bad bit range");
         if (n >= 0xFFFFFFFFull) throw GsError(GS_ERR_UNSUPPORTED, "n too large");
@@ -1169,6 +1415,7 @@ static std::vector<std::array<uint32_t, 4>> frame_slots(gs_scene* s) {
 int gs_debug_last_order(gs_ctx* c, gs_scene* s, uint32_t* out_keys, uint32_t* out_index, uint64_t cap,
                         uint64_t* out_n) {
     return guarded([&] {
+        if (c && !c->members.empty()) throw GsError(GS_ERR_UNSUPPORTED, "debug exports take a single-device context");
         if (!c || !s || !out_n) throw GsError(GS_ERR_INVALID, "null argument");
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         HIPCHK(hipSetDevice(c->device));
@@ -1189,6 +1436,7 @@ int gs_debug_last_order(gs_ctx* c, gs_scene* s, uint32_t* out_keys, uint32_t* ou
 
 int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
     return guarded([&] {
+        if (c && !c->members.empty()) throw GsError(GS_ERR_UNSUPPORTED, "debug exports take a single-device context");
         if (!c || !s || !out16) throw GsError(GS_ERR_INVALID, "null argument");
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         if (s->last_quirk) throw GsError(GS_ERR_UNSUPPORTED, "per-Gaussian records of a ref_quirks frame "
@@ -1234,6 +1482,7 @@ int gs_debug_last_records(gs_ctx* c, gs_scene* s, float* out16, uint64_t cap) {
 
 int gs_debug_last_slots(gs_ctx* c, gs_scene* s, uint32_t* out16, uint64_t cap, uint64_t* out_n) {
     return guarded([&] {
+        if (c && !c->members.empty()) throw GsError(GS_ERR_UNSUPPORTED, "debug exports take a single-device context");
         if (!c || !s || !out_n) throw GsError(GS_ERR_INVALID, "null argument");
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         HIPCHK(hipSetDevice(c->device));
@@ -1263,6 +1512,7 @@ int gs_debug_last_slots(gs_ctx* c, gs_scene* s, uint32_t* out16, uint64_t cap, u
 int gs_debug_tile_lists(gs_ctx* c, gs_scene* s, uint32_t* out_ranges, uint64_t ranges_cap, uint32_t* out_entries,
                         uint64_t entries_cap, uint64_t* out_tiles, uint64_t* out_entries_n) {
     return guarded([&] {
+        if (c && !c->members.empty()) throw GsError(GS_ERR_UNSUPPORTED, "debug exports take a single-device context");
         if (!c || !s || !out_tiles || !out_entries_n) throw GsError(GS_ERR_INVALID, "null argument");
         if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
         HIPCHK(hipSetDevice(c->device));

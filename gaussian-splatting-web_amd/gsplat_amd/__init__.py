@@ -25,7 +25,7 @@ GS_OK, GS_ERR_INVALID, GS_ERR_NO_DEVICE, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPOR
 
 # every symbol include/gsplat.h declares
 EXPORTED_SYMBOLS = (
-    "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy",
+    "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy", "gs_ctx_info",
     "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows",
     "gs_render", "gs_render_device", "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
     "gs_present_device", "gs_encode_png", "gs_look_at",
@@ -100,6 +100,7 @@ def lib():
         L.gs_ctx_create.argtypes = [P, I, ctypes.POINTER(P)]
         L.gs_ctx_destroy.argtypes = [P]
         L.gs_ctx_destroy.restype = None
+        L.gs_ctx_info.argtypes = [P, ctypes.POINTER(I), ctypes.POINTER(I)]
         L.gs_scene_upload.argtypes = [P, P, U64, I, ctypes.POINTER(P)]
         L.gs_scene_free.argtypes = [P]
         L.gs_scene_free.restype = None
@@ -243,15 +244,26 @@ def make_opts(accum=GS_ACCUM_FP32, out_format=GS_OUT_RGBA_F32, t_min=1e-4, strip
 
 
 # ------------------------------------------------------------------ context / scene / render
+GATHER_KINDS = {0: "none", 1: "rccl", 2: "peer_copy"}
+
+
 class Context:
-    """GpuContext equivalent: one HIP device."""
+    """GpuContext equivalent: one HIP device, or a device group (a list of devices: row strips on
+    each, one RCCL all-gather; see gs_ctx_create)."""
 
     def __init__(self, device=0):
         self.handle = ctypes.c_void_p()
         self.scenes = weakref.WeakSet()
-        dev = (ctypes.c_int * 1)(device)
-        _check(lib().gs_ctx_create(dev, 1, ctypes.byref(self.handle)))
+        devs = list(device) if isinstance(device, (list, tuple)) else [int(device)]
+        dev = (ctypes.c_int * len(devs))(*devs)
+        _check(lib().gs_ctx_create(dev, len(devs), ctypes.byref(self.handle)))
         _LIVE.add(self)
+
+    def info(self):
+        """(devices driven, gather kind: 'none' | 'rccl' | 'peer_copy')."""
+        nd, g = ctypes.c_int(), ctypes.c_int()
+        _check(lib().gs_ctx_info(self.handle, ctypes.byref(nd), ctypes.byref(g)))
+        return nd.value, GATHER_KINDS[g.value]
 
     def close(self):
         # scenes first: the C side frees attached scenes with the context anyway, but the

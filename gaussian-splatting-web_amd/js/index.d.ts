@@ -17,11 +17,12 @@ export interface RenderOptions {
 
 export declare class GpuContext {
     gpu: {api: 'hip'};
-    adapter: {deviceIndex: number; deviceCount: number} | null;
+    adapter: {deviceIndex: number | number[]; deviceCount: number} | null;
     device: unknown | null;  // native gs_ctx handle
-    constructor(gpu: {api: 'hip'}, adapter: {deviceIndex: number; deviceCount: number}, device: unknown);
+    constructor(gpu: {api: 'hip'}, adapter: {deviceIndex: number | number[]; deviceCount: number}, device: unknown);
     /** Rejects with a string when no HIP device exists (src/gpu_context.ts:12-26). */
-    static create(deviceIndex?: number): Promise<GpuContext>;
+    /** One HIP device, or a device group (row strips + one RCCL all-gather; image on the first). */
+    static create(deviceIndex?: number | number[]): Promise<GpuContext>;
     destroy(): void;
 }
 
@@ -86,7 +87,7 @@ export declare class Renderer {
     numGaussians: number;
     framebuffer: Float32Array | Uint16Array;  // SimpleRender.framebuffer contents
     frames: number;
-    static requestContext(gaussians: PackedGaussians, deviceIndex?: number): Promise<GpuContext>;
+    static requestContext(gaussians: PackedGaussians, deviceIndex?: number | number[]): Promise<GpuContext>;
     constructor(canvas: HeadlessCanvas, interactiveCamera: InteractiveCameraLike, gaussians: PackedGaussians,
                 context: GpuContext, fpsCounter?: {innerText: string; style: any}, options?: RenderOptions);
     /** Resolves after the next frame (src/renderer.ts:103-107). */

@@ -41,6 +41,8 @@ class GpuContext {
         this.device = device;    // native context handle (gs_ctx*)
     }
 
+    // deviceIndex: one HIP device, or an array of devices (a device group: the frame is split into
+    // row strips, one per device, gathered with one RCCL all-gather; the image lands on the first)
     static async create(deviceIndex = 0) {
         let n = 0;
         try {

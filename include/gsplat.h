@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 
 typedef struct gs_ctx gs_ctx;
 typedef struct gs_scene gs_scene;
@@ -119,9 +119,18 @@ int gs_abi_version(void);
 const char* gs_last_error(void);
 int gs_device_count(int* out_count);
 
-/* GpuContext.create: rejects (GS_ERR_NO_DEVICE) when no HIP device exists.  ndev == 1 for now;
- * `devices` may be NULL (device 0). */
+/* GpuContext.create: rejects (GS_ERR_NO_DEVICE) when no HIP device exists.  devices = NULL with
+ * ndev = 0: device 0.  ndev > 1 (<= 64) makes a device group: one context drives every listed
+ * device from this thread.  A scene uploaded to it is replicated on each device; a frame is split
+ * into ndev row strips (gs_strip_rows with strip_count = ndev), strip g rendered on devices[g], and
+ * the strips are gathered with ONE in-place RCCL all-gather over the devices (ncclCommInitAll;
+ * xGMI on MI355X) -- or, when the list repeats a device (tests on one GPU), with peer copies into
+ * devices[0].  The image is delivered on devices[0] (gs_render_device's out_dev and hip_stream
+ * belong to it).  gs_opts.strip_count must be 1 on a group. */
 int gs_ctx_create(const int* devices, int ndev, gs_ctx** out_ctx);
+typedef enum { GS_GATHER_NONE = 0, GS_GATHER_RCCL = 1, GS_GATHER_PEER_COPY = 2 } gs_gather_kind;
+/* Devices driven by the context and how a group gathers its strips (gs_gather_kind). */
+int gs_ctx_info(const gs_ctx* ctx, int* out_ndev, int* out_gather);
 /* Also frees every scene still attached to the context (do not free those scenes afterwards). */
 void gs_ctx_destroy(gs_ctx* ctx);
 

@@ -1,8 +1,10 @@
 """N>1 path on CPU: row strips + one all-gather (gloo, world_size 2 and 3), checked against the
 single-image render.  Each rank's strip renderer here is the oracle (no GPU in this container);
 the partitioning and the collective are the code bench.py runs over RCCL."""
+import json
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -68,3 +70,20 @@ def test_strip_allgather_gloo(world, size):
         p.join(120)
         assert p.exitcode == 0
     assert q.get(timeout=10) is True
+
+
+def test_bench_spawns_ranks(tmp_path):
+    """`python bench.py --gpus N` without torch.distributed.run starts N rank processes with the
+    launcher's environment (distinct RANK/LOCAL_RANK, one WORLD_SIZE, one 127.0.0.1 rendezvous) and
+    returns the worst exit status."""
+    import bench
+    probe = ("import json, os, sys; json.dump({k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', "
+             "'MASTER_ADDR', 'MASTER_PORT')}, open(os.path.join(%r, 'r' + os.environ['RANK']), 'w')); "
+             "sys.exit(int(os.environ['RANK']) == 2)" % str(tmp_path))
+    rc = bench.spawn_ranks(4, [sys.executable, "-c", probe])
+    assert rc == 1
+    envs = [json.load(open(tmp_path / ("r%d" % r))) for r in range(4)]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"] == [e["LOCAL_RANK"] for e in envs]
+    assert {e["WORLD_SIZE"] for e in envs} == {"4"} and {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"}
+    assert len({e["MASTER_PORT"] for e in envs}) == 1
+    assert bench.spawn_ranks(2, [sys.executable, "-c", "pass"]) == 0

@@ -1,0 +1,101 @@
+"""The C ABI's device group (gs_ctx_create with a device list): one context drives every device,
+strip g of G on devices[g], one gather into devices[0] (RCCL all-gather over distinct devices;
+peer copies when the list repeats a device, which is how a one-GPU box exercises the whole group
+path).  Every image must equal the single-device frame bit for bit."""
+import numpy as np
+import pytest
+
+from conftest import camera, load_scene
+
+pytestmark = pytest.mark.gpu
+
+gs = pytest.importorskip("gsplat_amd")
+
+
+@pytest.fixture(scope="module")
+def scene_data():
+    W, H, n = 800, 600, 200_000
+    return W, H, n, gs.synth_aos(n, 91, W, H), gs.bench_uniforms(W, H)
+
+
+@pytest.fixture(scope="module")
+def single_images(scene_data):
+    W, H, n, aos, u = scene_data
+    with gs.Context(0) as ctx:
+        sc = gs.Scene(ctx, aos, n, 16)
+        f32 = sc.render(u, W, H)
+        f16 = sc.render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, accum=gs.GS_ACCUM_FP16_TARGET))
+        n_vis = ctx.timings()["n_vis"]
+    return f32, f16, n_vis
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_group_host_render_matches_single(scene_data, single_images, G):
+    W, H, n, aos, u = scene_data
+    with gs.Context([0] * G) as gc:
+        assert gc.info() == (G, "peer_copy")
+        sc = gs.Scene(gc, aos, n, 16)
+        img = sc.render(u, W, H)
+        assert np.array_equal(img, single_images[0])
+        st = gc.timings()
+        assert st["n_vis"] >= single_images[2]  # per-strip visible counts: a splat may reach two strips
+        assert st["tile_row_begin"] == 0 and st["tile_row_end"] == (H + 15) // 16
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_group_device_frames_in_flight(scene_data, single_images, G):
+    """gs_render_device on a group: a burst of frames without host waits, f16 output on device 0."""
+    W, H, n, aos, u = scene_data
+    with gs.Context([0] * G) as gc:
+        sc = gs.Scene(gc, aos, n, 16)
+        o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, accum=gs.GS_ACCUM_FP16_TARGET)
+        bufs = [gs.DeviceBuffer(H * W * 8) for _ in range(5)]
+        for b in bufs:
+            sc.render_device(u, W, H, b.ptr.value, b.nbytes, None, o)
+        gc.sync()
+        for b in bufs:
+            got = np.empty((H, W, 4), np.float16)
+            b.to_host(got)
+            assert np.array_equal(got.view(np.uint16), single_images[1].view(np.uint16))
+            b.free()
+
+
+def test_group_ref_quirks(scene_data):
+    """ref_quirks on a group: every member keeps the same slot state, frame after frame."""
+    aos, n, nsh = load_scene("pc_short")
+    W, H = 1280, 720
+    with gs.Context(0) as ctx, gs.Context([0, 0, 0]) as gc:
+        a = gs.Scene(ctx, aos, n, nsh)
+        b = gs.Scene(gc, aos, n, nsh)
+        for cam in ["app", "close", "behind"]:
+            u, _ = camera("pc_short_" + cam, W, H)
+            o = gs.make_opts(ref_quirks=1)
+            assert np.array_equal(a.render(u, W, H, o), b.render(u, W, H, o))
+
+
+def test_group_arguments():
+    with pytest.raises(gs.GsError) as e:
+        gs.Context([0, 4096])
+    assert e.value.code == gs.GS_ERR_INVALID
+    with gs.Context([0, 0]) as gc:
+        sc = gs.Scene(gc, gs.synth_aos(1000, 1, 64, 64), 1000, 16)
+        with pytest.raises(gs.GsError) as e:
+            sc.render(gs.bench_uniforms(64, 64), 64, 64, gs.make_opts(strip_index=0, strip_count=2))
+        assert e.value.code == gs.GS_ERR_INVALID
+        with pytest.raises(gs.GsError) as e:
+            sc.last_slots()
+        assert e.value.code == gs.GS_ERR_UNSUPPORTED
+
+
+def test_group_distinct_devices_use_rccl():
+    """With two or more GPUs the group gathers with RCCL (not reachable on a one-GPU box)."""
+    if gs.device_count() < 2:
+        pytest.skip("one GPU")
+    W, H, n = 640, 480, 100_000
+    aos = gs.synth_aos(n, 93, W, H)
+    u = gs.bench_uniforms(W, H)
+    with gs.Context(0) as ctx, gs.Context([0, 1]) as gc:
+        assert gc.info() == (2, "rccl")
+        a = gs.Scene(ctx, aos, n, 16).render(u, W, H)
+        b = gs.Scene(gc, aos, n, 16).render(u, W, H)
+        assert np.array_equal(a, b)

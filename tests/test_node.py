@@ -31,7 +31,7 @@ def run_node(*args, timeout=120):
 def test_node_host_cpu():
     out = run_node(os.path.join(ROOT, "tests", "node", "host_checks.js"), os.path.join(GOLDEN, "cameras.json"))
     assert out["exports"] == EXPORTS
-    assert out["abi"] == 1
+    assert out["abi"] == 2
     if out["deviceCount"] == 0:
         assert out["createRejected"] == "string" and out["requestRejected"] == "string"
     assert out["ctorThrows"] is True
@@ -55,6 +55,26 @@ def test_node_host_cpu():
     import gsplat_amd as gs
     png = bytes.fromhex(out["png"])
     assert png == gs.encode_png(np.arange(3 * 2 * 4, dtype=np.uint8).reshape(2, 3, 4))
+
+
+@pytest.mark.gpu
+def test_node_device_group_gpu(tmp_path):
+    """GpuContext.create([0, 0, 0]): the Node drop-in driving a device group (three row strips, peer-
+    copy gather on one GPU) renders the single-device image bit for bit."""
+    import gsplat_amd as gs
+    W, H = 320, 200
+    n = 30_000
+    aos = gs.synth_aos(n, 81, W, H)
+    u = gs.bench_uniforms(W, H)
+    (tmp_path / "scene.bin").write_bytes(aos.tobytes())
+    (tmp_path / "uni.bin").write_bytes(u.tobytes())
+    out = run_node(os.path.join(ROOT, "tests", "node", "render_frames.js"), str(tmp_path / "scene.bin"), str(n),
+                   "16", str(tmp_path / "uni.bin"), str(W), str(H), str(tmp_path / "img.f32"), "2", "0,0,0")
+    assert out["frames"] == 2 and out["destroyed"] is True
+    img = np.fromfile(tmp_path / "img.f32", np.float32).reshape(H, W, 4)
+    with gs.Context(0) as ctx:
+        direct = gs.Scene(ctx, aos, n, 16).render(u, W, H)
+    assert np.array_equal(img, direct)
 
 
 @pytest.mark.gpu
