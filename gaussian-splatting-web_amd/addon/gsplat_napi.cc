@@ -411,6 +411,39 @@ napi_value Perspective(napi_env env, napi_callback_info info) {
     return new_f32(env, m, 16);
 }
 
+// cameraFromJSON (src/camera.ts:476-503): (rawCamera, canvasW, canvasH) -> {viewMatrix, perspective,
+// focalX, focalY}
+napi_value CameraFromJSON(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    get_args(env, info, 3, argv);
+    double pos[3], rot[9], fx = 0, fy = 0;
+    napi_value vpos, vrot, vfx, vfy;
+    bool ok = napi_get_named_property(env, argv[0], "position", &vpos) == napi_ok && vec3(env, vpos, pos) &&
+              napi_get_named_property(env, argv[0], "rotation", &vrot) == napi_ok &&
+              napi_get_named_property(env, argv[0], "fx", &vfx) == napi_ok &&
+              napi_get_value_double(env, vfx, &fx) == napi_ok &&
+              napi_get_named_property(env, argv[0], "fy", &vfy) == napi_ok &&
+              napi_get_value_double(env, vfy, &fy) == napi_ok;
+    for (uint32_t r = 0; ok && r < 3; ++r) {
+        napi_value row;
+        ok = napi_get_element(env, vrot, r, &row) == napi_ok && vec3(env, row, rot + 3 * r);
+    }
+    if (!ok) return throw_gs(env, GS_ERR_INVALID, "cameraFromJSON: needs position[3], rotation[3][3], fx, fy");
+    float view[16], proj[16], focal[2];
+    const int rc = gs_camera_from_json(pos, rot, fx, fy, (int)num(env, argv[1], 0), (int)num(env, argv[2], 0),
+                                       view, proj, focal);
+    if (rc) return throw_gs(env, rc, "gs_camera_from_json");
+    napi_value o, fxv, fyv;
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "viewMatrix", new_f32(env, view, 16));
+    napi_set_named_property(env, o, "perspective", new_f32(env, proj, 16));
+    napi_create_double(env, focal[0], &fxv);
+    napi_create_double(env, focal[1], &fyv);
+    napi_set_named_property(env, o, "focalX", fxv);
+    napi_set_named_property(env, o, "focalY", fyv);
+    return o;
+}
+
 napi_value CameraPosition(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     get_args(env, info, 1, argv);
@@ -523,6 +556,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"sceneFree", SceneFree}, {"render", Render}, {"renderAsync", RenderAsync},
         {"timings", Timings}, {"timingsReset", TimingsReset}, {"sync", Sync}, {"present", Present},
         {"lookAt", LookAt}, {"perspective", Perspective}, {"cameraPosition", CameraPosition},
+        {"cameraFromJSON", CameraFromJSON},
         {"packUniforms", PackUniforms}, {"stripRows", StripRows}, {"plyParse", PlyParse}, {"encodePng", EncodePng},
     };
     for (const auto& f : fns) {

@@ -127,6 +127,49 @@ int gs_camera_position(const float view[16], float out[3]) {
     return GS_OK;
 }
 
+// cameraFromJSON (src/camera.ts:476-503).  Every WM store rounds to f32; the arithmetic between
+// stores is JS double.
+int gs_camera_from_json(const double pos[3], const double rot[9], double fx, double fy, int W,
+                        int H, float view[16], float proj[16], float focal[2]) {
+    if (!pos || !rot || !view || !proj || W <= 0 || H <= 0) return GS_ERR_INVALID;
+    // focal2fov (:463-465), getProjectionMatrix (:19-42): P row-major in f32, then transposed.
+    const double fovx = 2.0 * std::atan((double)W / (2.0 * fx));
+    const double fovy = 2.0 * std::atan((double)H / (2.0 * fy));
+    const double zn = 0.2, zf = 100.0;
+    const double top = std::tan(fovy / 2) * zn, bottom = -top;
+    const double right = std::tan(fovx / 2) * zn, left = -right;
+    float P[16] = {0};
+    P[0] = f32((2.0 * zn) / (right - left));
+    P[5] = f32((2.0 * zn) / (top - bottom));
+    P[8] = f32((right + left) / (right - left));
+    P[9] = f32((top + bottom) / (top - bottom));
+    P[10] = f32(zf / (zf - zn));
+    P[11] = f32(-(zf * zn) / (zf - zn));
+    P[14] = 1.0f;
+    P[15] = 0.0f;
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) proj[4 * c + r] = P[4 * r + c];
+    // worldToCamFromRT (:467-473): mat3.create(rows...) stores the nine values column by column
+    // (WM create$3), fromMat3 widens to a mat4, translate(m, -t) in place (WM translate).
+    const float m[12] = {f32(rot[0]), f32(rot[1]), f32(rot[2]), 0, f32(rot[3]), f32(rot[4]),
+                         f32(rot[5]), 0, f32(rot[6]), f32(rot[7]), f32(rot[8]), 0};
+    for (int c = 0; c < 3; ++c) {
+        for (int r = 0; r < 3; ++r) view[4 * c + r] = m[4 * c + r];
+        view[4 * c + 3] = 0.0f;
+    }
+    view[12] = view[13] = view[14] = 0.0f;
+    view[15] = 1.0f;
+    const double v0 = f32(pos[0] * -1.0), v1 = f32(pos[1] * -1.0), v2 = f32(pos[2] * -1.0);
+    for (int r = 0; r < 4; ++r)
+        view[12 + r] = f32((double)view[r] * v0 + (double)view[4 + r] * v1 + (double)view[8 + r] * v2 +
+                           (double)view[12 + r]);
+    if (focal) {
+        focal[0] = f32(H);
+        focal[1] = f32(W);
+    }
+    return GS_OK;
+}
+
 // uniformLayout.pack (src/renderer.ts:24-33): 160 bytes.
 int gs_pack_uniforms(const float view[16], const float proj[16], const float cam_pos[3], float thx,
                      float thy, float fx, float fy, float scale_modifier, void* out160) {

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows",
     "gs_render", "gs_render_device", "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
     "gs_present_device", "gs_encode_png", "gs_look_at",
-    "gs_perspective", "gs_camera_position", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
+    "gs_perspective", "gs_camera_position", "gs_camera_from_json", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
     "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records", "gs_debug_last_slots",
     "gs_debug_tile_lists",
 )
@@ -120,6 +120,7 @@ def lib():
         L.gs_look_at.argtypes = [P, P, P, P]
         L.gs_perspective.argtypes = [D, D, D, D, P]
         L.gs_camera_position.argtypes = [P, P]
+        L.gs_camera_from_json.argtypes = [P, P, D, D, I, I, P, P, P]
         L.gs_pack_uniforms.argtypes = [P, P, P, F, F, F, F, F, P]
         L.gs_synth_aos.argtypes = [U64, U64, I, I, P]
         L.gs_ply_parse.argtypes = [P, U64, ctypes.POINTER(GsPlyInfo), P, U64]
@@ -160,6 +161,17 @@ def camera_position(view):
     out = np.zeros(3, np.float32)
     _check(lib().gs_camera_position(_ptr(v), _ptr(out)))
     return out
+
+
+def camera_from_json(cam, W, H):
+    """cameraFromJSON (src/camera.ts:476-503) of one cameras.json entry for a W x H canvas:
+    returns (view, proj, focal) with focal = the Camera's (focalX, focalY) = (H, W)."""
+    pos = np.ascontiguousarray(cam["position"], np.float64)
+    rot = np.ascontiguousarray(np.asarray(cam["rotation"], np.float64).reshape(9))
+    view, proj, focal = np.zeros(16, np.float32), np.zeros(16, np.float32), np.zeros(2, np.float32)
+    _check(lib().gs_camera_from_json(_ptr(pos), _ptr(rot), float(cam["fx"]), float(cam["fy"]), int(W), int(H),
+                                     _ptr(view), _ptr(proj), _ptr(focal)))
+    return view, proj, focal
 
 
 def pack_uniforms(view, proj, cam_pos=None, tan_half_fov=(0.0, 0.0), focal=(0.0, 0.0), scale_modifier=1.0):

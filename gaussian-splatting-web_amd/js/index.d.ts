@@ -39,6 +39,18 @@ export declare class PackedGaussians {
     static fromPly(plyArrayBuffer: ArrayBuffer): PackedGaussians;
 }
 
+/** One entry of an INRIA cameras.json (src/camera.ts:7-16). */
+export interface CameraRaw {
+    id?: number;
+    img_name?: string;
+    width?: number;
+    height?: number;
+    position: number[];
+    rotation: number[][];
+    fx: number;
+    fy: number;
+}
+
 export declare class Camera {
     height: number;
     width: number;
@@ -50,6 +62,7 @@ export declare class Camera {
     constructor(height: number, width: number, viewMatrix: Float32Array, perspective: Float32Array,
                 focalX: number, focalY: number, scaleModifier: number);
     static default(width: number, height: number): Camera;
+    static fromJSON(rawCamera: CameraRaw, canvasW: number, canvasH: number): Camera;
     static lookAt(eye: number[], target: number[], width: number, height: number, fovy?: number,
                   near?: number, far?: number): Camera;
     getPosition(): Float32Array;

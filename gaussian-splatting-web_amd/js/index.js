@@ -115,6 +115,13 @@ class Camera {
                           addon().perspective(fovy, width / height, near, far), width, height, 1);
     }
 
+    // cameraFromJSON (src/camera.ts:476-503): an INRIA cameras.json entry for a canvasW x canvasH
+    // canvas (+z forward, getProjectionMatrix(0.2, 100, fovX, fovY)); focalX/focalY = H/W as there
+    static fromJSON(rawCamera, canvasW, canvasH) {
+        const c = addon().cameraFromJSON(rawCamera, canvasW, canvasH);
+        return new Camera(canvasH, canvasW, c.viewMatrix, c.perspective, c.focalX, c.focalY, 1);
+    }
+
     // translation of inverse(view) (src/camera.ts:135-138)
     getPosition() {
         return addon().cameraPosition(this.viewMatrix);

@@ -194,6 +194,14 @@ int gs_encode_png(const uint8_t* rgba8, int W, int H, uint8_t* out, uint64_t cap
 int gs_look_at(const double eye[3], const double target[3], const double up[3], float out_view[16]);
 int gs_perspective(double fovy_radians, double aspect, double z_near, double z_far, float out_proj[16]);
 int gs_camera_position(const float view[16], float out_pos[3]);
+/* cameraFromJSON (src/camera.ts:476-503) for one INRIA cameras.json entry: position[3],
+ * rotation[9] (the JSON's 3x3 as given, rows flattened, handed to WM mat3.create), fx, fy, and the
+ * canvas size.  view = worldToCamFromRT (src/camera.ts:467-473), proj = getProjectionMatrix(0.2,
+ * 100, focal2fov(fx, W), focal2fov(fy, H)) (src/camera.ts:19-42, :463-465; +z forward).
+ * out_focal (optional) = the Camera's focalX/focalY, which the reference sets to (H, W). */
+int gs_camera_from_json(const double position[3], const double rotation[9], double fx, double fy,
+                        int canvas_w, int canvas_h, float out_view[16], float out_proj[16],
+                        float out_focal[2]);
 int gs_pack_uniforms(const float view[16], const float proj[16], const float cam_pos[3],
                      float tan_half_fov_x, float tan_half_fov_y, float focal_x, float focal_y,
                      float scale_modifier, void* out160);

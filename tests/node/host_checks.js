@@ -51,6 +51,16 @@ async function main() {
         out.cams.push({name: c.name, W: c.W, H: c.H, view: bits(cam.viewMatrix), proj: bits(cam.perspective),
                        campos: bits(cam.getPosition())});
     }
+    // Camera.fromJSON (src/camera.ts:476-503) for every cameras.json fixture
+    out.jsonCams = [];
+    for (const c of cams) {
+        if (c.kind !== 'json') continue;
+        const cam = gs.Camera.fromJSON(c.json, c.W, c.H);
+        const bits = (f) => Array.from(new Uint32Array(Float32Array.from(f).buffer));
+        out.jsonCams.push({name: c.name, W: c.W, H: c.H, view: bits(cam.viewMatrix), proj: bits(cam.perspective),
+                           campos: bits(cam.getPosition()), focal: [cam.focalX, cam.focalY],
+                           size: [cam.width, cam.height]});
+    }
     // uniform block packing (src/renderer.ts:24-33) of the first camera
     const c0 = gs.Camera.lookAt(cams[0].eye, cams[0].target, cams[0].W, cams[0].H);
     const u = a.packUniforms(c0.viewMatrix, c0.perspective, c0.getPosition(), 0.5, 0.25, 100, 200, 1);

@@ -110,6 +110,20 @@ def test_camera_position_json_cameras():
             assert np.array_equal(pos.view(np.uint32), np.array(c["campos"], np.uint32)), c["name"]
 
 
+def test_camera_from_json_matches_fixtures():
+    """gs_camera_from_json bit-exact vs camera.ts cameraFromJSON run with wgpu-matrix 2.9.1 by node."""
+    cams = [c for c in json.load(open(os.path.join(GOLDEN, "cameras.json"))) if c["kind"] == "json"]
+    assert len(cams) >= 8
+    for c in cams:
+        v, p, f = gs.camera_from_json(c["json"], c["W"], c["H"])
+        assert np.array_equal(v.view(np.uint32), np.array(c["view"], np.uint32)), c["name"]
+        assert np.array_equal(p.view(np.uint32), np.array(c["proj"], np.uint32)), c["name"]
+        assert np.array_equal(gs.camera_position(v).view(np.uint32), np.array(c["campos"], np.uint32))
+        assert f.tolist() == [c["H"], c["W"]]
+    with pytest.raises(gs.GsError):
+        gs.camera_from_json(cams[0]["json"], 0, 10)
+
+
 # --------------------------------------------------------------------------- synthetic scenes
 def test_synth_deterministic_and_hash():
     a = gs.synth_aos(1000, 1, 1920, 1080)

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.skipif(not NODE or not os.path.exists(ADDON), reason="n
 
 EXPORTS = sorted(["abiVersion", "lastError", "deviceCount", "ctxCreate", "ctxDestroy", "sceneUpload", "sceneFree",
                   "render", "renderAsync", "timings", "timingsReset", "sync", "present", "lookAt", "perspective",
-                  "cameraPosition", "packUniforms", "stripRows", "plyParse", "encodePng"])
+                  "cameraPosition", "cameraFromJSON", "packUniforms", "stripRows", "plyParse", "encodePng"])
 
 
 def run_node(*args, timeout=120):
@@ -41,6 +41,11 @@ def test_node_host_cpu():
     for c in out["cams"]:
         ref = cams[(c["name"], c["W"], c["H"])]
         assert c["view"] == ref["view"] and c["proj"] == ref["proj"] and c["campos"] == ref["campos"], c["name"]
+    assert len(out["jsonCams"]) >= 8
+    for c in out["jsonCams"]:
+        ref = cams[(c["name"], c["W"], c["H"])]
+        assert c["view"] == ref["view"] and c["proj"] == ref["proj"] and c["campos"] == ref["campos"], c["name"]
+        assert c["focal"] == [c["H"], c["W"]] and c["size"] == [c["W"], c["H"]]
     u = np.array(out["uniforms"], np.uint32).view(np.float32)
     ref = cams[(out["cams"][0]["name"], out["cams"][0]["W"], out["cams"][0]["H"])]
     assert np.array_equal(u[0:16].view(np.uint32), np.array(ref["view"], np.uint32))
