@@ -23,6 +23,7 @@
 //   draw order ....... src/renderer.ts:301-330 (init-sort grid :306), RS stable radix sort
 //   record layout .... src/ply.ts:249-257, src/packing.ts:146-291
 //   uniform layout ... src/renderer.ts:24-33
+//   present .......... src/post_process_render.ts:62-77
 
 #include <cmath>
 #include <cstdint>
@@ -484,6 +485,29 @@ int or_render(const void* aos, uint64_t n, int n_sh, const void* uni160, int W, 
         for (uint64_t i = 0; i < n; ++i)
             if (sp[i].visible) { st->n_vis++; st->k_tiles += (uint64_t)sp[i].ntiles; }
         st->blends = blends;
+    }
+    return 0;
+}
+
+// PostProcessRenderer fragmentMain (src/post_process_render.ts:62-77): the fragment at pixel
+// centre (x+.5, y+.5) samples uv = fragCoord / (W, H) with uv.y = 1 - uv.y, i.e. the texel centre
+// of row H-1-y (a sampler at a texel centre returns the texel), so the pass is a row flip; then
+// color.a = saturate(color.a * 1.5) and, below 0.99, color.a = pow(color.a, 4).  pow is WGSL's
+// builtin (exp2(4 log2 a) on most backends, a few ulp): restated with powf.
+int or_present(const float* in, int W, int H, float* out) {
+    if (!in || !out || W <= 0 || H <= 0) return -1;
+    for (int y = 0; y < H; ++y) {
+        const float* src = in + 4 * (size_t)(H - 1 - y) * W;
+        float* dst = out + 4 * (size_t)y * W;
+        for (int x = 0; x < W; ++x) {
+            dst[4 * x + 0] = src[4 * x + 0];
+            dst[4 * x + 1] = src[4 * x + 1];
+            dst[4 * x + 2] = src[4 * x + 2];
+            float a = src[4 * x + 3] * 1.5f;
+            a = a < 0.0f ? 0.0f : (a > 1.0f ? 1.0f : a);  // saturate
+            if (a < 0.99f) a = std::pow(a, 4.0f);
+            dst[4 * x + 3] = a;
+        }
     }
     return 0;
 }

@@ -44,6 +44,7 @@ def lib():
         L.or_composite.argtypes = [P, P, U64, I, I, I, F, P, P]
         L.or_render.argtypes = [P, U64, I, P, I, I, I, F, I, P, P, P, ctypes.POINTER(OrStats)]
         L.or_num_threads.restype = I
+        L.or_present.argtypes = [P, I, I, P]
         _lib = L
     return _lib
 
@@ -97,3 +98,11 @@ def render(aos, n, n_sh, uniforms, W, H, accum=0, t_min=1e-4, quirk=0, state=Non
 
 def num_threads():
     return lib().or_num_threads()
+
+
+def present(fb, W, H):
+    """PostProcessRenderer's pass (src/post_process_render.ts:62-77) on a W x H RGBA f32 framebuffer."""
+    a = np.ascontiguousarray(fb, np.float32)
+    out = np.empty((H, W, 4), np.float32)
+    assert lib().or_present(_p(a), W, H, _p(out)) == 0
+    return out

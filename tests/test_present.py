@@ -2,6 +2,9 @@
 on the device, and the PNG encoder used for visual diffs.
 
 CPU: gs_encode_png decodes (PIL, and an independent zlib parse) to the exact input pixels.
+Both against the oracle's restatement (oracle/gs_oracle.cpp or_present, pow(a, 4) as powf): the
+flip and RGB bit-exact, alpha within 4 ulp (WGSL's pow is exp2(4 log2 a), a few ulp; here it is
+evaluated as (a^2)^2).
 GPU: gs_present_device equals the host gs_present bit for bit (f32 out), or that result rounded
 to f16 (the reference's rgba16float canvas) / unorm8, from f32 and f16 framebuffers."""
 import os
@@ -15,6 +18,32 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gaussian-splatting-web_amd"))
 import gsplat_amd as gs  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import oracle_py as orc  # noqa: E402
+
+ALPHA_ULP = 4  # stated tolerance on the remapped alpha vs the oracle's powf
+
+
+def assert_present_matches_oracle(got, fb, W, H):
+    ref = orc.present(fb, W, H)
+    assert np.array_equal(got[..., :3].view(np.uint32), ref[..., :3].view(np.uint32))
+    ulp = np.abs(got[..., 3].view(np.int32).astype(np.int64) - ref[..., 3].view(np.int32).astype(np.int64))
+    assert int(ulp.max()) <= ALPHA_ULP, int(ulp.max())
+    # the >= 0.99 branch and saturation are exact
+    hi = ref[..., 3] >= 0.99
+    assert np.array_equal(got[..., 3][hi], ref[..., 3][hi])
+
+
+def test_present_host_vs_oracle():
+    W, H = 257, 131
+    rng = np.random.default_rng(5)
+    fb = rng.random((H, W, 4), dtype=np.float32)
+    a = fb[..., 3].reshape(-1)
+    a[:4096] = np.linspace(0.0, 0.7, 4096, dtype=np.float32)  # a ramp through both branches
+    a[4096:4106] = [0.0, -0.0, 1e-30, 0.66, 0.6599, 0.66001, 1.0, 2.0, -1.0, 0.65999997]
+    got = gs.present(fb, W, H)
+    assert_present_matches_oracle(got, fb, W, H)
+    assert np.array_equal(got[0, :, :3], fb[H - 1, :, :3])  # row 0 of the canvas = the framebuffer's last
 
 
 def _decode_png_stored(data):
@@ -81,6 +110,7 @@ def test_present_device_matches_host(gpu_ctx, fb_format):
     fb.to_host(fb_host)
     ref = gs.present(fb_host.astype(np.float32), W, H)  # host PostProcessRenderer
     assert ref[..., 3].max() > 0.5  # a non-trivial image
+    assert_present_matches_oracle(ref, fb_host.astype(np.float32), W, H)
     for fmt, dt in ((gs.GS_PRESENT_RGBA_F32, np.float32), (gs.GS_PRESENT_RGBA_F16, np.float16),
                     (gs.GS_PRESENT_RGBA8, np.uint8)):
         out = gs.DeviceBuffer(W * H * 4 * np.dtype(dt).itemsize)
@@ -90,6 +120,7 @@ def test_present_device_matches_host(gpu_ctx, fb_format):
         out.to_host(got)
         if dt == np.float32:
             assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+            assert_present_matches_oracle(got, fb_host.astype(np.float32), W, H)
         elif dt == np.float16:
             assert np.array_equal(got.view(np.uint16), ref.astype(np.float16).view(np.uint16))
         else:
