@@ -17,6 +17,7 @@
 #include <utility>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -169,6 +170,8 @@ struct FrameSet {
     uint32_t *c0 = nullptr, *c1 = nullptr;  // [parts]: slots per projection partition and chunk
     uint16_t* cand = nullptr;           // chunk-0 candidates per partition (k_cull): offsets
     uint32_t* units = nullptr;          // the frame's non-empty chunk-0 work units (k_cull)
+    uint32_t* plist = nullptr;          // chunk 1: partitions that may hold chunk-1 splats (k_chunk1)
+    uint32_t* order = nullptr;          // [tiles] the composite's tile order (k_tile_sort)
     uint32_t* sidx = nullptr;           // [slots] storage index of each composite slot
     FrameCtl* ctl = nullptr;            // zero at a frame's start (the frame's end clears it)
     StatShard* stats = nullptr;         // [kStatShards], zero at a frame's start (likewise)
@@ -211,6 +214,7 @@ struct gs_scene {
     uint32_t* d_seq = nullptr;
     uint32_t seq_next = 1;
     uint32_t stat_want[kFrameSets] = {};   // sequence number that completes the slot's frame
+    uint32_t stat_base[kFrameSets] = {};   // the slot's frame's saturation-histogram base (sat_bucket)
     bool stat_pending[kFrameSets] = {};
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
@@ -247,6 +251,23 @@ static constexpr int kDepthSortIpt = 8;
 #define GS_CHUNK_MARGIN 1.15f
 #endif
 static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
+// split the visible splats into two chunks when at least this share of the tiles saturated in the
+// last frame; chunk 1 then visits only the partitions that can reach an unsaturated tile
+#ifndef GS_SPLIT_SAT_FRAC
+#define GS_SPLIT_SAT_FRAC 0.2
+#endif
+static constexpr double kSplitSatFrac = GS_SPLIT_SAT_FRAC;
+// ... at this quantile of the saturated tiles' saturation depths (GS_SAT_QUANTILE overrides),
+// when the deepest saturation is more than kQuantileGain times deeper
+static constexpr float kQuantileGain = 1.5f;
+static double sat_quantile() {
+    static const double q = [] {
+        const char* e = std::getenv("GS_SAT_QUANTILE");
+        const double v = e ? std::atof(e) : 0.95;
+        return v > 0.0 && v <= 1.0 ? v : 0.95;
+    }();
+    return q;
+}
 static_assert(sizeof(FrameCtl) <= 256, "FrameCtl too large");
 
 static Records records(gs_scene* s, const FrameSet& F) {
@@ -268,7 +289,9 @@ static void ensure_tiles(FrameSet& F, int n_tiles) {
     dev_free(F.done);
     dev_free(F.bmat);
     dev_free(F.tbase);
+    dev_free(F.order);
     dev_alloc(F.ranges, (size_t)n_tiles);
+    dev_alloc(F.order, (size_t)n_tiles);
     dev_alloc(F.done, (size_t)n_tiles);
     dev_alloc(F.bmat, (size_t)kBinParts * n_tiles);
     dev_alloc(F.tbase, (size_t)n_tiles);
@@ -387,11 +410,32 @@ static void collect_stats(gs_scene* s, bool wait) {
             s->key_hi = l.key_max;
             s->have_krange = true;
         }
+        // the threshold sits past the depth at which all but a (1 - q) share of the saturated
+        // tiles saturated (the upper edge of that histogram bucket, then the margin); the
+        // later-saturating tiles complete in chunk 1
         uint32_t sat_tiles = 0;
-        for (int k = 0; k < kHistShards; ++k) sat_tiles += l.sat_tiles[k];
+        for (int k = 0; k < kSatBuckets; ++k) sat_tiles += l.sat_hist[k];
         uint32_t target = kNoSplit;
-        if (l.n_vis > 0 && l.sat_key != 0 && sat_tiles >= 0.5 * std::max(1, s->last_tiles))
-            target = scaled_threshold(l.sat_key, kChunkMargin);
+        if (l.n_vis > 0 && l.sat_key != 0 && sat_tiles >= kSplitSatFrac * std::max(1, s->last_tiles)) {
+            const double want = sat_quantile() * sat_tiles;
+            uint32_t cum = 0;
+            int b = 0;
+            for (; b < kSatBuckets - 1; ++b) {
+                cum += l.sat_hist[b];
+                if (cum >= want) break;
+            }
+            uint32_t edge = l.sat_key;
+            if (b < kSatBuckets - 1) {
+                const uint64_t e = ((uint64_t)s->stat_base[slot] + (uint64_t)b + 1) << kSatShift;
+                const uint32_t eq = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(e, 0xFFFFFFFEull), l.sat_key);
+                // the quantile only when the last tiles saturate much deeper than the rest (a
+                // moving camera, sparse regions): otherwise chunk 1's launches cost more than the
+                // smaller chunk 0 saves
+                const float dq = std::fabs(key_to_float(eq)), dm = std::fabs(key_to_float(l.sat_key));
+                if (dm > kQuantileGain * dq) edge = eq;
+            }
+            target = scaled_threshold(edge, kChunkMargin);
+        }
         if (target >= s->chunk_T || s->chunk_T == kNoSplit)
             s->chunk_T = target;
         else
@@ -562,6 +606,13 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     bp.tbase = F.tbase;
     bp.tvals = F.tvA;
     bp.rows = tr_end - tr_begin;
+    bp.order = F.order;
+    bp.stats = F.stats;
+    {  // twice the last frame's mean chunk-0 list length (a frame with no history: no long lists)
+        const uint64_t k0 = s->have_last ? s->last.k_chunk[0] : 0;
+        bp.heavy_len = k0 ? (uint32_t)std::min<uint64_t>(2 * k0 / (uint64_t)std::max(1, n_tiles), 0xFFFFFFFFull)
+                          : 0xFFFFFFFFu;
+    }
     TileSortParams tsp{};  // each tile's list into (depth key, index) order
     tsp.ranges = F.ranges;
     tsp.in = F.tvA;
@@ -573,6 +624,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     cp.ranges = F.ranges;
     cp.tvals = F.tvB;
     cp.rec = F.crec;
+    cp.order = F.order;
     cp.W = W;
     cp.H = H;
     cp.tiles_x = TX;
@@ -584,6 +636,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     cp.state = F.state;
     cp.done = F.done;
     cp.ctl = F.ctl;
+    cp.stats = F.stats;
+    cp.sat_base = s->have_krange ? (s->key_lo >> kSatShift) : 0u;
+    s->stat_base[slot] = cp.sat_base;
     cp.out = out;
     cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
     mark(EV_DSORT_0);
@@ -602,15 +657,18 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         Chunk1Params c1{};
         c1.pp = pp;
         c1.pp.sat = F.sat;
+        c1.pp.plist = F.plist;
         c1.pp.rec_all = 0;
         c1.bp = bp;
         c1.bp.cnt = F.c1;
         c1.bp.units = nullptr;  // chunk 1: every unit
         c1.bp.chunk = 1;
+        c1.bp.order = nullptr;
         c1.tp = tsp;
         c1.tp.done = F.done;
         c1.cp = cp;
         c1.cp.mode = kCompSecond;
+        c1.cp.order = nullptr;
         c1.sat = F.sat;
         c1.bar = F.bar;
         c1.two_chunks = two_chunks ? 1 : 0;
@@ -620,9 +678,16 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.host_ctl = s->d_ctl_slot + slot;
         c1.host_seq = s->d_seq + slot;
         c1.seq = q;
-        // 64 workgroups: chunk 1 is small when it has work at all, and a frame whose chunk 0
-        // saturated every tile pays only for these launching (LDS-heavy, beside the next frame)
-        launch_chunk1(c1, std::min(c->num_cus, 64), o.accum == GS_ACCUM_FP16_TARGET, st);
+        // While chunk 0 saturates every tile: k_chunk1 on 64 workgroups (the launch then only ends
+        // the frame; it is LDS-heavy and starts beside the next frame's kernels).  Its grid fits the
+        // device at once (one 256-thread workgroup per CU), so every workgroup becomes resident
+        // while the others wait at a grid barrier: the kernels beside it never wait for k_chunk1
+        // and finish.  Once a recent frame left tiles unsaturated: chunk 1 as separate launches
+        // at full occupancy (a kernel boundary costs less than a grid barrier), then the frame's end.
+        if (two_chunks && s->have_last && s->last.not_done > 0)
+            launch_chunk1_split(c1, o.accum == GS_ACCUM_FP16_TARGET, st);
+        else
+            launch_chunk1(c1, std::min(c->num_cus, 64), o.accum == GS_ACCUM_FP16_TARGET, st);
         if (two_chunks && o.timing == 1) mark(EV_COMP_1);
     }
     F.meta_clean = true;
@@ -1014,6 +1079,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 dev_alloc(F.c0, (size_t)proj_parts(n) + 1);
                 dev_alloc(F.c1, (size_t)proj_parts(n) + 1);
                 dev_alloc(F.units, (size_t)kUnitShards * unit_shard_cap(proj_parts(n)) + 1);
+                dev_alloc(F.plist, (size_t)proj_parts(n) + 1);
                 dev_alloc(F.cand, nslots);
                 dev_alloc(F.sidx, nslots);
                 ensure_tile_capacity(F, 4 * n + (1u << 20));
@@ -1103,11 +1169,13 @@ void gs_scene_free(gs_scene* s) {
         dev_free(F.c1);
         dev_free(F.cand);
         dev_free(F.units);
+        dev_free(F.plist);
         dev_free(F.sidx);
         dev_free(F.tvA); dev_free(F.tvB);
         dev_free(F.ranges);
         dev_free(F.bmat);
         dev_free(F.tbase);
+        dev_free(F.order);
         dev_free(F.done);
         dev_free(F.sat);
         dev_free(F.state);

@@ -43,6 +43,16 @@ constexpr uint32_t kRectHole = 0xFFFFFFFDu;   // a composite slot whose candidat
 constexpr uint32_t kErrOverflow = 1u;
 constexpr uint32_t kErrBarrier = 2u;   // a grid barrier of k_chunk1 timed out
 
+// Saturation-depth histogram: tile saturated at depth key k -> bucket (k >> 21) - base, clamped to
+// [0, kSatBuckets): quarter-octave buckets of depth from the last frame's nearest visible splat
+// (the base, set by the host).  The chunk controller places the threshold at a quantile of it.
+constexpr int kSatBuckets = 32;
+constexpr int kSatShift = 21;
+__host__ __device__ inline uint32_t sat_bucket(uint32_t key, uint32_t base) {
+    const int b = (int)(key >> kSatShift) - (int)base;
+    return (uint32_t)(b < 0 ? 0 : (b >= kSatBuckets ? kSatBuckets - 1 : b));
+}
+
 struct FrameCtl {                 // zeroed at the start of every frame
     unsigned long long k_total;   // sum of tile counts over visible splats (project)
     uint32_t n_vis;               // visible splats (project)
@@ -55,8 +65,9 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t key_max;             // largest depth key of a visible splat (project)
     uint32_t sat_key;             // depth key of the farthest splat a tile saturated at (the frame's end, k_chunk1)
     uint32_t unit_n[kUnitShards]; // chunk-0 work units per shard (k_cull; see ProjParams::units)
-    uint32_t sat_key_shard[kHistShards];  // per shard: the same, max over the shard's tiles
-    uint32_t sat_tiles[kHistShards];      // per shard: tiles saturated by the end of the frame
+    uint32_t c1_parts;            // chunk 1: projection partitions listed in ProjParams::plist (k_chunk1)
+    uint32_t sat_hist[kSatBuckets];  // tiles saturated by the end of the frame, by saturation depth
+                                     // (sat_bucket; summed from the shards at the frame's end)
 };
 
 // Per-frame counters that many workgroups add to, sharded so that no address takes more than a
@@ -67,7 +78,9 @@ struct StatShard {
     unsigned long long k_total;
     uint32_t n_vis, key_min_inv, key_max;
     uint32_t n_chunk[2];
-    uint32_t pad;
+    uint32_t sat_key;             // composite: max saturation key of the shard's tiles
+    uint32_t sat_hist[kSatBuckets];  // composite: the shard's tiles by saturation depth
+    uint32_t order_n[2];          // shards 0-7: the composite order of XCD band x (k_tile_sort)
 };
 
 // Bound of a projection partition (k_part_bounds, at upload): box of its finite positions,
@@ -146,8 +159,10 @@ struct ProjParams {
     const PartBound* bounds;  // [parts] (k_part_bounds)
     const uint32_t* orig;     // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx;           // [slots] storage index of each composite slot
-    // k_records: unsaturated-tile SAT of chunk 0 (k_sat); rec_all = every visible (debug)
+    // chunk 1: per strip tile row, prefix counts of the tiles chunk 0 left unsaturated
+    // (unsat_rows_body); rec_all: k_records dumps every visible Gaussian's record (debug)
     const uint32_t* sat;
+    uint32_t* plist;          // [parts] chunk 1: the partitions that may hold chunk-1 splats (k_chunk1)
     int rec_all;
     float cam[3];             // camera position (SH view direction)
     const float4* sh;         // [n][shq] packed SH coefficients
@@ -217,6 +232,10 @@ struct BinParams {
     uint32_t* tbase;              // [n_tiles] entries per tile, then (chunk 1's tile scan) the tile's begin
     uint32_t* tvals;              // out: composite slots, grouped by tile, unordered in a tile
     int rows;                     // tile rows of the strip
+    uint32_t* order;              // chunk 0 (nullable): the composite's tile order, lists longer than
+                                  // heavy_len first in each XCD band (k_bin_colscan)
+    StatShard* stats;             // order_n counters (shard x = band x)
+    uint32_t heavy_len;
 };
 
 // Per-tile sort of the tile lists (k_tile_sort): each tile's slots ordered by their sort key,
@@ -236,6 +255,7 @@ struct CompositeParams {
     const uint2* ranges;          // [n_tiles] (begin, end) into tvals
     const uint32_t* tvals;        // composite slots
     const float4* rec;            // composite records (3 float4 per slot)
+    const uint32_t* order;        // nullable: tile order (k_tile_sort); identity when null
     int W, H, tiles_x, tile_row_begin, row0;  // row0 = first image row of the output buffer
     int n_tiles;
     float t_min;
@@ -243,16 +263,18 @@ struct CompositeParams {
     float4* state;                // per pixel (rgb, T or dst.a) of unsaturated tiles, image rows
     uint8_t* done;                // per tile: 1 = saturated after chunk 0
     FrameCtl* ctl;
+    StatShard* stats;             // saturation statistics (shard tile % kStatShards)
+    uint32_t sat_base;            // sat_bucket's base
     void* out;                    // rows_padded x W pixels
     int out_f16;
 };
 
 struct Chunk1Params {
-    ProjParams pp;                // records_body: chunk-1 slots (pp.sat = the SAT)
+    ProjParams pp;                // chunk-1 slots (pp.sat = the unsaturated-tile row prefixes)
     BinParams bp;                 // chunk 1
     TileSortParams tp;
     CompositeParams cp;           // mode kCompSecond
-    uint32_t* sat;                // SAT of the unsaturated tiles (written by the first phase)
+    uint32_t* sat;                // unsaturated-tile row prefix counts (written by the first phase)
     uint32_t* bar;                // grid-barrier arrival counter, zero at launch (the frame's end zeroes it)
     int two_chunks;               // chunk 1 may have work (else only the frame's end runs)
     // the frame's end (frame_end_body): statistics shards, pinned-slot copy, sequence number
@@ -285,6 +307,8 @@ void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit
 // chunk 1 in one launch (grid: one workgroup per CU; returns at once when chunk 0 saturated every tile)
 struct Chunk1Params;
 void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t s);
+// the same as separate launches (for frames expected to leave tiles unsaturated), then the frame's end
+void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s);
 void launch_tile_sort(const TileSortParams& p, hipStream_t s);
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);
 void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void* out, hipStream_t s);

@@ -330,8 +330,10 @@ __device__ __forceinline__ bool pixel_rect(float cx, float cy, float hx, float h
 }
 
 // The same conservative cull from the Gaussian's cull plane (x, y, z, ||R(q) diag(s)||_F^2),
-// written at upload: false = provably invisible in this strip.
-__device__ __forceinline__ bool cull_keep(const ProjParams& p, float4 c, int row_lo, int row_hi, float& vz0) {
+// written at upload: false = provably invisible in this strip.  (cx0, cy0) +- hb bounds the pixel
+// centres its quad can cover.
+__device__ __forceinline__ bool cull_keep_box(const ProjParams& p, float4 c, int row_lo, int row_hi, float& vz0,
+                                              float& cx0, float& cy0, float& hb) {
 #pragma clang fp contract(off)
     const float x = c.x, y = c.y, z = c.z;
     vz0 = ((p.V[2] * x + p.V[6] * y) + p.V[10] * z) + p.V[14] * 1.0f;  // = project_footprint's vz
@@ -342,11 +344,15 @@ __device__ __forceinline__ bool cull_keep(const ProjParams& p, float4 c, int row
     const float cyc = ((p.PV[1] * x + p.PV[5] * y) + p.PV[9] * z) + p.PV[13];
     const float a = p.focal / vz0;
     const float trs = c.w * p.scale_mod * p.scale_mod;
-    const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w01_spec2 * trs + 0.6f)), 0.45f) * 1.02f + 2.0f;
-    const float cx0 = (cxc / cw + 1.0f) * (float)p.W * 0.5f;
-    const float cy0 = (1.0f - cyc / cw) * (float)p.H * 0.5f;
+    hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w01_spec2 * trs + 0.6f)), 0.45f) * 1.02f + 2.0f;
+    cx0 = (cxc / cw + 1.0f) * (float)p.W * 0.5f;
+    cy0 = (1.0f - cyc / cw) * (float)p.H * 0.5f;
     return !(cy0 + hb < (float)row_lo - 1.0f || cy0 - hb > (float)row_hi + 1.0f || cx0 + hb < -1.0f ||
              cx0 - hb > (float)p.W);
+}
+__device__ __forceinline__ bool cull_keep(const ProjParams& p, float4 c, int row_lo, int row_hi, float& vz0) {
+    float cx0, cy0, hb;
+    return cull_keep_box(p, c, row_lo, row_hi, vz0, cx0, cy0, hb);
 }
 
 // One Gaussian's projection: depth key, packed tile rect, tile count and projected record.
@@ -544,82 +550,48 @@ __device__ __forceinline__ void store_slot(const ProjParams& p, uint32_t slot, u
                                   __uint_as_float(o.bby));
 }
 
-// Chunk 1 (after chunk 0 left tiles unsaturated), or every visible Gaussian's per-Gaussian
-// record (rec_all, debug): from the cull plane, Gaussians at or past thresh that may be visible
-// are projected; the visible ones whose rect touches an unsaturated tile (the SAT of k_sat) get a
-// chunk-1 slot (slot_c1) with their record and colour.  Waves cover 64 consecutive Gaussians of
-// one projection partition: one counter add per wave.
+// Every visible Gaussian's per-Gaussian record (rec_all: the debug dump gs_debug_last_records):
+// the projection of k_project from the cull plane and geometry record, with its colour.
 __device__ __forceinline__ void records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
-    const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
-    const uint32_t lane = lane_id();
-    for (uint32_t i0 = blk * blockDim.x + (threadIdx.x & ~63u); i0 < p.n; i0 += nblk * blockDim.x) {
-        const uint32_t i = i0 + lane;
-        bool want = false;
+    for (uint32_t i = blk * blockDim.x + threadIdx.x; i < p.n; i += nblk * blockDim.x) {
         float vz;
-        if (i < p.n && cull_keep(p, p.cull[i], row_lo, row_hi, vz)) want = p.rec_all || sortable_key(vz) >= p.thresh;
         Proj o;
-        want = want && project_core(p, i, row_lo, row_hi, false, o);
-        if (want && !p.rec_all) {
-            const uint32_t pr = o.prect;
-            want = pr != kRectEmpty;
-            if (want && pr != kRectLarge) {
-                const uint32_t x0 = pr & 0xfffu, y0 = (pr >> 12) & 0xfffu;
-                const uint32_t x1 = x0 + ((pr >> 24) & 15u), y1 = y0 + (pr >> 28);
-                const uint32_t* a = p.sat + (uint64_t)(y0 - rb) * sw;
-                const uint32_t* b = p.sat + (uint64_t)(y1 + 1 - rb) * sw;
-                want = (b[x1 + 1] - b[x0]) - (a[x1 + 1] - a[x0]) != 0u;
-            }
-        }
-        if (p.rec_all) {
-            if (want) {
-                float4* r = rec_r01(p.rec, i);
-                r[0] = o.r0;
-                r[1] = o.r1;
-                p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles),
-                                          __uint_as_float(o.bbx), __uint_as_float(o.bby));
-                store_colour(p, i);
-            }
-            continue;
-        }
-        const uint64_t b = __ballot(want);
-        if (!b) continue;
-        uint32_t base = 0;
-        const uint32_t ntiles = want ? o.ntiles : 0u;
-        unsigned long long kt = ntiles;
-        for (int d = 32; d >= 1; d >>= 1) kt += __shfl_xor(kt, d, 64);
-        if (lane == 0) {
-            const uint32_t c = (uint32_t)__popcll(b);
-            base = atomicAdd(&p.c1[i0 / kProjTile], c);
-            StatShard* st = p.stats + (i0 >> 6) % kStatShards;
-            atomicAdd(&st->n_chunk[1], c);
-            atomicAdd(&st->k_total, kt);
-        }
-        base = __shfl(base, 0, 64);
-        if (want) {
-            const uint32_t slot = slot_c1(i0 / kProjTile, base + (uint32_t)__popcll(b & lanemask_lt()));
-            store_slot(p, slot, i, p.orig[i], o);
-            float4 c = colour_of(p, i);
-            c.w = __uint_as_float(o.key);
-            p.crec[3 * (uint64_t)slot + 2] = c;
-        }
+        if (!cull_keep(p, p.cull[i], row_lo, row_hi, vz) || !project_core(p, i, row_lo, row_hi, false, o)) continue;
+        float4* r = rec_r01(p.rec, i);
+        r[0] = o.r0;
+        r[1] = o.r1;
+        p.rec.r2[i] = make_float4(__uint_as_float(o.key), __uint_as_float(o.ntiles), __uint_as_float(o.bbx),
+                                  __uint_as_float(o.bby));
+        store_colour(p, i);
     }
 }
 
 __global__ __launch_bounds__(256) void k_records(ProjParams p) {
-    if (!p.rec_all && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
     records_body(p, blockIdx.x, gridDim.x);
 }
 
-// Can a Gaussian of partition b be a chunk-0 candidate of this frame (pass cull_keep with key <
-// thresh)?  The interval form of cull_keep over the partition's box, in float with slack far
-// above the roundings of both this bound and the per-Gaussian test (1e-4 of each term's
-// magnitude, 4 px on the quad bound): clip coordinates are affine (extremes at the 8 corners),
-// the ratios x/w, y/w take their extremes at the corners when every corner has w > 0, the quad
-// bound grows with focal / |vz| and ||R diag(s)||_F^2; key < thresh needs the box's smallest key.
-__device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, int row_hi) {
-    if (!b.nfin) return false;
+// The interval form of cull_keep over a partition's box, in float with slack far above the
+// roundings of both this bound and the per-Gaussian test (1e-4 of each term's magnitude, 4 px on
+// the quad bound): clip coordinates are affine (extremes at the 8 corners), the ratios x/w, y/w
+// take their extremes at the corners when every corner has w > 0, the quad bound grows with
+// focal / |vz| and ||R diag(s)||_F^2.  vis = false: no Gaussian of the box passes near/far;
+// [kmin, kmax] bounds the depth keys in the box; `bounded`: the pixel box [xl, xh] x [yl, yh]
+// (quad bound included) holds every pixel centre any quad of the box covers.
+struct PartTest {
+    bool vis, bounded;
+    uint32_t kmin, kmax;
+    float xl, xh, yl, yh;
+};
+__device__ PartTest part_test(const ProjParams& p, const PartBound& b) {
+    PartTest t;
+    t.vis = false;
+    t.bounded = false;
+    t.kmin = 0;
+    t.kmax = kSentinel;
+    t.xl = t.xh = t.yl = t.yh = 0.0f;
+    if (!b.nfin) return t;
     // coefficient rows: vz (V row 2), clip x, y, z, w (PV rows 0-3), column-major matrices
     const float C[5][4] = {{p.V[2], p.V[6], p.V[10], p.V[14]},
                            {p.PV[0], p.PV[4], p.PV[8], p.PV[12]},
@@ -641,18 +613,23 @@ __device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, 
         mn[k] = lo - sl[k];
         mx[k] = hi + sl[k];
     }
-    if (!(mx[4] > 0.0f)) return false;        // every clip w <= 0
-    if (!(mx[3] >= 0.0f)) return false;       // every clip z < 0 (near)
-    if (!(mn[3] <= mx[4])) return false;      // every clip z > w (far)
-    if (p.thresh != kSentinel) {              // the smallest depth key in the box
-        uint32_t kmin = 0;
-        if (mx[0] < 0.0f) kmin = sortable_key(mx[0]);
-        else if (mn[0] > 0.0f) kmin = sortable_key(mn[0]);
-        kmin = kmin > 64u ? kmin - 64u : 0u;
-        if (kmin >= p.thresh) return false;
+    if (!(mx[4] > 0.0f)) return t;        // every clip w <= 0
+    if (!(mx[3] >= 0.0f)) return t;       // every clip z < 0 (near)
+    if (!(mn[3] <= mx[4])) return t;      // every clip z > w (far)
+    t.vis = true;
+    // depth keys: negative vz keys grow with |vz|, non-negative ones with vz (sortable_key); 64
+    // keys of slack for the low-bit flip and rounding
+    if (mx[0] < 0.0f) {
+        t.kmin = sortable_key(mx[0]);
+        t.kmax = sortable_key(mn[0]);
+    } else {
+        t.kmin = mn[0] > 0.0f ? sortable_key(mn[0]) : 0u;
+        t.kmax = sortable_key(mx[0]);
     }
-    if (!(mn[4] > 0.0f)) return true;         // a corner with w <= 0: no ratio bound
-    if (!(mn[0] > 0.0f || mx[0] < 0.0f)) return true;  // vz crosses 0
+    t.kmin = t.kmin > 64u ? t.kmin - 64u : 0u;
+    t.kmax = t.kmax < kSentinel - 64u ? t.kmax + 64u : kSentinel;
+    if (!(mn[4] > 0.0f)) return t;         // a corner with w <= 0: no ratio bound
+    if (!(mn[0] > 0.0f || mx[0] < 0.0f)) return t;  // vz crosses 0
     float pxl = INFINITY, pxh = -INFINITY, pyl = INFINITY, pyh = -INFINITY;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {  // pixel centre of each corner
@@ -670,9 +647,141 @@ __device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, 
     // the corner ratios' own error: relative slack on the pixel extent plus 4 px
     const float hb = 4.0f * fmaxf(sqrtf(2.0f * (a * a * p.w01_spec2 * trs + 0.6f)), 0.45f) * 1.03f + 4.0f +
                      1e-3f * (float)max(p.W, p.H);
-    if (!(hb < 1e30f)) return true;
-    return !(pyh + hb < (float)row_lo - 1.0f || pyl - hb > (float)row_hi + 1.0f || pxh + hb < -1.0f ||
-             pxl - hb > (float)p.W);
+    if (!(hb < 1e30f)) return t;
+    t.bounded = true;
+    t.xl = pxl - hb;
+    t.xh = pxh + hb;
+    t.yl = pyl - hb;
+    t.yh = pyh + hb;
+    return t;
+}
+
+// Can a Gaussian of partition b be a chunk-0 candidate of this frame (pass cull_keep with key <
+// thresh)?
+__device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, int row_hi) {
+    const PartTest t = part_test(p, b);
+    if (!t.vis) return false;
+    if (p.thresh != kSentinel && t.kmin >= p.thresh) return false;
+    if (!t.bounded) return true;
+    return !(t.yh < (float)row_lo - 1.0f || t.yl > (float)row_hi + 1.0f || t.xh < -1.0f || t.xl > (float)p.W);
+}
+
+// Tiles of the strip that a pixel-centre box [xl, xh] x [yl, yh] (widened by 1 px) may touch;
+// false when it misses the strip.  NaN or infinite bounds widen to the strip's edges.
+__device__ __forceinline__ bool box_tiles(const ProjParams& p, float xl, float xh, float yl, float yh,
+                                          uint32_t& tx0, uint32_t& ty0, uint32_t& tx1, uint32_t& ty1) {
+    const float row_lo = (float)(p.tile_row_begin * kTile);
+    const float row_hi = (float)(min(p.tile_row_end * kTile, p.H) - 1);
+    if (yh < row_lo - 1.0f || yl > row_hi + 1.0f || xh < -1.0f || xl > (float)p.W) return false;
+    const float x0 = fminf(fmaxf(xl - 1.0f, 0.0f), (float)(p.W - 1));
+    const float x1 = fmaxf(fminf(xh + 1.0f, (float)(p.W - 1)), 0.0f);
+    const float y0 = fminf(fmaxf(yl - 1.0f, row_lo), row_hi);
+    const float y1 = fmaxf(fminf(yh + 1.0f, row_hi), row_lo);
+    tx0 = (uint32_t)x0 >> 4;
+    tx1 = (uint32_t)x1 >> 4;
+    ty0 = (uint32_t)y0 >> 4;
+    ty1 = (uint32_t)y1 >> 4;
+    return tx0 <= tx1 && ty0 <= ty1;
+}
+
+// Does the tile rectangle [tx0, tx1] x [ty0, ty1] (strip tile rows, absolute) hold a tile chunk 0
+// left unsaturated?  Two reads of the row prefix counts (unsat_rows_body) per row.
+__device__ __forceinline__ bool sat_any(const ProjParams& p, uint32_t tx0, uint32_t ty0, uint32_t tx1, uint32_t ty1) {
+    const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
+    for (uint32_t ty = ty0; ty <= ty1; ++ty) {
+        const uint32_t* row = p.sat + (uint64_t)(ty - rb) * sw;
+        if (row[tx1 + 1] != row[tx0]) return true;
+    }
+    return false;
+}
+
+// Can partition b hold a chunk-1 splat: a Gaussian at or past thresh whose quad may touch a tile
+// chunk 0 left unsaturated?
+__device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b) {
+    const PartTest t = part_test(p, b);
+    if (!t.vis || t.kmax < p.thresh) return false;
+    uint32_t tx0, ty0, tx1, ty1;
+    if (!t.bounded) {
+        tx0 = 0;
+        tx1 = (uint32_t)p.tiles_x - 1;
+        ty0 = (uint32_t)p.tile_row_begin;
+        ty1 = (uint32_t)p.tile_row_end - 1;
+    } else if (!box_tiles(p, t.xl, t.xh, t.yl, t.yh, tx0, ty0, tx1, ty1)) {
+        return false;
+    }
+    return sat_any(p, tx0, ty0, tx1, ty1);
+}
+
+// Chunk 1, step 1: every thread of the grid tests partitions (part_maybe_c1 against the row
+// prefix counts of the unsaturated tiles); the ones that may hold a chunk-1 splat are appended to plist (one
+// counter add per wave; list order does not matter: a partition's chunk-1 slots are its own).
+__device__ __forceinline__ void c1_parts_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
+    const uint32_t parts = proj_parts(p.n), lane = lane_id();
+    for (uint32_t q0 = blk * blockDim.x + (threadIdx.x & ~63u); q0 < parts; q0 += nblk * blockDim.x) {
+        const uint32_t q = q0 + lane;
+        const bool want = q < parts && part_maybe_c1(p, p.bounds[q]);
+        const uint64_t b = __ballot(want);
+        if (!b) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&p.ctl->c1_parts, (uint32_t)__popcll(b));
+        base = __shfl(base, 0, 64);
+        if (want) p.plist[base + (uint32_t)__popcll(b & lanemask_lt())] = q;
+    }
+}
+
+// Chunk 1, step 2: the listed partitions, one per workgroup iteration (waves take 64 consecutive
+// Gaussians).  From the cull plane, a Gaussian at or past thresh whose conservative box touches an
+// unsaturated tile is projected; the visible ones whose rect touches one get a chunk-1 slot
+// (slot_c1) with their record and colour.  The filter before project_core only skips Gaussians
+// the exact rect test after it would reject.
+__device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
+    const int row_lo = p.tile_row_begin * kTile;
+    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+    const uint32_t lane = lane_id(), nl = p.ctl->c1_parts;
+    for (uint32_t j = blk; j < nl; j += nblk) {
+        const uint32_t part = p.plist[j];
+        for (uint32_t r = threadIdx.x & ~63u; r < (uint32_t)kProjTile; r += blockDim.x) {
+            const uint32_t i0 = part * (uint32_t)kProjTile + r, i = i0 + lane;
+            bool want = false;
+            float vz, cx0, cy0, hb;
+            if (i < p.n && cull_keep_box(p, p.cull[i], row_lo, row_hi, vz, cx0, cy0, hb) && sortable_key(vz) >= p.thresh) {
+                uint32_t tx0, ty0, tx1, ty1;
+                want = box_tiles(p, cx0 - hb, cx0 + hb, cy0 - hb, cy0 + hb, tx0, ty0, tx1, ty1) &&
+                       sat_any(p, tx0, ty0, tx1, ty1);
+            }
+            Proj o;
+            want = want && project_core(p, i, row_lo, row_hi, false, o);
+            if (want) {
+                const uint32_t pr = o.prect;
+                want = pr != kRectEmpty;
+                if (want && pr != kRectLarge) {
+                    const uint32_t x0 = pr & 0xfffu, y0 = (pr >> 12) & 0xfffu;
+                    want = sat_any(p, x0, y0, x0 + ((pr >> 24) & 15u), y0 + (pr >> 28));
+                }
+            }
+            const uint64_t b = __ballot(want);
+            if (!b) continue;
+            uint32_t base = 0;
+            const uint32_t ntiles = want ? o.ntiles : 0u;
+            unsigned long long kt = ntiles;
+            for (int d = 32; d >= 1; d >>= 1) kt += __shfl_xor(kt, d, 64);
+            if (lane == 0) {
+                const uint32_t c = (uint32_t)__popcll(b);
+                base = atomicAdd(&p.c1[part], c);
+                StatShard* st = p.stats + (i0 >> 6) % kStatShards;
+                atomicAdd(&st->n_chunk[1], c);
+                atomicAdd(&st->k_total, kt);
+            }
+            base = __shfl(base, 0, 64);
+            if (want) {
+                const uint32_t slot = slot_c1(part, base + (uint32_t)__popcll(b & lanemask_lt()));
+                store_slot(p, slot, i, p.orig[i], o);
+                float4 c = colour_of(p, i);
+                c.w = __uint_as_float(o.key);
+                p.crec[3 * (uint64_t)slot + 2] = c;
+            }
+        }
+    }
 }
 
 // The frame's list of non-empty chunk-0 work units (k_cull appends them, kUnitShards shards).
@@ -1420,12 +1529,13 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
     __syncthreads();
 }
 
+template <bool LISTED>  // LISTED: chunk 0 (k_cull's unit list); else chunk 1 (every unit, counts from c1)
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     __shared__ uint32_t s_cnt[kBandTiles];
     __shared__ uint32_t s_pref[kBinMaxUnits + 1];
     __shared__ uint32_t s_tmp[kBinThreads / 64];
     if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
-    bin_count_body<kBinThreads, true>(p, blockIdx.x, s_cnt, s_pref, s_tmp);
+    bin_count_body<kBinThreads, LISTED>(p, blockIdx.x, s_cnt, s_pref, s_tmp);
 }
 
 // Per tile: exclusive prefix of its column of bmat over the partitions (in place) and the tile's
@@ -1461,6 +1571,31 @@ __device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, ui
             run += v[k];
         }
         if (w == 3) p.tbase[t] = run;
+    }
+    if (w == 3 && p.order) {  // the composite's tile order (chunk 0)
+        // XCD band x = tiles [x per, x per + per) is composited by the workgroups on XCD x in order;
+        // its tiles with more than heavy_len entries go first (counter order_n[0] of shard x), the
+        // rest from the band's end (order_n[1]), so the longest lists do not start in the last,
+        // partly filled round of workgroups.  One counter add per (wave, band, class).
+        const uint32_t per = (p.n_tiles + 7) >> 3;
+        const uint32_t x = ok ? t / per : 8u, band = min(per, p.n_tiles - min(p.n_tiles, x * per));
+        const bool heavy = ok && run > p.heavy_len;
+        const uint32_t tf = vb * kColTiles, tl = min(tf + kColTiles, p.n_tiles) - 1u;
+        for (uint32_t xb = tf / per; xb <= tl / per; ++xb) {  // the bands the wave's tiles fall in
+#pragma unroll
+            for (int cls = 0; cls < 2; ++cls) {
+                const bool mine = ok && x == xb && heavy == (cls == 0);
+                const uint64_t bb = __ballot(mine);
+                if (!bb) continue;
+                uint32_t base = 0;
+                if (lane == __builtin_ctzll(bb)) base = atomicAdd(&p.stats[xb].order_n[cls], (uint32_t)__popcll(bb));
+                base = __shfl(base, __builtin_ctzll(bb), 64);
+                if (mine) {
+                    const uint32_t q = base + (uint32_t)__popcll(bb & lanemask_lt());
+                    p.order[xb * per + (cls == 0 ? q : band - 1u - q)] = t;
+                }
+            }
+        }
     }
     __syncthreads();
 }
@@ -1623,6 +1758,7 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
     __syncthreads();
 }
 
+template <bool LISTED>
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_cur[kBandTiles];
     __shared__ uint32_t s_pref[kBinMaxUnits + 1];
@@ -1630,7 +1766,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     __shared__ uint32_t s_wide[kWideQueue];
     __shared__ uint32_t s_nw;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;
-    bin_emit_body<kBinThreads, true, true>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, &s_nw);
+    bin_emit_body<kBinThreads, true, LISTED>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, &s_nw);
 }
 
 // End of a frame: the statistic shards summed into FrameCtl (and zeroed), the saturation
@@ -1647,6 +1783,7 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
     stats[lane] = StatShard{};
     unsigned long long kt = sh.k_total;
     uint32_t nv = sh.n_vis, kmi = sh.key_min_inv, kma = sh.key_max, c0 = sh.n_chunk[0], c1 = sh.n_chunk[1];
+    uint32_t key = sh.sat_key;
     for (int d = 32; d >= 1; d >>= 1) {
         kt += __shfl_xor(kt, d, 64);
         nv += __shfl_xor(nv, d, 64);
@@ -1654,9 +1791,14 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
         c1 += __shfl_xor(c1, d, 64);
         kmi = max(kmi, (uint32_t)__shfl_xor(kmi, d, 64));
         kma = max(kma, (uint32_t)__shfl_xor(kma, d, 64));
+        key = max(key, (uint32_t)__shfl_xor(key, d, 64));
     }
-    uint32_t key = 0;
-    for (int k = 0; k < kHistShards; ++k) key = max(key, ctl->sat_key_shard[k]);
+#pragma unroll
+    for (int k = 0; k < kSatBuckets; ++k) {  // the shards' saturation histograms
+        uint32_t h = sh.sat_hist[k];
+        for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d, 64);
+        if (lane == 0) ctl->sat_hist[k] = h;
+    }
     if (lane == 0) {
         ctl->k_total = kt;
         ctl->n_vis = nv;
@@ -1671,46 +1813,35 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
     uint32_t* src = (uint32_t*)ctl;
     const uint32_t v = lane < kWords ? src[lane] : 0u;
     if (lane < kWords) ((uint32_t*)host_ctl)[lane] = v;
-    __threadfence_system();
+    // The slot and the sequence word are fine-grained host memory (uncached on the device): the
+    // slot's stores complete before the sequence store is issued (vmcnt(0)), and the host reads
+    // the slot only after it sees the sequence number.  No system-scope release: that would write
+    // the whole L2 back (the frame's dirty lines) for two cache-bypassing stores.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane < kWords) src[lane] = 0u;
 }
 
-// Summed-area table of the tiles chunk 0 left unsaturated (done == 0): one workgroup of NT
-// threads; row prefixes by waves, then column prefixes by threads, in `lds` when given and the
-// table fits, else in place in `sat`.
-template <int NT>
-__device__ __forceinline__ void sat_body(const uint8_t* __restrict__ done, int tiles_x, int rows, uint32_t* __restrict__ sat,
-                         uint32_t* lds) {
-    const uint32_t sw = (uint32_t)tiles_x + 1, words = sw * (uint32_t)(rows + 1);
-    uint32_t* t = (lds && words <= (uint32_t)kSatMaxWords) ? lds : sat;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    for (uint32_t x = tid; x < sw; x += NT) t[x] = 0;
-    for (int r = w; r < rows; r += NT / 64) {
-        uint32_t* row = t + (uint64_t)(r + 1) * sw;
+// Row prefix counts of the tiles chunk 0 left unsaturated (done == 0): row r of the strip at
+// sat[r * (tiles_x + 1)], entry x = unsaturated tiles among the row's first x.  One wave per row,
+// the rows spread over every wave of the grid (no sequential pass).
+__device__ __forceinline__ void unsat_rows_body(const uint8_t* __restrict__ done, int tiles_x, int rows,
+                                                uint32_t* __restrict__ sat) {
+    const uint32_t sw = (uint32_t)tiles_x + 1, lane = lane_id();
+    const uint32_t wpb = blockDim.x / 64, wave = blockIdx.x * wpb + (threadIdx.x >> 6);
+    for (uint32_t r = wave; r < (uint32_t)rows; r += gridDim.x * wpb) {
+        uint32_t* row = sat + (uint64_t)r * sw;
         uint32_t run = 0;
         if (lane == 0) row[0] = 0;
         for (int x0 = 0; x0 < tiles_x; x0 += 64) {
-            const int x = x0 + lane;
+            const int x = x0 + (int)lane;
             const uint32_t v = (x < tiles_x && !done[(uint64_t)r * tiles_x + x]) ? 1u : 0u;
             const uint64_t b = __ballot(v);
-            const uint32_t incl = run + __popcll(b & ((lanemask_lt() << 1) | 1ull));
-            if (x < tiles_x) row[x + 1] = incl;
+            if (x < tiles_x) row[x + 1] = run + __popcll(b & ((lanemask_lt() << 1) | 1ull));
             run += __popcll(b);
         }
     }
-    __syncthreads();
-    for (uint32_t x = tid; x < sw; x += NT) {
-        uint32_t acc = 0;
-        for (int r = 1; r <= rows; ++r) {
-            acc += t[(uint64_t)r * sw + x];
-            t[(uint64_t)r * sw + x] = acc;
-        }
-    }
-    __syncthreads();
-    if (t != sat)
-        for (uint32_t q = tid; q < words; q += NT) sat[q] = t[q];
 }
 
 // ============================================================================ k_tile_sort
@@ -2218,8 +2349,9 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 #endif
     const bool tile_done = __syncthreads_count(live0 || live1) == 0;
     if (tile_done && tid == 0 && n > 0) {  // saturation statistics for the chunk controller
-        atomicAdd(&p.ctl->sat_tiles[tile % kHistShards], 1u);
-        atomicMax(&p.ctl->sat_key_shard[tile % kHistShards], s_sat);
+        StatShard* sh = p.stats + tile % kStatShards;
+        atomicAdd(&sh->sat_hist[sat_bucket(s_sat, p.sat_base)], 1u);
+        atomicMax(&sh->sat_key, s_sat);
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {  // park the pixels for chunk 1
@@ -2255,8 +2387,8 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 template <bool FP16_TARGET>
 __global__ __launch_bounds__(128, 5) void k_composite(CompositeParams p) {
     const int per = (p.n_tiles + 7) >> 3;
-    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (tile < p.n_tiles) composite_tile<FP16_TARGET>(p, tile);
+    const int j = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // XCD band, position
+    if (j < p.n_tiles) composite_tile<FP16_TARGET>(p, p.order ? (int)p.order[j] : j);
 }
 
 // Quarter variant for frames with few tiles (row strips): 4 waves per tile, wave q owns the 8x8
@@ -2281,8 +2413,9 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
     uint32_t& s_sat = S.s_sat;
     const int tid = threadIdx.x;
     const int per = (p.n_tiles + 7) >> 3;
-    const int tile = (int)(vb & 7) * per + (int)(vb >> 3);
-    if (tile >= p.n_tiles) return;
+    const int j = (int)(vb & 7) * per + (int)(vb >> 3);  // XCD band, position
+    if (j >= p.n_tiles) return;
+    const int tile = p.order ? (int)p.order[j] : j;
     if (p.mode == kCompSecond && p.done[tile]) return;
     const int qw = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
@@ -2423,8 +2556,9 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
     }
     const bool tile_done = __syncthreads_count(live) == 0;
     if (tile_done && tid == 0 && n > 0) {
-        atomicAdd(&p.ctl->sat_tiles[tile % kHistShards], 1u);
-        atomicMax(&p.ctl->sat_key_shard[tile % kHistShards], s_sat);
+        StatShard* sh = p.stats + tile % kStatShards;
+        atomicAdd(&sh->sat_hist[sat_bucket(s_sat, p.sat_base)], 1u);
+        atomicMax(&sh->sat_key, s_sat);
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {
@@ -2458,8 +2592,9 @@ __global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
 // Chunk 1 as ONE launch.  It has work only in frames where chunk 0 left a tile unsaturated, so
 // its usual cost is this launch returning at once (eight gated launches cost ~35 us of floors).
 // When it runs, it is the chunk-0 pipeline's phases in order, separated by grid barriers, on a
-// grid of one 256-thread workgroup per CU (every workgroup co-resident): SAT of the unsaturated
-// tiles -> chunk-1 slots (records_body) -> bin count -> column scan -> tile scan -> emission ->
+// grid of one 256-thread workgroup per CU (every workgroup co-resident): row prefix counts of the unsaturated
+// tiles -> the partitions that may hold chunk-1 splats (c1_parts_body) -> their chunk-1 slots
+// (c1_records_body) -> bin count -> column scan -> tile scan -> emission ->
 // per-tile sort -> composite (kCompSecond) of the unsaturated tiles.
 
 // Grid barrier: bar[0] counts arrivals, bar[1] is a generation word that is never reset.  A
@@ -2496,15 +2631,30 @@ __device__ __forceinline__ void grid_sync(uint32_t* bar, FrameCtl* ctl) {
 constexpr size_t kBinLdsWords = kBandTiles + (kBinMaxUnits + 1) + 4 + kWideQueue + 1;
 constexpr size_t kChunk1Lds = std::max(std::max(kBinLdsWords * 4, sizeof(TsShared)), sizeof(CompQShared));
 
+#ifdef GS_C1_TIME
+// diagnostics builds only (make diag DIAGFLAGS=-DGS_C1_TIME): wall clock at k_chunk1's start and
+// after each of its grid barriers (workgroup 0), the last frame with chunk-1 work
+__device__ unsigned long long g_c1_time[16];
+#define C1_MARK(k) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_c1_time[k] = wall_clock64(); } while (0)
+#else
+#define C1_MARK(k) do { } while (0)
+#endif
+
 template <bool FP16_TARGET>
 __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* lds) {  // inlined: a
 // reference to the kernel argument must not force a copy of it into scratch
     FrameCtl* ctl = c.cp.ctl;
     const uint32_t G = gridDim.x, b = blockIdx.x;
-    if (b == 0) sat_body<256>(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat, nullptr);
+    C1_MARK(0);
+    unsat_rows_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat);
     grid_sync(c.bar, ctl);
-    records_body(c.pp, b, G);
+    C1_MARK(1);
+    c1_parts_body(c.pp, b, G);
     grid_sync(c.bar, ctl);
+    C1_MARK(2);
+    c1_records_body(c.pp, b, G);
+    grid_sync(c.bar, ctl);
+    C1_MARK(3);
     uint32_t* s_a = (uint32_t*)lds;
     uint32_t* s_pref = s_a + kBandTiles;
     uint32_t* s_tmp = s_pref + kBinMaxUnits + 1;
@@ -2513,18 +2663,24 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles);
     for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256, false>(c.bp, vb, s_a, s_pref, s_tmp);
     grid_sync(c.bar, ctl);
+    C1_MARK(4);
     const uint32_t ncol = (c.bp.n_tiles + kColTiles - 1) / kColTiles;
     for (uint32_t vb = b; vb < ncol; vb += G) colscan_body(c.bp, vb, (uint32_t(*)[kColTiles])lds);
     grid_sync(c.bar, ctl);
+    C1_MARK(5);
     if (b == 0) tile_scan_body<256>(c.bp, s_a);
     grid_sync(c.bar, ctl);
+    C1_MARK(6);
     for (uint32_t vb = b; vb < nbin; vb += G) bin_emit_body<256, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
     grid_sync(c.bar, ctl);
+    C1_MARK(7);
     const uint32_t ntb = 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
     for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body(c.tp, vb, *(TsShared*)lds);
     grid_sync(c.bar, ctl);
+    C1_MARK(8);
     for (uint32_t vb = b; vb < ntb; vb += G) composite_q_body<FP16_TARGET>(c.cp, vb, *(CompQShared*)lds);
-    grid_sync(c.bar, ctl);  // every phase done before the frame's end reads FrameCtl
+    grid_sync(c.bar, ctl);
+    C1_MARK(9);  // every phase done before the frame's end reads FrameCtl
 }
 
 template <bool FP16_TARGET>
@@ -2538,6 +2694,26 @@ __global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
     (void)G;
 }
 
+
+// Chunk 1 as separate launches, for frames the host expects to leave tiles unsaturated (a recent
+// frame did): the phases of chunk1_phases at full occupancy with a kernel boundary (~1.5 us) in
+// place of each grid barrier; every launch returns at once when chunk 0 saturated every tile.
+// Binning, per-tile sort and composite are the chunk-0 kernels with chunk-1 parameters.
+__global__ __launch_bounds__(256) void k_c1_rows(Chunk1Params c) {
+    if (c.cp.ctl->not_done == 0) return;
+    unsat_rows_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat);
+}
+__global__ __launch_bounds__(256) void k_c1_parts(ProjParams p) {
+    if (p.ctl->not_done == 0) return;
+    c1_parts_body(p, blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(256) void k_c1_records(ProjParams p) {
+    if (p.ctl->not_done == 0) return;
+    c1_records_body(p, blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(64) void k_frame_end(Chunk1Params c) {
+    frame_end_body(c.cp.ctl, c.stats, c.host_ctl, c.host_seq, c.seq);
+}
 
 // ============================================================================ ref_quirks
 // The reference's init-sort pass runs dispatchWorkgroups(max(N/8, 8)) workgroups of 8 threads
@@ -2722,9 +2898,15 @@ void launch_sort_pass(const SortPass& p, hipStream_t s) {
 void launch_bin(const BinParams& p, hipStream_t s) {
     if (p.n_tiles == 0) return;
     const unsigned grid = kBinParts * bin_bands(p.n_tiles);
-    hipLaunchKernelGGL(k_bin_count, dim3(grid), dim3(kBinThreads), 0, s, p);
+    if (p.units)
+        hipLaunchKernelGGL(k_bin_count<true>, dim3(grid), dim3(kBinThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_bin_count<false>, dim3(grid), dim3(kBinThreads), 0, s, p);
     hipLaunchKernelGGL(k_bin_colscan, dim3((p.n_tiles + kColTiles - 1) / kColTiles), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(k_bin_emit, dim3(grid), dim3(kBinThreads), 0, s, p);  // scans the tile totals itself
+    if (p.units)  // each workgroup scans the tile totals itself
+        hipLaunchKernelGGL(k_bin_emit<true>, dim3(grid), dim3(kBinThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_bin_emit<false>, dim3(grid), dim3(kBinThreads), 0, s, p);
 }
 void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return;
@@ -2737,6 +2919,24 @@ void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t 
         hipLaunchKernelGGL(k_chunk1<true>, dim3(grid), dim3(256), 0, s, c);
     else
         hipLaunchKernelGGL(k_chunk1<false>, dim3(grid), dim3(256), 0, s, c);
+}
+void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
+    if (c.two_chunks && c.cp.n_tiles > 0) {
+        const unsigned rows_grid = (unsigned)((c.bp.rows + 3) / 4);
+        hipLaunchKernelGGL(k_c1_rows, dim3(rows_grid), dim3(256), 0, s, c);
+        const unsigned parts = proj_parts(c.pp.n);
+        hipLaunchKernelGGL(k_c1_parts, dim3(std::max(1u, (parts + 255) / 256)), dim3(256), 0, s, c.pp);
+        hipLaunchKernelGGL(k_c1_records, dim3(kMaxGrid), dim3(256), 0, s, c.pp);
+        launch_bin(c.bp, s);
+        launch_tile_sort(c.tp, s);
+        // the unsaturated tiles only, each with a long list: 4 waves per tile at any frame size
+        const unsigned grid = 8u * (unsigned)((c.cp.n_tiles + 7) / 8);
+        if (accum_fp16)
+            hipLaunchKernelGGL(k_composite_q<true>, dim3(grid), dim3(256), 0, s, c.cp);
+        else
+            hipLaunchKernelGGL(k_composite_q<false>, dim3(grid), dim3(256), 0, s, c.cp);
+    }
+    hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, c);
 }
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;
@@ -2756,6 +2956,11 @@ void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
 
 }  // namespace gs
 
+#ifdef GS_C1_TIME
+extern "C" int gs_diag_c1_times(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_c1_time), 16 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef GS_COMP_DIAG
 extern "C" int gs_diag_comp_times(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_comp_time), (size_t)n * 24) == hipSuccess ? 0 : -1;

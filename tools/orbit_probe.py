@@ -21,8 +21,9 @@ def main():
     sc = gs.Scene(ctx, aos, N, 16)
     buf = gs.DeviceBuffer(H * W * 8)
     uo = [orbit_uniforms(W, H, k) for k in range(steps)]
-    for name, cf, timing in [("adaptive", 0.0, 0), ("one_chunk", 1.0, 0), ("adaptive_staged", 0.0, 1),
-                             ("one_chunk_staged", 1.0, 1)]:
+    modes = [("adaptive", 0.0, 0), ("one_chunk", 1.0, 0), ("adaptive_staged", 0.0, 1), ("one_chunk_staged", 1.0, 1)]
+    only = os.environ.get("MODE")  # one mode only (e.g. under rocprofv3)
+    for name, cf, timing in [m for m in modes if not only or m[0] == only]:
         o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, chunk_fraction=cf, timing=timing)
         for k in range(5):
             sc.render_device(uo[k], W, H, buf.ptr.value, buf.nbytes, None, o)
