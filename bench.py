@@ -107,6 +107,26 @@ def cpu_baseline(aos, n, W, H, u, budget_s=10.0, max_frames=10):
                                                                        time.perf_counter() - t_all)}
 
 
+def node_fps(n, seed, W, H, frames=100):
+    """The Node drop-in's frame rate (tools/node_fps.js: the reference's Renderer frame loop through
+    the N-API addon, same scene and camera; device-resident frames and host readback), or None
+    when node or the addon is absent."""
+    import shutil
+    import subprocess
+    addon_path = os.path.join(ROOT, "gaussian-splatting-web_amd", "lib", "gsplat_napi.node")
+    if not shutil.which("node") or not os.path.exists(addon_path):
+        return None
+    try:
+        r = subprocess.run(["node", os.path.join(ROOT, "tools", "node_fps.js"), str(n), str(seed), str(W), str(H),
+                            str(frames)], capture_output=True, text=True, timeout=180)
+        if r.returncode != 0:
+            return {"error": r.stderr[-300:]}
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        return {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}
+    except (subprocess.TimeoutExpired, ValueError) as e:
+        return {"error": str(e)[:300]}
+
+
 def orbit_uniforms(W, H, k, period=60):
     """A moving camera for the orbit loop: at the origin, yaw swinging +-25 deg and pitch +-8 deg
     around the bench view (-z), a new view every frame; part of the screen leaves the scene's
@@ -354,7 +374,10 @@ def main():
                                "peak": VALU_PEAK / 1e9, "unit": "G wave-instr/s",
                                "frac": round(valu / (stages[dom] * 1e-3) / VALU_PEAK, 4),
                                "source": traffic_src} if valu else None),
+            # SURVEY §8d's byte MODEL at the measured frame time: not bytes this design moves (see
+            # DESIGN §4 and the PMC traffic in profiles/), so not an HBM fraction
             "frame_roofline": {"bytes": int(fb), "frac": round(fb / (ms * 1e-3) / (world * HBM_PEAK), 4),
+                               "kind": "model bytes (SURVEY 8d), not measured traffic",
                                "compulsory_frac": round((236 * N + 16 * W * H) / (ms * 1e-3) / (world * HBM_PEAK), 4),
                                "formula": "236N + 148N_vis + 48K + 16WH (SURVEY 8d)"},
             "cpu_baseline": None,
@@ -362,10 +385,13 @@ def main():
         out.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(aos, N, W, H, u)
-        print(json.dumps(out), flush=True)
 
     scene.close()
     ctx.close()
+    if rank == 0:
+        if world == 1 and not args.no_extra:
+            out["node_fps"] = node_fps(N, seed, W, H)
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -306,6 +306,80 @@ napi_value RenderAsync(napi_env env, napi_callback_info info) {
     return promise;
 }
 
+// ---- device-resident frames (the reference's GPU framebuffer texture) ----------------------
+// fbAlloc(ctx, bytes) -> handle; fbFree(ctx, fb); fbRead(ctx, fb, typedArray): waits for the
+// context's frames, then copies the array's byte length out of the framebuffer.
+napi_value FbAlloc(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    get_args(env, info, 2, argv);
+    gs_ctx* c;
+    if (!get_handle(env, argv[0], &c)) return throw_gs(env, GS_ERR_INVALID, "fbAlloc: bad context");
+    void* dev = nullptr;
+    const int rc = gs_framebuffer_alloc(c, (uint64_t)num(env, argv[1], 0), &dev);
+    if (rc) return throw_gs(env, rc, "gs_framebuffer_alloc");
+    napi_value r;
+    NAPI_OK(napi_create_external(env, dev, nullptr, nullptr, &r));
+    return r;
+}
+
+napi_value FbFree(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    get_args(env, info, 2, argv);
+    gs_ctx* c;
+    void* dev;
+    if (!get_handle(env, argv[0], &c) || !get_handle(env, argv[1], &dev))
+        return throw_gs(env, GS_ERR_INVALID, "fbFree: bad handle");
+    const int rc = gs_framebuffer_free(c, dev);
+    if (rc) return throw_gs(env, rc, "gs_framebuffer_free");
+    return undefined(env);
+}
+
+napi_value FbRead(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    get_args(env, info, 3, argv);
+    gs_ctx* c;
+    void *dev, *host;
+    size_t len;
+    if (!get_handle(env, argv[0], &c) || !get_handle(env, argv[1], &dev))
+        return throw_gs(env, GS_ERR_INVALID, "fbRead: bad handle");
+    if (!get_bytes(env, argv[2], &host, &len)) return throw_gs(env, GS_ERR_INVALID, "fbRead: target must be a TypedArray");
+    const int rc = gs_framebuffer_read(c, dev, host, len);
+    if (rc) return throw_gs(env, rc, "gs_framebuffer_read");
+    return undefined(env);
+}
+
+// renderDevice(ctx, scene, uniforms, W, H, opts, fb, fbBytes): enqueues the frame into the device
+// framebuffer and returns (frames in flight; errors of earlier frames are thrown here).
+napi_value RenderDevice(napi_env env, napi_callback_info info) {
+    napi_value argv[8];
+    get_args(env, info, 8, argv);
+    RenderArgs a;
+    napi_value args7[7] = {argv[0], argv[1], argv[2], argv[3], argv[4], argv[5], nullptr};
+    napi_get_null(env, &args7[6]);
+    bool pending = false;
+    if (!parse_render(env, args7, &a) || (napi_is_exception_pending(env, &pending), pending)) return nullptr;
+    void* dev;
+    if (!get_handle(env, argv[6], &dev)) return throw_gs(env, GS_ERR_INVALID, "renderDevice: bad framebuffer");
+    const int rc = gs_render_device(a.c, a.s, a.uni, a.W, a.H, &a.opts, dev, (uint64_t)num(env, argv[7], 0), nullptr);
+    if (rc) return throw_gs(env, rc, "gs_render_device");
+    return undefined(env);
+}
+
+// presentDevice(ctx, fb, fbFormat, W, H, outFormat, outFb, outBytes): PostProcessRenderer on the device
+napi_value PresentDevice(napi_env env, napi_callback_info info) {
+    napi_value argv[8];
+    get_args(env, info, 8, argv);
+    gs_ctx* c;
+    void *fb, *out;
+    if (!get_handle(env, argv[0], &c) || !get_handle(env, argv[1], &fb) || !get_handle(env, argv[6], &out))
+        return throw_gs(env, GS_ERR_INVALID, "presentDevice: bad handle");
+    const int rc = gs_present_device(c, fb, (int)num(env, argv[2], 0), (int)num(env, argv[3], 0),
+                                     (int)num(env, argv[4], 0), (int)num(env, argv[5], 0), out,
+                                     (uint64_t)num(env, argv[7], 0), nullptr);
+    if (rc) return throw_gs(env, rc, "gs_present_device");
+    return undefined(env);
+}
+
 napi_value Timings(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     get_args(env, info, 1, argv);
@@ -473,6 +547,21 @@ napi_value PackUniforms(napi_env env, napi_callback_info info) {
 }
 
 // PackedGaussians(arrayBuffer) (src/ply.ts:200-355): {aos, numGaussians, shDegree, nShCoeffs, minPos, maxPos}
+// synthAos(n, seed, W, H) -> ArrayBuffer of n SH-degree-3 records (SURVEY §8d generator)
+napi_value SynthAos(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    get_args(env, info, 4, argv);
+    const double n = num(env, argv[0], -1);
+    if (!(n >= 0) || n * 320.0 > 2147483647.0) return throw_gs(env, GS_ERR_INVALID, "synthAos: bad count");
+    void* p = nullptr;
+    napi_value ab;
+    NAPI_OK(napi_create_arraybuffer(env, (size_t)n * 320, &p, &ab));
+    const int rc = gs_synth_aos((uint64_t)n, (uint64_t)num(env, argv[1], 1), (int)num(env, argv[2], 1920),
+                                (int)num(env, argv[3], 1080), p);
+    if (rc) return throw_gs(env, rc, "gs_synth_aos");
+    return ab;
+}
+
 napi_value PlyParse(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     get_args(env, info, 1, argv);
@@ -556,7 +645,8 @@ napi_value Init(napi_env env, napi_value exports) {
         {"sceneFree", SceneFree}, {"render", Render}, {"renderAsync", RenderAsync},
         {"timings", Timings}, {"timingsReset", TimingsReset}, {"sync", Sync}, {"present", Present},
         {"lookAt", LookAt}, {"perspective", Perspective}, {"cameraPosition", CameraPosition},
-        {"cameraFromJSON", CameraFromJSON},
+        {"cameraFromJSON", CameraFromJSON}, {"fbAlloc", FbAlloc}, {"fbFree", FbFree}, {"fbRead", FbRead},
+        {"renderDevice", RenderDevice}, {"presentDevice", PresentDevice}, {"synthAos", SynthAos},
         {"packUniforms", PackUniforms}, {"stripRows", StripRows}, {"plyParse", PlyParse}, {"encodePng", EncodePng},
     };
     for (const auto& f : fns) {

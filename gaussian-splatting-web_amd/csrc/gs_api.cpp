@@ -1315,6 +1315,45 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
     });
 }
 
+int gs_framebuffer_alloc(gs_ctx* c, uint64_t bytes, void** out) {
+    return guarded([&] {
+        if (!c || !out || bytes == 0) throw GsError(GS_ERR_INVALID, "null ctx/out or zero bytes");
+        *out = nullptr;
+        gs_ctx* d = c->members.empty() ? c : c->members[0];
+        HIPCHK(hipSetDevice(d->device));
+        if (hipMalloc(out, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            *out = nullptr;
+            throw GsError(GS_ERR_OOM, "framebuffer allocation failed");
+        }
+        return GS_OK;
+    });
+}
+
+int gs_framebuffer_free(gs_ctx* c, void* dev) {
+    return guarded([&] {
+        if (!c) throw GsError(GS_ERR_INVALID, "null ctx");
+        if (!dev) return GS_OK;
+        gs_ctx* d = c->members.empty() ? c : c->members[0];
+        HIPCHK(hipSetDevice(d->device));
+        HIPCHK(hipDeviceSynchronize());  // no frame in flight may still write it
+        HIPCHK(hipFree(dev));
+        return GS_OK;
+    });
+}
+
+int gs_framebuffer_read(gs_ctx* c, const void* dev, void* host, uint64_t bytes) {
+    return guarded([&] {
+        if (!c || !dev || !host) throw GsError(GS_ERR_INVALID, "null argument");
+        const int rc = gs_sync(c);
+        if (rc != GS_OK) throw GsError(rc, gs_last_error());
+        gs_ctx* d = c->members.empty() ? c : c->members[0];
+        HIPCHK(hipSetDevice(d->device));
+        HIPCHK(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
+        return GS_OK;
+    });
+}
+
 int gs_sync(gs_ctx* c) {
     return guarded([&] {
         if (!c) throw GsError(GS_ERR_INVALID, "null ctx");

@@ -27,7 +27,8 @@ GS_OK, GS_ERR_INVALID, GS_ERR_NO_DEVICE, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPOR
 EXPORTED_SYMBOLS = (
     "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy", "gs_ctx_info",
     "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows",
-    "gs_render", "gs_render_device", "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
+    "gs_render", "gs_render_device", "gs_framebuffer_alloc", "gs_framebuffer_free", "gs_framebuffer_read",
+    "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
     "gs_present_device", "gs_encode_png", "gs_look_at",
     "gs_perspective", "gs_camera_position", "gs_camera_from_json", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
     "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records", "gs_debug_last_slots",
@@ -111,6 +112,9 @@ def lib():
         L.gs_strip_rows.argtypes = [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]
         L.gs_render.argtypes = [P, P, P, I, I, ctypes.POINTER(GsOpts), P]
         L.gs_render_device.argtypes = [P, P, P, I, I, ctypes.POINTER(GsOpts), P, U64, P]
+        L.gs_framebuffer_alloc.argtypes = [P, U64, ctypes.POINTER(ctypes.c_void_p)]
+        L.gs_framebuffer_free.argtypes = [P, P]
+        L.gs_framebuffer_read.argtypes = [P, P, P, U64]
         L.gs_timings.argtypes = [P, ctypes.POINTER(GsStats)]
         L.gs_timings_reset.argtypes = [P]
         L.gs_sync.argtypes = [P]

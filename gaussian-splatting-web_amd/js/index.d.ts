@@ -13,6 +13,7 @@ export interface RenderOptions {
     stripCount?: number;
     timing?: number;
     chunkFraction?: number;  // 0 = adaptive
+    deviceResident?: boolean;  // frames stay in HBM (renderDevice); Renderer.readback() copies one out
 }
 
 export declare class GpuContext {
@@ -98,7 +99,8 @@ export declare class Renderer {
     interactiveCamera: InteractiveCameraLike;
     context: GpuContext;
     numGaussians: number;
-    framebuffer: Float32Array | Uint16Array;  // SimpleRender.framebuffer contents
+    framebuffer: Float32Array | Uint16Array | null;  // SimpleRender.framebuffer contents (null when deviceResident)
+    deviceFramebuffer: unknown;  // deviceResident: the framebuffer in HBM (addon handle)
     frames: number;
     static requestContext(gaussians: PackedGaussians, deviceIndex?: number | number[]): Promise<GpuContext>;
     constructor(canvas: HeadlessCanvas, interactiveCamera: InteractiveCameraLike, gaussians: PackedGaussians,
@@ -106,6 +108,8 @@ export declare class Renderer {
     /** Resolves after the next frame (src/renderer.ts:103-107). */
     destroy(): Promise<void>;
     resize(): void;
+    /** deviceResident: the last frame copied to host memory once the frames in flight are done. */
+    readback(target?: Float32Array | Uint16Array): Float32Array | Uint16Array;
     draw(nextFrameCallback: () => void): void;
     animate(forceDraw?: boolean): void;
     timings(): Record<string, number>;

@@ -180,7 +180,10 @@ class Renderer {
         this.lastDraw = now();
         this.numGaussians = gaussians.numGaussians;
         this.destroyCallback = null;
-        this.opts = Object.assign({accum: GS_ACCUM_FP32, outFormat: GS_OUT_RGBA_F32, tMin: 1e-4}, options);
+        // options: accum, outFormat, tMin, deviceResident (frames stay in HBM; readback() on request)
+        this.opts = Object.assign({accum: GS_ACCUM_FP32, outFormat: GS_OUT_RGBA_F32, tMin: 1e-4, deviceResident: false},
+                                  options);
+        this.deviceFramebuffer = null;
         this.frames = 0;
         // the AoS record buffer is borrowed for this call only (copied into HBM as SoA)
         this.scene = addon().sceneUpload(context.device, gaussians.gaussiansBuffer, gaussians.numGaussians,
@@ -191,6 +194,8 @@ class Renderer {
 
     destroyImpl() {
         if (this.destroyCallback === null) throw new Error('destroyImpl called without destroyCallback set!');
+        if (this.deviceFramebuffer && this.context.device) addon().fbFree(this.context.device, this.deviceFramebuffer);
+        this.deviceFramebuffer = null;
         if (this.scene && this.context.device) addon().sceneFree(this.scene);
         this.scene = null;
         this.context.destroy();
@@ -202,13 +207,47 @@ class Renderer {
         this.width = this.canvas.width;
         this.height = this.canvas.height;
         const px = this.width * this.height * 4;
+        if (this.opts.deviceResident) {
+            // the frame stays in HBM like the reference's framebuffer texture; readback() copies it
+            if (this.deviceFramebuffer) addon().fbFree(this.context.device, this.deviceFramebuffer);
+            this.fbBytes = px * (this.opts.outFormat === GS_OUT_RGBA_F16 ? 2 : 4);
+            this.deviceFramebuffer = addon().fbAlloc(this.context.device, this.fbBytes);
+            this.framebuffer = null;
+            this.image = null;
+            return;
+        }
         this.framebuffer = this.opts.outFormat === GS_OUT_RGBA_F16 ? new Uint16Array(px) : new Float32Array(px);
         this.image = this.canvas.present ? new Float32Array(px) : null;
+    }
+
+    // device-resident mode: the last frame's framebuffer (W x H RGBA, f32 or f16 as outFormat) copied
+    // into `target` (allocated when absent) once the frames in flight are done
+    readback(target) {
+        if (!this.deviceFramebuffer) throw new Error('readback: the renderer is not device-resident');
+        const px = this.width * this.height * 4;
+        const out = target || (this.opts.outFormat === GS_OUT_RGBA_F16 ? new Uint16Array(px) : new Float32Array(px));
+        addon().fbRead(this.context.device, this.deviceFramebuffer, out);
+        return out;
     }
 
     // render one frame (depth keys + sort + tile composite), then schedule nextFrameCallback
     draw(nextFrameCallback) {
         if (this.canvas.width !== this.width || this.canvas.height !== this.height) this.resize();
+        if (this.opts.deviceResident) {
+            // enqueue the frame (frames in flight, no readback) and go on: the reference's draw
+            // submits to the GPU queue and returns the same way
+            try {
+                addon().renderDevice(this.context.device, this.scene, this.uniforms, this.width, this.height, this.opts,
+                                     this.deviceFramebuffer, this.fbBytes);
+                this.frames++;
+                if (typeof this.canvas.onFrame === 'function') this.canvas.onFrame(this);
+            } catch (err) {
+                this.lastError = err;
+                if (typeof this.canvas.onError === 'function') this.canvas.onError(err);
+            }
+            raf(nextFrameCallback);
+            return;
+        }
         addon().renderAsync(this.context.device, this.scene, this.uniforms, this.width, this.height, this.opts,
                             this.framebuffer).then(() => {
             this.frames++;

@@ -164,6 +164,16 @@ int gs_render(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int W, int 
 int gs_render_device(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int W, int H,
                      const gs_opts* opts, void* out_dev, uint64_t out_bytes, void* hip_stream);
 
+/* Device framebuffers for gs_render_device / gs_present_device: the GPU-resident render target
+ * of the reference (SimpleRender's rgba16float `framebuffer` texture, src/simple_render.ts:499-505,
+ * read by the present pass) -- frames stay in HBM and are read back only on request.
+ * gs_framebuffer_alloc: `bytes` of device memory on the context's device (a group's first).
+ * gs_framebuffer_read: waits for the context's frames (gs_sync semantics, frame errors included),
+ * then copies `bytes` to host memory. */
+int gs_framebuffer_alloc(gs_ctx* ctx, uint64_t bytes, void** out_dev);
+int gs_framebuffer_free(gs_ctx* ctx, void* dev);
+int gs_framebuffer_read(gs_ctx* ctx, const void* dev, void* host, uint64_t bytes);
+
 int gs_timings(gs_ctx* ctx, gs_stats* out_stats);
 int gs_timings_reset(gs_ctx* ctx);
 int gs_sync(gs_ctx* ctx);

@@ -19,7 +19,8 @@ pytestmark = pytest.mark.skipif(not NODE or not os.path.exists(ADDON), reason="n
 
 EXPORTS = sorted(["abiVersion", "lastError", "deviceCount", "ctxCreate", "ctxDestroy", "sceneUpload", "sceneFree",
                   "render", "renderAsync", "timings", "timingsReset", "sync", "present", "lookAt", "perspective",
-                  "cameraPosition", "cameraFromJSON", "packUniforms", "stripRows", "plyParse", "encodePng"])
+                  "cameraPosition", "cameraFromJSON", "fbAlloc", "fbFree", "fbRead", "renderDevice", "presentDevice",
+                  "synthAos", "packUniforms", "stripRows", "plyParse", "encodePng"])
 
 
 def run_node(*args, timeout=120):
@@ -109,3 +110,13 @@ def test_node_frame_loop_gpu(tmp_path):
     assert np.array_equal(pres, gs.present(direct, W, H))
     sc.close()
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_node_device_resident_frame_loop():
+    """Renderer({deviceResident: true}): frames stay in HBM (renderDevice, frames in flight) and
+    readback() returns the same image as the host-readback loop; both frame rates are measured in JS
+    (tools/node_fps.js, also reported by bench.py as node_fps)."""
+    out = run_node(os.path.join(ROOT, "tools", "node_fps.js"), "40000", "3", "320", "200", "20", timeout=300)
+    assert out["same_image"] is True
+    assert out["device_resident_fps"] > 0 and out["host_readback_fps"] > 0

@@ -130,3 +130,24 @@ def test_present_device_matches_host(gpu_ctx, fb_format):
     assert bad == gs.GS_ERR_INVALID
     fb.free()
     sc.close()
+
+
+@pytest.mark.gpu
+def test_framebuffer_abi_roundtrip(gpu_ctx):
+    """gs_framebuffer_alloc / gs_render_device / gs_framebuffer_read / gs_framebuffer_free: a
+    device-resident frame read back equals the host-output render of the same frame."""
+    import ctypes
+    W, H, n = 256, 160, 30_000
+    aos = gs.synth_aos(n, 12, W, H)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    L = gs.lib()
+    dev = ctypes.c_void_p()
+    assert L.gs_framebuffer_alloc(gpu_ctx.handle, W * H * 16, ctypes.byref(dev)) == gs.GS_OK
+    assert L.gs_framebuffer_alloc(gpu_ctx.handle, 0, ctypes.byref(ctypes.c_void_p())) == gs.GS_ERR_INVALID
+    for _ in range(3):  # frames in flight into the same buffer
+        sc.render_device(u, W, H, dev.value, W * H * 16)
+    got = np.empty((H, W, 4), np.float32)
+    assert L.gs_framebuffer_read(gpu_ctx.handle, dev, got.ctypes.data_as(ctypes.c_void_p), got.nbytes) == gs.GS_OK
+    assert np.array_equal(got, sc.render(u, W, H))
+    assert L.gs_framebuffer_free(gpu_ctx.handle, dev) == gs.GS_OK

@@ -1,0 +1,59 @@
+'use strict';
+// Frame rate of the Node drop-in: the reference's frame loop (GpuContext.create -> new Renderer ->
+// animate/draw via the rAF shim) on the seeded synthetic scene at the bench camera, every frame
+// forced through the full path (camera marked dirty), measured in JS from the first frame's
+// callback to the last.  Two modes: deviceResident (frames stay in HBM, as the reference's
+// framebuffer texture; frames in flight) and host readback (renderAsync + a D2H copy per frame).
+// The device-resident mode's last frame is read back and compared with the host mode's.
+// Usage: node tools/node_fps.js <n> <seed> <W> <H> <frames>   -> one JSON line
+const path = require('path');
+const gs = require(path.join(__dirname, '..', 'gaussian-splatting-web_amd', 'js'));
+
+async function run(gaussians, W, H, frames, options) {
+    const a = gs.addon();
+    const cam = gs.Camera.lookAt([0, 0, 0], [0, 0, -1], W, H);
+    const icam = new gs.HeadlessCamera(cam);
+    const context = await gs.Renderer.requestContext(gaussians, 0);
+    const canvas = {width: W, height: H};
+    let seen = 0, t0 = 0n, t1 = 0n;
+    const done = new Promise((resolve, reject) => {
+        canvas.onError = reject;
+        canvas.onFrame = (r) => {
+            seen++;
+            if (seen === 5) t0 = process.hrtime.bigint();  // 5 warm-up frames
+            if (seen < frames + 5) icam.setDirty();
+            else { t1 = process.hrtime.bigint(); resolve(r); }
+        };
+    });
+    const renderer = new gs.Renderer(canvas, icam, gaussians, context, null, options);
+    const r = await done;
+    let img;
+    if (options.deviceResident) {
+        img = r.readback();  // waits for the frames in flight
+        t1 = process.hrtime.bigint();
+    } else {
+        img = r.framebuffer.slice();
+    }
+    const ms = Number(t1 - t0) / 1e6 / frames;
+    await renderer.destroy();
+    void a;
+    return {ms, img};
+}
+
+async function main() {
+    const [n, seed, W, H, frames] = process.argv.slice(2).map(Number);
+    const buf = gs.addon().synthAos(n, seed, W, H);
+    const gaussians = new gs.PackedGaussians(buf, n, 16);
+    const opts = {outFormat: gs.GS_OUT_RGBA_F16};
+    const dev = await run(gaussians, W, H, frames, Object.assign({deviceResident: true}, opts));
+    const host = await run(gaussians, W, H, frames, opts);
+    let same = dev.img.length === host.img.length;
+    for (let i = 0; same && i < dev.img.length; ++i) same = dev.img[i] === host.img[i];
+    console.log(JSON.stringify({n, W, H, frames, device_resident_fps: 1000 / dev.ms, device_resident_ms: dev.ms,
+                                host_readback_fps: 1000 / host.ms, host_readback_ms: host.ms, same_image: same}));
+}
+
+main().catch((e) => {
+    console.error('FAILED', e);
+    process.exit(1);
+});
