@@ -832,7 +832,7 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
     __shared__ unsigned long long s_mask[kProjRounds][kProjThreads / 64];
     __shared__ uint32_t s_base[kProjRounds][kProjThreads / 64];
-    __shared__ uint32_t s_total;
+    __shared__ uint32_t s_total, s_maybe;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     if (tid == 0) { s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
     uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
@@ -840,13 +840,19 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = proj_parts(p.n), ucap = unit_shard_cap(parts);
     for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        // the partition test first (part_maybe on its bound, uniform): a ruled-out partition
-        // costs one 32-B read; the chunk counts are zeroed here (c1: k_records adds to it)
-        const bool maybe = part_maybe(p, p.bounds[part], row_lo, row_hi);
-        if (tid == 0) {
-            p.c1[part] = 0;
-            if (!maybe) p.c0[part] = 0;
+        // the partition test first (part_maybe on its bound, by wave 0 alone): a ruled-out
+        // partition costs one 32-B read; the chunk counts are zeroed here (c1: chunk 1 adds to it)
+        if (w == 0) {
+            const bool m = part_maybe(p, p.bounds[part], row_lo, row_hi);
+            if (lane == 0) {
+                s_maybe = m;
+                p.c1[part] = 0;
+                if (!m) p.c0[part] = 0;
+            }
         }
+        __syncthreads();
+        const bool maybe = s_maybe;
+        __syncthreads();  // s_maybe is rewritten by the next partition's test
         if (!maybe) continue;
         const uint32_t p0 = part * kProjTile;
         float4 c[kProjRounds];
@@ -1775,38 +1781,49 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
 // system-scope release; the host reads it a frame or two later.  Then FrameCtl is zeroed for the
 // next frame.  One wave; lane l sums shard l.
 __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, FrameCtl* host_ctl, uint32_t* host_seq,
-                               uint32_t seq) {
+                               uint32_t seq, uint32_t* lds) {
     constexpr uint32_t kWords = sizeof(FrameCtl) / 4;
-    static_assert(kWords <= 64 && kStatShards == 64, "one wave");
+    constexpr uint32_t kShardWords = sizeof(StatShard) / 4, kStride = kShardWords | 1u;  // odd: no bank conflicts
+    static_assert(kWords <= 64 && kStatShards == 64 && kShardWords <= 64, "one wave");
+    static_assert(offsetof(StatShard, k_total) == 0 && offsetof(StatShard, n_vis) == 8 &&
+                  offsetof(StatShard, key_min_inv) == 12 && offsetof(StatShard, key_max) == 16 &&
+                  offsetof(StatShard, n_chunk) == 20 && offsetof(StatShard, sat_key) == 28 &&
+                  offsetof(StatShard, sat_hist) == 32, "StatShard word map");
     const uint32_t lane = threadIdx.x;
-    StatShard sh = stats[lane];
-    stats[lane] = StatShard{};
-    unsigned long long kt = sh.k_total;
-    uint32_t nv = sh.n_vis, kmi = sh.key_min_inv, kma = sh.key_max, c0 = sh.n_chunk[0], c1 = sh.n_chunk[1];
-    uint32_t key = sh.sat_key;
-    for (int d = 32; d >= 1; d >>= 1) {
-        kt += __shfl_xor(kt, d, 64);
-        nv += __shfl_xor(nv, d, 64);
-        c0 += __shfl_xor(c0, d, 64);
-        c1 += __shfl_xor(c1, d, 64);
-        kmi = max(kmi, (uint32_t)__shfl_xor(kmi, d, 64));
-        kma = max(kma, (uint32_t)__shfl_xor(kma, d, 64));
-        key = max(key, (uint32_t)__shfl_xor(key, d, 64));
-    }
+    // the shards transposed through LDS (lane = shard), then lane f reduces word f over the 64
+    // shards: a few LDS reads each instead of a shuffle tree per field
+    {
+        const uint32_t* sw = (const uint32_t*)(stats + lane);
+        uint32_t w[kShardWords];
 #pragma unroll
-    for (int k = 0; k < kSatBuckets; ++k) {  // the shards' saturation histograms
-        uint32_t h = sh.sat_hist[k];
-        for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d, 64);
-        if (lane == 0) ctl->sat_hist[k] = h;
+        for (uint32_t k = 0; k < kShardWords; ++k) w[k] = sw[k];
+        stats[lane] = StatShard{};
+#pragma unroll
+        for (uint32_t k = 0; k < kShardWords; ++k) lds[lane * kStride + k] = w[k];
     }
-    if (lane == 0) {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane == 0) {  // k_total (64-bit)
+        unsigned long long kt = 0;
+        for (uint32_t j = 0; j < kStatShards; ++j)
+            kt += (unsigned long long)lds[j * kStride] | ((unsigned long long)lds[j * kStride + 1] << 32);
         ctl->k_total = kt;
-        ctl->n_vis = nv;
-        ctl->key_min_inv = kmi;
-        ctl->key_max = kma;
-        ctl->n_chunk[0] = c0;
-        ctl->n_chunk[1] = c1;
-        ctl->sat_key = key;
+    } else if (lane >= 2 && lane < 8 + kSatBuckets) {
+        const bool is_max = lane == 3 || lane == 4 || lane == 7;  // key_min_inv, key_max, sat_key
+        uint32_t a = 0;
+        for (uint32_t j = 0; j < kStatShards; ++j) {
+            const uint32_t v = lds[j * kStride + lane];
+            a = is_max ? max(a, v) : a + v;
+        }
+        switch (lane) {
+            case 2: ctl->n_vis = a; break;
+            case 3: ctl->key_min_inv = a; break;
+            case 4: ctl->key_max = a; break;
+            case 5: ctl->n_chunk[0] = a; break;
+            case 6: ctl->n_chunk[1] = a; break;
+            case 7: ctl->sat_key = a; break;
+            default: ctl->sat_hist[lane - 8] = a; break;
+        }
     }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
@@ -2690,7 +2707,7 @@ __global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
     const uint32_t G = gridDim.x, b = blockIdx.x;
     if (c.two_chunks && ctl->not_done != 0) chunk1_phases<FP16_TARGET>(c, lds);  // else: chunk 0 saturated every tile
     // the frame's end (one wave): FrameCtl is read by no workgroup after this point
-    if (b == 0 && threadIdx.x < 64) frame_end_body(ctl, c.stats, c.host_ctl, c.host_seq, c.seq);
+    if (b == 0 && threadIdx.x < 64) frame_end_body(ctl, c.stats, c.host_ctl, c.host_seq, c.seq, (uint32_t*)lds);
     (void)G;
 }
 
@@ -2712,7 +2729,8 @@ __global__ __launch_bounds__(256) void k_c1_records(ProjParams p) {
     c1_records_body(p, blockIdx.x, gridDim.x);
 }
 __global__ __launch_bounds__(64) void k_frame_end(Chunk1Params c) {
-    frame_end_body(c.cp.ctl, c.stats, c.host_ctl, c.host_seq, c.seq);
+    __shared__ uint32_t lds[kStatShards * ((sizeof(StatShard) / 4) | 1u)];
+    frame_end_body(c.cp.ctl, c.stats, c.host_ctl, c.host_seq, c.seq, lds);
 }
 
 // ============================================================================ ref_quirks

@@ -8,7 +8,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="bench.py --steps 20 --warmup 5 --no-cpu-baseline"
+BENCH="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 $BENCH \
     > $OUT/stats.log 2>&1 || { tail -20 $OUT/stats.log; exit 1; }
 run() {  # name, counters...
