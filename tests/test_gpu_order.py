@@ -129,8 +129,8 @@ def test_slots_synthetic_strip(gpu_ctx):
 
 
 def test_chunk1_slots(gpu_ctx):
-    """Two-chunk frame: chunk-1 slots (k_chunk1's records_body) carry the same records as the
-    oracle, and every slot's chunk agrees with its key against the split."""
+    """Two-chunk frame: chunk-1 slots (c1_records_body, in k_chunk1 or k_c1_records) carry the same
+    records as the oracle, and every slot's chunk agrees with its key against the split."""
     W, H, n = 640, 360, 150_000
     aos = gs.synth_aos(n, 23, W, H).reshape(n, 80)
     right = np.nonzero(aos[:, 0] > 0)[0]
