@@ -171,6 +171,7 @@ struct FrameSet {
     uint16_t* cand = nullptr;           // chunk-0 candidates per partition (k_cull): offsets
     uint32_t* units = nullptr;          // the frame's non-empty chunk-0 work units (k_cull)
     uint32_t* plist = nullptr;          // chunk 1: partitions that may hold chunk-1 splats (k_chunk1)
+    uint32_t* plist0 = nullptr;         // chunk 0: partitions that may hold candidates (k_part_list)
     uint32_t* order = nullptr;          // [tiles] the composite's tile order (k_tile_sort)
     uint32_t* sidx = nullptr;           // [slots] storage index of each composite slot
     FrameCtl* ctl = nullptr;            // zero at a frame's start (the frame's end clears it)
@@ -567,6 +568,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.c1 = F.c1;
     pp.cand = F.cand;
     pp.units = F.units;
+    pp.plist0 = F.plist0;
     pp.bounds = s->bounds;
     pp.orig = s->orig;
     pp.sidx = F.sidx;
@@ -1080,6 +1082,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 dev_alloc(F.c1, (size_t)proj_parts(n) + 1);
                 dev_alloc(F.units, (size_t)kUnitShards * unit_shard_cap(proj_parts(n)) + 1);
                 dev_alloc(F.plist, (size_t)proj_parts(n) + 1);
+                dev_alloc(F.plist0, (size_t)proj_parts(n) + 1);
                 dev_alloc(F.cand, nslots);
                 dev_alloc(F.sidx, nslots);
                 ensure_tile_capacity(F, 4 * n + (1u << 20));
@@ -1170,6 +1173,7 @@ void gs_scene_free(gs_scene* s) {
         dev_free(F.cand);
         dev_free(F.units);
         dev_free(F.plist);
+        dev_free(F.plist0);
         dev_free(F.sidx);
         dev_free(F.tvA); dev_free(F.tvB);
         dev_free(F.ranges);

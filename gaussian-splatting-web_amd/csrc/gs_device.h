@@ -66,6 +66,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t sat_key;             // depth key of the farthest splat a tile saturated at (the frame's end, k_chunk1)
     uint32_t unit_n[kUnitShards]; // chunk-0 work units per shard (k_cull; see ProjParams::units)
     uint32_t c1_parts;            // chunk 1: projection partitions listed in ProjParams::plist (k_chunk1)
+    uint32_t c0_parts;            // chunk 0: projection partitions listed in ProjParams::plist0 (k_part_list)
     uint32_t sat_hist[kSatBuckets];  // tiles saturated by the end of the frame, by saturation depth
                                      // (sat_bucket; summed from the shards at the frame's end)
 };
@@ -163,6 +164,7 @@ struct ProjParams {
     // (unsat_rows_body); rec_all: k_records dumps every visible Gaussian's record (debug)
     const uint32_t* sat;
     uint32_t* plist;          // [parts] chunk 1: the partitions that may hold chunk-1 splats (k_chunk1)
+    uint32_t* plist0;         // [parts] chunk 0: the partitions that may hold candidates (k_part_list)
     int rec_all;
     float cam[3];             // camera position (SH view direction)
     const float4* sh;         // [n][shq] packed SH coefficients

@@ -71,6 +71,14 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp
 // each projection partition (kProjTile consecutive slots) for the per-partition cull.
 
 // ordered-uint encoding of a float (monotone), for min / max with integer atomics
+#ifdef GS_KTIME
+// diagnostics builds only: per-workgroup wall-clock stamps of the projection kernels
+// (kernel k: 0 k_cull, 1 k_project; stamp 0 entry, 1 after the first dependent loads, 2 exit | items << 40)
+__device__ unsigned long long g_kt[2][8192][6];
+#define KT_MARK(kk_, ii_, xx_) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_kt[kk_][blockIdx.x][ii_] = (wall_clock64() & 0xffffffffffull) | ((unsigned long long)(xx_) << 40); } while (0)
+#else
+#define KT_MARK(kk_, ii_, xx_) do { } while (0)
+#endif
 __device__ __forceinline__ uint32_t f2ord(float f) {
     const uint32_t u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -828,32 +836,47 @@ __device__ __forceinline__ uint32_t unit_at(const UnitList& L, uint32_t j) {
 // slots; its non-empty work units are appended to the frame's list); survivors at or past thresh
 // are only counted (n_vis is exact when the frame has one chunk and no partition was ruled out
 // by the threshold) and enter the depth range.
+// Projection, phase 0: the partition test (part_maybe on each partition's bound), one lane per
+// partition; the partitions that may hold a chunk-0 candidate are appended to plist0 (one counter
+// add per wave; list order does not matter: a partition's slots and units are its own).  Every
+// partition's chunk counts are zeroed here (k_cull sets c0 of the listed ones, chunk 1 adds to c1).
+// A ruled-out partition costs one 32-B read and one lane, and k_cull's workgroups visit only the
+// listed ones (a strip lists about an eighth of them).
+__global__ __launch_bounds__(256) void k_part_list(ProjParams p) {
+    const int row_lo = p.tile_row_begin * kTile;
+    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+    const uint32_t parts = proj_parts(p.n), lane = lane_id();
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool want = q < parts && part_maybe(p, p.bounds[q], row_lo, row_hi);
+    if (q < parts) {
+        p.c1[q] = 0;
+        if (!want) p.c0[q] = 0;
+    }
+    const uint64_t b = __ballot(want);
+    if (!b) return;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&p.ctl->c0_parts, (uint32_t)__popcll(b));
+    base = __shfl(base, 0, 64);
+    if (want) p.plist0[base + (uint32_t)__popcll(b & lanemask_lt())] = q;
+}
+
 __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
     __shared__ unsigned long long s_mask[kProjRounds][kProjThreads / 64];
     __shared__ uint32_t s_base[kProjRounds][kProjThreads / 64];
-    __shared__ uint32_t s_total, s_maybe;
+    __shared__ uint32_t s_total;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     if (tid == 0) { s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
     uint32_t my_vis = 0, my_kmin_inv = 0, my_kmax = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = proj_parts(p.n), ucap = unit_shard_cap(parts);
-    for (uint32_t part = blockIdx.x; part < parts; part += gridDim.x) {
-        // the partition test first (part_maybe on its bound, by wave 0 alone): a ruled-out
-        // partition costs one 32-B read; the chunk counts are zeroed here (c1: chunk 1 adds to it)
-        if (w == 0) {
-            const bool m = part_maybe(p, p.bounds[part], row_lo, row_hi);
-            if (lane == 0) {
-                s_maybe = m;
-                p.c1[part] = 0;
-                if (!m) p.c0[part] = 0;
-            }
-        }
-        __syncthreads();
-        const bool maybe = s_maybe;
-        __syncthreads();  // s_maybe is rewritten by the next partition's test
-        if (!maybe) continue;
+    KT_MARK(0, 0, 0);
+    const uint32_t nl = p.ctl->c0_parts;  // the partitions k_part_list kept
+    uint32_t kt_items = 0;
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
+        const uint32_t part = p.plist0[j];
+        if (kt_items++ == 0) KT_MARK(0, 1, part);
         const uint32_t p0 = part * kProjTile;
         float4 c[kProjRounds];
 #pragma unroll
@@ -919,6 +942,7 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
         atomicMax(&st->key_min_inv, s_kmin_inv);
         atomicMax(&st->key_max, s_kmax);
     }
+    KT_MARK(0, 2, kt_items);
 }
 
 // Projection, phase B: candidate q of a partition (slot slot_c0(part, q)) projected from its
@@ -941,9 +965,12 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     unsigned long long my_k = 0;
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+    KT_MARK(1, 0, 0);
     const UnitList L = load_units(p.units, p.ctl, proj_parts(p.n));
+    uint32_t kt_items = 0;
     for (uint32_t j = blockIdx.x; j < L.total; j += gridDim.x) {
         const uint32_t u = unit_at(L, j), id = unit_id(u);
+        if (kt_items++ == 0) KT_MARK(1, 1, id);
         const uint32_t part = id / kProjRounds, q = (id % kProjRounds) * kProjThreads + tid;
         const uint32_t p0 = part * kProjTile;
         if ((uint32_t)tid >= unit_count(u)) continue;
@@ -995,12 +1022,21 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
             g2 = gi[2];
         }
         Proj o;
+#ifdef GS_KTIME
+        if (kt_items == 1) { if (g0.x == 12345.0f) KT_MARK(1, 5, 0); KT_MARK(1, 3, 0); }
+#endif
         if (project_core_g(p, i, g0, g1, g2, row_lo, row_hi, false, o)) {
             store_slot(p, slot, i, oi, o);
             if (o.prect != kRectEmpty) {  // the SH colour of a splat that binds a tile
                 float4 col;
                 if (SH12) {
+#ifdef GS_KTIME
+                    if (kt_items == 1) KT_MARK(1, 4, 0);
+#endif
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef GS_KTIME
+                    if (kt_items == 1) KT_MARK(1, 5, 0);
+#endif
                     col = sh_colour<64>(&s_sh[wv][0][lane], 12, g0.x, g0.y, g0.z, p.cam);
                 } else {
                     col = sh_colour(p.sh + (uint64_t)i * p.shq, p.shq, g0.x, g0.y, g0.z, p.cam);
@@ -1031,6 +1067,7 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
         atomicMax(&st->key_min_inv, s_kmin_inv);
         atomicMax(&st->key_max, s_kmax);
     }
+    KT_MARK(1, 2, kt_items);
 }
 
 // ============================================================================ radix pass
@@ -2881,9 +2918,16 @@ void launch_quirk_gather(const uint32_t* skeys, const uint32_t* svals, const uin
 void launch_project(const ProjParams& p, hipStream_t s) {
     const uint32_t parts = proj_parts(p.n);
     if (!parts) return;
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, parts));
+#ifndef GS_CULL_GRID
+#define GS_CULL_GRID 2048
+#endif
+#ifndef GS_PROJ_GRID
+#define GS_PROJ_GRID 1536
+#endif
+    hipLaunchKernelGGL(k_part_list, dim3((parts + 255) / 256), dim3(256), 0, s, p);
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(GS_CULL_GRID, parts));
     hipLaunchKernelGGL(k_cull, dim3(grid), dim3(kProjThreads), 0, s, p);
-    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (uint64_t)parts * kProjRounds));
+    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(GS_PROJ_GRID, (uint64_t)parts * kProjRounds));
     if (p.shq == 12)
         hipLaunchKernelGGL(k_project<true>, dim3(ugrid), dim3(kProjThreads), 0, s, p);
     else
@@ -2977,6 +3021,11 @@ void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
 #ifdef GS_C1_TIME
 extern "C" int gs_diag_c1_times(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_c1_time), 16 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
+#ifdef GS_KTIME
+extern "C" int gs_diag_kt(unsigned long long* out) {  // out: 2 x 8192 x 6
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_kt), sizeof(gs::g_kt)) == hipSuccess ? 0 : -1;
 }
 #endif
 #ifdef GS_COMP_DIAG

@@ -82,6 +82,8 @@ def main():
     heavy = np.argsort(-d_)[:10]
     print("longest (tile, tx, ty, start, dur):",
           [(int(t), int(t % TX), int(t // TX), round(float(b[t]), 1), round(float(d_[t]), 1), int(nl[t])) for t in heavy])
+    if os.environ.get("SAVE"):  # per-tile arrays for offline scheduling studies
+        np.savez(os.environ["SAVE"], start=b, end=e, n=nl, blends=blends, xcc=xcc, cu=cu)
     sc.close()
     ctx.close()
 
