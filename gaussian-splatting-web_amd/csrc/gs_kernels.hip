@@ -951,11 +951,12 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
 // splat in the reference's expression order: sh_colour) its colour in its slot, an invisible one
 // leaves the slot a hole (rect kRectHole).  Publishes the visible count, their tile total, the depth range.
 template <bool SH12>  // SH12: degree-3 scenes (12 coefficient quads), staged through LDS
-__global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
+__global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
     __shared__ unsigned long long s_k;
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
-    // per wave: the SH quads of its 64 candidates, [quad][lane], loaded straight into LDS
-    // (global_load_lds: no registers held, in flight while the footprint is computed)
+    // per wave: the SH quads of its 64 candidates, [candidate][quad] (viewed flat), loaded
+    // straight into LDS (global_load_lds: no registers held, in flight while the footprint is
+    // computed)
     __shared__ float4 s_sh[SH12 ? kProjThreads / 64 : 1][SH12 ? 12 : 1][64];
     const int tid = threadIdx.x;
     const int wv = tid >> 6, lane = tid & 63;
@@ -968,89 +969,119 @@ __global__ __launch_bounds__(kProjThreads) void k_project(ProjParams p) {
     KT_MARK(1, 0, 0);
     const UnitList L = load_units(p.units, p.ctl, proj_parts(p.n));
     uint32_t kt_items = 0;
-    for (uint32_t j = blockIdx.x; j < L.total; j += gridDim.x) {
-        const uint32_t u = unit_at(L, j), id = unit_id(u);
+    // The workgroup's units are software-pipelined: the next unit's list entry is loaded when this
+    // unit starts and its candidate offset once this unit's footprint is computed, so a unit
+    // starts with its geometry loads instead of two dependent round trips (list -> candidate).
+    auto cand_of = [&](uint32_t uu) -> uint32_t {
+        const uint32_t id = unit_id(uu);
+        return (uint32_t)tid < unit_count(uu)
+                   ? (uint32_t)p.cand[(id / kProjRounds) * kProjTile + (id % kProjRounds) * kProjThreads + tid]
+                   : 0u;
+    };
+    uint32_t j = blockIdx.x;
+    uint32_t u = j < L.total ? unit_at(L, j) : 0u;
+    uint32_t cq = j < L.total ? cand_of(u) : 0u;
+    for (; j < L.total; j += gridDim.x) {
+        const uint32_t id = unit_id(u), jn = j + gridDim.x;
+        const uint32_t un = jn < L.total ? unit_at(L, jn) : 0u;
         if (kt_items++ == 0) KT_MARK(1, 1, id);
         const uint32_t part = id / kProjRounds, q = (id % kProjRounds) * kProjThreads + tid;
         const uint32_t p0 = part * kProjTile;
-        if ((uint32_t)tid >= unit_count(u)) continue;
-        const uint32_t cq = p.cand[p0 + q];
+        const bool act = (uint32_t)tid < unit_count(u);
         const uint32_t slot = slot_c0(part, q);
         const uint32_t i = p0 + cq;
-        uint32_t oi;
+        uint32_t oi = 0;
         float4 g0, g1, g2;
-        if (SH12) {
-            // one asm block: the geometry record into registers, then the 12 SH quads straight
-            // into this wave's LDS staging (global_load_lds: lane l lands at M0 + the
-            // instruction's offset + 16 l, so M0 steps by 1024 - 16 per quad),
-            // then a wait for the geometry alone (vmcnt counts in issue order: 12 still in
-            // flight).  The compiler does not see these loads, so it cannot drain them early.
-            const float4* gp = p.geo + 3 * (uint64_t)i;
-            const float4* sp = p.sh + 12 * (uint64_t)i;
-            const uint32_t* op = p.orig + i;
-            uint32_t m0save;
-            const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)&s_sh[wv][0][0]);
-            asm volatile(
-                "s_mov_b32 %[msave], m0\n"
-                "global_load_dword %[oi], %[op], off\n"
-                "global_load_dwordx4 %[g0], %[gp], off\n"
-                "global_load_dwordx4 %[g1], %[gp], off offset:16\n"
-                "global_load_dwordx4 %[g2], %[gp], off offset:32\n"
-                "s_mov_b32 m0, %[lds]\n s_nop 0\n"
-                "global_load_lds_dwordx4 %[sp], off\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:16\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:32\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:48\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:64\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:80\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:96\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:112\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:128\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:144\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:160\n"
-                "s_add_u32 m0, m0, 0x3f0\n s_nop 0\n global_load_lds_dwordx4 %[sp], off offset:176\n"
-                "s_waitcnt vmcnt(12)\n"
-                "s_mov_b32 m0, %[msave]\n"  // M0 restored (the compiler's value, if it holds one)
-                : [g0] "=&v"(g0), [g1] "=&v"(g1), [g2] "=&v"(g2), [oi] "=&v"(oi), [msave] "=&s"(m0save)
-                : [gp] "v"(gp), [sp] "v"(sp), [op] "v"(op), [lds] "s"(lds)
-                : "memory");
-        } else {
-            oi = p.orig[i];
-            const float4* gi = p.geo + 3 * (uint64_t)i;
-            g0 = gi[0];
-            g1 = gi[1];
-            g2 = gi[2];
-        }
         Proj o;
-#ifdef GS_KTIME
-        if (kt_items == 1) { if (g0.x == 12345.0f) KT_MARK(1, 5, 0); KT_MARK(1, 3, 0); }
-#endif
-        if (project_core_g(p, i, g0, g1, g2, row_lo, row_hi, false, o)) {
-            store_slot(p, slot, i, oi, o);
-            if (o.prect != kRectEmpty) {  // the SH colour of a splat that binds a tile
-                float4 col;
-                if (SH12) {
-#ifdef GS_KTIME
-                    if (kt_items == 1) KT_MARK(1, 4, 0);
-#endif
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef GS_KTIME
-                    if (kt_items == 1) KT_MARK(1, 5, 0);
-#endif
-                    col = sh_colour<64>(&s_sh[wv][0][lane], 12, g0.x, g0.y, g0.z, p.cam);
-                } else {
-                    col = sh_colour(p.sh + (uint64_t)i * p.shq, p.shq, g0.x, g0.y, g0.z, p.cam);
-                }
-                col.w = __uint_as_float(o.key);
-                p.crec[3 * (uint64_t)slot + 2] = col;
+        bool vis = false;
+        if (SH12) {
+            // Coalesced staging through this wave's 12 KiB of LDS.  Every piece is 1 KiB in which
+            // consecutive lanes take consecutive 16-B chunks of one candidate's record (lane l of
+            // piece k: chunk (64 k + l) % m of candidate (64 k + l) / m, m = 3 geometry / 12 SH
+            // chunks), so a piece touches about 9 cache lines instead of up to 64.  The SH layout
+            // is [candidate][12 quads]: its pieces 0-8 land at once, the geometry's 3 pieces in the
+            // last 3 KiB; once the geometry is read out, SH pieces 9-11 land there.  Every lane
+            // takes part (an inactive candidate reads its partition's first record).
+            const uint32_t ia = act ? i : p0;
+            const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)&s_sh[wv][0][0]);
+            // an opaque copy of the lane id: the pieces' source lanes are recomputed per unit
+            // instead of being hoisted into 15 loop-invariant registers (k_project sits at the
+            // 168-VGPR limit of 3 waves per SIMD)
+            uint32_t ln;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"((uint32_t)lane));
+            auto piece = [&](const float4* src, uint32_t dst) {
+                uint32_t m0save;
+                asm volatile(
+                    "s_mov_b32 %[msave], m0\n"
+                    "s_mov_b32 m0, %[lds]\n s_nop 0\n"
+                    "global_load_lds_dwordx4 %[sp], off\n"
+                    "s_mov_b32 m0, %[msave]\n"
+                    : [msave] "=&s"(m0save)
+                    : [sp] "v"(src), [lds] "s"(dst)
+                    : "memory");
+            };
+            asm volatile("global_load_dword %[oi], %[op], off" : [oi] "=&v"(oi) : [op] "v"(p.orig + ia) : "memory");
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t idx = 64u * k + ln, sc = idx / 3u, ch = idx % 3u;
+                const uint32_t isrc = (uint32_t)__shfl((int)ia, (int)sc, 64);
+                piece(p.geo + 3 * (uint64_t)isrc + ch, lds + 9216u + 1024u * k);
             }
-            ++my_vis;
-            my_k += o.ntiles;
-            my_kmin_inv = max(my_kmin_inv, ~o.key);
-            my_kmax = max(my_kmax, o.key);
-        } else {
-            p.srect[slot] = kRectHole;
+            auto sh_piece = [&](int k) {
+                const uint32_t idx = 64u * k + ln, sc = idx / 12u, ch = idx % 12u;
+                const uint32_t isrc = (uint32_t)__shfl((int)ia, (int)sc, 64);
+                piece(p.sh + 12 * (uint64_t)isrc + ch, lds + 1024u * k);
+            };
+#pragma unroll
+            for (int k = 0; k < 9; ++k) sh_piece(k);
+            // the geometry (issued before the 9 SH pieces) is in LDS once at most 9 are outstanding
+            asm volatile("s_waitcnt vmcnt(9)" : "+v"(oi) :: "memory");
+            const float4* sg = (const float4*)&s_sh[wv][0][0] + 576 + 3 * lane;
+            g0 = sg[0];
+            g1 = sg[1];
+            g2 = sg[2];
+            // the reads are done before SH pieces 9-11 overwrite the geometry's staging
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int k = 9; k < 12; ++k) sh_piece(k);
         }
+        if (act) {
+            if (!SH12) {
+                oi = p.orig[i];
+                const float4* gi = p.geo + 3 * (uint64_t)i;
+                g0 = gi[0];
+                g1 = gi[1];
+                g2 = gi[2];
+            }
+            vis = project_core_g(p, i, g0, g1, g2, row_lo, row_hi, false, o);
+        }
+        // the next unit's candidate: its load overlaps this unit's colour and stores (waiting for
+        // the unit entry also drains this unit's SH loads, which are due by now)
+        const uint32_t cqn = jn < L.total ? cand_of(un) : 0u;
+        if (act) {
+            if (vis) {
+                store_slot(p, slot, i, oi, o);
+                if (o.prect != kRectEmpty) {  // the SH colour of a splat that binds a tile
+                    float4 col;
+                    if (SH12) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        col = sh_colour<1>(&s_sh[wv][0][0] + 12 * lane, 12, g0.x, g0.y, g0.z, p.cam);
+                    } else {
+                        col = sh_colour(p.sh + (uint64_t)i * p.shq, p.shq, g0.x, g0.y, g0.z, p.cam);
+                    }
+                    col.w = __uint_as_float(o.key);
+                    p.crec[3 * (uint64_t)slot + 2] = col;
+                }
+                ++my_vis;
+                my_k += o.ntiles;
+                my_kmin_inv = max(my_kmin_inv, ~o.key);
+                my_kmax = max(my_kmax, o.key);
+            } else {
+                p.srect[slot] = kRectHole;
+            }
+        }
+        u = un;
+        cq = cqn;
     }
     if (my_vis) {
         atomicAdd(&s_vis, my_vis);
