@@ -585,8 +585,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     mark(EV_PROJ1);
 
     // ---- chunk 0: bin -> per-tile sort -> composite.  Chunk 1 (the splats at or past T that
-    // touch a tile chunk 0 left unsaturated) is one cooperative launch enqueued behind it that
-    // returns at once when chunk 0 saturated every tile (k_chunk1).
+    // touch a tile chunk 0 left unsaturated) is one launch enqueued behind it (64 workgroups,
+    // grid barriers) that returns at once when chunk 0 saturated every tile (k_chunk1), or
+    // separate launches when a recent frame left tiles unsaturated.
     BinParams bp{};
     bp.skey = F.skey;
     bp.sidx = F.sidx;
@@ -652,6 +653,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     HIPCHK(hipStreamWaitEvent(cst, F.ev_early, 0));
     st = cst;  // the composite (the caller's buffer) and the frame's end, in call order
     mark(EV_RANGES_0);
+    if (sc > 1 && tr_begin * kTile + rows_padded > H) {  // the last strip's rows past the image are
+        // padding (gs_strip_rows): defined as zero (transparent black); no kernel writes them
+        const size_t valid = (size_t)std::max(0, H - tr_begin * kTile), px = cp.out_f16 ? 8 : 16;
+        HIPCHK(hipMemsetAsync((char*)out + valid * (size_t)W * px, 0, ((size_t)rows_padded - valid) * (size_t)W * px, st));
+    }
     launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
     mark(EV_COMP_0);
     {  // chunk 1 (when chunk 0 left tiles unsaturated), then the frame's end: statistics into the

@@ -3,18 +3,22 @@
 // Upload (once per scene): k_bbox, k_morton, a device radix sort (k_radix_*), k_transpose (the
 // reference AoS record, src/ply.ts:249-257 -> geometry records, packed SH, cull planes, Morton
 // storage order), k_part_bounds.
-// Per frame (8 launches, no host round trip):
-//   k_cull        per 1024-Gaussian partition: bound test, then per Gaussian the depth key
-//                 (src/shaders.ts:36-68) and a conservative cull; chunk-0 candidates + work units
+// Per frame (9 launches, no host round trip):
+//   k_part_list   per 1024-Gaussian partition (one lane each): bound test -> list of partitions
+//   k_cull        per listed partition: per Gaussian the depth key (src/shaders.ts:36-68) and a
+//                 conservative cull; chunk-0 candidates + work units
 //   k_project     per candidate: vs_points (src/simple_render.ts:217-332) and the SH colour
 //                 (:26-66), the composite slot record, sort key and packed tile rectangle
+//                 (geometry and SH staged through LDS in coalesced 1-KiB pieces)
 //   k_bin_count / k_bin_colscan / k_bin_emit   two-level counting sort of (tile, slot) entries
 //   k_tile_sort   per tile: its slots by (depth key, reference index) = the reference's stable
 //                 depth sort (src/renderer.ts:175-183) restricted to the tile
 //   k_composite   16x16 tile: front-to-back "under" blending of fs_main's alpha
 //                 (src/simple_render.ts:169-200, blend state :455-471), batches staged in LDS
-//   k_chunk1      chunk 1 (tiles chunk 0 left unsaturated) as one cooperative launch, then the
-//                 frame's end (statistics shards -> FrameCtl -> pinned host slot)
+//   k_chunk1      chunk 1 (tiles chunk 0 left unsaturated) as one launch of 64 co-resident
+//                 workgroups with grid barriers (a plain launch: one 256-thread workgroup per CU
+//                 at most, so the grid always fits beside the other kernels), then the frame's
+//                 end (statistics shards -> FrameCtl -> pinned host slot)
 //
 // Inter-workgroup hand-offs (the grid barrier) follow cdna_hip_programming.md Guideline 16:
 // agent-scope release / acquire, bounded spins, counters zeroed by the frame's end.
@@ -76,7 +80,10 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp
 // (kernel k: 0 k_cull, 1 k_project; stamp 0 entry, 1 after the first dependent loads, 2 exit | items << 40)
 __device__ unsigned long long g_kt[2][8192][6];
 #define KT_MARK(kk_, ii_, xx_) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_kt[kk_][blockIdx.x][ii_] = (wall_clock64() & 0xffffffffffull) | ((unsigned long long)(xx_) << 40); } while (0)
+__device__ unsigned long long g_fe[8];  // the frame's end: wall clock at its steps (lane 0 of block 0)
+#define FE_MARK(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_fe[k] = wall_clock64(); } while (0)
 #else
+#define FE_MARK(k) do { } while (0)
 #define KT_MARK(kk_, ii_, xx_) do { } while (0)
 #endif
 __device__ __forceinline__ uint32_t f2ord(float f) {
@@ -1858,6 +1865,17 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
                   offsetof(StatShard, n_chunk) == 20 && offsetof(StatShard, sat_key) == 28 &&
                   offsetof(StatShard, sat_hist) == 32, "StatShard word map");
     const uint32_t lane = threadIdx.x;
+    FE_MARK(0);
+#ifdef GS_KTIME
+    {  // diagnostics: latency of one load of FrameCtl, then of one shard word
+        const uint32_t a = __hip_atomic_load(&ctl->n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a == 0xdeadbeefu) FE_MARK(7);
+        FE_MARK(6);
+        const uint32_t b2 = __hip_atomic_load(&stats[lane].n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (b2 == 0xdeadbeefu) FE_MARK(6);
+        FE_MARK(7);
+    }
+#endif
     // the shards transposed through LDS (lane = shard), then lane f reduces word f over the 64
     // shards: a few LDS reads each instead of a shuffle tree per field
     {
@@ -1871,6 +1889,7 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    FE_MARK(1);
     if (lane == 0) {  // k_total (64-bit)
         unsigned long long kt = 0;
         for (uint32_t j = 0; j < kStatShards; ++j)
@@ -1895,6 +1914,7 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
     }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
+    FE_MARK(2);
     uint32_t* src = (uint32_t*)ctl;
     const uint32_t v = lane < kWords ? src[lane] : 0u;
     if (lane < kWords) ((uint32_t*)host_ctl)[lane] = v;
@@ -1904,8 +1924,10 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
     // the whole L2 back (the frame's dirty lines) for two cache-bypassing stores.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+    FE_MARK(3);
     if (lane == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (lane < kWords) src[lane] = 0u;
+    FE_MARK(4);
 }
 
 // Row prefix counts of the tiles chunk 0 left unsaturated (done == 0): row r of the strip at
@@ -2773,6 +2795,7 @@ __global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kChunk1Lds];
     FrameCtl* ctl = c.cp.ctl;
     const uint32_t G = gridDim.x, b = blockIdx.x;
+    FE_MARK(5);
     if (c.two_chunks && ctl->not_done != 0) chunk1_phases<FP16_TARGET>(c, lds);  // else: chunk 0 saturated every tile
     // the frame's end (one wave): FrameCtl is read by no workgroup after this point
     if (b == 0 && threadIdx.x < 64) frame_end_body(ctl, c.stats, c.host_ctl, c.host_seq, c.seq, (uint32_t*)lds);
@@ -3057,6 +3080,9 @@ extern "C" int gs_diag_c1_times(unsigned long long* out) {
 #ifdef GS_KTIME
 extern "C" int gs_diag_kt(unsigned long long* out) {  // out: 2 x 8192 x 6
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_kt), sizeof(gs::g_kt)) == hipSuccess ? 0 : -1;
+}
+extern "C" int gs_diag_fe(unsigned long long* out) {  // out: 8
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_fe), sizeof(gs::g_fe)) == hipSuccess ? 0 : -1;
 }
 #endif
 #ifdef GS_COMP_DIAG

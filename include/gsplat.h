@@ -144,7 +144,8 @@ void gs_opts_default(gs_opts* opts);
 /* Rows of image covered by strip `strip_index` of `strip_count`: tile rows
  * [s*ceil(TR/G), min((s+1)*ceil(TR/G), TR)), TR = ceil(H/16).  *row0 = first image row,
  * *rows_padded = ceil(TR/G)*16 (every strip's output buffer has this many rows, so an
- * all-gather of the G strip buffers is the image followed by padding rows). */
+ * all-gather of the G strip buffers is the image followed by padding rows; a render writes its
+ * padding rows as zero). */
 int gs_strip_rows(int H, int strip_index, int strip_count, int* row0, int* rows_padded);
 
 /* Render one frame.  out_host_or_null: W*H pixels (strip_count == 1) or rows_padded*W pixels

@@ -190,8 +190,9 @@ def test_strips_match_full_image(gpu_ctx):
     full = sc.render(u, W, H)
     for G in (2, 3, 8):
         parts = [sc.render(u, W, H, gs.make_opts(strip_index=g, strip_count=G)) for g in range(G)]
-        img = np.concatenate(parts, axis=0)[:H]
-        assert np.array_equal(img, full), G
+        img = np.concatenate(parts, axis=0)
+        assert np.array_equal(img[:H], full), G
+        assert not img[H:].any(), G  # padding rows past the image: zero
 
 
 def test_deterministic(gpu_ctx):
@@ -525,13 +526,85 @@ def test_pipelined_frames_match_single_frames(gpu_ctx, size):
         for j, ((sc, u, o), b, ref) in enumerate(zip(seq, bufs, refs)):
             got = np.empty(ref.shape, np.float16)
             b.to_host(got)
-            # a strip's rows past the image (padding to whole tiles) are never written
+            # a strip's rows past the image (padding to whole tiles) are written as zero
             row0 = gs.strip_rows(H, o.strip_index, o.strip_count)[0] if o.strip_count > 1 else 0
             valid = min(ref.shape[0], H - row0)
-            bad = (got[:valid].view(np.uint16) != ref[:valid].view(np.uint16)).any(axis=2)
+            bad = (got.view(np.uint16) != ref.view(np.uint16)).any(axis=2)
             rows = np.nonzero(bad.any(axis=1))[0]
             assert not bad.any(), (j, int(bad.sum()), rows[:3].tolist(), rows[-3:].tolist(), o.strip_count)
+            assert not got[valid:].view(np.uint16).any()
     for b in bufs:
         b.free()
     sa.close()
     sb.close()
+
+
+def _sparse_right_scene(n, seed, W, H):
+    """Right half of the screen sparse (most of its splats moved behind the camera): its tiles
+    never saturate, so chunk 1 has work in every frame with a chunk split."""
+    aos = gs.synth_aos(n, seed, W, H).reshape(n, 80)
+    right = np.nonzero(aos[:, 0] > 0)[0]
+    aos[right[np.arange(right.size) % 50 != 0], 2] = 5.0
+    return aos.reshape(-1)
+
+
+def test_chunk1_frames_back_to_back(gpu_ctx):
+    """Many two-chunk frames with unsaturated tiles enqueued without host waits (k_chunk1 with its
+    grid barriers, then the separate chunk-1 launches once the host has seen unsaturated tiles):
+    no device fault is reported and every frame equals the same frame rendered alone."""
+    W, H = 640, 360
+    n = 150_000
+    sc = gs.Scene(gpu_ctx, _sparse_right_scene(n, 23, W, H), n, 16)
+    ua = gs.bench_uniforms(W, H)
+    ub = gs.pack_uniforms(gs.look_at((0.5, 0.3, 0.0), (0.0, 0.0, -10.0)), gs.perspective(1.04719755, W / H, 0.03, 1000.0))
+    F16 = gs.GS_OUT_RGBA_F16
+    cases = [(ua, 0.02), (ub, 0.1), (ua, 0.3), (ub, 0.02)]
+    refs = [sc.render(u, W, H, gs.make_opts(out_format=F16, chunk_fraction=f)) for u, f in cases]
+    bufs = [gs.DeviceBuffer(H * W * 8) for _ in range(24)]
+    for k, b in enumerate(bufs):
+        u, f = cases[k % len(cases)]
+        sc.render_device(u, W, H, b.ptr.value, b.nbytes, None, gs.make_opts(out_format=F16, chunk_fraction=f))
+    gpu_ctx.sync()  # raises GsError if any frame's chunk-1 barrier timed out
+    assert gpu_ctx.timings()["tiles_unsaturated"] > 0
+    for k, b in enumerate(bufs):
+        got = np.empty(refs[0].shape, np.float16)
+        b.to_host(got)
+        assert np.array_equal(got.view(np.uint16), refs[k % len(cases)].view(np.uint16)), k
+        b.free()
+    sc.close()
+
+
+def test_device_frame_overflow_reported(gpu_ctx):
+    """A device-resident frame whose tile lists exceed the capacity (huge splats covering the
+    screen) is reported by a later gs_render_device / gs_sync call, not hidden by the clean frames
+    after it; once the capacity has grown, frames equal gs_render's."""
+    W, H = 1280, 720
+    n = 3000
+    aos = gs.synth_aos(n, 41, W, H).reshape(n, 80)
+    aos[:, 4:7] = np.abs(aos[:, 2:3]) * 2.0  # every splat's quad covers the screen
+    aos[:, 12] = -5.0  # faint: the composite walks whole lists
+    aos = aos.reshape(-1)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    u = gs.bench_uniforms(W, H)
+    o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, chunk_fraction=1.0)
+    buf = gs.DeviceBuffer(H * W * 8)
+    errors = []
+    for _ in range(6):
+        try:
+            sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
+        except gs.GsError as e:
+            errors.append(str(e))
+    try:
+        gpu_ctx.sync()
+    except gs.GsError as e:
+        errors.append(str(e))
+    assert errors and all("capacity" in e for e in errors), errors
+    for _ in range(3):
+        sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
+    gpu_ctx.sync()
+    got = np.empty((H, W, 4), np.float16)
+    buf.to_host(got)
+    ref = sc.render(u, W, H, o)
+    assert np.array_equal(got.view(np.uint16), ref.view(np.uint16))
+    buf.free()
+    sc.close()

@@ -57,6 +57,11 @@ def main():
         kt = np.zeros((2, 8192, 6), dtype=np.uint64)
         L.gs_diag_kt(kt.ctypes.data_as(ctypes.c_void_p))
         print("== G=%d strip %d" % (G, g))
+        fe = np.zeros(8, dtype=np.uint64)
+        L.gs_diag_fe(fe.ctypes.data_as(ctypes.c_void_p))
+        f = fe.astype(np.int64)
+        print("frame end (us from k_chunk1 entry): start %.2f  shards in %.2f  reduced %.2f  host copy done %.2f  end %.2f" %
+              tuple((f[k] - f[5]) / 100.0 for k in range(5)), " ctl word %.2f shard word %.2f" % ((f[6] - f[5]) / 100.0, (f[7] - f[5]) / 100.0))
         report("k_cull", kt[0])
         report("k_project", kt[1])
         # clear for the next configuration: render with stamps zeroed is not possible from here,
