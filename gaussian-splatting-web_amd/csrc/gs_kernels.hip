@@ -2264,7 +2264,8 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     const float4* __restrict__ rec = p.rec;
     const uint32_t* __restrict__ tvals = p.tvals;
     const float L = 2.0f * kSqrtLog2e, amin = 1.0f / 255.0f, t_min = p.t_min;
-    const uint64_t pix0 = (uint64_t)py * p.W + px, pix1 = pix0 + 8 * (uint64_t)p.W;  // state index
+    // parked-state index of the lane's pixels (a function, not a value held across the blend loop)
+    auto pix_of = [&](int r) -> uint64_t { return (uint64_t)(py + 8 * r) * p.W + px; };
     f2 cr = {0.0f, 0.0f}, cg = {0.0f, 0.0f}, cb = {0.0f, 0.0f};
     f2 T = {1.0f, 1.0f};   // FP32: transmittance
     f2 ca = {0.0f, 0.0f};  // FP16_TARGET: dst.a
@@ -2273,12 +2274,12 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 #endif
     if (p.mode == kCompSecond) {
         if (in0) {
-            const float4 st = p.state[pix0];
+            const float4 st = p.state[pix_of(0)];
             cr.x = st.x; cg.x = st.y; cb.x = st.z;
             if (FP16_TARGET) ca.x = st.w; else T.x = st.w;
         }
         if (in1) {
-            const float4 st = p.state[pix1];
+            const float4 st = p.state[pix_of(1)];
             cr.y = st.x; cg.y = st.y; cb.y = st.z;
             if (FP16_TARGET) ca.y = st.w; else T.y = st.w;
         }
@@ -2316,11 +2317,12 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         const float cxr = ga.x - (float)tx0, cyr = ga.y - (float)ty0;
         const float c0u = -__builtin_fmaf(cxr, ga.z, cyr * ga.w);
         const float c0v = -__builtin_fmaf(cxr, gb.x, cyr * gb.y);
-        // staged as [b, a, d, c] [c0u, slot, c0v, log2 op] [r, g, b, key]: every value a packed
-        // op broadcasts sits in the low half of an aligned register pair (no moves in the blend)
+        // staged as [b, a, d, c] [r, c0u, g, c0v] [b, log2 op, slot, key]: every value a packed
+        // op broadcasts sits in the low half of an aligned register pair (no moves in the blend;
+        // log2 op is broadcast from a high half by op_sel)
         sR[buf][tid][0] = make_float4(ga.w, ga.z, gb.y, gb.x);
-        sR[buf][tid][1] = make_float4(c0u, __uint_as_float(gs_), c0v, gb.z);
-        sR[buf][tid][2] = gc;
+        sR[buf][tid][1] = make_float4(gc.x, c0u, gc.y, c0v);
+        sR[buf][tid][2] = make_float4(gc.z, gb.z, __uint_as_float(gs_), gc.w);
         // the splat's pixel columns within this tile's rows (ellipse; the binning's margins)
         uint32_t ul = 0u, uh = 0u;
         const bool cols = gv && ellipse_cols(ellipse_of(ga, gb), (uint32_t)(ty0 >> 4), ul, uh);
@@ -2339,12 +2341,15 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         const float4 A = *(const float4*)(sRb + off);
         const float4 B = *(const float4*)(sRb + off + 16);
         const float4 C = *(const float4*)(sRb + off + 32);
+        // staged as [b, a, d, c] [r, c0u, g, c0v] [b, log2 op, slot, key]: each colour channel a
+        // packed fma broadcasts is the low half of an aligned register pair (no moves)
+        const float c0u = B.y, c0v = B.w, l2op = C.y, kr = B.x, kg = B.z, kb = C.x;
         // every rounding is spelled out (explicit fma or contraction off), so each inlined copy of
         // this blend rounds identically and the image cannot depend on where batches split
-        const f2 u = __builtin_elementwise_fma(ly, (f2)A.x, (f2)__builtin_fmaf(lx, A.y, B.x));
-        const f2 v = __builtin_elementwise_fma(ly, (f2)A.z, (f2)__builtin_fmaf(lx, A.w, B.z));
+        const f2 u = __builtin_elementwise_fma(ly, (f2)A.x, (f2)__builtin_fmaf(lx, A.y, c0u));
+        const f2 v = __builtin_elementwise_fma(ly, (f2)A.z, (f2)__builtin_fmaf(lx, A.w, c0v));
         const f2 qd = __builtin_elementwise_fma(u, u, v * v);
-        const f2 e = (f2)B.w - qd;
+        const f2 e = (f2)l2op - qd;
         const float a0 = __builtin_amdgcn_exp2f(e.x), a1 = __builtin_amdgcn_exp2f(e.y);
         const bool hit0 = live0 && fmaxf(fabsf(u.x), fabsf(v.x)) <= L && a0 >= amin;
         const bool hit1 = live1 && fmaxf(fabsf(u.y), fabsf(v.y)) <= L && a1 >= amin;
@@ -2366,17 +2371,17 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
             // the blend unit: src * (1 - dst.a) + dst, stored as fp16 (as the oracle does it)
             if (hit0) {
                 const float om = 1.0f - ca.x;
-                cr.x = (float)(_Float16)((C.x * a0) * om + cr.x);
-                cg.x = (float)(_Float16)((C.y * a0) * om + cg.x);
-                cb.x = (float)(_Float16)((C.z * a0) * om + cb.x);
+                cr.x = (float)(_Float16)((kr * a0) * om + cr.x);
+                cg.x = (float)(_Float16)((kg * a0) * om + cg.x);
+                cb.x = (float)(_Float16)((kb * a0) * om + cb.x);
                 ca.x = (float)(_Float16)(a0 * om + ca.x);
                 live0 = ca.x < 1.0f;  // dst.a == 1: later blends add exactly zero
             }
             if (hit1) {
                 const float om = 1.0f - ca.y;
-                cr.y = (float)(_Float16)((C.x * a1) * om + cr.y);
-                cg.y = (float)(_Float16)((C.y * a1) * om + cg.y);
-                cb.y = (float)(_Float16)((C.z * a1) * om + cb.y);
+                cr.y = (float)(_Float16)((kr * a1) * om + cr.y);
+                cg.y = (float)(_Float16)((kg * a1) * om + cg.y);
+                cb.y = (float)(_Float16)((kb * a1) * om + cb.y);
                 ca.y = (float)(_Float16)(a1 * om + ca.y);
                 live1 = ca.y < 1.0f;
             }
@@ -2385,9 +2390,9 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
             // (no contraction: T - am T must not become one fma, k_composite_q rounds it twice)
             const f2 am = {hit0 ? a0 : 0.0f, hit1 ? a1 : 0.0f};
             const f2 s2 = am * T;  // = hit ? a T : 0 (T is finite and >= 0)
-            cr = __builtin_elementwise_fma((f2)C.x, s2, cr);
-            cg = __builtin_elementwise_fma((f2)C.y, s2, cg);
-            cb = __builtin_elementwise_fma((f2)C.z, s2, cb);
+            cr = __builtin_elementwise_fma((f2)kr, s2, cr);
+            cg = __builtin_elementwise_fma((f2)kg, s2, cg);
+            cb = __builtin_elementwise_fma((f2)kb, s2, cb);
             T = T - s2;
             live0 = live0 && T.x >= t_min;
             live1 = live1 && T.y >= t_min;
@@ -2462,8 +2467,8 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {  // park the pixels for chunk 1
-            if (in0) p.state[pix0] = make_float4(cr.x, cg.x, cb.x, FP16_TARGET ? ca.x : T.x);
-            if (in1) p.state[pix1] = make_float4(cr.y, cg.y, cb.y, FP16_TARGET ? ca.y : T.y);
+            if (in0) p.state[pix_of(0)] = make_float4(cr.x, cg.x, cb.x, FP16_TARGET ? ca.x : T.x);
+            if (in1) p.state[pix_of(1)] = make_float4(cr.y, cg.y, cb.y, FP16_TARGET ? ca.y : T.y);
             if (tid == 0) {
                 p.done[tile] = 0;
                 atomicAdd(&p.ctl->not_done, 1u);
@@ -2573,8 +2578,8 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
         const float c0u = -__builtin_fmaf(cxr, ga.z, cyr * ga.w);
         const float c0v = -__builtin_fmaf(cxr, gb.x, cyr * gb.y);
         sR[buf][tid][0] = make_float4(ga.w, ga.z, gb.y, gb.x);  // as k_composite
-        sR[buf][tid][1] = make_float4(c0u, __uint_as_float(gs_), c0v, gb.z);
-        sR[buf][tid][2] = gc;
+        sR[buf][tid][1] = make_float4(gc.x, c0u, gc.y, c0v);
+        sR[buf][tid][2] = make_float4(gc.z, gb.z, __uint_as_float(gs_), gc.w);
         const Ellipse el = ellipse_of(ga, gb);
 #pragma unroll
         for (int hy = 0; hy < 2; ++hy) {  // the splat's columns within the quarter row band
@@ -2595,28 +2600,31 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
         const float4 A = *(const float4*)(sRb + off);
         const float4 B = *(const float4*)(sRb + off + 16);
         const float4 C = *(const float4*)(sRb + off + 32);
+        // staged as [b, a, d, c] [r, c0u, g, c0v] [b, log2 op, slot, key]: each colour channel a
+        // packed fma broadcasts is the low half of an aligned register pair (no moves)
+        const float c0u = B.y, c0v = B.w, l2op = C.y, kr = B.x, kg = B.z, kb = C.x;
         // the same roundings as k_composite's packed pair
-        const float u = __builtin_fmaf(ly, A.x, __builtin_fmaf(lx, A.y, B.x));
-        const float v = __builtin_fmaf(ly, A.z, __builtin_fmaf(lx, A.w, B.z));
+        const float u = __builtin_fmaf(ly, A.x, __builtin_fmaf(lx, A.y, c0u));
+        const float v = __builtin_fmaf(ly, A.z, __builtin_fmaf(lx, A.w, c0v));
         const float qd = __builtin_fmaf(u, u, v * v);
-        const float e = B.w - qd;
+        const float e = l2op - qd;
         const float a = __builtin_amdgcn_exp2f(e);
         const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && a >= amin;
         if (FP16_TARGET) {
 #pragma clang fp contract(off)
             if (hit) {
                 const float om = 1.0f - ca;
-                cr = (float)(_Float16)((C.x * a) * om + cr);
-                cg = (float)(_Float16)((C.y * a) * om + cg);
-                cb = (float)(_Float16)((C.z * a) * om + cb);
+                cr = (float)(_Float16)((kr * a) * om + cr);
+                cg = (float)(_Float16)((kg * a) * om + cg);
+                cb = (float)(_Float16)((kb * a) * om + cb);
                 ca = (float)(_Float16)(a * om + ca);
                 live = ca < 1.0f;
             }
         } else {
             const float s = hit ? a * T : 0.0f;
-            cr = __builtin_fmaf(C.x, s, cr);
-            cg = __builtin_fmaf(C.y, s, cg);
-            cb = __builtin_fmaf(C.z, s, cb);
+            cr = __builtin_fmaf(kr, s, cr);
+            cg = __builtin_fmaf(kg, s, cg);
+            cb = __builtin_fmaf(kb, s, cb);
             T = T - s;
             live = live && T >= t_min;
         }
@@ -3063,10 +3071,13 @@ void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
         else
             hipLaunchKernelGGL(k_composite_q<false>, dim3(grid), dim3(256), 0, s, p);
     } else {
+#ifndef GS_COMP_DYN_LDS
+#define GS_COMP_DYN_LDS 0
+#endif
         if (accum_fp16)
-            hipLaunchKernelGGL(k_composite<true>, dim3(grid), dim3(128), 0, s, p);
+            hipLaunchKernelGGL(k_composite<true>, dim3(grid), dim3(128), GS_COMP_DYN_LDS, s, p);
         else
-            hipLaunchKernelGGL(k_composite<false>, dim3(grid), dim3(128), 0, s, p);
+            hipLaunchKernelGGL(k_composite<false>, dim3(grid), dim3(128), GS_COMP_DYN_LDS, s, p);
     }
 }
 
