@@ -53,18 +53,26 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-// Exclusive scan over a 256-thread block; returns exclusive prefix, *total = block sum.
-// `tmp` = 4 words of LDS.  Contains __syncthreads().
-__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp, uint32_t* total) {
+// Exclusive scan over an NT-thread block; returns exclusive prefix, *total = block sum.
+// `tmp` = NT / 64 words of LDS.  Contains __syncthreads() (wave barriers at NT = 64).
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* tmp, uint32_t* total) {
     const uint32_t incl = wave_incl_scan(v);
     const int w = threadIdx.x >> 6;
     if (lane_id() == 63) tmp[w] = incl;
     __syncthreads();
-    uint32_t base = 0;
-    for (int i = 0; i < w; ++i) base += tmp[i];
-    *total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) {
+        if (i < w) base += tmp[i];
+        tot += tmp[i];
+    }
+    *total = tot;
     __syncthreads();
     return base + incl - v;
+}
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* tmp, uint32_t* total) {
+    return block_excl_scan<256>(v, tmp, total);
 }
 
 // ============================================================================ scene upload
@@ -1959,21 +1967,34 @@ __device__ __forceinline__ void unsat_rows_body(const uint8_t* __restrict__ done
 // when a bucket is heavy).  Longer lists go in rounds of <= kTsCap consecutive keys: a bucket
 // histogram of the remaining keys picks the round's upper bound, the round's elements are
 // gathered into LDS and sorted the same way.  The output depends only on the keys.
-constexpr int kTsThreads = 256;
-constexpr int kTsIpt = 8;
-constexpr uint32_t kTsCap = kTsThreads * kTsIpt;  // entries per round
-constexpr int kTsBucketBits = 10;
-constexpr uint32_t kTsBuckets = 1u << kTsBucketBits;
+// The shape is a template (TsCfg): chunk 0's lists (a few hundred entries at most tiles) are
+// sorted by 128-thread workgroups (TsSmall: 16 KB of LDS and <= 96 VGPRs, five workgroups per
+// SIMD pair instead of one 256-thread workgroup per SIMD; 50 -> 40 us at the bench frame);
+// chunk 1's lists (thousands of entries in the few tiles that never saturate) by TsBig, as in
+// k_chunk1's 256-thread workgroups.
+template <int NT_, int IPT_, int BB_>
+struct TsCfg {
+    static constexpr int NT = NT_;                            // threads
+    static constexpr int IPT = IPT_;                          // entries per thread and round
+    static constexpr uint32_t Cap = (uint32_t)(NT_ * IPT_);   // entries per round
+    static constexpr int BB = BB_;                            // bucket bits
+    static constexpr uint32_t Buckets = 1u << BB_;
+    static_assert(NT_ % 64 == 0 && (1 << BB_) % NT_ == 0, "tile sort shape");
+};
+using TsBig = TsCfg<256, 8, 10>;
+using TsSmall = TsCfg<128, 8, 9>;
 constexpr uint32_t kTsHeavy = 64;  // largest bucket ranked by counting
 
-struct TsShared {
-    unsigned long long k[kTsCap];
-    uint32_t v[kTsCap];
-    uint32_t cnt[kTsBuckets];
-    uint32_t start[kTsBuckets];
+template <class C>
+struct TsSharedT {
+    unsigned long long k[C::Cap];
+    uint32_t v[C::Cap];
+    uint32_t cnt[C::Buckets];
+    uint32_t start[C::Buckets];
     unsigned long long red[8];
     uint32_t tmp[8];
 };
+using TsShared = TsSharedT<TsBig>;
 
 __device__ __forceinline__ unsigned long long ts_key(const TileSortParams& p, uint32_t g) {
     if (!p.skey) return g;
@@ -1981,6 +2002,7 @@ __device__ __forceinline__ unsigned long long ts_key(const TileSortParams& p, ui
     return ((unsigned long long)k.x << 32) | k.y;
 }
 
+template <int NT>
 __device__ __forceinline__ void block_minmax64(unsigned long long& mn, unsigned long long& mx, unsigned long long* s) {
     for (int d = 32; d >= 1; d >>= 1) {
         mn = min(mn, (unsigned long long)__shfl_xor(mn, d, 64));
@@ -1992,21 +2014,30 @@ __device__ __forceinline__ void block_minmax64(unsigned long long& mn, unsigned 
         s[4 + w] = mx;
     }
     __syncthreads();
-    mn = min(min(s[0], s[1]), min(s[2], s[3]));
-    mx = max(max(s[4], s[5]), max(s[6], s[7]));
+    mn = s[0];
+    mx = s[4];
+#pragma unroll
+    for (int i = 1; i < NT / 64; ++i) {
+        mn = min(mn, s[i]);
+        mx = max(mx, s[4 + i]);
+    }
     __syncthreads();
 }
 
+template <class C>
 __device__ __forceinline__ int ts_shift(unsigned long long span) {
-    return span == 0 ? 0 : max(0, 64 - (int)__clzll(span) - kTsBucketBits);
+    return span == 0 ? 0 : max(0, 64 - (int)__clzll(span) - C::BB);
 }
 
-// Sort n <= kTsCap elements held in registers (element j*256 + tid of k/v) with keys in
+// Sort n <= C::Cap elements held in registers (element j * NT + tid of k/v) with keys in
 // [kmin, kmax]; out[rank] = value.
-__device__ void ts_segment(TsShared& S, const unsigned long long (&k)[kTsIpt], const uint32_t (&v)[kTsIpt],
+template <class C>
+__device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT], const uint32_t (&v)[C::IPT],
                            uint32_t n, unsigned long long kmin, unsigned long long kmax, uint32_t* __restrict__ out) {
+    constexpr int kTsThreads = C::NT, kTsIpt = C::IPT;
+    constexpr uint32_t kTsBuckets = C::Buckets;
     const int tid = threadIdx.x;
-    const int s = ts_shift(kmax - kmin);
+    const int s = ts_shift<C>(kmax - kmin);
     for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;
     __syncthreads();
     uint32_t bk[kTsIpt];
@@ -2028,7 +2059,7 @@ __device__ void ts_segment(TsShared& S, const unsigned long long (&k)[kTsIpt], c
         big = max(big, c[q]);
     }
     uint32_t total;
-    uint32_t b = block_excl_scan256(sum, S.tmp, &total);
+    uint32_t b = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
 #pragma unroll
     for (int q = 0; q < per; ++q) {
         S.start[per * tid + q] = b;
@@ -2085,7 +2116,10 @@ __device__ void ts_segment(TsShared& S, const unsigned long long (&k)[kTsIpt], c
     __syncthreads();
 }
 
-__device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t vb, TsShared& S) {
+template <class C>
+__device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t vb, TsSharedT<C>& S) {
+    constexpr int kTsThreads = C::NT, kTsIpt = C::IPT;
+    constexpr uint32_t kTsCap = C::Cap, kTsBuckets = C::Buckets;
     const int per = (p.n_tiles + 7) >> 3;  // XCD-banded, as k_composite
     const int tile = (int)(vb & 7) * per + (int)(vb >> 3);
     if (tile >= p.n_tiles) return;
@@ -2116,8 +2150,8 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
                 mx = max(mx, k[j]);
             }
         }
-        block_minmax64(mn, mx, S.red);
-        ts_segment(S, k, v, L, mn, mx, out);
+        block_minmax64<kTsThreads>(mn, mx, S.red);
+        ts_segment<C>(S, k, v, L, mn, mx, out);
         return;
     }
     // long list: rounds of <= kTsCap consecutive keys
@@ -2127,7 +2161,7 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
         kmin = min(kmin, key);
         kmax = max(kmax, key);
     }
-    block_minmax64(kmin, kmax, S.red);
+    block_minmax64<kTsThreads>(kmin, kmax, S.red);
     unsigned long long lo = kmin, hi = 0ull;
     uint32_t done_n = 0;
     constexpr int perb = kTsBuckets / kTsThreads;
@@ -2136,7 +2170,7 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
         if (bounded) {  // hi: the largest bucket boundary with <= kTsCap keys in [lo, hi)
             unsigned long long span = kmax - lo;
             for (;;) {
-                const int s = ts_shift(span);
+                const int s = ts_shift<C>(span);
                 for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;
                 __syncthreads();
                 for (uint32_t i = tid; i < L; i += kTsThreads) {
@@ -2151,7 +2185,7 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
                     sum += c[q];
                 }
                 uint32_t total;
-                uint32_t run = block_excl_scan256(sum, S.tmp, &total);
+                uint32_t run = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
                 uint32_t fit = 0;
 #pragma unroll
                 for (int q = 0; q < perb; ++q) {
@@ -2159,7 +2193,7 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
                     fit += run <= kTsCap ? 1u : 0u;
                 }
                 uint32_t m;
-                block_excl_scan256(fit, S.tmp, &m);  // buckets whose prefix fits (a prefix of them)
+                block_excl_scan<kTsThreads>(fit, S.tmp, &m);  // buckets whose prefix fits (a prefix of them)
                 if (m >= 1) {
                     hi = lo + ((unsigned long long)m << s);
                     break;
@@ -2193,16 +2227,20 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
                 mx = max(mx, k[j]);
             }
         }
-        block_minmax64(mn, mx, S.red);  // (its barriers order the LDS reads before ts_segment)
-        ts_segment(S, k, v, nc, mn, mx, out + done_n);
+        block_minmax64<kTsThreads>(mn, mx, S.red);  // (its barriers order the LDS reads before ts_segment)
+        ts_segment<C>(S, k, v, nc, mn, mx, out + done_n);
         done_n += nc;
         lo = hi;
     }
 }
 
-__global__ __launch_bounds__(kTsThreads) void k_tile_sort(TileSortParams p) {
-    __shared__ TsShared S;
-    tile_sort_body(p, blockIdx.x, S);
+__global__ __launch_bounds__(TsSmall::NT, 5) void k_tile_sort(TileSortParams p) {
+    __shared__ TsSharedT<TsSmall> S;
+    tile_sort_body<TsSmall>(p, blockIdx.x, S);
+}
+__global__ __launch_bounds__(TsBig::NT, 4) void k_tile_sort_big(TileSortParams p) {
+    __shared__ TsSharedT<TsBig> S;
+    tile_sort_body<TsBig>(p, blockIdx.x, S);
 }
 
 // ============================================================================ k_composite
@@ -2790,7 +2828,7 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     grid_sync(c.bar, ctl);
     C1_MARK(7);
     const uint32_t ntb = 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
-    for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body(c.tp, vb, *(TsShared*)lds);
+    for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body<TsBig>(c.tp, vb, *(TsShared*)lds);
     grid_sync(c.bar, ctl);
     C1_MARK(8);
     for (uint32_t vb = b; vb < ntb; vb += G) composite_q_body<FP16_TARGET>(c.cp, vb, *(CompQShared*)lds);
@@ -3035,7 +3073,10 @@ void launch_bin(const BinParams& p, hipStream_t s) {
 void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return;
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
-    hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(kTsThreads), 0, s, p);
+    if (p.done)  // chunk 1: the unsaturated tiles' long lists
+        hipLaunchKernelGGL(k_tile_sort_big, dim3(grid), dim3(TsBig::NT), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(TsSmall::NT), 0, s, p);
 }
 void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t s) {
     if (!c.two_chunks || c.cp.n_tiles <= 0) grid = 1;  // the frame's end only
