@@ -84,6 +84,19 @@ def pmc_valu(kernel):
     return tot or None
 
 
+def pmc_frame():
+    """HBM bytes of one whole frame (every kernel launch of a steady-state frame, FETCH_SIZE x2 +
+    WRITE_SIZE) and the serialised kernel time, from the committed PMC profile of this bench command."""
+    prof = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc.json")) \
+        if os.path.isdir(os.path.join(ROOT, "profiles")) else []
+    if not prof:
+        return None
+    d = json.load(open(os.path.join(ROOT, "profiles", prof[-1])))
+    b = sum(e.get("traffic_bytes", 0.0) for e in d.values())
+    us = sum(e.get("mean_us", 0.0) for e in d.values())
+    return {"bytes": int(b), "kernel_us_serialised": round(us, 1), "source": prof[-1]} if b else None
+
+
 def frame_bytes(n, n_vis, k, W, H):
     """B = 236 N + 148 N_vis + 48 K + 16 W H."""
     return 236 * n + 148 * n_vis + 48 * k + 16 * W * H
@@ -380,8 +393,15 @@ def main():
                                "kind": "model bytes (SURVEY 8d), not measured traffic",
                                "compulsory_frac": round((236 * N + 16 * W * H) / (ms * 1e-3) / (world * HBM_PEAK), 4),
                                "formula": "236N + 148N_vis + 48K + 16WH (SURVEY 8d)"},
+            # measured: the PMC bytes of every kernel of one frame over the live frame time
+            "frame_traffic": None,
             "cpu_baseline": None,
         }
+        pf = pmc_frame() if world == 1 else None
+        if pf:
+            pf["frac"] = round(pf["bytes"] / (ms * 1e-3) / HBM_PEAK, 4)
+            pf["achieved_GBs"] = round(pf["bytes"] / (ms * 1e-3) / 1e9, 1)
+            out["frame_traffic"] = pf
         out.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(aos, N, W, H, u)

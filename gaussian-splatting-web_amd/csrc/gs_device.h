@@ -22,7 +22,8 @@ constexpr int kUnitShards = 8;        // the frame's work-unit list, sharded (Fr
 constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per radix partition
 constexpr int kBinThreads = 1024;     // binning workgroup (one partition of the chunk's ranks)
 constexpr int kBinParts = 256;        // binning partitions per chunk (rows of BinParams::bmat)
-constexpr int kBandTiles = 8192;      // tiles per binning band (LDS counters / cursors)
+constexpr int kBandTiles = 8192;      // tiles per binning band inside k_chunk1 (static LDS)
+constexpr int kBandTilesMax = 36000;  // largest band of the binning launches (dynamic LDS)
 constexpr int kHistShards = 8;        // global histograms sharded by blockIdx % 8 (XCD group)
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // key of a culled Gaussian (no visible splat has it)
 constexpr int kRecFloats = 16;        // 64-B projected record
@@ -238,6 +239,8 @@ struct BinParams {
                                   // heavy_len first in each XCD band (k_bin_colscan)
     StatShard* stats;             // order_n counters (shard x = band x)
     uint32_t heavy_len;
+    uint32_t band_tiles;          // tiles per binning band (LDS counters / cursors; set by the launcher)
+    uint32_t pref_words;          // LDS words of the per-partition unit prefix (set by the launcher)
 };
 
 // Per-tile sort of the tile lists (k_tile_sort): each tile's slots ordered by their sort key,
@@ -320,6 +323,8 @@ __host__ __device__ inline uint32_t sort_parts(uint64_t n, int ipt) {
     const uint64_t t = (uint64_t)kSortThreads * (uint64_t)ipt;
     return (uint32_t)((n + t - 1) / t);
 }
-__host__ __device__ inline uint32_t bin_bands(uint32_t n_tiles) { return (n_tiles + kBandTiles - 1) / kBandTiles; }
+__host__ __device__ inline uint32_t bin_bands(uint32_t n_tiles, uint32_t band_tiles) {
+    return (n_tiles + band_tiles - 1) / band_tiles;
+}
 
 }  // namespace gs

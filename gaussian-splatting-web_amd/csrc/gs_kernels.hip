@@ -1503,6 +1503,7 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
 //                  position with an LDS atomic (lists are unordered inside a tile: k_tile_sort)
 // Count and emission walk the same ellipse rows, so a tile's count and its entries agree.
 constexpr uint32_t kBinMaxUnits = 4096;  // units per binning partition (scenes up to 2^28 Gaussians)
+constexpr uint32_t kWideQueue = 512;     // wide splats queued per binning workgroup (k_bin_emit)
 
 // The chunk's work units: chunk 0 the frame's list (k_cull), chunk 1 every unit of every partition.
 __device__ __forceinline__ UnitList bin_unit_list(const BinParams& p) {
@@ -1601,7 +1602,7 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
 template <int NT, bool LISTED>
 __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp) {
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
-    const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
+    const uint32_t t_lo = band * p.band_tiles, t_hi = min(p.n_tiles, t_lo + p.band_tiles);
     for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += NT) s_cnt[t] = 0;
     const UnitList L = bin_unit_list(p);
     const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
@@ -1618,11 +1619,23 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
     __syncthreads();
 }
 
+// The binning launches size their LDS to the frame: band_tiles counters (one band up to
+// kBandTilesMax tiles, so a 4K frame's splats are walked once, not once per 8192-tile band) and
+// pref_words of unit prefix (the partition's units at most); a row strip's binning then needs a
+// few KB and fits beside the composite of the frame before it.
+__device__ __forceinline__ uint32_t* bin_lds() {
+    extern __shared__ uint32_t dyn_lds[];
+    return dyn_lds;
+}
+__host__ __device__ inline size_t bin_lds_words(uint32_t band_tiles, uint32_t pref_words) {
+    return (size_t)band_tiles + pref_words + kBinThreads / 64 + kWideQueue + 1;
+}
+
 template <bool LISTED>  // LISTED: chunk 0 (k_cull's unit list); else chunk 1 (every unit, counts from c1)
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
-    __shared__ uint32_t s_cnt[kBandTiles];
-    __shared__ uint32_t s_pref[kBinMaxUnits + 1];
-    __shared__ uint32_t s_tmp[kBinThreads / 64];
+    uint32_t* s_cnt = bin_lds();
+    uint32_t* s_pref = s_cnt + p.band_tiles;
+    uint32_t* s_tmp = s_pref + p.pref_words;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
     bin_count_body<kBinThreads, LISTED>(p, blockIdx.x, s_cnt, s_pref, s_tmp);
 }
@@ -1744,7 +1757,6 @@ __device__ __forceinline__ void tile_scan_body(const BinParams& p, uint32_t* s_w
 // Wide splats (>= kWideTiles box tiles) are queued in LDS by the thread that meets them and
 // emitted row by row by whole waves (lanes over columns); the queue holds kWideQueue splats,
 // beyond that the thread emits its splat itself.
-constexpr uint32_t kWideQueue = 512;
 
 // SCAN: tbase holds the tile totals (colscan) and every workgroup scans them itself up to its
 // band's end (the tile scan, repeated per workgroup from L2 instead of one more launch on
@@ -1755,7 +1767,7 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
                               uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
-    const uint32_t t_lo = band * kBandTiles, t_hi = min(p.n_tiles, t_lo + kBandTiles);
+    const uint32_t t_lo = band * p.band_tiles, t_hi = min(p.n_tiles, t_lo + p.band_tiles);
     const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     const uint32_t cap = p.capacity;
     if (SCAN) {
@@ -1849,13 +1861,13 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
 
 template <bool LISTED>
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
-    __shared__ uint32_t s_cur[kBandTiles];
-    __shared__ uint32_t s_pref[kBinMaxUnits + 1];
-    __shared__ uint32_t s_tmp[kBinThreads / 64];
-    __shared__ uint32_t s_wide[kWideQueue];
-    __shared__ uint32_t s_nw;
+    uint32_t* s_cur = bin_lds();
+    uint32_t* s_pref = s_cur + p.band_tiles;
+    uint32_t* s_tmp = s_pref + p.pref_words;
+    uint32_t* s_wide = s_tmp + kBinThreads / 64;
+    uint32_t* s_nw = s_wide + kWideQueue;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;
-    bin_emit_body<kBinThreads, true, LISTED>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, &s_nw);
+    bin_emit_body<kBinThreads, true, LISTED>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, s_nw);
 }
 
 // End of a frame: the statistic shards summed into FrameCtl (and zeroed), the saturation
@@ -2813,7 +2825,7 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     uint32_t* s_tmp = s_pref + kBinMaxUnits + 1;
     uint32_t* s_wide = s_tmp + 4;
     uint32_t* s_nw = s_wide + kWideQueue;
-    const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles);
+    const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles, c.bp.band_tiles);
     for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256, false>(c.bp, vb, s_a, s_pref, s_tmp);
     grid_sync(c.bar, ctl);
     C1_MARK(4);
@@ -3057,18 +3069,32 @@ void launch_sort_pass(const SortPass& p, hipStream_t s) {
         default: sort_pass_ipt<16>(p, s); break;
     }
 }
-void launch_bin(const BinParams& p, hipStream_t s) {
-    if (p.n_tiles == 0) return;
-    const unsigned grid = kBinParts * bin_bands(p.n_tiles);
+void launch_bin(const BinParams& p0, hipStream_t s) {
+    if (p0.n_tiles == 0) return;
+    static const bool lds_ok = [] {  // dynamic LDS past the default 64 KB
+        const int mx = (int)(bin_lds_words(kBandTilesMax, kBinMaxUnits + 1) * 4);
+        for (const void* f : {(const void*)k_bin_count<true>, (const void*)k_bin_count<false>,
+                              (const void*)k_bin_emit<true>, (const void*)k_bin_emit<false>})
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess) return false;
+        return true;
+    }();
+    (void)lds_ok;
+    BinParams p = p0;
+    const uint32_t bands = (p.n_tiles + kBandTilesMax - 1) / kBandTilesMax;
+    p.band_tiles = (p.n_tiles + bands - 1) / bands;  // equal bands
+    // units of one binning partition: at most ceil(all units / kBinParts)
+    p.pref_words = std::min<uint32_t>(kBinMaxUnits, (p.parts * (uint32_t)kProjRounds + kBinParts - 1) / kBinParts) + 1;
+    const size_t lds = bin_lds_words(p.band_tiles, p.pref_words) * 4;
+    const unsigned grid = kBinParts * bin_bands(p.n_tiles, p.band_tiles);
     if (p.units)
-        hipLaunchKernelGGL(k_bin_count<true>, dim3(grid), dim3(kBinThreads), 0, s, p);
+        hipLaunchKernelGGL(k_bin_count<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
     else
-        hipLaunchKernelGGL(k_bin_count<false>, dim3(grid), dim3(kBinThreads), 0, s, p);
+        hipLaunchKernelGGL(k_bin_count<false>, dim3(grid), dim3(kBinThreads), lds, s, p);
     hipLaunchKernelGGL(k_bin_colscan, dim3((p.n_tiles + kColTiles - 1) / kColTiles), dim3(256), 0, s, p);
     if (p.units)  // each workgroup scans the tile totals itself
-        hipLaunchKernelGGL(k_bin_emit<true>, dim3(grid), dim3(kBinThreads), 0, s, p);
+        hipLaunchKernelGGL(k_bin_emit<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
     else
-        hipLaunchKernelGGL(k_bin_emit<false>, dim3(grid), dim3(kBinThreads), 0, s, p);
+        hipLaunchKernelGGL(k_bin_emit<false>, dim3(grid), dim3(kBinThreads), lds, s, p);
 }
 void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return;
@@ -3078,8 +3104,11 @@ void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     else
         hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(TsSmall::NT), 0, s, p);
 }
-void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t s) {
-    if (!c.two_chunks || c.cp.n_tiles <= 0) grid = 1;  // the frame's end only
+void launch_chunk1(const Chunk1Params& c0, int grid, int accum_fp16, hipStream_t s) {
+    if (!c0.two_chunks || c0.cp.n_tiles <= 0) grid = 1;  // the frame's end only
+    Chunk1Params c = c0;  // k_chunk1's binning phases: static LDS, 8192-tile bands
+    c.bp.band_tiles = kBandTiles;
+    c.bp.pref_words = kBinMaxUnits + 1;
     if (accum_fp16)
         hipLaunchKernelGGL(k_chunk1<true>, dim3(grid), dim3(256), 0, s, c);
     else
