@@ -28,7 +28,10 @@ constexpr int kHistShards = 8;        // global histograms sharded by blockIdx %
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // key of a culled Gaussian (no visible splat has it)
 constexpr int kRecFloats = 16;        // 64-B projected record
 constexpr int kMaxGrid = 2048;        // persistent grids: 8 workgroups per CU
-constexpr uint32_t kWideTiles = 32;     // splats binding >= this many tiles are emitted row-wise
+#ifndef GS_WIDE_TILES
+#define GS_WIDE_TILES 256
+#endif
+constexpr uint32_t kWideTiles = GS_WIDE_TILES;  // splats binding >= this many tiles: walked by whole waves
 constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
 constexpr int kMaxMerge = 16;           // compacted radix input: partitions per downsweep workgroup
 constexpr uint32_t kGroupParts = 32;    // radix partitions per group sum (the downsweep's offsets)
@@ -241,6 +244,7 @@ struct BinParams {
     uint32_t heavy_len;
     uint32_t band_tiles;          // tiles per binning band (LDS counters / cursors; set by the launcher)
     uint32_t pref_words;          // LDS words of the per-partition unit prefix (set by the launcher)
+    uint32_t wide_cap;            // LDS queue of wide splats per workgroup (set by the launcher)
 };
 
 // Per-tile sort of the tile lists (k_tile_sort): each tile's slots ordered by their sort key,

@@ -1503,7 +1503,9 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
 //                  position with an LDS atomic (lists are unordered inside a tile: k_tile_sort)
 // Count and emission walk the same ellipse rows, so a tile's count and its entries agree.
 constexpr uint32_t kBinMaxUnits = 4096;  // units per binning partition (scenes up to 2^28 Gaussians)
-constexpr uint32_t kWideQueue = 512;     // wide splats queued per binning workgroup (k_bin_emit)
+constexpr uint32_t kWideQueue = 512;     // wide splats queued per binning workgroup (k_chunk1)
+constexpr uint32_t kWideQueueMax = 8192; // ... and at most, in the binning launches
+constexpr size_t kBinLdsMaxWords = 40448; // 158 KiB: the binning launches' dynamic LDS bound
 
 // The chunk's work units: chunk 0 the frame's list (k_cull), chunk 1 every unit of every partition.
 __device__ __forceinline__ UnitList bin_unit_list(const BinParams& p) {
@@ -1598,21 +1600,61 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
     }
 }
 
+// Entries of a wide splat (slot g) in tiles [t_lo, t_hi), walked by a whole wave: lane l takes
+// cells l, l + 64, ... of the splat's tile box (in the band), each testing its cell against the
+// ellipse's column range in the cell's tile row.  f(tile) per entry.
+template <class F>
+__device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uint32_t t_lo, uint32_t t_hi, F&& f) {
+    const uint32_t lane = lane_id();
+    const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
+    TileRect tr;
+    rect_unpack(p, p.srect[g], p.sidx[g], tr);
+    const float4* q = p.crec + 3 * (uint64_t)g;
+    const Ellipse e = ellipse_of(q[0], q[1]);
+    const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
+    if (ya > yb) return;
+    const uint32_t w = tr.x1 - tr.x0 + 1, cells = w * (yb - ya + 1);
+    for (uint32_t c = lane; c < cells; c += 64) {
+        const uint32_t ty = ya + c / w, x = tr.x0 + c % w;
+        uint32_t xa, xb;
+        if (!ellipse_row(e, ty, xa, xb) || x < xa || x > xb) continue;
+        const uint32_t t = (ty - rb) * tx + x;
+        if (t < t_lo || t >= t_hi || (p.chunk == 1 && p.done[t])) continue;
+        f(t);
+    }
+}
+
 // Binning partition / band vb: counts of its splats' entries per tile of the band -> bmat row.
+// Wide splats (>= kWideTiles box tiles) are queued in LDS (up to wide_cap) and counted by whole
+// waves, as k_bin_emit emits them.
 template <int NT, bool LISTED>
-__device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp) {
+__device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp,
+                                               uint32_t* s_wide, uint32_t* s_nw_p) {
+    uint32_t& s_nw = *s_nw_p;
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * p.band_tiles, t_hi = min(p.n_tiles, t_lo + p.band_tiles);
     for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += NT) s_cnt[t] = 0;
+    if (threadIdx.x == 0) s_nw = 0;
     const UnitList L = bin_unit_list(p);
     const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
     for (uint32_t r = threadIdx.x; r < total; r += NT) {
         const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
+        if (rect_wide(tr)) {
+            const uint32_t qi = atomicAdd(&s_nw, 1u);
+            if (qi < p.wide_cap) {
+                s_wide[qi] = g;
+                continue;
+            }
+        }
         const float4* q = p.crec + 3 * (uint64_t)g;
         splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
     }
+    __syncthreads();
+    const uint32_t nq = min(s_nw, p.wide_cap);
+    for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64)  // wave-uniform
+        wide_entries(p, s_wide[qi], t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
     __syncthreads();
     uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) row[t] = s_cnt[t - t_lo];
@@ -1627,8 +1669,8 @@ __device__ __forceinline__ uint32_t* bin_lds() {
     extern __shared__ uint32_t dyn_lds[];
     return dyn_lds;
 }
-__host__ __device__ inline size_t bin_lds_words(uint32_t band_tiles, uint32_t pref_words) {
-    return (size_t)band_tiles + pref_words + kBinThreads / 64 + kWideQueue + 1;
+__host__ __device__ inline size_t bin_lds_words(uint32_t band_tiles, uint32_t pref_words, uint32_t wide_cap) {
+    return (size_t)band_tiles + pref_words + kBinThreads / 64 + wide_cap + 1;
 }
 
 template <bool LISTED>  // LISTED: chunk 0 (k_cull's unit list); else chunk 1 (every unit, counts from c1)
@@ -1636,8 +1678,10 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     uint32_t* s_cnt = bin_lds();
     uint32_t* s_pref = s_cnt + p.band_tiles;
     uint32_t* s_tmp = s_pref + p.pref_words;
+    uint32_t* s_wide = s_tmp + kBinThreads / 64;
+    uint32_t* s_nw = s_wide + p.wide_cap;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
-    bin_count_body<kBinThreads, LISTED>(p, blockIdx.x, s_cnt, s_pref, s_tmp);
+    bin_count_body<kBinThreads, LISTED>(p, blockIdx.x, s_cnt, s_pref, s_tmp, s_wide, s_nw);
 }
 
 // Per tile: exclusive prefix of its column of bmat over the partitions (in place) and the tile's
@@ -1819,7 +1863,7 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
         if (rect_wide(tr)) {
             const uint32_t qi = atomicAdd(&s_nw, 1u);
-            if (qi < kWideQueue) {
+            if (qi < p.wide_cap) {
                 s_wide[qi] = g;
                 continue;
             }
@@ -1831,30 +1875,14 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
         });
     }
     __syncthreads();
-    const uint32_t nq = min(s_nw, kWideQueue);
+    const uint32_t nq = min(s_nw, p.wide_cap);
     if (threadIdx.x == 0 && s_nw) atomicAdd(&p.ctl->wide_n[p.chunk], s_nw);  // statistics
-    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
-    for (uint32_t qi = wave; qi < nq; qi += NT / 64) {  // wave-uniform
+    for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64) {  // wave-uniform
         const uint32_t g = s_wide[qi];
-        TileRect tr;
-        rect_unpack(p, p.srect[g], p.sidx[g], tr);
-        const float4* q = p.crec + 3 * (uint64_t)g;
-        const Ellipse e = ellipse_of(q[0], q[1]);
-        const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
-        for (uint32_t ty = ya; ty <= yb; ++ty) {
-            uint32_t xa, xb;
-            if (!ellipse_row(e, ty, xa, xb)) continue;
-            xa = max(xa, tr.x0);
-            xb = min(xb, tr.x1);
-            const uint32_t t0 = (ty - rb) * tx;
-            for (uint32_t x = xa + lane; x <= xb; x += 64) {
-                const uint32_t t = t0 + x;
-                if (t < t_lo || t >= t_hi || (p.chunk == 1 && p.done[t])) continue;
-                const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
-                if (pos < cap) p.tvals[pos] = g;
-            }
-        }
+        wide_entries(p, g, t_lo, t_hi, [&](uint32_t t) {
+            const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
+            if (pos < cap) p.tvals[pos] = g;
+        });
     }
     __syncthreads();
 }
@@ -1865,7 +1893,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     uint32_t* s_pref = s_cur + p.band_tiles;
     uint32_t* s_tmp = s_pref + p.pref_words;
     uint32_t* s_wide = s_tmp + kBinThreads / 64;
-    uint32_t* s_nw = s_wide + kWideQueue;
+    uint32_t* s_nw = s_wide + p.wide_cap;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;
     bin_emit_body<kBinThreads, true, LISTED>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, s_nw);
 }
@@ -2826,7 +2854,7 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     uint32_t* s_wide = s_tmp + 4;
     uint32_t* s_nw = s_wide + kWideQueue;
     const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles, c.bp.band_tiles);
-    for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256, false>(c.bp, vb, s_a, s_pref, s_tmp);
+    for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
     grid_sync(c.bar, ctl);
     C1_MARK(4);
     const uint32_t ncol = (c.bp.n_tiles + kColTiles - 1) / kColTiles;
@@ -3072,7 +3100,7 @@ void launch_sort_pass(const SortPass& p, hipStream_t s) {
 void launch_bin(const BinParams& p0, hipStream_t s) {
     if (p0.n_tiles == 0) return;
     static const bool lds_ok = [] {  // dynamic LDS past the default 64 KB
-        const int mx = (int)(bin_lds_words(kBandTilesMax, kBinMaxUnits + 1) * 4);
+        const int mx = (int)(kBinLdsMaxWords * 4);
         for (const void* f : {(const void*)k_bin_count<true>, (const void*)k_bin_count<false>,
                               (const void*)k_bin_emit<true>, (const void*)k_bin_emit<false>})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess) return false;
@@ -3084,7 +3112,11 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
     p.band_tiles = (p.n_tiles + bands - 1) / bands;  // equal bands
     // units of one binning partition: at most ceil(all units / kBinParts)
     p.pref_words = std::min<uint32_t>(kBinMaxUnits, (p.parts * (uint32_t)kProjRounds + kBinParts - 1) / kBinParts) + 1;
-    const size_t lds = bin_lds_words(p.band_tiles, p.pref_words) * 4;
+    // wide-splat queue: larger frames hold more splats that cover many tiles (near splats at 4K);
+    // a splat past the queue is walked by its own thread
+    const uint32_t room = (uint32_t)(kBinLdsMaxWords - bin_lds_words(p.band_tiles, p.pref_words, 0));
+    p.wide_cap = std::min(room, std::max(kWideQueue, std::min(kWideQueueMax, p.n_tiles / 4)));
+    const size_t lds = bin_lds_words(p.band_tiles, p.pref_words, p.wide_cap) * 4;
     const unsigned grid = kBinParts * bin_bands(p.n_tiles, p.band_tiles);
     if (p.units)
         hipLaunchKernelGGL(k_bin_count<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
@@ -3109,6 +3141,7 @@ void launch_chunk1(const Chunk1Params& c0, int grid, int accum_fp16, hipStream_t
     Chunk1Params c = c0;  // k_chunk1's binning phases: static LDS, 8192-tile bands
     c.bp.band_tiles = kBandTiles;
     c.bp.pref_words = kBinMaxUnits + 1;
+    c.bp.wide_cap = kWideQueue;
     if (accum_fp16)
         hipLaunchKernelGGL(k_chunk1<true>, dim3(grid), dim3(256), 0, s, c);
     else

@@ -13,8 +13,8 @@ from gsplat_amd.strips import strip_geometry  # noqa: E402
 
 
 def main():
-    N, W, H = int(os.environ.get("N", 6_100_000)), 1920, 1080
-    aos = gs.synth_aos(N, 6, W, H)
+    N, W, H = int(os.environ.get("N", 6_100_000)), int(os.environ.get("W", 1920)), int(os.environ.get("H", 1080))
+    aos = gs.synth_aos(N, int(os.environ.get("SEED", 6)), W, H)
     u = gs.bench_uniforms(W, H)
     ctx = gs.Context(0)
     base = 0.0
