@@ -94,6 +94,13 @@ enum { ST_TOTAL, ST_PROJECT, ST_SORT, ST_BIN, ST_TSORT, ST_RANGES, ST_COMPOSITE,
 // Frames in flight: per-frame buffers (FrameSet), statistics slots and timing events rotate over
 // this many frames; frame f reuses frame f - kFrameSets's set once that frame has ended.
 constexpr int kFrameSets = GS_FRAME_SETS;
+// Frame statistics and timing events rotate over more slots than there are frame sets: the host
+// reads a frame's statistics (and its events) whenever they have arrived and never waits for the
+// frame kFrameSets back to enqueue the next one (the sets' reuse is ordered on the device).  With
+// kFrameSets slots the host blocked every third row-strip frame for the one three back
+// (G = 8 strip: enqueue p50 34 us, p90 280 us, so at most ~1.5 frames ran on the GPU at once).
+constexpr int kStatSlots = 8;
+static_assert(kStatSlots >= kFrameSets && kStatSlots * 4 <= 64, "statistics slots (h_seq: 64 B)");
 constexpr int kDeepTiles = 1536;  // frames of at most this many tiles keep kFrameSets in flight
 
 struct FrameEvents {
@@ -134,7 +141,7 @@ struct gs_ctx {
     hipStream_t stream = nullptr;
     void* d_out = nullptr;
     size_t d_out_bytes = 0;
-    FrameEvents fe[kFrameSets];  // rotating: frame t's events are read once frame t + kFrameSets needs the slot
+    FrameEvents fe[kStatSlots];  // rotating: frame t's events are read once frame t + kStatSlots needs the slot
     int fe_cur = 0;
     double acc_ms[ST_COUNT] = {};
     uint32_t acc_frames = 0;    // frames timed at level 1 (every stage)
@@ -208,15 +215,15 @@ struct gs_scene {
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     int last_tiles = 0;                 // tiles of the last frame's strip
     // asynchronous frame statistics (chunk controller, capacity): the frame's end (k_chunk1) stores FrameCtl into
-    // a pinned slot and then publishes a sequence number there; kFrameSets slots (frames in flight)
-    FrameCtl* h_ctl = nullptr;    // pinned, coherent, device-mapped (d_ctl_slot): kFrameSets slots
+    // a pinned slot and then publishes a sequence number there; kStatSlots slots
+    FrameCtl* h_ctl = nullptr;    // pinned, coherent, device-mapped (d_ctl_slot): kStatSlots slots
     uint32_t* h_seq = nullptr;    // pinned, coherent, device-mapped (d_seq): per slot
     FrameCtl* d_ctl_slot = nullptr;
     uint32_t* d_seq = nullptr;
     uint32_t seq_next = 1;
-    uint32_t stat_want[kFrameSets] = {};   // sequence number that completes the slot's frame
-    uint32_t stat_base[kFrameSets] = {};   // the slot's frame's saturation-histogram base (sat_bucket)
-    bool stat_pending[kFrameSets] = {};
+    uint32_t stat_want[kStatSlots] = {};   // sequence number that completes the slot's frame
+    uint32_t stat_base[kStatSlots] = {};   // the slot's frame's saturation-histogram base (sat_bucket)
+    bool stat_pending[kStatSlots] = {};
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
     uint32_t pending_err = 0;   // error bits of every harvested frame not yet reported (sticky)
@@ -388,8 +395,8 @@ static bool wait_slot(gs_scene* s, int slot, hipStream_t st) {
 
 // Latest frame statistics that have arrived on the host; `wait` blocks for the newest frame.
 static void collect_stats(gs_scene* s, bool wait) {
-    for (int k = 0; k < kFrameSets; ++k) {
-        const int slot = (s->stat_cur + k) % kFrameSets;  // oldest slot first
+    for (int k = 0; k < kStatSlots; ++k) {
+        const int slot = (s->stat_cur + k) % kStatSlots;  // oldest slot first
         if (!s->stat_pending[slot]) continue;
         if (!seq_arrived(s, slot)) {
             if (!wait) continue;
@@ -470,7 +477,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     if (o.timing == 1) HIPCHK(hipStreamWaitEvent(st, s->fs[s->last_fs].ev_out, 0));
     collect_stats(s, false);
     const int slot = s->stat_cur;  // this frame's statistics slot
-    if (s->stat_pending[slot]) {  // the slot's last frame (kFrameSets ago): its statistics first
+    if (s->stat_pending[slot]) {  // the slot's last frame (kStatSlots ago): its statistics first
         wait_slot(s, slot, nullptr);
         collect_stats(s, false);
         s->stat_pending[slot] = false;
@@ -707,10 +714,10 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     HIPCHK(hipGetLastError());
     if (timed) {
         fe.pending = true;
-        c->fe_cur = (c->fe_cur + 1) % kFrameSets;
+        c->fe_cur = (c->fe_cur + 1) % kStatSlots;
     }
     s->stat_pending[slot] = true;  // frame statistics arrive asynchronously (k_chunk1)
-    s->stat_cur = (s->stat_cur + 1) % kFrameSets;
+    s->stat_cur = (s->stat_cur + 1) % kStatSlots;
     s->have_frame = true;
     c->last_scene = s;
     c->stats.n = s->n;
@@ -1094,7 +1101,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 ensure_tile_capacity(F, 4 * n + (1u << 20));
             }
             const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
-            HIPCHK(hipHostMalloc((void**)&s->h_ctl, kFrameSets * sizeof(FrameCtl), hf));
+            HIPCHK(hipHostMalloc((void**)&s->h_ctl, kStatSlots * sizeof(FrameCtl), hf));
             HIPCHK(hipHostMalloc((void**)&s->h_seq, 64, hf));
             std::memset(s->h_seq, 0, 64);
             HIPCHK(hipHostGetDevicePointer((void**)&s->d_ctl_slot, s->h_ctl, 0));
@@ -1415,7 +1422,7 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
             return GS_OK;
         }
         HIPCHK(hipSetDevice(c->device));
-        for (int k = 1; k <= kFrameSets; ++k) harvest(c, c->fe[(c->fe_cur + k) % kFrameSets]);  // oldest first
+        for (int k = 1; k <= kStatSlots; ++k) harvest(c, c->fe[(c->fe_cur + k) % kStatSlots]);  // oldest first
         gs_stats st = c->stats;
         if (c->last_scene) {
             collect_stats(c->last_scene, true);

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Host-side cost of enqueuing bench frames: wall time of N render_device calls (no sync) vs the
-time until the GPU drains, at timing levels 0 and 2."""
+time until the GPU drains, at timing levels 0 and 2 (env GS / STRIP: one row strip of GS)."""
 import os
 import sys
 import time
@@ -17,8 +17,9 @@ def main():
     ctx = gs.Context(0)
     sc = gs.Scene(ctx, aos, N, 16)
     buf = gs.DeviceBuffer(H * W * 8)
+    G, S = int(os.environ.get("GS", "1")), int(os.environ.get("STRIP", "0"))
     for lvl in (0, 2, 0):
-        o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=lvl)
+        o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=lvl, strip_index=S, strip_count=G)
         for _ in range(10):
             sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
         ctx.sync()
