@@ -224,7 +224,11 @@ def main():
     if launched:
         import torch
         from gsplat_amd.strips import StripPipeline
-        stream = torch.cuda.current_stream()
+        # a stream of our own for the frames: the default stream's handle is 0, which the C ABI
+        # reads as "the context's stream", and the strip pipeline's events must be recorded on the
+        # stream the frame's composite actually ran on
+        stream = torch.cuda.Stream()
+        torch.cuda.set_stream(stream)
         pipe = StripPipeline(rows_padded, W, dtype=torch.float16)  # gather t beside render t+1
 
         def frame_u(uu):
