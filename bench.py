@@ -337,8 +337,11 @@ def main():
     a_bytes = algorithmic_bytes(dom, N, ex["n_vis"], st["k_entries"], W, rows_here,
                                 n_chunk0=int(round(st["chunk_fraction"] * st["n_vis"])))
     achieved = a_bytes / (stages[dom] * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(dom)
-    valu = pmc_valu(dom) if world == 1 else None
+    # the committed PMC profile is of the default command (configs[3] on one GPU): its counters
+    # only describe that workload
+    profiled = world == 1 and args.config == 3 and (N, W, H) == (N0, W0, H0)
+    traffic, traffic_src = pmc_traffic(dom) if profiled else (None, None)
+    valu = pmc_valu(dom) if profiled else None
     fb = frame_bytes(N, n_vis_all, k_all, W, H)
 
     if rank == 0:
@@ -401,7 +404,7 @@ def main():
             "frame_traffic": None,
             "cpu_baseline": None,
         }
-        pf = pmc_frame() if world == 1 else None
+        pf = pmc_frame() if profiled else None
         if pf:
             pf["frac"] = round(pf["bytes"] / (ms * 1e-3) / HBM_PEAK, 4)
             pf["achieved_GBs"] = round(pf["bytes"] / (ms * 1e-3) / 1e9, 1)
@@ -413,7 +416,7 @@ def main():
     scene.close()
     ctx.close()
     if rank == 0:
-        if world == 1 and not args.no_extra:
+        if world == 1 and not args.no_extra and args.config == 3:
             out["node_fps"] = node_fps(N, seed, W, H)
         print(json.dumps(out), flush=True)
     if dist is not None:
