@@ -99,6 +99,10 @@ constexpr int kFrameSets = GS_FRAME_SETS;
 // frame kFrameSets back to enqueue the next one (the sets' reuse is ordered on the device).  With
 // kFrameSets slots the host blocked every third row-strip frame for the one three back
 // (G = 8 strip: enqueue p50 34 us, p90 280 us, so at most ~1.5 frames ran on the GPU at once).
+#ifndef GS_SET_STREAMS
+#define GS_SET_STREAMS kFrameSets
+#endif
+constexpr int kSetStreams = GS_SET_STREAMS;  // distinct streams of the frame sets
 constexpr int kStatSlots = 8;
 static_assert(kStatSlots >= kFrameSets && kStatSlots * 4 <= 64, "statistics slots (h_seq: 64 B)");
 constexpr int kDeepTiles = 1536;  // frames of at most this many tiles keep kFrameSets in flight
@@ -1076,10 +1080,19 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->bounds, (size_t)proj_parts(n) + 1);
             dev_alloc(s->orig, (size_t)n + 1);
-            for (FrameSet& F : s->fs) {
-                HIPCHK(hipStreamCreateWithFlags(&F.stream, hipStreamNonBlocking));
-                HIPCHK(hipEventCreateWithFlags(&F.ev_early, hipEventDisableTiming));
-                HIPCHK(hipEventCreateWithFlags(&F.ev_out, hipEventDisableTiming));
+            for (int k = 0; k < kFrameSets; ++k) {
+                FrameSet& F = s->fs[k];
+                // (high-priority set streams, like more hardware queues, ran every kernel slower:
+                // G = 8 strip 0.09 -> 0.20 ms)
+                if (k < kSetStreams) HIPCHK(hipStreamCreateWithFlags(&F.stream, hipStreamNonBlocking));
+                else  // sets share streams: set k runs on set k % kSetStreams's stream
+                    F.stream = s->fs[k % kSetStreams].stream;
+                // the set's events order work on this device only (the host paces on ev_out and
+                // reads frame data through its own protocols): no system-scope fence when they
+                // are recorded (the default writes back and invalidates the caches; the composite
+                // then waited ~17 us on the set stream's per-tile sort, now ~13-15 us)
+                HIPCHK(hipEventCreateWithFlags(&F.ev_early, hipEventDisableTiming | hipEventDisableSystemFence));
+                HIPCHK(hipEventCreateWithFlags(&F.ev_out, hipEventDisableTiming | hipEventDisableSystemFence));
                 HIPCHK(hipEventRecord(F.ev_out, F.stream));  // "the last frame on this set ended"
                 dev_alloc(F.r2, (size_t)std::max<uint64_t>(n, 1));
                 dev_alloc(F.crec, 3 * ((size_t)proj_parts(n) * kProjTile + 1));
@@ -1198,8 +1211,9 @@ void gs_scene_free(gs_scene* s) {
         dev_free(F.state);
         if (F.ev_early) (void)hipEventDestroy(F.ev_early);
         if (F.ev_out) (void)hipEventDestroy(F.ev_out);
-        if (F.stream) (void)hipStreamDestroy(F.stream);
     }
+    for (int k = 0; k < kSetStreams; ++k)  // (sets past kSetStreams share these)
+        if (s->fs[k].stream) (void)hipStreamDestroy(s->fs[k].stream);
     dev_free(s->bounds);
     dev_free(s->orig);
     dev_free(s->qk); dev_free(s->qv); dev_free(s->qK); dev_free(s->qV); dev_free(s->qK2); dev_free(s->qV2);
