@@ -1907,7 +1907,7 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
                                uint32_t seq, uint32_t* lds) {
     constexpr uint32_t kWords = sizeof(FrameCtl) / 4;
     constexpr uint32_t kShardWords = sizeof(StatShard) / 4, kStride = kShardWords | 1u;  // odd: no bank conflicts
-    static_assert(kWords <= 64 && kStatShards == 64 && kShardWords <= 64, "one wave");
+    static_assert(kWords <= 64 && kStatShards <= 64 && kStatShards >= 8 && kShardWords <= 64, "one wave");
     static_assert(offsetof(StatShard, k_total) == 0 && offsetof(StatShard, n_vis) == 8 &&
                   offsetof(StatShard, key_min_inv) == 12 && offsetof(StatShard, key_max) == 16 &&
                   offsetof(StatShard, n_chunk) == 20 && offsetof(StatShard, sat_key) == 28 &&
@@ -1924,16 +1924,23 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
         FE_MARK(7);
     }
 #endif
-    // the shards transposed through LDS (lane = shard), then lane f reduces word f over the 64
-    // shards: a few LDS reads each instead of a shuffle tree per field
+    // the shards into LDS (row = shard) as one flat array of lane-consecutive words, then lane f
+    // reduces word f over the shards: a few LDS reads each instead of a shuffle tree per field
     {
-        const uint32_t* sw = (const uint32_t*)(stats + lane);
-        uint32_t w[kShardWords];
+        constexpr uint32_t kAll = kStatShards * kShardWords, kPer = (kAll + 63) / 64;
+        const uint32_t* sw = (const uint32_t*)stats;
+        uint32_t* sz = (uint32_t*)stats;
+        uint32_t w[kPer];
 #pragma unroll
-        for (uint32_t k = 0; k < kShardWords; ++k) w[k] = sw[k];
-        stats[lane] = StatShard{};
+        for (uint32_t k = 0; k < kPer; ++k) w[k] = k * 64 + lane < kAll ? sw[k * 64 + lane] : 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < kShardWords; ++k) lds[lane * kStride + k] = w[k];
+        for (uint32_t k = 0; k < kPer; ++k)
+            if (k * 64 + lane < kAll) sz[k * 64 + lane] = 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t i = k * 64 + lane;
+            if (i < kAll) lds[(i / kShardWords) * kStride + i % kShardWords] = w[k];
+        }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
