@@ -31,7 +31,9 @@ def main():
                 continue
             o = gs.make_opts(strip_index=g, strip_count=G, timing=int(os.environ.get("TIMING", "1")),
                              out_format=gs.GS_OUT_RGBA_F16)
-            for _ in range(5):
+            # warm-up: the scene's chunk controller was last fed another strip's statistics,
+            # which reach the host up to 8 frames late
+            for _ in range(int(os.environ.get("WARMUP", 20))):
                 sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
             ctx.sync()
             ctx.timings_reset()
