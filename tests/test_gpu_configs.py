@@ -83,3 +83,29 @@ def test_config4_50m_4k(gpu_ctx):
     assert st_gpu["n_vis"] == st["n_vis"]
     r = image_close_fp32(img, ref, name=None)
     assert r[2], r
+
+
+@pytest.mark.timeout(300)
+def test_two_binning_bands_5120x2880(gpu_ctx):
+    """A frame past one binning band (320 x 180 = 57 600 tiles > kBandTilesMax = 36 000: the
+    launches split it into two equal bands, each walking every splat for its rows): every pixel
+    against the oracle, a chunk split bit-identical to one chunk, and its 4 row strips
+    bit-identical to the full frame."""
+    W, H, n = 5120, 2880, 200_000
+    aos = gs.synth_aos(n, 3, W, H)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    img = sc.render(u, W, H, gs.make_opts(chunk_fraction=1.0))
+    ref, st = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=1e-4)
+    assert gpu_ctx.timings()["n_vis"] == st["n_vis"]
+    r = image_close_fp32(img, ref, name="bands_5k")
+    assert r[2], r
+    split = sc.render(u, W, H, gs.make_opts(chunk_fraction=0.25))
+    assert np.array_equal(split, img)
+    G = 4
+    rows = []
+    for g in range(G):
+        s = sc.render(u, W, H, gs.make_opts(chunk_fraction=1.0, strip_index=g, strip_count=G))
+        rows.append(s)
+    full = np.concatenate(rows, axis=0)[:H]
+    assert np.array_equal(full, img)
