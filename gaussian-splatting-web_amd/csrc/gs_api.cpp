@@ -233,6 +233,7 @@ struct gs_scene {
     uint32_t pending_err = 0;   // error bits of every harvested frame not yet reported (sticky)
     bool have_last = false;
     uint32_t chunk_T = kNoSplit;        // adaptive chunk threshold for the next frame
+    float last_view[16] = {};           // the last frame's view matrix (a moving camera widens T)
     uint32_t key_lo = 0, key_hi = 0;    // depth-key range of the last frame's visible splats
     bool have_krange = false;
     bool have_frame = false;
@@ -265,6 +266,10 @@ static constexpr int kDepthSortIpt = 8;
 #define GS_CHUNK_MARGIN 1.05f
 #endif
 static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
+#ifndef GS_MOVING_MARGIN
+#define GS_MOVING_MARGIN 1.10f
+#endif
+static constexpr float kMovingMargin = GS_MOVING_MARGIN;  // extra depth margin while the view changes
 // split the visible splats into two chunks when at least this share of the tiles saturated in the
 // last frame; chunk 1 then visits only the partitions that can reach an unsaturated tile
 #ifndef GS_SPLIT_SAT_FRAC
@@ -495,6 +500,13 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     // diagnostics (chunk_fraction in (0,1): the depth 2^-t <= chunk_fraction of the way from the
     // last frame's nearest to its farthest visible splat; one chunk until a frame was seen)
     uint32_t T = s->chunk_T;
+    {  // the statistics are a few frames old: while the camera moves, the depth at which tiles
+       // saturate moves too, so the threshold gets a wider margin (1.05 x 1.10 ~ the 1.15 used for
+       // every frame until round 2); a still camera keeps the tight one
+        const bool moving = std::memcmp(s->last_view, uni, sizeof(s->last_view)) != 0;
+        std::memcpy(s->last_view, uni, sizeof(s->last_view));
+        if (moving && T != kNoSplit) T = scaled_threshold(T, kMovingMargin);
+    }
     if (o.chunk_fraction >= 1.0f) {
         T = kNoSplit;
     } else if (o.chunk_fraction > 0.0f) {
