@@ -141,14 +141,8 @@ def node_fps(n, seed, W, H, frames=100):
 
 
 def orbit_uniforms(W, H, k, period=60):
-    """A moving camera for the orbit loop: at the origin, yaw swinging +-25 deg and pitch +-8 deg
-    around the bench view (-z), a new view every frame; part of the screen leaves the scene's
-    frustum, so tiles go unsaturated and the chunk split moves."""
-    a = 2 * np.pi * k / period
-    yaw, pitch = np.radians(25.0) * np.sin(a), np.radians(8.0) * np.sin(2 * a)
-    target = (np.sin(yaw) * np.cos(pitch), np.sin(pitch), -np.cos(yaw) * np.cos(pitch))
-    view = gs.look_at((0.0, 0.0, 0.0), target)
-    return gs.pack_uniforms(view, gs.perspective(1.04719755, W / H, 0.03, 1000.0), focal=(W, H))
+    """The orbit loop's camera (gsplat_amd.orbit_uniforms: yaw +-25 deg, pitch +-8 deg)."""
+    return gs.orbit_uniforms(W, H, k, period)
 
 
 def spawn_ranks(n, cmd=None):

@@ -409,6 +409,10 @@ napi_value Timings(napi_env env, napi_callback_info info) {
     put("msTileSort", st.ms_tile_sort);
     put("msRanges", st.ms_ranges);
     put("msComposite", st.ms_composite);
+    put("framesRendered", st.frames_rendered);
+    put("framesChunked", st.frames_chunked);
+    put("framesUnsat", st.frames_unsat);
+    put("framesSeeded", st.frames_seeded);
     return o;
 }
 

@@ -141,7 +141,10 @@ uint32_t scaled_threshold(uint32_t k, float factor) {
 
 struct gs_ctx {
     int device = 0;
-    int num_cus = 256;            // k_chunk1's grid: one workgroup per CU
+    int num_cus = 256;
+    int c1_occ = 0;               // k_chunk1 workgroups resident per CU (occupancy query)
+    int c1_grid = 0;              // k_chunk1's grid: chunk1_grid(c1_occ, num_cus), co-resident
+    uint64_t spin_ticks = 20000000;  // grid-barrier timeout: 200 ms of the device's wall clock
     hipStream_t stream = nullptr;
     void* d_out = nullptr;
     size_t d_out_bytes = 0;
@@ -152,6 +155,9 @@ struct gs_ctx {
     double acc_comp_ms = 0.0;   // composite time of every timed frame (levels 1 and 2)
     uint32_t comp_frames = 0;
     gs_stats stats{};
+    // frame counts since gs_timings_reset (gs_stats::frames_*)
+    uint32_t n_rendered = 0, n_chunked = 0, n_unsat = 0, n_seeded = 0;
+    std::vector<std::pair<void*, uint64_t>> fbufs;  // gs_framebuffer_alloc'd buffers and their sizes
     gs_scene* last_scene = nullptr;
     std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
     // A device group (gs_ctx_create with ndev > 1): one single-device member context per entry;
@@ -231,6 +237,7 @@ struct gs_scene {
     int stat_cur = 0;
     FrameCtl last{};            // latest harvested statistics
     uint32_t pending_err = 0;   // error bits of every harvested frame not yet reported (sticky)
+    uint64_t overflow_k = 0;    // largest k_total of a harvested frame that overflowed the tile lists
     bool have_last = false;
     uint32_t chunk_T = kNoSplit;        // adaptive chunk threshold for the next frame
     float last_view[16] = {};           // the last frame's view matrix (a moving camera widens T)
@@ -418,6 +425,8 @@ static void collect_stats(gs_scene* s, bool wait) {
         }
         s->last = s->h_ctl[slot];
         s->pending_err |= s->last.err;  // an older frame's error is not overwritten by a newer clean frame
+        if (s->last.err & kErrOverflow) s->overflow_k = std::max<uint64_t>(s->overflow_k, s->last.k_total);
+        if (s->last.not_done > 0) s->ctx->n_unsat++;
         s->have_last = true;
         s->stat_pending[slot] = false;
         // chunk controller: chunk 0 = the splats nearer than 1.15x the depth at which the last
@@ -526,6 +535,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     }
     s->last_quirk = quirk;
     const bool two_chunks = T != kNoSplit;
+    c->n_rendered++;
+    c->n_chunked += two_chunks ? 1u : 0u;
     if (two_chunks) {
         ensure_state(F, (uint64_t)W * H);
         ensure_sat(F, (size_t)(tr_end - tr_begin + 1) * (TX + 1) + 2 + (size_t)(tr_end - tr_begin) * ((TX + 63) / 64) * 2);
@@ -704,6 +715,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.cp.order = nullptr;
         c1.sat = F.sat;
         c1.bar = F.bar;
+        c1.spin_ticks = c->spin_ticks;
         c1.two_chunks = two_chunks ? 1 : 0;
         const uint32_t q = s->seq_next++;
         s->stat_want[slot] = q;
@@ -720,7 +732,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         if (two_chunks && s->have_last && s->last.not_done > 0)
             launch_chunk1_split(c1, o.accum == GS_ACCUM_FP16_TARGET, st);
         else
-            launch_chunk1(c1, std::min(c->num_cus, 64), o.accum == GS_ACCUM_FP16_TARGET, st);
+            launch_chunk1(c1, c->c1_grid, o.accum == GS_ACCUM_FP16_TARGET, st);
         if (two_chunks && o.timing == 1) mark(EV_COMP_1);
     }
     F.meta_clean = true;
@@ -774,10 +786,19 @@ static size_t out_bytes_for(int W, int H, const gs_opts& o) {
     return rows * (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
 }
 
+// After a tile-list overflow: every frame set grows to the largest total of the frames that
+// overflowed (a later, smaller frame's total would grow them too little).
+static void grow_after_overflow(gs_scene* s) {
+    const uint64_t k = std::max<uint64_t>(s->overflow_k, s->last.k_total);
+    for (FrameSet& F : s->fs) ensure_tile_capacity(F, k);
+    s->overflow_k = 0;
+}
+
 // Frame errors surface here: every frame's FrameCtl comes back asynchronously, so an error of a
 // frame rendered with gs_render_device is reported by a later call (gsplat.h).  The error bits of
 // every harvested frame accumulate in pending_err until reported.
 static void check_frame_errors(gs_scene* s) {
+    HIPCHK(hipSetDevice(s->ctx->device));  // a device group's member: its own device
     collect_stats(s, true);
     const uint32_t e = s->pending_err;
     s->pending_err = 0;
@@ -787,7 +808,7 @@ static void check_frame_errors(gs_scene* s) {
         throw GsError(GS_ERR_DEVICE_FAULT, "chunk-1 grid barrier timed out (workgroups not co-resident)");
     }
     if (e & kErrOverflow) {
-        for (FrameSet& F : s->fs) ensure_tile_capacity(F, s->last.k_total);
+        grow_after_overflow(s);
         throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded; capacity grown, render again");
     }
 }
@@ -1014,6 +1035,16 @@ static gs_ctx* create_single(int dev) {
         int cus = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         if (cus > 0) c->num_cus = cus;
+        // k_chunk1's grid barrier needs every workgroup resident at once: its grid is sized from
+        // the occupancy query, and a device that cannot hold it is refused here
+        c->c1_occ = chunk1_occupancy();
+        c->c1_grid = chunk1_grid(c->c1_occ, c->num_cus);
+        if (c->c1_grid <= 0)
+            throw GsError(GS_ERR_UNSUPPORTED, "k_chunk1 cannot be resident on this device (occupancy " +
+                                                  std::to_string(c->c1_occ) + " per CU)");
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+            c->spin_ticks = (uint64_t)khz * 200u;  // 200 ms
         HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         for (auto& f : c->fe)
             for (auto& e : f.ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -1272,8 +1303,9 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
         if (out_bytes < out_bytes_for(W, H, o)) throw GsError(GS_ERR_INVALID, "output buffer too small");
         if (!c->members.empty()) {  // the image (H rows) into out_dev on the first device
             for (gs_scene* m : s->members)
-                if (m->pending_err & (kErrOverflow | kErrBarrier)) check_frame_errors(m);
+                if (m->pending_err & (kErrOverflow | kErrBarrier)) check_frame_errors(m);  // (sets m's device)
             gs_ctx* m0 = c->members[0];
+            HIPCHK(hipSetDevice(m0->device));
             hipStream_t st0 = stream ? (hipStream_t)stream : m0->stream;
             void* full = render_group(c, s, (const float*)uni, W, H, o, st0);
             HIPCHK(hipMemcpyAsync(out_dev, full, out_bytes_for(W, H, o), hipMemcpyDeviceToDevice, st0));
@@ -1332,7 +1364,7 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
                     if (m->pending_err & kErrOverflow) {
                         overflow = true;
                         m->pending_err = 0;
-                        for (FrameSet& F : m->fs) ensure_tile_capacity(F, m->last.k_total);
+                        grow_after_overflow(m);
                     }
                 }
                 HIPCHK(hipSetDevice(c->members[0]->device));
@@ -1353,7 +1385,7 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
             if (!(s->pending_err & kErrOverflow)) break;
             s->pending_err = 0;
             if (attempt >= 2) throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded");
-            for (FrameSet& F : s->fs) ensure_tile_capacity(F, s->last.k_total);  // grow, render again
+            grow_after_overflow(s);  // grow, render again
         }
         if (out_host) HIPCHK(hipMemcpy(out_host, c->d_out, bytes, hipMemcpyDeviceToHost));
         return GS_OK;
@@ -1371,6 +1403,7 @@ int gs_framebuffer_alloc(gs_ctx* c, uint64_t bytes, void** out) {
             *out = nullptr;
             throw GsError(GS_ERR_OOM, "framebuffer allocation failed");
         }
+        c->fbufs.emplace_back(*out, bytes);
         return GS_OK;
     });
 }
@@ -1383,6 +1416,9 @@ int gs_framebuffer_free(gs_ctx* c, void* dev) {
         HIPCHK(hipSetDevice(d->device));
         HIPCHK(hipDeviceSynchronize());  // no frame in flight may still write it
         HIPCHK(hipFree(dev));
+        auto& v = c->fbufs;
+        v.erase(std::remove_if(v.begin(), v.end(), [&](const std::pair<void*, uint64_t>& e) { return e.first == dev; }),
+                v.end());
         return GS_OK;
     });
 }
@@ -1390,6 +1426,19 @@ int gs_framebuffer_free(gs_ctx* c, void* dev) {
 int gs_framebuffer_read(gs_ctx* c, const void* dev, void* host, uint64_t bytes) {
     return guarded([&] {
         if (!c || !dev || !host) throw GsError(GS_ERR_INVALID, "null argument");
+        {  // a framebuffer of this context: the read stays inside its allocation
+            const char* p = (const char*)dev;
+            bool ok = false;
+            for (const auto& e : c->fbufs) {
+                const char* b = (const char*)e.first;
+                if (p >= b && p < b + e.second) {
+                    ok = bytes <= e.second - (uint64_t)(p - b);
+                    if (!ok) throw GsError(GS_ERR_INVALID, "read past the end of the framebuffer");
+                    break;
+                }
+            }
+            if (!ok) throw GsError(GS_ERR_INVALID, "not a framebuffer of this context (gs_framebuffer_alloc)");
+        }
         const int rc = gs_sync(c);
         if (rc != GS_OK) throw GsError(rc, gs_last_error());
         gs_ctx* d = c->members.empty() ? c : c->members[0];
@@ -1438,6 +1487,9 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
                 a.k_chunk1 += m.k_chunk1;
                 a.wide_chunk0 += m.wide_chunk0;
                 a.wide_chunk1 += m.wide_chunk1;
+                a.frames_unsat += m.frames_unsat;
+                a.frames_chunked = std::max(a.frames_chunked, m.frames_chunked);
+                a.frames_seeded = std::max(a.frames_seeded, m.frames_seeded);
                 a.tile_row_end = std::max(a.tile_row_end, m.tile_row_end);
                 for (float* f : {&a.ms_total, &a.ms_project, &a.ms_sort, &a.ms_bin, &a.ms_tile_sort, &a.ms_ranges,
                                  &a.ms_composite, &a.ms_other}) {
@@ -1466,6 +1518,11 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
             st.chunk_fraction = l.n_vis ? (float)l.n_chunk[0] / (float)l.n_vis : 0.0f;
         }
         st.frames = (int32_t)c->comp_frames;
+        for (gs_scene* s : c->scenes) collect_stats(s, false);
+        st.frames_rendered = c->n_rendered;
+        st.frames_chunked = c->n_chunked;
+        st.frames_unsat = c->n_unsat;
+        st.frames_seeded = c->n_seeded;
         const double k = c->acc_frames ? 1.0 / c->acc_frames : 0.0;
         st.ms_total = (float)(c->acc_ms[ST_TOTAL] * k);
         st.ms_project = (float)(c->acc_ms[ST_PROJECT] * k);
@@ -1491,12 +1548,26 @@ int gs_timings_reset(gs_ctx* c) {
         }
         if (!c->members.empty()) return GS_OK;
         HIPCHK(hipSetDevice(c->device));
-        harvest(c, c->fe[0]);
-        harvest(c, c->fe[1]);
+        for (int k = 1; k <= kStatSlots; ++k) harvest(c, c->fe[(c->fe_cur + k) % kStatSlots]);  // every pending frame
+        for (gs_scene* s : c->scenes) collect_stats(s, true);  // their frame counts before the reset
+        c->n_rendered = c->n_chunked = c->n_unsat = c->n_seeded = 0;
         for (auto& v : c->acc_ms) v = 0.0;
         c->acc_frames = 0;
         c->acc_comp_ms = 0.0;
         c->comp_frames = 0;
+        return GS_OK;
+    });
+}
+
+int gs_debug_chunk1_grid(const gs_ctx* c, int occupancy, int cus, int* out_grid, int* out_occupancy) {
+    return guarded([&] {
+        if (!out_grid) throw GsError(GS_ERR_INVALID, "null out_grid");
+        if (c && !c->members.empty()) c = c->members[0];
+        const int occ = c ? c->c1_occ : occupancy;
+        const int g = c ? c->c1_grid : chunk1_grid(occupancy, cus);
+        *out_grid = g;
+        if (out_occupancy) *out_occupancy = occ;
+        if (g <= 0) throw GsError(GS_ERR_UNSUPPORTED, "k_chunk1's grid cannot be resident");
         return GS_OK;
     });
 }

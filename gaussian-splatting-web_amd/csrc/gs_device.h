@@ -290,6 +290,7 @@ struct Chunk1Params {
     CompositeParams cp;           // mode kCompSecond
     uint32_t* sat;                // unsaturated-tile row prefix counts (written by the first phase)
     uint32_t* bar;                // grid-barrier arrival counter, zero at launch (the frame's end zeroes it)
+    uint64_t spin_ticks;          // grid-barrier timeout in wall-clock ticks
     int two_chunks;               // chunk 1 may have work (else only the frame's end runs)
     // the frame's end (frame_end_body): statistics shards, pinned-slot copy, sequence number
     StatShard* stats;
@@ -321,6 +322,17 @@ void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit
 // chunk 1 in one launch (grid: one workgroup per CU; returns at once when chunk 0 saturated every tile)
 struct Chunk1Params;
 void launch_chunk1(const Chunk1Params& c, int grid, int accum_fp16, hipStream_t s);
+// k_chunk1 workgroups (256 threads) resident per CU on this device (0: query failed)
+int chunk1_occupancy();
+// k_chunk1's grid for `occupancy` workgroups per CU on `cus` CUs: at most 64 and at most what
+// fits the device at once (co-residency of the grid barrier); 0 when nothing fits
+__host__ __device__ inline int chunk1_grid(int occupancy, int cus) {
+    if (occupancy <= 0 || cus <= 0) return 0;
+    const long fit = (long)occupancy * cus;  // workgroups the device holds at once
+    long g = fit < 64 ? fit : 64;
+    if (g > cus) g = cus;  // one per CU at most: it is LDS-heavy and starts beside the next frame's kernels
+    return (int)g;
+}
 // the same as separate launches (for frames expected to leave tiles unsaturated), then the frame's end
 void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s);
 void launch_tile_sort(const TileSortParams& p, hipStream_t s);

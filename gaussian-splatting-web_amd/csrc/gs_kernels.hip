@@ -2802,9 +2802,15 @@ __global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
 // generation (release), the others spin until the generation moves (acquire).  The count is zero
 // again whenever every workgroup has left a barrier, so no one resets it while another workgroup may
 // still be polling (a reset at the frame's end raced with the last barrier's stragglers).  Agent
-// scope (cdna_hip_programming.md Guideline 16); bounded spin: a timeout sets kErrBarrier, and the
-// host zeroes bar[] before the next launch of the set.
-__device__ __forceinline__ void grid_sync(uint32_t* bar, FrameCtl* ctl) {
+// scope (cdna_hip_programming.md Guideline 16).
+// Residency: the grid is at most occupancy x CUs of k_chunk1 alone (queried at context creation,
+// chunk1_occupancy; the context refuses a device where it is not) and no kernel beside it waits
+// for it, so once the kernels launched before and beside it drain, every workgroup is resident.
+// Bounded spin: `spin_ticks` of the 100 MHz wall clock (~200 ms, set by the host from the
+// device's clock rate; far above any one kernel's duration, so only a grid that can never become
+// resident times out).  A timeout sets kErrBarrier: a synchronous gs_render fails its own frame,
+// gs_render_device reports it on its next call, and the host zeroes bar[] before the set's next launch.
+__device__ __forceinline__ void grid_sync(uint32_t* bar, FrameCtl* ctl, uint64_t spin_ticks) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its stores
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2815,8 +2821,9 @@ __device__ __forceinline__ void grid_sync(uint32_t* bar, FrameCtl* ctl) {
             __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
+        const uint64_t t0 = wall_clock64();
         for (uint32_t spins = 0; __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen;) {
-            if (++spins > (1u << 26)) {
+            if ((++spins & 63u) == 0u && wall_clock64() - t0 > spin_ticks) {
                 atomicOr(&ctl->err, kErrBarrier);
                 break;
             }
@@ -2847,13 +2854,13 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     const uint32_t G = gridDim.x, b = blockIdx.x;
     C1_MARK(0);
     unsat_rows_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(1);
     c1_parts_body(c.pp, b, G);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(2);
     c1_records_body(c.pp, b, G);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(3);
     uint32_t* s_a = (uint32_t*)lds;
     uint32_t* s_pref = s_a + kBandTiles;
@@ -2862,24 +2869,24 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     uint32_t* s_nw = s_wide + kWideQueue;
     const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles, c.bp.band_tiles);
     for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(4);
     const uint32_t ncol = (c.bp.n_tiles + kColTiles - 1) / kColTiles;
     for (uint32_t vb = b; vb < ncol; vb += G) colscan_body(c.bp, vb, (uint32_t(*)[kColTiles])lds);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(5);
     if (b == 0) tile_scan_body<256>(c.bp, s_a);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(6);
     for (uint32_t vb = b; vb < nbin; vb += G) bin_emit_body<256, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(7);
     const uint32_t ntb = 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
     for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body<TsBig>(c.tp, vb, *(TsShared*)lds);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(8);
     for (uint32_t vb = b; vb < ntb; vb += G) composite_q_body<FP16_TARGET>(c.cp, vb, *(CompQShared*)lds);
-    grid_sync(c.bar, ctl);
+    grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(9);  // every phase done before the frame's end reads FrameCtl
 }
 
@@ -3153,6 +3160,13 @@ void launch_chunk1(const Chunk1Params& c0, int grid, int accum_fp16, hipStream_t
         hipLaunchKernelGGL(k_chunk1<true>, dim3(grid), dim3(256), 0, s, c);
     else
         hipLaunchKernelGGL(k_chunk1<false>, dim3(grid), dim3(256), 0, s, c);
+}
+int chunk1_occupancy() {
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_chunk1<false>, 256, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chunk1<true>, 256, 0) != hipSuccess)
+        return 0;
+    return std::min(a, b);
 }
 void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
     if (c.two_chunks && c.cp.n_tiles > 0) {

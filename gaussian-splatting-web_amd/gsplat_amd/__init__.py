@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
     "gs_present_device", "gs_encode_png", "gs_look_at",
     "gs_perspective", "gs_camera_position", "gs_camera_from_json", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
-    "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records", "gs_debug_last_slots",
+    "gs_debug_chunk1_grid", "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records", "gs_debug_last_slots",
     "gs_debug_tile_lists",
 )
 
@@ -63,7 +63,9 @@ class GsStats(ctypes.Structure):
                 ("ms_tile_sort", ctypes.c_float), ("ms_ranges", ctypes.c_float),
                 ("ms_composite", ctypes.c_float), ("ms_other", ctypes.c_float),
                 ("k_chunk0", ctypes.c_uint32), ("k_chunk1", ctypes.c_uint32),
-                ("wide_chunk0", ctypes.c_uint32), ("wide_chunk1", ctypes.c_uint32)]
+                ("wide_chunk0", ctypes.c_uint32), ("wide_chunk1", ctypes.c_uint32),
+                ("frames_rendered", ctypes.c_uint32), ("frames_chunked", ctypes.c_uint32),
+                ("frames_unsat", ctypes.c_uint32), ("frames_seeded", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -128,6 +130,7 @@ def lib():
         L.gs_pack_uniforms.argtypes = [P, P, P, F, F, F, F, F, P]
         L.gs_synth_aos.argtypes = [U64, U64, I, I, P]
         L.gs_ply_parse.argtypes = [P, U64, ctypes.POINTER(GsPlyInfo), P, U64]
+        L.gs_debug_chunk1_grid.argtypes = [P, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]
         L.gs_debug_sort_pairs.argtypes = [P, P, P, U64, I, I]
         L.gs_debug_last_order.argtypes = [P, P, P, P, U64, ctypes.POINTER(U64)]
         L.gs_debug_last_records.argtypes = [P, P, P, U64]
@@ -195,6 +198,17 @@ def bench_uniforms(W, H):
     return pack_uniforms(view, proj, focal=(W, H))
 
 
+def orbit_uniforms(W, H, k, period=60):
+    """bench.py's moving camera, frame k: at the origin, yaw swinging +-25 deg and pitch +-8 deg
+    around the bench view (-z), a new view every frame; part of the screen leaves the scene's
+    frustum, so tiles go unsaturated and the chunk split moves."""
+    a = 2 * np.pi * k / period
+    yaw, pitch = np.radians(25.0) * np.sin(a), np.radians(8.0) * np.sin(2 * a)
+    target = (np.sin(yaw) * np.cos(pitch), np.sin(pitch), -np.cos(yaw) * np.cos(pitch))
+    view = look_at((0.0, 0.0, 0.0), target)
+    return pack_uniforms(view, perspective(1.04719755, W / H, 0.03, 1000.0), focal=(W, H))
+
+
 def synth_aos(n, seed, W=1920, H=1080):
     """Seeded synthetic scene as reference AoS records (320 B each, SH degree 3)."""
     out = np.empty(n * 80, np.float32)
@@ -241,6 +255,14 @@ def strip_rows(H, strip_index, strip_count):
     r0, rp = ctypes.c_int(), ctypes.c_int()
     _check(lib().gs_strip_rows(int(H), int(strip_index), int(strip_count), ctypes.byref(r0), ctypes.byref(rp)))
     return r0.value, rp.value
+
+
+def chunk1_grid(ctx=None, occupancy=0, cus=0):
+    """(k_chunk1 grid, occupancy per CU): of a context, or for the given occupancy and CU count."""
+    g, o = ctypes.c_int(), ctypes.c_int()
+    _check(lib().gs_debug_chunk1_grid(ctx.handle if ctx is not None else None, int(occupancy), int(cus),
+                                      ctypes.byref(g), ctypes.byref(o)))
+    return g.value, o.value
 
 
 def device_count():

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2
+#define GS_ABI_VERSION 3
 
 typedef struct gs_ctx gs_ctx;
 typedef struct gs_scene gs_scene;
@@ -112,6 +112,13 @@ typedef struct gs_stats {
                              = 0 (kept for the ABI); composite = chunk 0's composite */
     uint32_t k_chunk0, k_chunk1;  /* pairs binned per chunk (last frame) */
     uint32_t wide_chunk0, wide_chunk1;  /* splats of >= 32 tiles emitted row-wise, per chunk */
+    /* frame counts since gs_timings_reset (every frame, timed or not): */
+    uint32_t frames_rendered;  /* frames enqueued */
+    uint32_t frames_chunked;   /* ... rendered with a depth split (two chunks) */
+    uint32_t frames_unsat;     /* ... whose chunk 0 left tiles unsaturated (chunk 1 composited them;
+                                  counted when the frame's statistics arrive) */
+    uint32_t frames_seeded;    /* ... whose split depth came from the frame's own coarse depth
+                                  estimate (no usable history: a first frame or a camera cut) */
 } gs_stats;
 
 /* ---- library / device ---------------------------------------------------------------------- */
@@ -170,7 +177,8 @@ int gs_render_device(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int 
  * read by the present pass) -- frames stay in HBM and are read back only on request.
  * gs_framebuffer_alloc: `bytes` of device memory on the context's device (a group's first).
  * gs_framebuffer_read: waits for the context's frames (gs_sync semantics, frame errors included),
- * then copies `bytes` to host memory. */
+ * then copies `bytes` to host memory; `dev` must lie inside a buffer gs_framebuffer_alloc made on
+ * this context and the read must end inside it (else GS_ERR_INVALID). */
 int gs_framebuffer_alloc(gs_ctx* ctx, uint64_t bytes, void** out_dev);
 int gs_framebuffer_free(gs_ctx* ctx, void* dev);
 int gs_framebuffer_read(gs_ctx* ctx, const void* dev, void* host, uint64_t bytes);
@@ -240,6 +248,12 @@ typedef struct gs_ply_info {
 int gs_ply_parse(const void* ply, uint64_t bytes, gs_ply_info* info, void* out_aos, uint64_t out_bytes);
 
 /* ---- checks used by tests ------------------------------------------------------------------ */
+/* Chunk 1's single-launch form (k_chunk1) separates its phases with grid barriers, so its whole
+ * grid must be resident at once: the grid is min(64, CUs, occupancy x CUs) with the occupancy of
+ * k_chunk1 queried at context creation (gs_ctx_create fails with GS_ERR_UNSUPPORTED when it is 0).
+ * ctx != NULL: that context's grid and measured occupancy; ctx == NULL: the grid for the given
+ * occupancy (workgroups per CU) and CU count (GS_ERR_UNSUPPORTED when nothing fits). */
+int gs_debug_chunk1_grid(const gs_ctx* ctx, int occupancy, int cus, int* out_grid, int* out_occupancy);
 /* Stable ascending GPU radix sort of (key,value) on bits [begin_bit,end_bit): host in/out. */
 int gs_debug_sort_pairs(gs_ctx* ctx, uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit,
                         int end_bit);

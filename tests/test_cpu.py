@@ -258,7 +258,7 @@ def test_abi_exports_every_declared_symbol():
     L = gs.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.gs_abi_version() == 2
+    assert L.gs_abi_version() == 3
 
 
 def test_abi_rejects_without_device():
@@ -290,3 +290,16 @@ def test_kernel_resources_no_scratch():
         assert k in res, (k, sorted(res))
         assert res[k]["scratch"] == 0, (k, res[k])
     assert res["k_composite<false>"]["vgpr"] <= 96, res["k_composite<false>"]
+
+
+def test_chunk1_grid_residency_rule():
+    """k_chunk1's grid barrier needs its whole grid resident: grid = min(64, CUs, occupancy x CUs),
+    refused (GS_ERR_UNSUPPORTED) when no workgroup fits (gs_debug_chunk1_grid, host logic)."""
+    assert gs.chunk1_grid(None, 1, 256) == (64, 1)
+    assert gs.chunk1_grid(None, 4, 256) == (64, 4)
+    assert gs.chunk1_grid(None, 1, 40) == (40, 1)   # fewer CUs than 64: one per CU
+    assert gs.chunk1_grid(None, 2, 16) == (16, 2)
+    for occ, cus in ((0, 256), (1, 0), (-1, 8)):
+        with pytest.raises(gs.GsError) as e:
+            gs.chunk1_grid(None, occ, cus)
+        assert e.value.code == gs.GS_ERR_UNSUPPORTED

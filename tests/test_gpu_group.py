@@ -99,3 +99,10 @@ def test_group_distinct_devices_use_rccl():
         a = gs.Scene(ctx, aos, n, 16).render(u, W, H)
         b = gs.Scene(gc, aos, n, 16).render(u, W, H)
         assert np.array_equal(a, b)
+
+
+def test_chunk1_grid_is_resident(gpu_ctx):
+    """The context sized k_chunk1's grid from the occupancy query of this device."""
+    grid, occ = gs.chunk1_grid(gpu_ctx)
+    assert occ >= 1 and 1 <= grid <= 64
+    assert grid == gs.chunk1_grid(None, occ, 256)[0] or grid <= occ * 256

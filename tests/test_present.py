@@ -150,4 +150,16 @@ def test_framebuffer_abi_roundtrip(gpu_ctx):
     got = np.empty((H, W, 4), np.float32)
     assert L.gs_framebuffer_read(gpu_ctx.handle, dev, got.ctypes.data_as(ctypes.c_void_p), got.nbytes) == gs.GS_OK
     assert np.array_equal(got, sc.render(u, W, H))
+    # a read past the allocation, or of memory the context did not allocate, is refused
+    big = np.empty(W * H * 16 + 64, np.uint8)
+    assert L.gs_framebuffer_read(gpu_ctx.handle, dev, big.ctypes.data_as(ctypes.c_void_p), big.nbytes) == \
+        gs.GS_ERR_INVALID
+    tail = ctypes.c_void_p(dev.value + W * H * 8)
+    assert L.gs_framebuffer_read(gpu_ctx.handle, tail, big.ctypes.data_as(ctypes.c_void_p), W * H * 8) == gs.GS_OK
+    assert L.gs_framebuffer_read(gpu_ctx.handle, tail, big.ctypes.data_as(ctypes.c_void_p), W * H * 8 + 1) == \
+        gs.GS_ERR_INVALID
+    other = gs.DeviceBuffer(1024)
+    assert L.gs_framebuffer_read(gpu_ctx.handle, other.ptr, big.ctypes.data_as(ctypes.c_void_p), 16) == \
+        gs.GS_ERR_INVALID
+    other.free()
     assert L.gs_framebuffer_free(gpu_ctx.handle, dev) == gs.GS_OK

@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 if [ -n "$K" ]; then KARG=(-k "$K"); else KARG=(); fi
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread "${KARG[@]}" > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread "${KARG[@]}" > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
 python3 -c "import json;d=json.loads(open('$OUT/bench.log').read().strip().splitlines()[-1]);print('fps',d['fps'],'ms',d['ms_per_step'],d['stages_ms'])"
