@@ -301,6 +301,37 @@ def main():
                           "value_msplats": round(N * args.steps / el / 1e6, 3),
                           "tiles_unsaturated_last": st_o["tiles_unsaturated"], "k_chunk1_last": st_o["k_chunk1"],
                           "camera": "origin, yaw +-25 deg, pitch +-8 deg, period 60 frames"}
+        # camera cuts: every frame a view far from the last one (gsplat_amd.COLD_VIEWS, a cycle of
+        # 4), so no frame has saturation history from its own view: the chunk controller's cold path
+        uc = [gs.cold_uniforms(W, H, k) for k in range(len(gs.COLD_VIEWS))]
+        for k in range(args.warmup):
+            frame_u(uc[k % len(uc)])
+        sync()
+        ctx.timings_reset()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            frame_u(uc[k % len(uc)])
+        sync()
+        el_c = time.perf_counter() - t0
+        st_c = ctx.timings()
+        lat_c = []
+        for k in range(2 * len(uc)):  # each frame waited for: the worst single cold frame
+            t0 = time.perf_counter()
+            frame_u(uc[k % len(uc)])
+            sync()
+            lat_c.append(time.perf_counter() - t0)
+        worst_c = max(lat_c)
+        if launched and world > 1:
+            import torch
+            tt = torch.tensor([el_c, worst_c], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el_c, worst_c = float(tt[0]), float(tt[1])
+        extra["cold"] = {"fps": round(args.steps / el_c, 2), "ms_per_step": round(el_c / args.steps * 1e3, 4),
+                         "value_msplats": round(N * args.steps / el_c / 1e6, 3),
+                         "worst_frame_ms": round(worst_c * 1e3, 4),
+                         "median_frame_ms": round(float(np.median(lat_c)) * 1e3, 4),
+                         "frames_cold": st_c["frames_seeded"], "frames": st_c["frames_rendered"],
+                         "camera": "a cut every frame: cycle of %d views (gsplat_amd.COLD_VIEWS)" % len(uc)}
     # one untimed one-chunk frame for the exact visible count and K of SURVEY 8d's byte model
     # (with a chunk split the pipeline never projects the splats past it)
     cur["opts"] = gs.make_opts(strip_index=rank, strip_count=world, chunk_fraction=1.0,

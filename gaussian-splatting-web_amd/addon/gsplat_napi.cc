@@ -413,6 +413,7 @@ napi_value Timings(napi_env env, napi_callback_info info) {
     put("framesChunked", st.frames_chunked);
     put("framesUnsat", st.frames_unsat);
     put("framesSeeded", st.frames_seeded);
+    put("chunkDepth", st.chunk_depth);
     return o;
 }
 

@@ -207,6 +207,8 @@ struct FrameSet {
     int tiles_cap = 0;
     float4* state = nullptr;
     uint64_t state_cap = 0;
+    float* seedh = nullptr;             // seeded frames: alpha mass by coarse cell and depth bucket (zero between frames)
+    size_t seed_cap = 0;
 };
 
 struct gs_scene {
@@ -241,6 +243,11 @@ struct gs_scene {
     bool have_last = false;
     uint32_t chunk_T = kNoSplit;        // adaptive chunk threshold for the next frame
     float last_view[16] = {};           // the last frame's view matrix (a moving camera widens T)
+    float last_campos[3] = {};          // ... and camera position (camera cuts)
+    bool have_view = false;
+    uint32_t cut_seq = 0;               // statistics of frames before this sequence number (the
+                                        // last camera cut) do not steer the chunk controller
+    bool hist_ok = false;               // the controller has statistics of this view (since the last cut)
     uint32_t key_lo = 0, key_hi = 0;    // depth-key range of the last frame's visible splats
     bool have_krange = false;
     bool have_frame = false;
@@ -329,6 +336,14 @@ static void ensure_sat(FrameSet& F, size_t words) {
     dev_free(F.sat);
     dev_alloc(F.sat, words);
     F.sat_cap = words;
+}
+
+static void ensure_seed(FrameSet& F, size_t words) {
+    if (words <= F.seed_cap && F.seedh) return;
+    dev_free(F.seedh);
+    dev_alloc(F.seedh, words);
+    HIPCHK(hipMemset(F.seedh, 0, words * sizeof(float)));  // k_seed_pick re-zeroes what it read
+    F.seed_cap = words;
 }
 
 static void ensure_state(FrameSet& F, uint64_t pixels) {
@@ -429,6 +444,8 @@ static void collect_stats(gs_scene* s, bool wait) {
         if (s->last.not_done > 0) s->ctx->n_unsat++;
         s->have_last = true;
         s->stat_pending[slot] = false;
+        if (s->stat_want[slot] < s->cut_seq) continue;  // a view before the last camera cut
+        s->hist_ok = true;
         // chunk controller: chunk 0 = the splats nearer than 1.15x the depth at which the last
         // tile saturated (measured by the composite), rising at once, decaying slowly (3 % of
         // depth per frame); frames where most tiles never saturate use one chunk
@@ -473,6 +490,53 @@ static void collect_stats(gs_scene* s, bool wait) {
 
 static void quirk_prepare(gs_scene* s, const float* uni, hipStream_t st);
 
+// Seeded frames (k_seed_*): the alpha mass per pixel taken as saturation (sum of alpha >=
+// -ln(1e-4) = 9.21 leaves T < 1e-4), GS_SEED_TAU overrides; GS_SEED=0 disables seeding (a cold
+// frame is then one chunk).
+static double seed_tau() {
+    static const double v = [] {
+        const char* e = std::getenv("GS_SEED_TAU");
+        const double x = e ? std::atof(e) : 9.21;
+        return x > 0.0 ? x : 9.21;
+    }();
+    return v;
+}
+static bool seed_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("GS_SEED");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+// Depth bucket 0 of the seed histogram: the near plane's key (clip z = 0 on the view axis:
+// vz = -P[14] / P[10]); the buckets are sat_bucket's quarter octaves of depth from there.
+static uint32_t seed_base(const float* uni) {
+    const float p10 = uni[16 + 10], p14 = uni[16 + 14];
+    const float vz = p10 != 0.0f ? -p14 / p10 : 0.0f;
+    if (!std::isfinite(vz) || vz == 0.0f) return 0u;
+    return float_to_key(vz) >> kSatShift;
+}
+
+// A camera cut: the view turned by more than kCutAngle against the last frame, or the camera moved
+// by more than kCutShift of the depth at which the last frame's tiles saturated.  The chunk
+// controller's history (saturation depths of earlier frames) then describes another view.
+constexpr float kCutCos = 0.98480775f;  // cos 10 deg
+constexpr float kCutShift = 0.1f;
+static bool camera_cut(const gs_scene* s, const float* uni) {
+    if (!s->have_view) return false;
+    const float* a = s->last_view;  // view row 2 (column-major): the camera's depth axis in world space
+    const double da = std::sqrt((double)a[2] * a[2] + (double)a[6] * a[6] + (double)a[10] * a[10]);
+    const double db = std::sqrt((double)uni[2] * uni[2] + (double)uni[6] * uni[6] + (double)uni[10] * uni[10]);
+    const double dot = (double)a[2] * uni[2] + (double)a[6] * uni[6] + (double)a[10] * uni[10];
+    if (!(da > 0.0 && db > 0.0) || !(dot >= kCutCos * da * db)) return true;
+    if (!s->have_last) return false;
+    const uint32_t ref = s->last.sat_key ? s->last.sat_key : s->key_hi;
+    const double dref = std::fabs((double)key_to_float(ref)) / da;  // world units (the view's scale is da)
+    double d2 = 0.0;
+    for (int k = 0; k < 3; ++k) d2 += ((double)uni[32 + k] - s->last_campos[k]) * ((double)uni[32 + k] - s->last_campos[k]);
+    return std::isfinite(dref) && dref > 0.0 && std::sqrt(d2) > kCutShift * dref;
+}
+
 // The per-frame pipeline.  `out` is device memory of rows_padded*W (strip) or H*W pixels.
 static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o,
                          void* out, hipStream_t st) {
@@ -508,14 +572,22 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     // chunk threshold: adaptive, one chunk (chunk_fraction >= 1), or a fixed split for tests and
     // diagnostics (chunk_fraction in (0,1): the depth 2^-t <= chunk_fraction of the way from the
     // last frame's nearest to its farthest visible splat; one chunk until a frame was seen)
+    if (camera_cut(s, uni)) {  // the earlier frames' saturation depths say nothing about this view
+        s->cut_seq = s->seq_next;
+        s->chunk_T = kNoSplit;
+        s->hist_ok = false;
+    }
     uint32_t T = s->chunk_T;
     {  // the statistics are a few frames old: while the camera moves, the depth at which tiles
        // saturate moves too, so the threshold gets a wider margin (1.05 x 1.10 ~ the 1.15 used for
        // every frame until round 2); a still camera keeps the tight one
         const bool moving = std::memcmp(s->last_view, uni, sizeof(s->last_view)) != 0;
         std::memcpy(s->last_view, uni, sizeof(s->last_view));
+        std::memcpy(s->last_campos, uni + 32, sizeof(s->last_campos));
+        s->have_view = true;
         if (moving && T != kNoSplit) T = scaled_threshold(T, kMovingMargin);
     }
+    const bool cold = !s->hist_ok && o.chunk_fraction == 0.0f && !o.ref_quirks;  // no usable history
     if (o.chunk_fraction >= 1.0f) {
         T = kNoSplit;
     } else if (o.chunk_fraction > 0.0f) {
@@ -534,9 +606,15 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         quirk_prepare(s, uni, F.stream);
     }
     s->last_quirk = quirk;
-    const bool two_chunks = T != kNoSplit;
+    // no usable history: the frame estimates its own threshold on the device (k_seed_*)
+    const bool seeded = cold && n_tiles > 0 && s->n > 0 && seed_enabled();
+    const bool two_chunks = T != kNoSplit || seeded;
     c->n_rendered++;
     c->n_chunked += two_chunks ? 1u : 0u;
+    c->n_seeded += seeded ? 1u : 0u;
+    const int seed_cx = (W + kSeedCell - 1) / kSeedCell;
+    const int seed_cy = ((std::min(tr_end * kTile, H) - tr_begin * kTile) + kSeedCell - 1) / kSeedCell;
+    if (seeded) ensure_seed(F, (size_t)seed_cx * std::max(seed_cy, 1) * kSeedBuckets);
     if (two_chunks) {
         ensure_state(F, (uint64_t)W * H);
         ensure_sat(F, (size_t)(tr_end - tr_begin + 1) * (TX + 1) + 2 + (size_t)(tr_end - tr_begin) * ((TX + 63) / 64) * 2);
@@ -608,6 +686,17 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.bounds = s->bounds;
     pp.orig = s->orig;
     pp.sidx = F.sidx;
+    if (seeded) {
+        pp.thresh = kNoSplit;
+        pp.thresh_dev = &F.ctl->seed_T;
+        pp.seedh = F.seedh;
+        const uint64_t runs = (s->n + kSeedRun - 1) / kSeedRun, want = (uint64_t)kSeedRunsPerCell * seed_cx * seed_cy;
+        pp.seed_stride = (uint32_t)std::max<uint64_t>(1u, runs / std::max<uint64_t>(want, 1));
+        pp.seed_base = seed_base(uni);
+        pp.seed_cx = seed_cx;
+        pp.seed_cy = seed_cy;
+        pp.seed_tau = seed_tau();
+    }
     if (quirk) {  // the frame runs on the draw-ordered copy; each slot's sort key = (0, draw rank)
         pp.geo = s->qgeo;
         pp.cull = s->qcull;
@@ -617,6 +706,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         pp.key_zero = 1;
     }
     mark(EV_PROJ0);
+    if (seeded) launch_seed(pp, st);
     launch_project(pp, st);
     mark(EV_PROJ1);
 
@@ -729,7 +819,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         // while the others wait at a grid barrier: the kernels beside it never wait for k_chunk1
         // and finish.  Once a recent frame left tiles unsaturated: chunk 1 as separate launches
         // at full occupancy (a kernel boundary costs less than a grid barrier), then the frame's end.
-        if (two_chunks && s->have_last && s->last.not_done > 0)
+        if (two_chunks && (seeded || (s->have_last && s->last.not_done > 0)))
             launch_chunk1_split(c1, o.accum == GS_ACCUM_FP16_TARGET, st);
         else
             launch_chunk1(c1, c->c1_grid, o.accum == GS_ACCUM_FP16_TARGET, st);
@@ -1254,6 +1344,7 @@ void gs_scene_free(gs_scene* s) {
         dev_free(F.done);
         dev_free(F.sat);
         dev_free(F.state);
+        dev_free(F.seedh);
         if (F.ev_early) (void)hipEventDestroy(F.ev_early);
         if (F.ev_out) (void)hipEventDestroy(F.ev_out);
     }
@@ -1516,6 +1607,7 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
             st.wide_chunk0 = l.wide_n[0];
             st.wide_chunk1 = l.wide_n[1];
             st.chunk_fraction = l.n_vis ? (float)l.n_chunk[0] / (float)l.n_vis : 0.0f;
+            st.chunk_depth = l.frame_T == kNoSplit ? 0.0f : std::fabs(key_to_float(l.frame_T));
         }
         st.frames = (int32_t)c->comp_frames;
         for (gs_scene* s : c->scenes) collect_stats(s, false);

@@ -71,6 +71,8 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t unit_n[kUnitShards]; // chunk-0 work units per shard (k_cull; see ProjParams::units)
     uint32_t c1_parts;            // chunk 1: projection partitions listed in ProjParams::plist (k_chunk1)
     uint32_t c0_parts;            // chunk 0: projection partitions listed in ProjParams::plist0 (k_part_list)
+    uint32_t seed_T;              // a seeded frame's chunk threshold (k_seed_pick; ProjParams::thresh_dev)
+    uint32_t frame_T;             // the frame's chunk threshold, whichever its source (k_part_list)
     uint32_t sat_hist[kSatBuckets];  // tiles saturated by the end of the frame, by saturation depth
                                      // (sat_bucket; summed from the shards at the frame's end)
 };
@@ -179,7 +181,23 @@ struct ProjParams {
     const float4* sh;         // [n][shq] packed SH coefficients
     uint32_t shq;             // sh_quads(n_sh)
     uint32_t key_zero;        // ref_quirks: slot sort key (0, draw rank) -- orig holds the rank
+    // A seeded frame (no usable history: a first frame, a camera cut) takes its chunk threshold
+    // from the device (thresh_dev = &FrameCtl::seed_T, written by k_seed_pick) instead of thresh.
+    const uint32_t* thresh_dev;
+    float* seedh;             // [cells][kSeedBuckets] alpha mass by coarse cell and depth bucket
+    uint32_t seed_stride;     // one sampled run of kSeedRun Gaussians per seed_stride runs
+    uint32_t seed_base;       // depth bucket 0 = keys from (seed_base << kSatShift): the near plane
+    int seed_cx, seed_cy;     // coarse cells (kSeedCell px) across the frame / strip
+    float seed_tau;           // alpha mass per pixel taken as saturation
 };
+
+// Coarse depth estimate of a seeded frame: sampled Gaussians' alpha mass op * 2 pi sigma^2 by
+// 64x64-pixel cell and quarter-octave depth bucket (sat_bucket's, from the near plane)
+constexpr int kSeedCell = 64;
+constexpr int kSeedBuckets = 64;
+constexpr int kSeedRun = 16;            // a sample = a run of 16 consecutive storage slots (Morton order)
+constexpr int kSeedRunsPerCell = 64;    // about this many sampled runs per cell
+
 
 // Element filter of a radix pass (the first pass of a depth chunk decides chunk membership).
 enum RadixFilter {
@@ -315,6 +333,8 @@ void launch_quirk_gather(const uint32_t* skeys, const uint32_t* svals, const uin
                          uint32_t shq, const float4* geo, const float4* shade, const float4* cull, float4* dgeo,
                          float4* dshade, float4* dcull, uint32_t* dorig, uint32_t* qk, uint32_t* qv, hipStream_t s);
 void launch_project(const ProjParams& p, hipStream_t s);
+// seeded frames, before launch_project: the coarse alpha-mass histogram, then the threshold
+void launch_seed(const ProjParams& p, hipStream_t s);
 void launch_records(const ProjParams& p, hipStream_t s);  // chunk-1 slots (or, rec_all, every record)
 void launch_sort_pass(const SortPass& p, hipStream_t s);
 void launch_bin(const BinParams& p, hipStream_t s);    // count, tile scan, emit, wide rows

@@ -679,12 +679,18 @@ __device__ PartTest part_test(const ProjParams& p, const PartBound& b) {
     return t;
 }
 
+// The frame's chunk threshold: the host's (from earlier frames) or, in a seeded frame, the one
+// k_seed_pick left in FrameCtl.
+__device__ __forceinline__ uint32_t frame_thresh(const ProjParams& p) {
+    return p.thresh_dev ? *p.thresh_dev : p.thresh;
+}
+
 // Can a Gaussian of partition b be a chunk-0 candidate of this frame (pass cull_keep with key <
-// thresh)?
-__device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, int row_hi) {
+// T)?
+__device__ bool part_maybe(const ProjParams& p, const PartBound& b, int row_lo, int row_hi, uint32_t T) {
     const PartTest t = part_test(p, b);
     if (!t.vis) return false;
-    if (p.thresh != kSentinel && t.kmin >= p.thresh) return false;
+    if (T != kSentinel && t.kmin >= T) return false;
     if (!t.bounded) return true;
     return !(t.yh < (float)row_lo - 1.0f || t.yl > (float)row_hi + 1.0f || t.xh < -1.0f || t.xl > (float)p.W);
 }
@@ -720,9 +726,9 @@ __device__ __forceinline__ bool sat_any(const ProjParams& p, uint32_t tx0, uint3
 
 // Can partition b hold a chunk-1 splat: a Gaussian at or past thresh whose quad may touch a tile
 // chunk 0 left unsaturated?
-__device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b) {
+__device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b, uint32_t T) {
     const PartTest t = part_test(p, b);
-    if (!t.vis || t.kmax < p.thresh) return false;
+    if (!t.vis || t.kmax < T) return false;
     uint32_t tx0, ty0, tx1, ty1;
     if (!t.bounded) {
         tx0 = 0;
@@ -739,10 +745,10 @@ __device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b) {
 // prefix counts of the unsaturated tiles); the ones that may hold a chunk-1 splat are appended to plist (one
 // counter add per wave; list order does not matter: a partition's chunk-1 slots are its own).
 __device__ __forceinline__ void c1_parts_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
-    const uint32_t parts = proj_parts(p.n), lane = lane_id();
+    const uint32_t parts = proj_parts(p.n), lane = lane_id(), T = frame_thresh(p);
     for (uint32_t q0 = blk * blockDim.x + (threadIdx.x & ~63u); q0 < parts; q0 += nblk * blockDim.x) {
         const uint32_t q = q0 + lane;
-        const bool want = q < parts && part_maybe_c1(p, p.bounds[q]);
+        const bool want = q < parts && part_maybe_c1(p, p.bounds[q], T);
         const uint64_t b = __ballot(want);
         if (!b) continue;
         uint32_t base = 0;
@@ -760,14 +766,14 @@ __device__ __forceinline__ void c1_parts_body(const ProjParams& p, uint32_t blk,
 __device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
-    const uint32_t lane = lane_id(), nl = p.ctl->c1_parts;
+    const uint32_t lane = lane_id(), nl = p.ctl->c1_parts, T = frame_thresh(p);
     for (uint32_t j = blk; j < nl; j += nblk) {
         const uint32_t part = p.plist[j];
         for (uint32_t r = threadIdx.x & ~63u; r < (uint32_t)kProjTile; r += blockDim.x) {
             const uint32_t i0 = part * (uint32_t)kProjTile + r, i = i0 + lane;
             bool want = false;
             float vz, cx0, cy0, hb;
-            if (i < p.n && cull_keep_box(p, p.cull[i], row_lo, row_hi, vz, cx0, cy0, hb) && sortable_key(vz) >= p.thresh) {
+            if (i < p.n && cull_keep_box(p, p.cull[i], row_lo, row_hi, vz, cx0, cy0, hb) && sortable_key(vz) >= T) {
                 uint32_t tx0, ty0, tx1, ty1;
                 want = box_tiles(p, cx0 - hb, cx0 + hb, cy0 - hb, cy0 + hb, tx0, ty0, tx1, ty1) &&
                        sat_any(p, tx0, ty0, tx1, ty1);
@@ -862,7 +868,9 @@ __global__ __launch_bounds__(256) void k_part_list(ProjParams p) {
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = proj_parts(p.n), lane = lane_id();
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool want = q < parts && part_maybe(p, p.bounds[q], row_lo, row_hi);
+    const uint32_t T = frame_thresh(p);
+    if (q == 0) p.ctl->frame_T = T;
+    const bool want = q < parts && part_maybe(p, p.bounds[q], row_lo, row_hi, T);
     if (q < parts) {
         p.c1[q] = 0;
         if (!want) p.c0[q] = 0;
@@ -873,6 +881,100 @@ __global__ __launch_bounds__(256) void k_part_list(ProjParams p) {
     if (lane == 0) base = atomicAdd(&p.ctl->c0_parts, (uint32_t)__popcll(b));
     base = __shfl(base, 0, 64);
     if (want) p.plist0[base + (uint32_t)__popcll(b & lanemask_lt())] = q;
+}
+
+// ---- seeded frames: a frame with no usable history (the first frame of a scene, a camera cut)
+// takes its chunk threshold from a coarse estimate of where its tiles saturate, instead of running
+// every visible splat as one chunk.  k_seed_hist: a sample of the scene (every seed_stride-th
+// run of kSeedRun storage slots; about kSeedRunsPerCell runs per cell, as each run of Morton-ordered
+// Gaussians is one small clump of the scene) through the
+// exact near/far test and the conservative screen box; each kept Gaussian adds its alpha mass,
+// op * 2 pi sigma^2 (sigma^2 ~ a^2 ||R diag(s)||_F^2 / 3 + 0.3, the per-axis variance of its 2-D
+// footprint; the integral of op exp(-d^T C^-1 d / 2)), weighted by the stride, to the 64x64-px
+// cells of its 2-sigma box at its quarter-octave depth bucket.  k_seed_pick: per cell the first
+// depth bucket at which the mass per pixel reaches seed_tau (sum alpha >= -ln t_min: saturated),
+// then the chunk controller's rule on those depths (the 95 % quantile of the saturating cells'
+// buckets, its upper edge, depth x 1.10; one chunk when under 20 % of the cells saturate).  The
+// threshold only moves work between the chunks: the image does not depend on it.
+__device__ __forceinline__ float key_depth(uint32_t k) {  // the float a depth key encodes
+    return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : (k ^ 0x80000001u));
+}
+
+__global__ __launch_bounds__(256) void k_seed_hist(ProjParams p) {
+    const int row_lo = p.tile_row_begin * kTile;
+    const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
+    const uint32_t nrun = (p.n + kSeedRun - 1) / kSeedRun;
+    const uint32_t nsr = (nrun + p.seed_stride - 1) / p.seed_stride;
+    const float wgt = (float)p.seed_stride * 6.28318531f;
+    constexpr uint32_t kRunsPerBlock = 256 / kSeedRun;
+    for (uint32_t sr = blockIdx.x * kRunsPerBlock + threadIdx.x / kSeedRun; sr < nsr; sr += gridDim.x * kRunsPerBlock) {
+        const uint32_t i = sr * p.seed_stride * kSeedRun + threadIdx.x % kSeedRun;
+        if (i >= p.n) continue;
+        const float4 c = p.cull[i];
+        float vz, cx0, cy0, hb;
+        if (!cull_keep_box(p, c, row_lo, row_hi, vz, cx0, cy0, hb)) continue;
+        const float op = 1.0f / (1.0f + __expf(-p.geo[3 * (uint64_t)i].w));
+        const float a = p.focal / vz;
+        const float var = a * a * c.w * p.scale_mod * p.scale_mod * (1.0f / 3.0f) + 0.3f;
+        if (!(op >= 1.0f / 255.0f) || !(var < 1e12f)) continue;
+        const float r = 2.0f * sqrtf(var);
+        const float fx0 = floorf((cx0 - r) * (1.0f / kSeedCell)), fx1 = floorf((cx0 + r) * (1.0f / kSeedCell));
+        const float fy0 = floorf((cy0 - r - (float)row_lo) * (1.0f / kSeedCell));
+        const float fy1 = floorf((cy0 + r - (float)row_lo) * (1.0f / kSeedCell));
+        const float share = op * var * wgt / ((fx1 - fx0 + 1.0f) * (fy1 - fy0 + 1.0f));
+        const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, (float)(p.seed_cx - 1));
+        const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, (float)(p.seed_cy - 1));
+        const int b = min(max((int)(sortable_key(vz) >> kSatShift) - (int)p.seed_base, 0), kSeedBuckets - 1);
+        int cells = 0;
+        for (int y = y0; y <= y1 && cells < 1024; ++y)
+            for (int x = x0; x <= x1 && cells < 1024; ++x, ++cells)
+                atomicAdd(&p.seedh[((uint64_t)y * p.seed_cx + x) * kSeedBuckets + b], share);
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_seed_pick(ProjParams p) {
+    __shared__ uint32_t s_hist[kSeedBuckets];
+    const int tid = threadIdx.x;
+    if (tid < kSeedBuckets) s_hist[tid] = 0;
+    __syncthreads();
+    const int rows = min(p.tile_row_end * kTile, p.H) - p.tile_row_begin * kTile;
+    const int cells = p.seed_cx * p.seed_cy;
+    for (int q = tid; q < cells; q += 1024) {
+        const int cx = q % p.seed_cx, cy = q / p.seed_cx;
+        const float px = (float)(min(kSeedCell, p.W - cx * kSeedCell) * min(kSeedCell, rows - cy * kSeedCell));
+        const float need = p.seed_tau * px;
+        float* h = p.seedh + (uint64_t)q * kSeedBuckets;
+        float cum = 0.0f;
+        int sb = -1;
+        for (int b = 0; b < kSeedBuckets; ++b) {
+            cum += h[b];
+            h[b] = 0.0f;  // zero for the next seeded frame
+            if (sb < 0 && cum >= need) sb = b;
+        }
+        if (sb >= 0) atomicAdd(&s_hist[sb], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t sat = 0;
+        for (int b = 0; b < kSeedBuckets; ++b) sat += s_hist[b];
+        uint32_t T = kSentinel;
+        if (cells > 0 && (float)sat >= 0.2f * (float)cells) {
+            const float want = 0.95f * (float)sat;
+            uint32_t cum = 0;
+            int b = 0;
+            for (; b < kSeedBuckets - 1; ++b) {
+                cum += s_hist[b];
+                if ((float)cum >= want) break;
+            }
+            const uint64_t e = ((uint64_t)p.seed_base + (uint64_t)b + 1) << kSatShift;
+            const float v = key_depth((uint32_t)min<uint64_t>(e, 0xFFFFFFFEull)) * 1.10f;
+            if (isfinite(v)) {
+                const uint32_t k = sortable_key(v);
+                T = k >= kSentinel - 1u ? kSentinel : k + 1u;
+            }
+        }
+        p.ctl->seed_T = T;
+    }
 }
 
 __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
@@ -888,6 +990,7 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     const uint32_t parts = proj_parts(p.n), ucap = unit_shard_cap(parts);
     KT_MARK(0, 0, 0);
     const uint32_t nl = p.ctl->c0_parts;  // the partitions k_part_list kept
+    const uint32_t T = frame_thresh(p);
     uint32_t kt_items = 0;
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
         const uint32_t part = p.plist0[j];
@@ -907,7 +1010,7 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
             float vz;
             if (i < p.n && cull_keep(p, c[it], row_lo, row_hi, vz)) {
                 const uint32_t key = sortable_key(vz);
-                cd = key < p.thresh;
+                cd = key < T;
                 if (!cd) {  // past the threshold: counted, not projected
                     ++my_vis;
                     my_kmin_inv = max(my_kmin_inv, ~key);
@@ -972,7 +1075,10 @@ __global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
     // per wave: the SH quads of its 64 candidates, [candidate][quad] (viewed flat), loaded
     // straight into LDS (global_load_lds: no registers held, in flight while the footprint is
     // computed)
-    __shared__ float4 s_sh[SH12 ? kProjThreads / 64 : 1][SH12 ? 12 : 1][64];
+    // ([candidate][13 quads]: 12 coefficient quads and one of padding, so the 16 lanes of each
+    // ds_read_b128 group land on 16 distinct 16-B slots of the bank row; a 12-quad stride put
+    // them on 4, a 4-way conflict on every coefficient read)
+    __shared__ float4 s_sh[SH12 ? kProjThreads / 64 : 1][SH12 ? 13 : 1][64];
     const int tid = threadIdx.x;
     const int wv = tid >> 6, lane = tid & 63;
     if (tid == 0) { s_k = 0; s_vis = 0; s_kmin_inv = 0; s_kmax = 0; }
@@ -1010,13 +1116,14 @@ __global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
         Proj o;
         bool vis = false;
         if (SH12) {
-            // Coalesced staging through this wave's 12 KiB of LDS.  Every piece is 1 KiB in which
+            // Coalesced staging through this wave's 13 KiB of LDS.  Every piece is 1 KiB in which
             // consecutive lanes take consecutive 16-B chunks of one candidate's record (lane l of
-            // piece k: chunk (64 k + l) % m of candidate (64 k + l) / m, m = 3 geometry / 12 SH
-            // chunks), so a piece touches about 9 cache lines instead of up to 64.  The SH layout
-            // is [candidate][12 quads]: its pieces 0-8 land at once, the geometry's 3 pieces in the
-            // last 3 KiB; once the geometry is read out, SH pieces 9-11 land there.  Every lane
-            // takes part (an inactive candidate reads its partition's first record).
+            // piece k: chunk (64 k + l) % m of candidate (64 k + l) / m, m = 3 geometry / 13 SH
+            // chunks, SH chunk 12 = padding, loaded as a repeat of chunk 11), so a piece touches
+            // about 9 cache lines instead of up to 64.  The SH layout is [candidate][13 quads]: its
+            // pieces 0-9 land at once, the geometry's 3 pieces in the last 3 KiB; once the
+            // geometry is read out, SH pieces 10-12 land there.  Every lane takes part (an
+            // inactive candidate reads its partition's first record).
             const uint32_t ia = act ? i : p0;
             const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)&s_sh[wv][0][0]);
             // an opaque copy of the lane id: the pieces' source lanes are recomputed per unit
@@ -1040,25 +1147,25 @@ __global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
             for (int k = 0; k < 3; ++k) {
                 const uint32_t idx = 64u * k + ln, sc = idx / 3u, ch = idx % 3u;
                 const uint32_t isrc = (uint32_t)__shfl((int)ia, (int)sc, 64);
-                piece(p.geo + 3 * (uint64_t)isrc + ch, lds + 9216u + 1024u * k);
+                piece(p.geo + 3 * (uint64_t)isrc + ch, lds + 10240u + 1024u * k);
             }
             auto sh_piece = [&](int k) {
-                const uint32_t idx = 64u * k + ln, sc = idx / 12u, ch = idx % 12u;
+                const uint32_t idx = 64u * k + ln, sc = idx / 13u, ch = min(idx % 13u, 11u);
                 const uint32_t isrc = (uint32_t)__shfl((int)ia, (int)sc, 64);
                 piece(p.sh + 12 * (uint64_t)isrc + ch, lds + 1024u * k);
             };
 #pragma unroll
-            for (int k = 0; k < 9; ++k) sh_piece(k);
-            // the geometry (issued before the 9 SH pieces) is in LDS once at most 9 are outstanding
-            asm volatile("s_waitcnt vmcnt(9)" : "+v"(oi) :: "memory");
-            const float4* sg = (const float4*)&s_sh[wv][0][0] + 576 + 3 * lane;
+            for (int k = 0; k < 10; ++k) sh_piece(k);
+            // the geometry (issued before the 10 SH pieces) is in LDS once at most 10 are outstanding
+            asm volatile("s_waitcnt vmcnt(10)" : "+v"(oi) :: "memory");
+            const float4* sg = (const float4*)&s_sh[wv][0][0] + 640 + 3 * lane;
             g0 = sg[0];
             g1 = sg[1];
             g2 = sg[2];
-            // the reads are done before SH pieces 9-11 overwrite the geometry's staging
+            // the reads are done before SH pieces 10-12 overwrite the geometry's staging
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int k = 9; k < 12; ++k) sh_piece(k);
+            for (int k = 10; k < 13; ++k) sh_piece(k);
         }
         if (act) {
             if (!SH12) {
@@ -1080,7 +1187,7 @@ __global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
                     float4 col;
                     if (SH12) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        col = sh_colour<1>(&s_sh[wv][0][0] + 12 * lane, 12, g0.x, g0.y, g0.z, p.cam);
+                        col = sh_colour<1>(&s_sh[wv][0][0] + 13 * lane, 12, g0.x, g0.y, g0.z, p.cam);
                     } else {
                         col = sh_colour(p.sh + (uint64_t)i * p.shq, p.shq, g0.x, g0.y, g0.z, p.cam);
                     }
@@ -3086,6 +3193,12 @@ void launch_project(const ProjParams& p, hipStream_t s) {
         hipLaunchKernelGGL(k_project<true>, dim3(ugrid), dim3(kProjThreads), 0, s, p);
     else
         hipLaunchKernelGGL(k_project<false>, dim3(ugrid), dim3(kProjThreads), 0, s, p);
+}
+void launch_seed(const ProjParams& p, hipStream_t s) {
+    const uint32_t nrun = (p.n + kSeedRun - 1) / kSeedRun;
+    const uint32_t nsr = (nrun + p.seed_stride - 1) / std::max(1u, p.seed_stride);
+    if (nsr) hipLaunchKernelGGL(k_seed_hist, dim3(std::min<uint32_t>(4096, (nsr + 15) / 16)), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_seed_pick, dim3(1), dim3(1024), 0, s, p);
 }
 void launch_records(const ProjParams& p, hipStream_t s) {
     if (!p.n) return;

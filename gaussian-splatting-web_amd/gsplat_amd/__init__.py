@@ -65,7 +65,8 @@ class GsStats(ctypes.Structure):
                 ("k_chunk0", ctypes.c_uint32), ("k_chunk1", ctypes.c_uint32),
                 ("wide_chunk0", ctypes.c_uint32), ("wide_chunk1", ctypes.c_uint32),
                 ("frames_rendered", ctypes.c_uint32), ("frames_chunked", ctypes.c_uint32),
-                ("frames_unsat", ctypes.c_uint32), ("frames_seeded", ctypes.c_uint32)]
+                ("frames_unsat", ctypes.c_uint32), ("frames_seeded", ctypes.c_uint32),
+                ("chunk_depth", ctypes.c_float)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -206,6 +207,24 @@ def orbit_uniforms(W, H, k, period=60):
     yaw, pitch = np.radians(25.0) * np.sin(a), np.radians(8.0) * np.sin(2 * a)
     target = (np.sin(yaw) * np.cos(pitch), np.sin(pitch), -np.cos(yaw) * np.cos(pitch))
     view = look_at((0.0, 0.0, 0.0), target)
+    return pack_uniforms(view, perspective(1.04719755, W / H, 0.03, 1000.0), focal=(W, H))
+
+
+# bench.py's camera cuts: four views of the synthetic scene (Gaussians fill the
+# bench view's frustum at depths 2..20 along -z), each far from the others in direction or
+# position, so every frame of the cycle starts without usable saturation history
+COLD_VIEWS = (
+    ((0.0, 0.0, 0.0), (0.0, 0.0, -1.0)),       # the bench view
+    ((0.0, 0.0, -6.0), (0.0, 0.0, -7.0)),      # from inside the scene, same direction
+    ((0.0, 0.0, 0.0), (0.34, -0.1, -0.94)),    # turned 20 deg right, 6 deg down
+    ((1.5, 0.8, -2.0), (-1.0, -0.5, -12.0)),   # moved and turned left
+)
+
+
+def cold_uniforms(W, H, k):
+    """View k % 4 of bench.py's camera-cut cycle (COLD_VIEWS)."""
+    eye, target = COLD_VIEWS[k % len(COLD_VIEWS)]
+    view = look_at(eye, target)
     return pack_uniforms(view, perspective(1.04719755, W / H, 0.03, 1000.0), focal=(W, H))
 
 

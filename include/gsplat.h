@@ -119,6 +119,7 @@ typedef struct gs_stats {
                                   counted when the frame's statistics arrive) */
     uint32_t frames_seeded;    /* ... whose split depth came from the frame's own coarse depth
                                   estimate (no usable history: a first frame or a camera cut) */
+    float chunk_depth;         /* |view depth| of the last frame's chunk split (0: one chunk) */
 } gs_stats;
 
 /* ---- library / device ---------------------------------------------------------------------- */

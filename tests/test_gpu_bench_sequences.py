@@ -12,8 +12,11 @@ against the CPU oracle at the fp32 bar (tests/test_gpu_parity.py):
           two chunks, chunk 0 saturates every tile);
   orbit   bench.py's moving camera (gsplat_amd.orbit_uniforms, 5 warm-up + 60 frames): a new
           view every frame, tiles left unsaturated, chunk 1 composited on its split launches;
+  cold    bench.py's camera cuts (gsplat_amd.COLD_VIEWS, a cycle of 4 views far apart): every
+          frame starts without saturation history of its view, so it is *seeded* (its chunk
+          threshold comes from the frame's own coarse depth estimate, k_seed_hist/k_seed_pick);
   50 M    10 orbit frames of configs[4] at 3840x2160 (tests/test_gpu_configs.py holds its
-          one-chunk frame against the oracle).
+          one-chunk frame against the oracle), then its camera cuts.
 
 Reference semantics: every dirty frame is a full re-sort and redraw (src/renderer.ts:301-330),
 so each frame must equal its one-chunk render whatever the controller did before it.
@@ -120,6 +123,30 @@ def test_bench_orbit_sequence(gpu_ctx, bench_scene):
         _vs_oracle(aos, N3, views[k], W, H, imgs[k], "bench_orbit_%d" % k)
 
 
+@pytest.mark.timeout(600)
+def test_bench_cold_sequence(gpu_ctx, bench_scene):
+    aos, sc = bench_scene
+    W, H = W3, H3
+    o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=2)
+    views = [gs.cold_uniforms(W, H, k) for k in range(12)]
+    bufs = [gs.DeviceBuffer(W * H * 8) for _ in range(12)]
+    _frames(sc, gpu_ctx, [gs.bench_uniforms(W, H)] * 5, W, H, o, bufs[:1] * 5)  # history of another view
+    gpu_ctx.timings_reset()
+    imgs = _frames(sc, gpu_ctx, views, W, H, o, bufs)
+    st = gpu_ctx.timings()
+    for b in bufs:
+        b.free()
+    assert st["frames_rendered"] == 12
+    # every frame is a cut (the bench view first: a cut from the history's static view only
+    # through position, which it shares -- so at least the other 11)
+    assert st["frames_seeded"] >= 11 and st["frames_chunked"] >= 11, st
+    for k, im in enumerate(imgs):
+        one = _one_chunk(sc, views[k], W, H)
+        assert np.array_equal(_bits(im), _bits(one)), "cold frame %d (view %d) differs from one chunk" % (k, k % 4)
+    for k in (1, 3):  # from inside the scene; moved and turned
+        _vs_oracle(aos, N3, views[k], W, H, imgs[k], "bench_cold_%d" % k)
+
+
 @pytest.mark.timeout(900)
 def test_orbit_50m_4k(gpu_ctx):
     """configs[4]'s scene under the moving camera at 3840x2160: 5 static warm-up frames, then 10
@@ -142,4 +169,15 @@ def test_orbit_50m_4k(gpu_ctx):
     assert st["frames_chunked"] >= 8, st
     for k, im in enumerate(imgs):
         assert np.array_equal(_bits(im), _bits(_one_chunk(sc, views[k], W, H))), "4K orbit frame %d" % k
+    # camera cuts at 4K: seeded frames
+    views = [gs.cold_uniforms(W, H, k) for k in range(4)]
+    bufs = [gs.DeviceBuffer(W * H * 8) for _ in range(4)]
+    gpu_ctx.timings_reset()
+    imgs = _frames(sc, gpu_ctx, views, W, H, o, bufs)
+    st = gpu_ctx.timings()
+    for b in bufs:
+        b.free()
+    assert st["frames_seeded"] >= 3, st
+    for k, im in enumerate(imgs):
+        assert np.array_equal(_bits(im), _bits(_one_chunk(sc, views[k], W, H))), "4K cold frame %d" % k
     sc.close()
