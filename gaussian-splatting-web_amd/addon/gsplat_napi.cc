@@ -116,6 +116,8 @@ void read_opts(napi_env env, napi_value o, gs_opts* opts) {
     opts->strip_count = (int32_t)field("stripCount", opts->strip_count);
     opts->timing = (int32_t)field("timing", opts->timing);
     opts->chunk_fraction = (float)field("chunkFraction", opts->chunk_fraction);
+    opts->tile_row_begin = (int32_t)field("tileRowBegin", opts->tile_row_begin);
+    opts->tile_row_end = (int32_t)field("tileRowEnd", opts->tile_row_end);
 }
 
 // ---- library / device --------------------------------------------------------------------
@@ -235,7 +237,10 @@ napi_value parse_render(napi_env env, napi_value* argv, RenderArgs* a) {
         if (!get_bytes(env, argv[6], &a->out, &a->out_len))
             return throw_gs(env, GS_ERR_INVALID, "render: out must be a TypedArray or null");
         int row0 = 0, rows = a->H;
-        if (a->opts.strip_count > 1) gs_strip_rows(a->H, a->opts.strip_index, a->opts.strip_count, &row0, &rows);
+        if (a->opts.tile_row_end > 0)
+            rows = std::min(16 * a->opts.tile_row_end, a->H) - 16 * a->opts.tile_row_begin;
+        else if (a->opts.strip_count > 1)
+            gs_strip_rows(a->H, a->opts.strip_index, a->opts.strip_count, &row0, &rows);
         const size_t need = (size_t)rows * (size_t)a->W * (a->opts.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
         if (a->out_len < need) return throw_gs(env, GS_ERR_INVALID, "render: out buffer too small");
     }

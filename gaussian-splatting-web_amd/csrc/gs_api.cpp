@@ -166,9 +166,17 @@ struct gs_ctx {
     // buffer.  A device list with repeats (tests on one GPU) gathers with peer copies instead.
     std::vector<gs_ctx*> members;
     std::vector<ncclComm_t> comms;
-    std::vector<void*> gfull;          // [member] the gathered image buffer (G strips, padded)
-    std::vector<size_t> gfull_bytes;
-    std::vector<hipEvent_t> gev;       // [member] strip rendered (peer-copy gather)
+    // member g >= 1 renders into one of two strip buffers on its device (double-buffered: frame
+    // f + 1 renders while frame f's strip is sent); member 0 renders straight into the image
+    std::vector<std::array<void*, 2>> gbuf;
+    std::vector<size_t> gbuf_bytes;
+    std::vector<hipStream_t> gstream;  // [member] the gather's stream (sends; member 0: receives)
+    std::vector<hipEvent_t> gev_rendered;             // [member] strip rendered (on the member's stream)
+    std::vector<std::array<hipEvent_t, 2>> gev_sent;  // [member][buffer] strip sent (buffer free again)
+    hipEvent_t gev_entry = nullptr, gev_gathered = nullptr;  // device 0: the caller's stream at entry, image complete
+    std::vector<int> gbounds;          // tile-row boundaries of the members' strips (G + 1), K-balanced
+    int gH = 0;                        // the image height gbounds were made for
+    uint32_t gframe = 0;               // frames since gbounds were (re)made
 };
 
 // Everything one frame writes.  kFrameSets sets, used by frames in turn, each with its own stream
@@ -378,6 +386,73 @@ static void strip_geometry(int H, int si, int sc, int& tr_begin, int& tr_end, in
     rows_padded = per * kTile;
 }
 
+// The rows a frame renders and its output buffer: tile rows [tb, te); the buffer holds `rows`
+// image rows from image row `row0` (`pad` of them past the image: zero padding of the last
+// equal strip).  Explicit tile-row ranges (gs_opts.tile_row_end > 0) have no padding.
+struct FrameRows {
+    int tb, te, row0, rows, pad;
+};
+static FrameRows frame_rows(int H, const gs_opts& o) {
+    FrameRows r{};
+    if (o.tile_row_end > 0) {
+        r.tb = o.tile_row_begin;
+        r.te = o.tile_row_end;
+        r.row0 = r.tb * kTile;
+        r.rows = std::min(r.te * kTile, H) - r.row0;
+        return r;
+    }
+    const int sc = std::max(1, o.strip_count);
+    int rp;
+    strip_geometry(H, o.strip_index, sc, r.tb, r.te, rp);
+    r.row0 = sc > 1 ? r.tb * kTile : 0;
+    r.rows = sc > 1 ? rp : H;
+    r.pad = sc > 1 ? std::min(rp, std::max(0, r.row0 + rp - H)) : 0;
+    return r;
+}
+
+// gs_opts of the caller, read up to its struct_size (callers built against an older header pass a
+// shorter struct; the fields past it keep their defaults).
+static gs_opts read_opts(const gs_opts* opts) {
+    gs_opts o;
+    gs_opts_default(&o);
+    if (opts) {
+        const size_t n = std::min<size_t>(sizeof(gs_opts), opts->struct_size ? opts->struct_size : sizeof(gs_opts));
+        std::memcpy(&o, opts, n);
+        o.struct_size = sizeof(gs_opts);
+    }
+    return o;
+}
+
+// K-balanced strips: new tile-row boundaries that equalise the strips' costs, the cost of each
+// current strip taken as spread evenly over its rows, each boundary moved half way to that
+// model's cut (every strip keeps >= 1 row when TR >= G).
+static void balance_bounds(int G, int TR, const int* b, const double* cost, int* nb) {
+    double total = 0.0;
+    for (int g = 0; g < G; ++g) total += std::max(0.0, cost[g]);
+    nb[0] = 0;
+    nb[G] = TR;
+    if (!(total > 0.0) || TR < G) {
+        for (int g = 1; g < G; ++g) nb[g] = b[g];
+        return;
+    }
+    int seg = 0;
+    double cum = 0.0;  // cost of rows [0, b[seg])
+    for (int k = 1; k < G; ++k) {
+        const double want = total * k / G;
+        while (seg < G - 1 && cum + std::max(0.0, cost[seg]) < want) cum += std::max(0.0, cost[seg++]);
+        const int rows = b[seg + 1] - b[seg];
+        const double c = std::max(0.0, cost[seg]);
+        const double x = b[seg] + (c > 0.0 && rows > 0 ? (want - cum) / c * rows : 0.0);
+        // half way from the old boundary: the even-spread model over- or undershoots where the
+        // cost is concentrated (a dense band of rows); damped, the feedback converges
+        int r = (int)std::lround(0.5 * (x + b[k]));
+        if (r == b[k] && std::fabs(x - b[k]) >= 0.5) r += x > b[k] ? 1 : -1;  // at least one row toward it
+        r = std::max(r, nb[k - 1] + 1);
+        r = std::min(r, TR - (G - k));
+        nb[k] = r;
+    }
+}
+
 static void harvest(gs_ctx* c, FrameEvents& f) {
     if (!f.pending) return;
     auto el = [&](int a, int b) {
@@ -540,9 +615,8 @@ static bool camera_cut(const gs_scene* s, const float* uni) {
 // The per-frame pipeline.  `out` is device memory of rows_padded*W (strip) or H*W pixels.
 static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o,
                          void* out, hipStream_t st) {
-    int tr_begin, tr_end, rows_padded;
-    const int sc = std::max(1, o.strip_count);
-    strip_geometry(H, o.strip_index, sc, tr_begin, tr_end, rows_padded);
+    const FrameRows fr = frame_rows(H, o);
+    const int tr_begin = fr.tb, tr_end = fr.te;
     const int TX = (W + kTile - 1) / kTile;
     const int n_tiles = TX * (tr_end - tr_begin);
     FrameSet& F = s->fs[s->cur_fs];
@@ -758,7 +832,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     cp.H = H;
     cp.tiles_x = TX;
     cp.tile_row_begin = tr_begin;
-    cp.row0 = sc > 1 ? tr_begin * kTile : 0;
+    cp.row0 = fr.row0;
     cp.n_tiles = n_tiles;
     cp.t_min = o.t_min;
     cp.mode = two_chunks ? kCompFirst : kCompSingle;
@@ -779,10 +853,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     HIPCHK(hipStreamWaitEvent(cst, F.ev_early, 0));
     st = cst;  // the composite (the caller's buffer) and the frame's end, in call order
     mark(EV_RANGES_0);
-    if (sc > 1 && tr_begin * kTile + rows_padded > H) {  // the last strip's rows past the image are
-        // padding (gs_strip_rows): defined as zero (transparent black); no kernel writes them
-        const size_t valid = (size_t)std::max(0, H - tr_begin * kTile), px = cp.out_f16 ? 8 : 16;
-        HIPCHK(hipMemsetAsync((char*)out + valid * (size_t)W * px, 0, ((size_t)rows_padded - valid) * (size_t)W * px, st));
+    if (fr.pad > 0) {  // the last equal strip's rows past the image are padding (gs_strip_rows):
+        // defined as zero (transparent black); no kernel writes them
+        const size_t px = cp.out_f16 ? 8 : 16;
+        HIPCHK(hipMemsetAsync((char*)out + (size_t)(fr.rows - fr.pad) * (size_t)W * px, 0,
+                              (size_t)fr.pad * (size_t)W * px, st));
     }
     launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
     mark(EV_COMP_0);
@@ -854,8 +929,17 @@ static void validate_render_args(gs_ctx* c, gs_scene* s, const void* uni, int W,
         throw GsError(GS_ERR_INVALID, "a device group renders its row strips itself (strip_count must be 1)");
     if (W <= 0 || H <= 0 || W > 65535 || H > 65535) throw GsError(GS_ERR_INVALID, "bad image size");
     if (o) {
-        if (o->strip_count < 1 || o->strip_index < 0 || o->strip_index >= o->strip_count)
+        const gs_opts oo = read_opts(o);
+        if (oo.strip_count < 1 || oo.strip_index < 0 || oo.strip_index >= oo.strip_count)
             throw GsError(GS_ERR_INVALID, "bad strip index/count");
+        if (oo.tile_row_end != 0 || oo.tile_row_begin != 0) {
+            const int TR = (H + kTile - 1) / kTile;
+            if (oo.strip_count != 1) throw GsError(GS_ERR_INVALID, "an explicit tile-row range takes strip_count 1");
+            if (!c->members.empty())
+                throw GsError(GS_ERR_INVALID, "a device group chooses its strips itself (no explicit tile-row range)");
+            if (oo.tile_row_begin < 0 || oo.tile_row_end <= oo.tile_row_begin || oo.tile_row_end > TR)
+                throw GsError(GS_ERR_INVALID, "bad tile-row range");
+        }
         if (o->accum != GS_ACCUM_FP32 && o->accum != GS_ACCUM_FP16_TARGET)
             throw GsError(GS_ERR_INVALID, "bad accum mode");
         if (o->out_format != GS_OUT_RGBA_F32 && o->out_format != GS_OUT_RGBA_F16)
@@ -870,10 +954,7 @@ static void validate_render_args(gs_ctx* c, gs_scene* s, const void* uni, int W,
 }
 
 static size_t out_bytes_for(int W, int H, const gs_opts& o) {
-    int tb, te, rows_padded;
-    strip_geometry(H, o.strip_index, std::max(1, o.strip_count), tb, te, rows_padded);
-    const size_t rows = o.strip_count > 1 ? (size_t)rows_padded : (size_t)H;
-    return rows * (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
+    return (size_t)frame_rows(H, o).rows * (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
 }
 
 // After a tile-list overflow: every frame set grows to the largest total of the frames that
@@ -982,63 +1063,119 @@ static void quirk_prepare(gs_scene* s, const float* uni, hipStream_t st) {
     s->qdraw = r.second;
 }
 
-// A device group's frame (gs_ctx::members): member g renders row strip g of G into slice g of its
-// G-strip buffer, then the gather fills member 0's buffer (RCCL: one in-place all-gather, every
-// member's buffer; repeated devices: peer copies into member 0's).  Enqueue only: the image is on
-// member 0, ordered on st0 (the caller's stream there, or member 0's own).  Returns that buffer.
-static void* render_group(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o, hipStream_t st0) {
+// A device group's frame (gs_ctx::members): member g renders tile rows [gbounds[g], gbounds[g+1])
+// of the image -- member 0 straight into `out` (device 0, H rows), member g >= 1 into one of its two
+// strip buffers -- and the strips travel to member 0 only: RCCL send/receive pairs over the
+// communicators of ncclCommInitAll (distinct devices, xGMI), or peer copies (a list that repeats a
+// device: the one-GPU tests).  The transfers run on the members' gather streams, so member g's
+// next frame renders into its other buffer while this frame's strip is sent.  The strips are
+// K-balanced: every kRebalanceFrames frames the boundaries move so that each member's binned
+// entries (plus a per-tile cost) are equal (balance_bounds).  Enqueue only: the image is complete
+// on device 0 in stream order of st0.
+constexpr uint32_t kRebalanceFrames = 8;
+constexpr double kTileCost = 32.0;  // a tile's fixed cost in binned-entry units (its scan, sort and composite start)
+
+static void rebalance_group(gs_ctx* c, gs_scene* s, int W, int TR) {
     const int G = (int)c->members.size();
-    int tb, te, rp;
-    strip_geometry(H, 0, G, tb, te, rp);
-    const size_t bpp = o.out_format == GS_OUT_RGBA_F16 ? 8 : 16;
-    const size_t strip_bytes = (size_t)rp * W * bpp, full_bytes = strip_bytes * G;
-    auto stream_of = [&](int g) { return g == 0 ? st0 : c->members[g]->stream; };
+    const int TX = (W + kTile - 1) / kTile;
+    std::vector<double> cost(G, 0.0);
     for (int g = 0; g < G; ++g) {
+        gs_scene* m = s->members[g];
+        if (!m->have_last) return;  // no statistics yet
+        const int rows = c->gbounds[g + 1] - c->gbounds[g];
+        cost[g] = (double)m->last.k_chunk[0] + (double)m->last.k_chunk[1] + kTileCost * TX * rows;
+    }
+    std::vector<int> nb(G + 1);
+    balance_bounds(G, TR, c->gbounds.data(), cost.data(), nb.data());
+    c->gbounds = nb;
+}
+
+static void render_group(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o, void* out,
+                         hipStream_t st0) {
+    const int G = (int)c->members.size();
+    const int TR = (H + kTile - 1) / kTile;
+    const size_t row_bytes = (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
+    if (c->gH != H || (int)c->gbounds.size() != G + 1) {  // even strips until statistics arrive
+        c->gbounds.assign(G + 1, 0);
+        for (int g = 0; g <= G; ++g) c->gbounds[g] = (int)((int64_t)g * TR / G);
+        c->gH = H;
+        c->gframe = 0;
+    } else if (++c->gframe % kRebalanceFrames == 0) {
+        rebalance_group(c, s, W, TR);
+    }
+    const int buf = (int)(c->gframe & 1u);
+    auto stream_of = [&](int g) { return g == 0 ? st0 : c->members[g]->stream; };
+    const int dev0 = c->members[0]->device;
+    // the transfers into `out` start after the caller's earlier work on it
+    HIPCHK(hipSetDevice(dev0));
+    HIPCHK(hipEventRecord(c->gev_entry, st0));
+    HIPCHK(hipStreamWaitEvent(c->gstream[0], c->gev_entry, 0));
+    for (int g = 0; g < G; ++g) {
+        const int tb = c->gbounds[g], te = c->gbounds[g + 1];
+        if (tb >= te) continue;
         gs_ctx* m = c->members[g];
         HIPCHK(hipSetDevice(m->device));
-        if (c->gfull_bytes[g] < full_bytes) {
-            if (c->gfull[g]) {
-                HIPCHK(hipDeviceSynchronize());
-                HIPCHK(hipFree(c->gfull[g]));
-                c->gfull[g] = nullptr;
-                c->gfull_bytes[g] = 0;
-            }
-            HIPCHK(hipMalloc(&c->gfull[g], full_bytes));
-            c->gfull_bytes[g] = full_bytes;
-        }
         gs_opts og = o;
-        og.strip_index = g;
-        og.strip_count = G;
-        render_frame(m, s->members[g], uni, W, H, og, (char*)c->gfull[g] + g * strip_bytes, stream_of(g));
+        og.strip_index = 0;
+        og.strip_count = 1;
+        og.tile_row_begin = tb;
+        og.tile_row_end = te;
+        void* dst = (char*)out + (size_t)tb * kTile * row_bytes;
+        if (g > 0) {
+            const size_t need = (size_t)H * row_bytes;  // any strip fits: the bounds move
+            if (c->gbuf_bytes[g] < need) {
+                HIPCHK(hipDeviceSynchronize());
+                for (void*& p : c->gbuf[g]) {
+                    if (p) HIPCHK(hipFree(p));
+                    p = nullptr;
+                }
+                c->gbuf_bytes[g] = 0;
+                for (void*& p : c->gbuf[g]) HIPCHK(hipMalloc(&p, need));
+                c->gbuf_bytes[g] = need;
+            }
+            dst = c->gbuf[g][buf];
+            HIPCHK(hipStreamWaitEvent(stream_of(g), c->gev_sent[g][buf], 0));  // frame f - 2's send of it
+        }
+        render_frame(m, s->members[g], uni, W, H, og, dst, stream_of(g));
+        if (g > 0) HIPCHK(hipEventRecord(c->gev_rendered[g], stream_of(g)));
     }
     if (!c->comms.empty()) {
+        for (int g = 1; g < G; ++g) {
+            HIPCHK(hipSetDevice(c->members[g]->device));
+            HIPCHK(hipStreamWaitEvent(c->gstream[g], c->gev_rendered[g], 0));
+        }
         ncclResult_t r = ncclGroupStart();
-        for (int g = 0; g < G && r == ncclSuccess; ++g)
-            r = ncclAllGather((char*)c->gfull[g] + g * strip_bytes, c->gfull[g], strip_bytes, ncclUint8, c->comms[g],
-                              stream_of(g));
+        for (int g = 1; g < G && r == ncclSuccess; ++g) {
+            const int tb = c->gbounds[g], te = c->gbounds[g + 1];
+            if (tb >= te) continue;
+            const size_t bytes = (size_t)(std::min(te * kTile, H) - tb * kTile) * row_bytes;
+            r = ncclSend(c->gbuf[g][buf], bytes, ncclUint8, 0, c->comms[g], c->gstream[g]);
+            if (r == ncclSuccess)
+                r = ncclRecv((char*)out + (size_t)tb * kTile * row_bytes, bytes, ncclUint8, g, c->comms[0], c->gstream[0]);
+        }
         const ncclResult_t r2 = ncclGroupEnd();
         if (r != ncclSuccess || r2 != ncclSuccess)
-            throw GsError(GS_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-    } else {
+            throw GsError(GS_ERR_HIP, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
         for (int g = 1; g < G; ++g) {
             HIPCHK(hipSetDevice(c->members[g]->device));
-            HIPCHK(hipEventRecord(c->gev[g], stream_of(g)));
-            HIPCHK(hipSetDevice(c->members[0]->device));
-            HIPCHK(hipStreamWaitEvent(st0, c->gev[g], 0));
-            HIPCHK(hipMemcpyPeerAsync((char*)c->gfull[0] + g * strip_bytes, c->members[0]->device,
-                                      (char*)c->gfull[g] + g * strip_bytes, c->members[g]->device, strip_bytes, st0));
+            HIPCHK(hipEventRecord(c->gev_sent[g][buf], c->gstream[g]));
         }
-        // member g's next frame rewrites its slice only after this frame's copy of it
-        HIPCHK(hipSetDevice(c->members[0]->device));
-        HIPCHK(hipEventRecord(c->gev[0], st0));
+    } else {
+        HIPCHK(hipSetDevice(dev0));
         for (int g = 1; g < G; ++g) {
-            HIPCHK(hipSetDevice(c->members[g]->device));
-            HIPCHK(hipStreamWaitEvent(stream_of(g), c->gev[0], 0));
+            const int tb = c->gbounds[g], te = c->gbounds[g + 1];
+            if (tb >= te) continue;
+            const size_t bytes = (size_t)(std::min(te * kTile, H) - tb * kTile) * row_bytes;
+            HIPCHK(hipStreamWaitEvent(c->gstream[0], c->gev_rendered[g], 0));
+            HIPCHK(hipMemcpyPeerAsync((char*)out + (size_t)tb * kTile * row_bytes, dev0, c->gbuf[g][buf],
+                                      c->members[g]->device, bytes, c->gstream[0]));
+            HIPCHK(hipEventRecord(c->gev_sent[g][buf], c->gstream[0]));
         }
     }
-    HIPCHK(hipSetDevice(c->members[0]->device));
+    HIPCHK(hipSetDevice(dev0));
+    HIPCHK(hipEventRecord(c->gev_gathered, c->gstream[0]));
+    HIPCHK(hipStreamWaitEvent(st0, c->gev_gathered, 0));
     c->last_scene = s;
-    return c->gfull[0];
 }
 
 extern "C" {
@@ -1101,13 +1238,28 @@ int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
                     throw GsError(GS_ERR_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
                 }
             }
-            c->gfull.assign(ndev, nullptr);
-            c->gfull_bytes.assign(ndev, 0);
-            c->gev.assign(ndev, nullptr);
+            c->gbuf.assign(ndev, {nullptr, nullptr});
+            c->gbuf_bytes.assign(ndev, 0);
+            c->gstream.assign(ndev, nullptr);
+            c->gev_rendered.assign(ndev, nullptr);
+            c->gev_sent.assign(ndev, {nullptr, nullptr});
+            const bool rccl = !c->comms.empty();
             for (int g = 0; g < ndev; ++g) {
                 HIPCHK(hipSetDevice(devices[g]));
-                HIPCHK(hipEventCreateWithFlags(&c->gev[g], hipEventDisableTiming));
+                HIPCHK(hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking));
+                HIPCHK(hipEventCreateWithFlags(&c->gev_rendered[g], hipEventDisableTiming));
+                if (g == 0) {
+                    HIPCHK(hipEventCreateWithFlags(&c->gev_entry, hipEventDisableTiming));
+                    HIPCHK(hipEventCreateWithFlags(&c->gev_gathered, hipEventDisableTiming));
+                }
             }
+            for (int g = 1; g < ndev; ++g)  // recorded where the strip is sent: member g's gather
+                for (hipEvent_t& e : c->gev_sent[g]) {  // stream (RCCL) or device 0's (peer copies)
+                    const int d = rccl ? devices[g] : devices[0];
+                    HIPCHK(hipSetDevice(d));
+                    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    HIPCHK(hipEventRecord(e, c->gstream[rccl ? g : 0]));  // "the buffer is free"
+                }
         } catch (...) {
             gs_ctx_destroy(c);
             throw;
@@ -1152,8 +1304,22 @@ void gs_ctx_destroy(gs_ctx* c) {
         for (size_t g = 0; g < c->members.size(); ++g) {
             (void)hipSetDevice(c->members[g]->device);
             (void)hipDeviceSynchronize();
-            if (g < c->gfull.size() && c->gfull[g]) (void)hipFree(c->gfull[g]);
-            if (g < c->gev.size() && c->gev[g]) (void)hipEventDestroy(c->gev[g]);
+            if (g < c->gbuf.size())
+                for (void* p : c->gbuf[g])
+                    if (p) (void)hipFree(p);
+        }
+        for (size_t g = 0; g < c->members.size(); ++g) {
+            (void)hipSetDevice(c->members[g]->device);
+            if (g < c->gev_rendered.size() && c->gev_rendered[g]) (void)hipEventDestroy(c->gev_rendered[g]);
+            if (g < c->gstream.size() && c->gstream[g]) (void)hipStreamDestroy(c->gstream[g]);
+        }
+        for (size_t g = 0; g < c->gev_sent.size(); ++g)
+            for (hipEvent_t e : c->gev_sent[g])
+                if (e) (void)hipEventDestroy(e);
+        if (!c->members.empty()) {
+            (void)hipSetDevice(c->members[0]->device);
+            if (c->gev_entry) (void)hipEventDestroy(c->gev_entry);
+            if (c->gev_gathered) (void)hipEventDestroy(c->gev_gathered);
         }
         for (ncclComm_t m : c->comms)
             if (m) (void)ncclCommDestroy(m);
@@ -1371,6 +1537,32 @@ int gs_ctx_info(const gs_ctx* c, int* out_ndev, int* out_gather) {
     });
 }
 
+int gs_balance_strips(int G, int tile_rows, const int* bounds, const double* cost, int* out_bounds) {
+    return guarded([&] {
+        if (G < 1 || G > 4096 || tile_rows < 1 || !bounds || !cost || !out_bounds)
+            throw GsError(GS_ERR_INVALID, "bad balance arguments");
+        if (bounds[0] != 0 || bounds[G] != tile_rows) throw GsError(GS_ERR_INVALID, "bounds must span [0, tile_rows]");
+        for (int g = 0; g < G; ++g)
+            if (bounds[g + 1] < bounds[g]) throw GsError(GS_ERR_INVALID, "bounds must not decrease");
+        for (int g = 0; g < G; ++g)
+            if (!std::isfinite(cost[g])) throw GsError(GS_ERR_INVALID, "non-finite cost");
+        std::vector<int> nb(G + 1);
+        balance_bounds(G, tile_rows, bounds, cost, nb.data());
+        std::copy(nb.begin(), nb.end(), out_bounds);
+        return GS_OK;
+    });
+}
+
+int gs_ctx_strips(const gs_ctx* c, int* out_bounds, int capacity, int* out_n) {
+    return guarded([&] {
+        if (!c || !out_n) throw GsError(GS_ERR_INVALID, "null argument");
+        *out_n = c->members.empty() ? 0 : (int)c->gbounds.size();
+        if (out_bounds)
+            for (int k = 0; k < *out_n && k < capacity; ++k) out_bounds[k] = c->gbounds[k];
+        return GS_OK;
+    });
+}
+
 int gs_strip_rows(int H, int si, int sc, int* row0, int* rows_padded) {
     return guarded([&] {
         if (H <= 0 || sc < 1 || si < 0 || si >= sc || !row0 || !rows_padded)
@@ -1387,9 +1579,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
                      void* out_dev, uint64_t out_bytes, void* stream) {
     return guarded([&] {
         validate_render_args(c, s, uni, W, H, opts);
-        gs_opts o;
-        gs_opts_default(&o);
-        if (opts) o = *opts;
+        const gs_opts o = read_opts(opts);
         if (!out_dev) throw GsError(GS_ERR_INVALID, "null output");
         if (out_bytes < out_bytes_for(W, H, o)) throw GsError(GS_ERR_INVALID, "output buffer too small");
         if (!c->members.empty()) {  // the image (H rows) into out_dev on the first device
@@ -1398,8 +1588,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
             gs_ctx* m0 = c->members[0];
             HIPCHK(hipSetDevice(m0->device));
             hipStream_t st0 = stream ? (hipStream_t)stream : m0->stream;
-            void* full = render_group(c, s, (const float*)uni, W, H, o, st0);
-            HIPCHK(hipMemcpyAsync(out_dev, full, out_bytes_for(W, H, o), hipMemcpyDeviceToDevice, st0));
+            render_group(c, s, (const float*)uni, W, H, o, out_dev, st0);
             return GS_OK;
         }
         HIPCHK(hipSetDevice(c->device));
@@ -1438,13 +1627,14 @@ int gs_present_device(gs_ctx* c, const void* fb_dev, int fb_format, int W, int H
 int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_opts* opts, void* out_host) {
     return guarded([&] {
         validate_render_args(c, s, uni, W, H, opts);
-        gs_opts o;
-        gs_opts_default(&o);
-        if (opts) o = *opts;
+        const gs_opts o = read_opts(opts);
         const size_t bytes = out_bytes_for(W, H, o);
         if (!c->members.empty()) {
+            HIPCHK(hipSetDevice(c->members[0]->device));
+            ensure_out(c->members[0], bytes);
+            void* full = c->members[0]->d_out;
             for (int attempt = 0;; ++attempt) {
-                void* full = render_group(c, s, (const float*)uni, W, H, o, c->members[0]->stream);
+                render_group(c, s, (const float*)uni, W, H, o, full, c->members[0]->stream);
                 bool overflow = false;
                 for (size_t g = 0; g < c->members.size(); ++g) {
                     HIPCHK(hipSetDevice(c->members[g]->device));

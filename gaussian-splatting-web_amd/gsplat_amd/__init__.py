@@ -26,7 +26,7 @@ GS_OK, GS_ERR_INVALID, GS_ERR_NO_DEVICE, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPOR
 # every symbol include/gsplat.h declares
 EXPORTED_SYMBOLS = (
     "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy", "gs_ctx_info",
-    "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows",
+    "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows", "gs_balance_strips", "gs_ctx_strips",
     "gs_render", "gs_render_device", "gs_framebuffer_alloc", "gs_framebuffer_free", "gs_framebuffer_read",
     "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
     "gs_present_device", "gs_encode_png", "gs_look_at",
@@ -49,7 +49,8 @@ class GsOpts(ctypes.Structure):
                 ("out_format", ctypes.c_int32), ("t_min", ctypes.c_float),
                 ("ref_quirks", ctypes.c_int32), ("strip_index", ctypes.c_int32),
                 ("strip_count", ctypes.c_int32), ("timing", ctypes.c_int32),
-                ("chunk_fraction", ctypes.c_float)]
+                ("chunk_fraction", ctypes.c_float), ("tile_row_begin", ctypes.c_int32),
+                ("tile_row_end", ctypes.c_int32)]
 
 
 class GsStats(ctypes.Structure):
@@ -113,6 +114,8 @@ def lib():
         L.gs_opts_default.argtypes = [ctypes.POINTER(GsOpts)]
         L.gs_opts_default.restype = None
         L.gs_strip_rows.argtypes = [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)]
+        L.gs_balance_strips.argtypes = [I, I, P, P, P]
+        L.gs_ctx_strips.argtypes = [P, P, I, ctypes.POINTER(I)]
         L.gs_render.argtypes = [P, P, P, I, I, ctypes.POINTER(GsOpts), P]
         L.gs_render_device.argtypes = [P, P, P, I, I, ctypes.POINTER(GsOpts), P, U64, P]
         L.gs_framebuffer_alloc.argtypes = [P, U64, ctypes.POINTER(ctypes.c_void_p)]
@@ -291,13 +294,27 @@ def device_count():
 
 
 def make_opts(accum=GS_ACCUM_FP32, out_format=GS_OUT_RGBA_F32, t_min=1e-4, strip_index=0, strip_count=1,
-              timing=0, ref_quirks=0, chunk_fraction=0.0):
+              timing=0, ref_quirks=0, chunk_fraction=0.0, tile_rows=None):
+    """gs_opts; tile_rows = (begin, end): an explicit strip of tile rows [begin, end)."""
     o = GsOpts()
     lib().gs_opts_default(ctypes.byref(o))
     o.accum, o.out_format, o.t_min = accum, out_format, t_min
     o.strip_index, o.strip_count, o.timing, o.ref_quirks = strip_index, strip_count, timing, ref_quirks
     o.chunk_fraction = chunk_fraction
+    if tile_rows is not None:
+        o.tile_row_begin, o.tile_row_end = int(tile_rows[0]), int(tile_rows[1])
     return o
+
+
+def balance_strips(bounds, cost):
+    """gs_balance_strips: K-balanced tile-row boundaries from the current ones and the strips' costs."""
+    b = np.ascontiguousarray(bounds, np.int32)
+    c = np.ascontiguousarray(cost, np.float64)
+    G = b.size - 1
+    assert c.size == G
+    out = np.zeros(G + 1, np.int32)
+    _check(lib().gs_balance_strips(G, int(b[-1]), _ptr(b), _ptr(c), _ptr(out)))
+    return out
 
 
 # ------------------------------------------------------------------ context / scene / render
@@ -321,6 +338,14 @@ class Context:
         nd, g = ctypes.c_int(), ctypes.c_int()
         _check(lib().gs_ctx_info(self.handle, ctypes.byref(nd), ctypes.byref(g)))
         return nd.value, GATHER_KINDS[g.value]
+
+    def strips(self):
+        """A device group's strip boundaries (tile rows, G + 1 values; empty on one device)."""
+        n = ctypes.c_int()
+        _check(lib().gs_ctx_strips(self.handle, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, np.int32)
+        _check(lib().gs_ctx_strips(self.handle, _ptr(out), n.value, ctypes.byref(n)))
+        return out
 
     def close(self):
         # scenes first: the C side frees attached scenes with the context anyway, but the
@@ -386,7 +411,10 @@ class Scene:
 
     def render(self, uniforms, W, H, opts=None):
         o = opts if opts is not None else make_opts()
-        rows = H if o.strip_count <= 1 else strip_rows(H, o.strip_index, o.strip_count)[1]
+        if o.tile_row_end > 0:
+            rows = min(16 * o.tile_row_end, H) - 16 * o.tile_row_begin
+        else:
+            rows = H if o.strip_count <= 1 else strip_rows(H, o.strip_index, o.strip_count)[1]
         if o.out_format == GS_OUT_RGBA_F16:
             out = np.empty((rows, W, 4), np.float16)
         else:

@@ -88,6 +88,39 @@ class StripPipeline:
             torch.cuda.current_stream().wait_stream(self.side)
 
 
+def even_bounds(H, count):
+    """Tile-row boundaries (count + 1) of the even split (floor(g * TR / count))."""
+    tr = (H + TILE - 1) // TILE
+    return [g * tr // count for g in range(count + 1)]
+
+
+def balanced_bounds(bounds, local_cost, group=None, device=None):
+    """K-balanced strips across ranks (SURVEY §8e "later"): every rank contributes its strip's
+    cost (e.g. binned entries, gs_stats k_entries, plus a per-tile term), one small all-gather
+    gives every rank the same vector, and gs_balance_strips (deterministic host arithmetic) turns
+    it into the same new boundaries on every rank.  Returns the new boundaries (a list)."""
+    import torch
+    import torch.distributed as dist
+    import gsplat_amd as gs
+    world = dist.get_world_size(group)
+    mine = torch.tensor([float(local_cost)], dtype=torch.float64, device=device)
+    allc = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allc, mine, group=group)
+    cost = [float(c.item()) for c in allc]
+    return [int(b) for b in gs.balance_strips(bounds, cost)]
+
+
+def assemble_uneven(full, bounds, rows_cap, H):
+    """The image from an all-gather of padded uneven strips: rank g's buffer (rows_cap rows) holds
+    tile rows [bounds[g], bounds[g+1])."""
+    import torch
+    parts = []
+    for g in range(len(bounds) - 1):
+        rows = max(0, min(bounds[g + 1] * TILE, H) - bounds[g] * TILE)
+        parts.append(full[g * rows_cap:g * rows_cap + rows])
+    return torch.cat(parts, 0)
+
+
 def assemble(full, H):
     """Crop the gathered buffer to the H image rows."""
     return full[:H]
@@ -97,4 +130,5 @@ def padded_rows_total(H, count):
     return strip_geometry(H, 0, count)[1] * count
 
 
-__all__ = ["strip_geometry", "gather_strips", "StripPipeline", "assemble", "padded_rows_total"]
+__all__ = ["strip_geometry", "gather_strips", "StripPipeline", "assemble", "padded_rows_total", "even_bounds",
+           "balanced_bounds", "assemble_uneven"]

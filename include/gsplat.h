@@ -88,6 +88,12 @@ typedef struct gs_opts {
                              >= 1 = one chunk, (0,1) = fixed split at the depth 2^-t <=
                              chunk_fraction of the way from the last frame's nearest to its
                              farthest visible splat (tests/diagnostics) */
+    /* (ABI 3) an explicit strip: with tile_row_end > 0, render only tile rows [tile_row_begin,
+       tile_row_end) of the image (16-px rows, 0 <= begin < end <= ceil(H/16); strip_count must be
+       1; not on a device group, which chooses its own strips).  The output holds image rows
+       [16*tile_row_begin, min(16*tile_row_end, H)), no padding.  K-balanced strips: gs_balance_strips. */
+    int32_t tile_row_begin;
+    int32_t tile_row_end;
 } gs_opts;
 
 typedef struct gs_stats {
@@ -130,15 +136,21 @@ int gs_device_count(int* out_count);
 /* GpuContext.create: rejects (GS_ERR_NO_DEVICE) when no HIP device exists.  devices = NULL with
  * ndev = 0: device 0.  ndev > 1 (<= 64) makes a device group: one context drives every listed
  * device from this thread.  A scene uploaded to it is replicated on each device; a frame is split
- * into ndev row strips (gs_strip_rows with strip_count = ndev), strip g rendered on devices[g], and
- * the strips are gathered with ONE in-place RCCL all-gather over the devices (ncclCommInitAll;
- * xGMI on MI355X) -- or, when the list repeats a device (tests on one GPU), with peer copies into
- * devices[0].  The image is delivered on devices[0] (gs_render_device's out_dev and hip_stream
+ * into ndev row strips, strip g rendered on devices[g], and the strips are gathered into
+ * devices[0] over RCCL (ncclCommInitAll; xGMI on MI355X) -- or, when the list repeats a device
+ * (tests on one GPU), with peer copies.  The image is delivered on devices[0] (gs_render_device's out_dev and hip_stream
  * belong to it).  gs_opts.strip_count must be 1 on a group. */
 int gs_ctx_create(const int* devices, int ndev, gs_ctx** out_ctx);
+/* (A group's strips are K-balanced (gs_balance_strips on the members' binned entries, every 8
+ * frames) and each member's strip goes to devices[0] only: RCCL send/receive pairs on per-member
+ * gather streams, double-buffered, so frame f + 1 renders while frame f's strips travel.) */
 typedef enum { GS_GATHER_NONE = 0, GS_GATHER_RCCL = 1, GS_GATHER_PEER_COPY = 2 } gs_gather_kind;
 /* Devices driven by the context and how a group gathers its strips (gs_gather_kind). */
 int gs_ctx_info(const gs_ctx* ctx, int* out_ndev, int* out_gather);
+/* A device group's current strip boundaries in tile rows (G + 1 values; strip g = [b[g], b[g+1]))
+ * for the last frame size; *out_n = G + 1 (0 before the first frame or on a single device).
+ * out_bounds may be NULL (count only). */
+int gs_ctx_strips(const gs_ctx* ctx, int* out_bounds, int capacity, int* out_n);
 /* Also frees every scene still attached to the context (do not free those scenes afterwards). */
 void gs_ctx_destroy(gs_ctx* ctx);
 
@@ -148,6 +160,15 @@ void gs_scene_free(gs_scene* scene);
 uint64_t gs_scene_count(const gs_scene* scene);
 
 void gs_opts_default(gs_opts* opts);
+
+/* K-balanced row strips: new tile-row boundaries out_bounds[0..G] (0 = first, TR =
+ * last) that equalise the strips' costs, given the current boundaries bounds[0..G] and each
+ * strip's measured cost under them (e.g. its binned entries, gs_stats k_entries, plus a per-tile
+ * term), the cost of a strip taken as spread evenly over its rows; each boundary moves half way
+ * to that model's cut (damped: fed back frame after frame it converges).  Every strip keeps >= 1 tile
+ * row when TR >= G.  Deterministic host arithmetic: ranks that feed it the same (all-gathered)
+ * costs get the same boundaries.  A device group rebalances itself every 8 frames this way. */
+int gs_balance_strips(int G, int tile_rows, const int* bounds, const double* cost, int* out_bounds);
 
 /* Rows of image covered by strip `strip_index` of `strip_count`: tile rows
  * [s*ceil(TR/G), min((s+1)*ceil(TR/G), TR)), TR = ceil(H/16).  *row0 = first image row,

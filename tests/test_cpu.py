@@ -303,3 +303,38 @@ def test_chunk1_grid_residency_rule():
         with pytest.raises(gs.GsError) as e:
             gs.chunk1_grid(None, occ, cus)
         assert e.value.code == gs.GS_ERR_UNSUPPORTED
+
+
+def test_balance_strips_equalises_cost():
+    """gs_balance_strips (K-balanced row strips): the cost of each current strip is
+    spread evenly over its rows and new boundaries equalise it."""
+    # two strips of 10 rows, the first three times as costly: the model's cut is 400/2 / 30 per
+    # row = 6.7, and the boundary moves half way there (damped)
+    assert list(gs.balance_strips([0, 10, 20], [300.0, 100.0])) == [0, 8, 20]
+    # uniform cost: even strips stay
+    assert list(gs.balance_strips([0, 17, 34, 51, 68], [5.0, 5.0, 5.0, 5.0])) == [0, 17, 34, 51, 68]
+    # zero cost, or more strips than rows: unchanged
+    assert list(gs.balance_strips([0, 3, 6], [0.0, 0.0])) == [0, 3, 6]
+    assert list(gs.balance_strips([0, 1, 1, 2], [1.0, 0.0, 5.0])) == [0, 1, 1, 2]
+    # every strip keeps a row even when one strip holds all the cost
+    b = gs.balance_strips([0, 2, 4, 6, 8], [0.0, 0.0, 0.0, 100.0])
+    assert (np.diff(b) >= 1).all() and b[0] == 0 and b[-1] == 8
+    for bad in (([0, 5, 4], [1.0, 1.0]), ([1, 5, 10], [1.0, 1.0]), ([0, 5, 10], [1.0, float("nan")])):
+        with pytest.raises(gs.GsError):
+            gs.balance_strips(*bad)
+
+
+def test_balance_strips_converges():
+    """Fed back the strips' true costs frame after frame (a dense band of rows, as a real scene's
+    horizon), the boundaries converge to within 15 % of equal cost for G = 2, 4, 8."""
+    TR = 68
+    rows = np.ones(TR)
+    rows[20:32] = 25.0  # a dense band
+    for G in (2, 4, 8):
+        b = np.array([g * TR // G for g in range(G + 1)], np.int32)
+        for _ in range(12):
+            cost = [rows[b[g]:b[g + 1]].sum() for g in range(G)]
+            b = gs.balance_strips(b, cost)
+        cost = np.array([rows[b[g]:b[g + 1]].sum() for g in range(G)])
+        # a single row can exceed the ideal share: the bound is the row granularity
+        assert cost.max() <= max(1.15 * cost.sum() / G, cost.sum() / G + rows.max()), (G, b, cost)

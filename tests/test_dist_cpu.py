@@ -51,8 +51,30 @@ def _worker(rank, world, port, W, H, q):
         f = pipe.submit()
         pipe.finish()
         ok_pipe = ok_pipe and np.array_equal(assemble(f, H).numpy(), img)
+    # K-balanced uneven strips: costs all-gathered, the same boundaries on every rank, the strips
+    # (explicit tile rows, padded to a common height for the all-gather) assemble to the image
+    from gsplat_amd.strips import assemble_uneven, balanced_bounds, even_bounds
+    bounds = even_bounds(H, world)
+    tr = (H + 15) // 16
+    ok_bal = True
+    for _ in range(4):
+        mine = float((rank + 1) ** 3 * (bounds[rank + 1] - bounds[rank]))  # rank-dependent density
+        nb = balanced_bounds(bounds, mine)
+        chk = [torch.zeros(world + 1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(chk, torch.tensor(nb, dtype=torch.int64))
+        ok_bal = ok_bal and all(c.tolist() == nb for c in chk) and nb[0] == 0 and nb[-1] == tr
+        bounds = nb
+    cap = 16 * max(b - a for a, b in zip(bounds[:-1], bounds[1:]))
+    s = torch.zeros((cap, W, 4), dtype=torch.float32)
+    r0, r1 = 16 * bounds[rank], min(16 * bounds[rank + 1], H)
+    s[:r1 - r0] = torch.from_numpy(img[r0:r1])
+    full = torch.zeros((world * cap, W, 4), dtype=torch.float32)
+    dist.all_gather_into_tensor(full, s)
+    ok_bal = ok_bal and np.array_equal(assemble_uneven(full, bounds, cap, H).numpy(), img)
+    if 1 < world < tr:
+        ok_bal = ok_bal and bounds != even_bounds(H, world)  # the costly last ranks' strips shrank
     if rank == 0:
-        q.put(bool(np.array_equal(out, img)) and ok_pipe)
+        q.put(bool(np.array_equal(out, img)) and ok_pipe and ok_bal)
     dist.barrier()
     dist.destroy_process_group()
 

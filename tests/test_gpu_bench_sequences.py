@@ -81,9 +81,10 @@ def test_bench_static_sequence(gpu_ctx, bench_scene):
     for b in bufs:
         b.free()
     assert st["frames_rendered"] == 15
-    # the controller's steady state: a depth split on (nearly) every frame, no tile left for chunk 1
-    assert st["frames_chunked"] >= 10, st
-    assert st["frames_unsat"] == 0 and st["tiles_unsaturated"] == 0, st
+    # the controller's steady state: a depth split on every frame (the first ones seeded: no
+    # history yet), and once the statistics arrive no tile is left for chunk 1
+    assert st["frames_chunked"] >= 14 and st["frames_seeded"] >= 1, st
+    assert st["frames_unsat"] <= 3 and st["tiles_unsaturated"] == 0, st
     one = _one_chunk(sc, u, W, H)
     # chunk 0's splats (last frame) over the exact visible count of the one-chunk frame (the
     # chunked frame's own n_vis skips partitions wholly past the split), as bench.py reports it

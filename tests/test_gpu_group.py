@@ -106,3 +106,70 @@ def test_chunk1_grid_is_resident(gpu_ctx):
     grid, occ = gs.chunk1_grid(gpu_ctx)
     assert occ >= 1 and 1 <= grid <= 64
     assert grid == gs.chunk1_grid(None, occ, 256)[0] or grid <= occ * 256
+
+
+def test_explicit_tile_rows_match_full(scene_data, single_images):
+    """gs_opts.tile_row_begin/end (explicit, uneven strips): the strips laid end to end are the
+    full frame bit for bit, f32 and f16 output."""
+    W, H, n, aos, u = scene_data
+    TR = (H + 15) // 16
+    cuts = [0, 3, 4, 21, TR]
+    with gs.Context(0) as ctx:
+        sc = gs.Scene(ctx, aos, n, 16)
+        parts = [sc.render(u, W, H, gs.make_opts(tile_rows=(a, b))) for a, b in zip(cuts[:-1], cuts[1:])]
+        assert [p.shape[0] for p in parts] == [min(16 * b, H) - 16 * a for a, b in zip(cuts[:-1], cuts[1:])]
+        assert np.array_equal(np.concatenate(parts, axis=0), single_images[0])
+        o16 = dict(out_format=gs.GS_OUT_RGBA_F16, accum=gs.GS_ACCUM_FP16_TARGET)
+        parts = [sc.render(u, W, H, gs.make_opts(tile_rows=(a, b), **o16)) for a, b in zip(cuts[:-1], cuts[1:])]
+        assert np.array_equal(np.concatenate(parts, axis=0).view(np.uint16), single_images[1].view(np.uint16))
+        for bad in ((0, TR + 1), (5, 5), (-1, 3)):
+            with pytest.raises(gs.GsError) as e:
+                sc.render(u, W, H, gs.make_opts(tile_rows=bad))
+            assert e.value.code == gs.GS_ERR_INVALID
+        with pytest.raises(gs.GsError):
+            sc.render(u, W, H, gs.make_opts(tile_rows=(0, 4), strip_index=0, strip_count=2))
+
+
+def _top_heavy_scene(n, seed, W, H):
+    """The synthetic scene with most Gaussians pulled into the top quarter of the view: the
+    strips' costs differ several-fold."""
+    a = gs.synth_aos(n, seed, W, H).reshape(n, 80)
+    rng = np.random.default_rng(seed)
+    pick = rng.random(n) < 0.75
+    d = -a[pick, 2]
+    a[pick, 1] = d * np.tan(np.radians(30.0)) * rng.uniform(0.5, 1.0, pick.sum()).astype(np.float32)
+    return a.reshape(-1)
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_group_k_balanced_strips(G):
+    """A device group on a top-heavy scene: after a few rebalances (every 8 frames) the strip
+    boundaries have moved off the even split toward the dense rows, and every frame -- before,
+    during and after the moves -- equals the single-device frame bit for bit."""
+    W, H, n = 640, 480, 150_000
+    aos = _top_heavy_scene(n, 7, W, H)
+    u = gs.bench_uniforms(W, H)
+    with gs.Context(0) as ctx:
+        ref = gs.Scene(ctx, aos, n, 16).render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16))
+    with gs.Context([0] * G) as gc:
+        sc = gs.Scene(gc, aos, n, 16)
+        o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16)
+        bufs = [gs.DeviceBuffer(H * W * 8) for _ in range(6)]
+        bounds = []
+        for rnd in range(6):  # 6 x 6 frames in flight, waiting between rounds (statistics arrive)
+            for b in bufs:
+                sc.render_device(u, W, H, b.ptr.value, b.nbytes, None, o)
+            gc.sync()
+            bounds.append(gc.strips())
+            for b in bufs:
+                got = np.empty((H, W, 4), np.float16)
+                b.to_host(got)
+                assert np.array_equal(got.view(np.uint16), ref.view(np.uint16)), (rnd, bounds[-1])
+        for b in bufs:
+            b.free()
+        TR = (H + 15) // 16
+        even = [g * TR // G for g in range(G + 1)]
+        assert list(bounds[0]) == even or bounds[0][1] < even[1]
+        assert bounds[-1][1] < even[1], bounds  # the first strip shrank toward the dense top rows
+        img = sc.render(u, W, H, o)  # the synchronous path on moved strips
+        assert np.array_equal(img.view(np.uint16), ref.view(np.uint16))
