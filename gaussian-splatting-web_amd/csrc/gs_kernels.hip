@@ -1685,8 +1685,9 @@ __device__ __forceinline__ uint32_t bin_slot(const BinParams& p, const UnitList&
     return p.chunk ? slot_c1(part, q) : slot_c0(part, q);
 }
 
-// Entries of one splat (composite slot g) in tiles [t_lo, t_hi): f(tile) per entry.  Rows whose
-// column range is wide are left to `wide` (returns false: not handled) when it accepts them.
+// Entries of one splat (composite slot g) in tiles [t_lo, t_hi): f(tile) per entry.  (Starting
+// each lane's walk at a lane-dependent row and column, so that neighbouring splats' LDS counter
+// atomics stop colliding, measured binning 72 -> 78 us: the collisions are cheaper than the walk.)
 template <class F>
 __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect& tr, const Ellipse& e,
                                               uint32_t t_lo, uint32_t t_hi, F&& f) {
@@ -2429,35 +2430,50 @@ __device__ unsigned long long g_comp_time[16384][3];  // per tile: start | n << 
 #endif
 constexpr int kQuarterTiles = GS_QUARTER_TILES;  // at most this many tiles: k_composite_q
 typedef float f2 __attribute__((ext_vector_type(2)));
+#ifndef GS_COMP_WAVES
+#define GS_COMP_WAVES 5
+#endif
 
+// Lanes and lists.  Wave h owns the 8-wide column half h of the tile; its lanes 0-31 hold the
+// top 8x8 quarter (rows 0-7) and lanes 32-63 the bottom one, two vertically adjacent pixels per
+// lane, blended as a packed float2.  Each quarter has its own list (the splats whose ellipse
+// reaches the quarter: its columns within the quarter's 8 rows), and the two lists are walked in
+// lockstep: at step k lanes 0-31 blend top[k] and lanes 32-63 bottom[k] (a null record past a
+// list's end).  A ds_read_b128 serves lanes {0-31} and {32-63} in separate lane groups, so two
+// distinct addresses per wave cost what one broadcast address does: a step costs what a step over
+// one half-tile list did, and a splat that reaches only one quarter no longer costs a whole step
+// of the wave (max(|top|, |bottom|) steps instead of |top u bottom|).
 template <bool FP16_TARGET>
 __device__ __forceinline__ void composite_tile(const CompositeParams& p, const int tile) {
     // staged record per batch entry: [0] c0u, c0v, a, b  [1] c, d, log2(op), slot (bits)
-    // [2] r, g, b, -   with u = a lx + b ly + c0u, v = c lx + d ly + c0v in tile-local pixels
-    __shared__ float4 sR[2][kCompBatch][3];
-    __shared__ uint16_t sL[2][2][kCompBatch];  // per half: LDS byte offsets of the staged records in sR
-                                               // (no multiply when a wave walks its list), segment =
-                                               // producing wave
-    __shared__ uint32_t sN[2][2][2];           // per half, per producing wave: list length
-    __shared__ uint32_t s_sat;                 // depth key of the splat that saturated the last wave
+    // [2] r, g, b, -   with u = a lx + b ly + c0u, v = c lx + d ly + c0v in tile-local pixels;
+    // entry kCompBatch of buffer 1 is the null record (log2 op = -inf: alpha 0, nothing blended)
+    __shared__ float4 sR[2][kCompBatch + 1][3];
+    __shared__ uint16_t sL[2][2][2][kCompBatch];  // per half, per quarter (top/bottom): LDS byte
+                                                  // offsets of the staged records in sR (segment =
+                                                  // producing wave, tail filled with the null record)
+    __shared__ uint32_t sN[2][2][2][2];           // per half, quarter, producing wave: list length
+    __shared__ uint32_t s_sat;                    // depth key of the splat that saturated the last wave
     const int tid = threadIdx.x;
     if (p.mode == kCompSecond && p.done[tile]) return;
 #ifdef GS_COMP_DIAG
     const unsigned long long t_begin = wall_clock64();
 #endif
     const int h = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int qr = lane >> 5, m = lane & 31;  // the lane's quarter (0 top, 1 bottom), position in it
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
     const int tx0 = tx * kTile, ty0 = ty * kTile;
-    const int px = tx0 + h * 8 + (lane & 7), py = ty0 + (lane >> 3);  // pixels (px, py), (px, py + 8)
-    const bool in0 = px < p.W && py < p.H, in1 = px < p.W && py + 8 < p.H;
+    const int px = tx0 + h * 8 + (m & 7), py = ty0 + qr * 8 + 2 * (m >> 3);  // pixels (px, py), (px, py + 1)
+    const bool in0 = px < p.W && py < p.H, in1 = px < p.W && py + 1 < p.H;
     const float lx = (float)(px - tx0) + 0.5f;  // tile-local pixel centres
-    const f2 ly = {(float)(py - ty0) + 0.5f, (float)(py - ty0) + 8.5f};
+    const f2 ly = {(float)(py - ty0) + 0.5f, (float)(py - ty0) + 1.5f};
     const uint2 range = p.ranges[tile];
     const float4* __restrict__ rec = p.rec;
     const uint32_t* __restrict__ tvals = p.tvals;
     const float L = 2.0f * kSqrtLog2e, amin = 1.0f / 255.0f, t_min = p.t_min;
+    constexpr uint32_t kNullOff = (uint32_t)((kCompBatch + 1 + kCompBatch) * 3 * 16);  // sR[1][kCompBatch]
     // parked-state index of the lane's pixels (a function, not a value held across the blend loop)
-    auto pix_of = [&](int r) -> uint64_t { return (uint64_t)(py + 8 * r) * p.W + px; };
+    auto pix_of = [&](int r) -> uint64_t { return (uint64_t)(py + r) * p.W + px; };
     f2 cr = {0.0f, 0.0f}, cg = {0.0f, 0.0f}, cb = {0.0f, 0.0f};
     f2 T = {1.0f, 1.0f};   // FP32: transmittance
     f2 ca = {0.0f, 0.0f};  // FP16_TARGET: dst.a
@@ -2476,13 +2492,17 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
             if (FP16_TARGET) ca.y = st.w; else T.y = st.w;
         }
     }
+    if (!FP16_TARGET) {  // the pixel test reads liveness from T: pixels off the image never blend
+        if (!in0) T.x = -1.0f;
+        if (!in1) T.y = -1.0f;
+    }
     bool live0 = in0 && (FP16_TARGET ? ca.x < 1.0f : T.x >= t_min);
     bool live1 = in1 && (FP16_TARGET ? ca.y < 1.0f : T.y >= t_min);
     bool wave_live = __any(live0 || live1);
 
     const uint32_t n = range.y - range.x;
     const uint32_t nb = (n + kCompBatch - 1) / kCompBatch;
-    float4 ga, gb, gc;
+    float4 ga, gb;  // the next batch's records in flight: geometry only (colour at park time)
     uint32_t gs_ = 0;
     bool gv = false;
     // the batch's slot ids are loaded one batch ahead of its records, so the record loads of batch
@@ -2500,12 +2520,12 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
             const float4* r = rec + 3 * (uint64_t)gs_;
             ga = r[0];
             gb = r[1];
-            gc = r[2];
         }
         if (batch + 1 < nb) load_slots(batch + 1);
     };
     auto park = [&](int buf) {
         // offsets of the axes' linear forms at the tile origin (explicit roundings, see blend)
+        const float4 gc = gv ? rec[3 * (uint64_t)gs_ + 2] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float cxr = ga.x - (float)tx0, cyr = ga.y - (float)ty0;
         const float c0u = -__builtin_fmaf(cxr, ga.z, cyr * ga.w);
         const float c0v = -__builtin_fmaf(cxr, gb.x, cyr * gb.y);
@@ -2515,17 +2535,25 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         sR[buf][tid][0] = make_float4(ga.w, ga.z, gb.y, gb.x);
         sR[buf][tid][1] = make_float4(gc.x, c0u, gc.y, c0v);
         sR[buf][tid][2] = make_float4(gc.z, gb.z, __uint_as_float(gs_), gc.w);
-        // the splat's pixel columns within this tile's rows (ellipse; the binning's margins)
-        uint32_t ul = 0u, uh = 0u;
-        const bool cols = gv && ellipse_cols(ellipse_of(ga, gb), (uint32_t)(ty0 >> 4), ul, uh);
-        const int x0 = (int)ul, x1 = (int)uh;
+        // the splat's pixel columns within each quarter's 8 rows (ellipse; the binning's margins),
+        // against both column halves: 4 lists, each compacted per producing wave by a ballot; the
+        // slots past a list's end hold the null record
+        const Ellipse el = ellipse_of(ga, gb);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int qx = tx0 + q * 8;
-            const bool hit = cols && x0 <= qx + 7 && x1 >= qx;
-            const uint64_t b = __ballot(hit);
-            if (hit) sL[buf][q][h * 64 + __popcll(b & lanemask_lt())] = (uint16_t)(((buf * kCompBatch + tid) * 3) * 16);
-            if (lane == 0) sN[buf][q][h] = (uint32_t)__popcll(b);
+        for (int hy = 0; hy < 2; ++hy) {
+            uint32_t ul = 0u, uh = 0u;
+            const bool cols = gv && ellipse_cols_band(el, (uint32_t)(ty0 + 8 * hy), (uint32_t)(ty0 + 8 * hy + 7), ul, uh);
+#pragma unroll
+            for (int hx = 0; hx < 2; ++hx) {
+                const int qx = tx0 + hx * 8;
+                const bool hit = cols && (int)ul <= qx + 7 && (int)uh >= qx;
+                const uint64_t b = __ballot(hit);
+                const uint32_t cnt = (uint32_t)__popcll(b);
+                uint16_t* Lq = &sL[buf][hx][hy][h * 64];
+                if (hit) Lq[__popcll(b & lanemask_lt())] = (uint16_t)(((buf * (kCompBatch + 1) + tid) * 3) * 16);
+                if ((uint32_t)lane >= cnt) Lq[lane] = (uint16_t)kNullOff;
+                if (lane == 0) sN[buf][hx][hy][h] = cnt;
+            }
         }
     };
     const char* const sRb = (const char*)&sR[0][0][0];
@@ -2543,17 +2571,25 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         const f2 qd = __builtin_elementwise_fma(u, u, v * v);
         const f2 e = (f2)l2op - qd;
         const float a0 = __builtin_amdgcn_exp2f(e.x), a1 = __builtin_amdgcn_exp2f(e.y);
-        const bool hit0 = live0 && fmaxf(fabsf(u.x), fabsf(v.x)) <= L && a0 >= amin;
-        const bool hit1 = live1 && fmaxf(fabsf(u.y), fabsf(v.y)) <= L && a1 >= amin;
+        // FP16_TARGET: lane masks (live from dst.a).  FP32: one sign per pixel,
+        // z = min(L - max(|u|,|v|), a - amin, T - t_min) >= 0 — each difference is exact in sign, so
+        // this is the box, alpha and liveness test bit for bit (pixels off the image hold T = -1) —
+        // and the accepted alpha is selected by z's sign bit with a bitfield insert, not through
+        // lane masks combined on the scalar unit (whose VCC round trips cost wait states)
+        const float z0 = fminf(fminf(L - fmaxf(fabsf(u.x), fabsf(v.x)), a0 - amin), T.x - t_min);
+        const float z1 = fminf(fminf(L - fmaxf(fabsf(u.y), fabsf(v.y)), a1 - amin), T.y - t_min);
+        const bool hit0 = FP16_TARGET ? live0 && fmaxf(fabsf(u.x), fabsf(v.x)) <= L && a0 >= amin : z0 >= 0.0f;
+        const bool hit1 = FP16_TARGET ? live1 && fmaxf(fabsf(u.y), fabsf(v.y)) <= L && a1 >= amin : z1 >= 0.0f;
 #ifdef GS_COMP_STATS
         {
             const uint64_t b0 = __ballot(hit0), b1 = __ballot(hit1);
             dg[0] += 1;
             dg[1] += __popcll(__ballot(live0)) + __popcll(__ballot(live1));
             dg[2] += __popcll(b0) + __popcll(b1);
-            dg[3] += (b0 | b1) == 0;
-            dg[4] += b0 != 0 && b1 == 0;
-            dg[5] += b0 == 0 && b1 != 0;
+            const uint64_t hb = b0 | b1;  // lanes 0-31: top quarter, 32-63: bottom quarter
+            dg[3] += hb == 0;
+            dg[4] += (hb & 0xffffffffull) != 0 && (hb >> 32) == 0;
+            dg[5] += (hb & 0xffffffffull) == 0 && (hb >> 32) != 0;
             const float r = e.x > e.y ? e.x : e.y;  // best of the pair, ignoring the quad box
             dg[6] += __popcll(__ballot(r >= -7.99f));
         }
@@ -2586,14 +2622,15 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
             cg = __builtin_elementwise_fma((f2)kg, s2, cg);
             cb = __builtin_elementwise_fma((f2)kb, s2, cb);
             T = T - s2;
-            live0 = live0 && T.x >= t_min;
-            live1 = live1 && T.y >= t_min;
+            live0 = T.x >= t_min;  // (pixels off the image: T = -1)
+            live1 = T.y >= t_min;
         }
     };
 #ifdef GS_COMP_DIAG
     if (tid == 0) dg[7] = n;
 #endif
     if (tid == 0) s_sat = 0;
+    if (tid < 3) sR[1][kCompBatch][tid] = make_float4(0.0f, tid == 2 ? -INFINITY : 0.0f, 0.0f, 0.0f);
     if (nb > 0) {
         load_slots(0);
         gather(0);
@@ -2605,10 +2642,12 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         if (b + 1 < nb) gather(b + 1);  // in flight while this batch is blended
         if (wave_live) {
             for (int seg = 0; seg < 2 && wave_live; ++seg) {
-                const int cnt = (int)sN[cur][h][seg];
-                const uint16_t* list = &sL[cur][h][seg * 64];
+                // both quarters' lists of this producing wave, in lockstep (the shorter one's tail
+                // is the null record)
+                const int cnt = (int)max(sN[cur][h][0][seg], sN[cur][h][1][seg]);
+                const uint16_t* list = &sL[cur][h][qr][seg * 64];  // this lane's quarter
                 int k = 0;
-                for (; k + 3 < cnt; k += 4) {  // saturation checked every 4 splats
+                for (; k + 3 < cnt; k += 4) {  // saturation checked every 4 steps
                     const uint32_t o3 = list[k + 3];
                     blend(list[k]);
                     blend(list[k + 1]);
@@ -2616,7 +2655,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                     blend(o3);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + o3 + 44));
+                        if (m == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + o3 + 44));
                         break;
                     }
                 }
@@ -2625,7 +2664,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                     blend(ok);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (lane == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + ok + 44));
+                        if (m == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + ok + 44));
                     }
                 }
             }
@@ -2670,7 +2709,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         if (tid == 0) p.done[tile] = 1;
     }
     if (!FP16_TARGET) ca = (f2)1.0f - T;
-    const uint64_t o0 = (uint64_t)(py - p.row0) * p.W + px, o1 = o0 + 8 * (uint64_t)p.W;
+    const uint64_t o0 = (uint64_t)(py - p.row0) * p.W + px, o1 = o0 + (uint64_t)p.W;
     if (p.out_f16) {
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         if (in0) ((h4*)p.out)[o0] = h4{(_Float16)cr.x, (_Float16)cg.x, (_Float16)cb.x, (_Float16)ca.x};
@@ -2689,7 +2728,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 // resident grid with per-band ticket counters (278 us), an equal static share per workgroup
 // (285 us) and one ticket counter for all bands (352 us) were all slower than this (230 us).
 template <bool FP16_TARGET>
-__global__ __launch_bounds__(128, 5) void k_composite(CompositeParams p) {
+__global__ __launch_bounds__(128, GS_COMP_WAVES) void k_composite(CompositeParams p) {
     const int per = (p.n_tiles + 7) >> 3;
     const int j = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // XCD band, position
     if (j < p.n_tiles) composite_tile<FP16_TARGET>(p, p.order ? (int)p.order[j] : j);
