@@ -1555,15 +1555,16 @@ __device__ __forceinline__ Ellipse ellipse_of(const float4 q0, const float4 q1) 
 
 // Pixel columns [pl, ph] of a band of pixel rows (a tile row: 16 ty .. 16 ty + 15) holding a
 // pixel centre of the ellipse, inside the box; false when there is none.
-__device__ __forceinline__ bool ellipse_cols_band(const Ellipse& e, uint32_t y0, uint32_t y1, uint32_t& pl_,
-                                                  uint32_t& ph_) {  // pixel rows y0 .. y1
+// dy0 / dy1: the band's first and last pixel-row centres minus the ellipse centre's y.
+__device__ __forceinline__ bool ellipse_cols_dy(const Ellipse& e, float dy0, float dy1, uint32_t& pl_,
+                                                uint32_t& ph_) {
     if (!e.ok) {
         pl_ = e.px0;
         ph_ = e.px1;
         return true;
     }
-    const float lo = fmaxf((float)y0 + 0.5f - e.cy, -e.hy);
-    const float hi = fminf((float)y1 + 0.5f - e.cy, e.hy);
+    const float lo = fmaxf(dy0, -e.hy);
+    const float hi = fminf(dy1, e.hy);
     if (!(lo <= hi)) return false;
     const float d1 = fminf(fmaxf(e.dys, lo), hi), d0 = fminf(fmaxf(-e.dys, lo), hi);
     const float g1 = fsqrt(fmaxf(e.m00 * e.l - e.det * d1 * d1, 0.0f));
@@ -1581,6 +1582,11 @@ __device__ __forceinline__ bool ellipse_cols_band(const Ellipse& e, uint32_t y0,
     pl_ = (uint32_t)pl;
     ph_ = (uint32_t)ph;
     return true;
+}
+
+__device__ __forceinline__ bool ellipse_cols_band(const Ellipse& e, uint32_t y0, uint32_t y1, uint32_t& pl_,
+                                                  uint32_t& ph_) {  // pixel rows y0 .. y1
+    return ellipse_cols_dy(e, (float)y0 + 0.5f - e.cy, (float)y1 + 0.5f - e.cy, pl_, ph_);
 }
 
 __device__ __forceinline__ bool ellipse_cols(const Ellipse& e, uint32_t ty, uint32_t& pl_, uint32_t& ph_) {
@@ -2472,8 +2478,21 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     const uint32_t* __restrict__ tvals = p.tvals;
     const float L = 2.0f * kSqrtLog2e, amin = 1.0f / 255.0f, t_min = p.t_min;
     constexpr uint32_t kNullOff = (uint32_t)((kCompBatch + 1 + kCompBatch) * 3 * 16);  // sR[1][kCompBatch]
-    // parked-state index of the lane's pixels (a function, not a value held across the blend loop)
+    // the lane's pixel coordinates, recomputed where needed after the blend loop from the lane id
+    // (mbcnt: not folded into the values computed before the loop, so none of them is held
+    // across it — held, they were spilled)
+    auto lane_pix = [&](int& x, int& y) {
+        const int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)), mm = l & 31;
+        x = tx0 + h * 8 + (mm & 7);
+        y = ty0 + (l >> 5) * 8 + 2 * (mm >> 3);
+    };
+    // parked-state index of the lane's pixels
     auto pix_of = [&](int r) -> uint64_t { return (uint64_t)(py + r) * p.W + px; };
+    auto pix_late = [&](int r) -> uint64_t {
+        int x, y;
+        lane_pix(x, y);
+        return (uint64_t)(y + r) * p.W + x;
+    };
     f2 cr = {0.0f, 0.0f}, cg = {0.0f, 0.0f}, cb = {0.0f, 0.0f};
     f2 T = {1.0f, 1.0f};   // FP32: transmittance
     f2 ca = {0.0f, 0.0f};  // FP16_TARGET: dst.a
@@ -2542,7 +2561,9 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 #pragma unroll
         for (int hy = 0; hy < 2; ++hy) {
             uint32_t ul = 0u, uh = 0u;
-            const bool cols = gv && ellipse_cols_band(el, (uint32_t)(ty0 + 8 * hy), (uint32_t)(ty0 + 8 * hy + 7), ul, uh);
+            // rows relative to the centre from the tile-relative centre (literal row offsets: no
+            // per-tile float constants held across the blend loop)
+            const bool cols = gv && ellipse_cols_dy(el, (0.5f + 8.0f * hy) - cyr, (7.5f + 8.0f * hy) - cyr, ul, uh);
 #pragma unroll
             for (int hx = 0; hx < 2; ++hx) {
                 const int qx = tx0 + hx * 8;
@@ -2698,8 +2719,8 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {  // park the pixels for chunk 1
-            if (in0) p.state[pix_of(0)] = make_float4(cr.x, cg.x, cb.x, FP16_TARGET ? ca.x : T.x);
-            if (in1) p.state[pix_of(1)] = make_float4(cr.y, cg.y, cb.y, FP16_TARGET ? ca.y : T.y);
+            if (in0) p.state[pix_late(0)] = make_float4(cr.x, cg.x, cb.x, FP16_TARGET ? ca.x : T.x);
+            if (in1) p.state[pix_late(1)] = make_float4(cr.y, cg.y, cb.y, FP16_TARGET ? ca.y : T.y);
             if (tid == 0) {
                 p.done[tile] = 0;
                 atomicAdd(&p.ctl->not_done, 1u);
@@ -2709,7 +2730,9 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         if (tid == 0) p.done[tile] = 1;
     }
     if (!FP16_TARGET) ca = (f2)1.0f - T;
-    const uint64_t o0 = (uint64_t)(py - p.row0) * p.W + px, o1 = o0 + (uint64_t)p.W;
+    int ox, oy;
+    lane_pix(ox, oy);
+    const uint64_t o0 = (uint64_t)(oy - p.row0) * p.W + ox, o1 = o0 + (uint64_t)p.W;
     if (p.out_f16) {
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         if (in0) ((h4*)p.out)[o0] = h4{(_Float16)cr.x, (_Float16)cg.x, (_Float16)cb.x, (_Float16)ca.x};
