@@ -2431,8 +2431,11 @@ constexpr int kCompBatch = 128;
 __device__ unsigned long long g_comp_cnt[16384][2][8];  // per tile and wave (plain stores: no atomics)
 __device__ unsigned long long g_comp_time[16384][3];  // per tile: start | n << 40, end | blends << 40, hw ids
 #endif
+// Chunk 0 of frames with at most this many tiles is composited by k_composite_q (4 waves per
+// tile).  0: never — with the lockstep quarter lists k_composite is faster for row strips too
+// (G = 8 strip 0.087 -> 0.082 ms); k_composite_q stays chunk 1's kernel (a few long lists).
 #ifndef GS_QUARTER_TILES
-#define GS_QUARTER_TILES 1536
+#define GS_QUARTER_TILES 0
 #endif
 constexpr int kQuarterTiles = GS_QUARTER_TILES;  // at most this many tiles: k_composite_q
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -3364,7 +3367,7 @@ void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
     if (p.n_tiles <= 0) return;
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);  // see k_composite's tile order
-    if (p.n_tiles <= kQuarterTiles) {  // few tiles (row strips): 4 waves per tile
+    if (p.n_tiles <= kQuarterTiles) {  // (see kQuarterTiles)
         if (accum_fp16)
             hipLaunchKernelGGL(k_composite_q<true>, dim3(grid), dim3(256), 0, s, p);
         else
