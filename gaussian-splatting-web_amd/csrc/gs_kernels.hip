@@ -2443,6 +2443,31 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define GS_COMP_WAVES 5
 #endif
 
+// Row bands per half-tile wave (lists walked in lockstep, see below): 2 (8x8 quarters, lane
+// halves) or 4 (8x4 bands, one per ds_read_b128 lane group).  Four measured slower at the bench
+// frame (composite 202 -> 214 us: four band tests per entry in the park step, and the larger list
+// area leaves 9 instead of 10 workgroups per CU), so two is the default.
+#ifndef GS_COMP_BANDS
+#define GS_COMP_BANDS 2
+#endif
+constexpr int kBands = GS_COMP_BANDS;
+constexpr int kBandRows = 16 / kBands;
+static_assert(kBands == 2 || kBands == 4, "row bands per wave");
+// Lane l of a wave -> (row band, index in the band).  Two bands: lanes 0-31 and 32-63.  Four: the
+// lane groups a ds_read_b128 serves in one LDS cycle each, {0-3,12-15,20-27}, {4-11,16-19,28-31}
+// and the same +32 (MI355X_MICROARCH.md, LDS): quads q = (l & 31) >> 2 in {1,2,4,7} form the second
+// group (mask 0x96); a quad's index base in its group is 4 (q >> 1).
+__device__ __forceinline__ void band_lane(int l, int& band, int& idx) {
+    if (kBands == 2) {
+        band = l >> 5;
+        idx = l & 31;
+    } else {
+        const int q = (l & 31) >> 2;
+        band = ((0x96 >> q) & 1) + 2 * (l >> 5);
+        idx = ((q >> 1) << 2) | (l & 3);
+    }
+}
+
 // Lanes and lists.  Wave h owns the 8-wide column half h of the tile; its lanes 0-31 hold the
 // top 8x8 quarter (rows 0-7) and lanes 32-63 the bottom one, two vertically adjacent pixels per
 // lane, blended as a packed float2.  Each quarter has its own list (the splats whose ellipse
@@ -2458,10 +2483,10 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     // [2] r, g, b, -   with u = a lx + b ly + c0u, v = c lx + d ly + c0v in tile-local pixels;
     // entry kCompBatch of buffer 1 is the null record (log2 op = -inf: alpha 0, nothing blended)
     __shared__ float4 sR[2][kCompBatch + 1][3];
-    __shared__ uint16_t sL[2][2][2][kCompBatch];  // per half, per quarter (top/bottom): LDS byte
-                                                  // offsets of the staged records in sR (segment =
-                                                  // producing wave, tail filled with the null record)
-    __shared__ uint32_t sN[2][2][2][2];           // per half, quarter, producing wave: list length
+    __shared__ uint16_t sL[2][2][kBands][kCompBatch];  // per half, per row band: LDS byte offsets
+                                                       // of the staged records in sR (segment =
+                                                       // producing wave, tail: the null record)
+    __shared__ uint32_t sN[2][2][kBands][2];           // per half, band, producing wave: list length
     __shared__ uint32_t s_sat;                    // depth key of the splat that saturated the last wave
     const int tid = threadIdx.x;
     if (p.mode == kCompSecond && p.done[tile]) return;
@@ -2469,10 +2494,11 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     const unsigned long long t_begin = wall_clock64();
 #endif
     const int h = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int qr = lane >> 5, m = lane & 31;  // the lane's quarter (0 top, 1 bottom), position in it
+    int qr, m;  // the lane's row band and its position in the band (band_lane)
+    band_lane(lane, qr, m);
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
     const int tx0 = tx * kTile, ty0 = ty * kTile;
-    const int px = tx0 + h * 8 + (m & 7), py = ty0 + qr * 8 + 2 * (m >> 3);  // pixels (px, py), (px, py + 1)
+    const int px = tx0 + h * 8 + (m & 7), py = ty0 + qr * kBandRows + 2 * (m >> 3);  // pixels (px, py), (px, py + 1)
     const bool in0 = px < p.W && py < p.H, in1 = px < p.W && py + 1 < p.H;
     const float lx = (float)(px - tx0) + 0.5f;  // tile-local pixel centres
     const f2 ly = {(float)(py - ty0) + 0.5f, (float)(py - ty0) + 1.5f};
@@ -2485,9 +2511,11 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     // (mbcnt: not folded into the values computed before the loop, so none of them is held
     // across it — held, they were spilled)
     auto lane_pix = [&](int& x, int& y) {
-        const int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)), mm = l & 31;
+        const int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        int bb, mm;
+        band_lane(l, bb, mm);
         x = tx0 + h * 8 + (mm & 7);
-        y = ty0 + (l >> 5) * 8 + 2 * (mm >> 3);
+        y = ty0 + bb * kBandRows + 2 * (mm >> 3);
     };
     // parked-state index of the lane's pixels
     auto pix_of = [&](int r) -> uint64_t { return (uint64_t)(py + r) * p.W + px; };
@@ -2562,11 +2590,12 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         // slots past a list's end hold the null record
         const Ellipse el = ellipse_of(ga, gb);
 #pragma unroll
-        for (int hy = 0; hy < 2; ++hy) {
+        for (int hy = 0; hy < kBands; ++hy) {
             uint32_t ul = 0u, uh = 0u;
             // rows relative to the centre from the tile-relative centre (literal row offsets: no
             // per-tile float constants held across the blend loop)
-            const bool cols = gv && ellipse_cols_dy(el, (0.5f + 8.0f * hy) - cyr, (7.5f + 8.0f * hy) - cyr, ul, uh);
+            const bool cols = gv && ellipse_cols_dy(el, (0.5f + (float)(kBandRows * hy)) - cyr,
+                                                    ((float)kBandRows - 0.5f + (float)(kBandRows * hy)) - cyr, ul, uh);
 #pragma unroll
             for (int hx = 0; hx < 2; ++hx) {
                 const int qx = tx0 + hx * 8;
@@ -2668,8 +2697,11 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
             for (int seg = 0; seg < 2 && wave_live; ++seg) {
                 // both quarters' lists of this producing wave, in lockstep (the shorter one's tail
                 // is the null record)
-                const int cnt = (int)max(sN[cur][h][0][seg], sN[cur][h][1][seg]);
-                const uint16_t* list = &sL[cur][h][qr][seg * 64];  // this lane's quarter
+                uint32_t cmax = sN[cur][h][0][seg];
+#pragma unroll
+                for (int bb = 1; bb < kBands; ++bb) cmax = max(cmax, sN[cur][h][bb][seg]);
+                const int cnt = (int)cmax;
+                const uint16_t* list = &sL[cur][h][qr][seg * 64];  // this lane's band
                 int k = 0;
                 for (; k + 3 < cnt; k += 4) {  // saturation checked every 4 steps
                     const uint32_t o3 = list[k + 3];
