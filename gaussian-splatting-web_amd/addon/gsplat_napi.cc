@@ -353,6 +353,97 @@ napi_value FbRead(napi_env env, napi_callback_info info) {
     return undefined(env);
 }
 
+// hostRegister(ctx, typedArray) / hostUnregister(ctx, typedArray): page-lock a host array so
+// readbacks into it are asynchronous DMA (gs_host_register); unregister before dropping it.
+napi_value HostRegister(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    get_args(env, info, 2, argv);
+    gs_ctx* c;
+    void* host;
+    size_t len;
+    if (!get_handle(env, argv[0], &c)) return throw_gs(env, GS_ERR_INVALID, "hostRegister: bad context");
+    if (!get_bytes(env, argv[1], &host, &len)) return throw_gs(env, GS_ERR_INVALID, "hostRegister: not a TypedArray");
+    const int rc = gs_host_register(c, host, len);
+    if (rc) return throw_gs(env, rc, "gs_host_register");
+    return undefined(env);
+}
+
+napi_value HostUnregister(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    get_args(env, info, 2, argv);
+    gs_ctx* c;
+    void* host;
+    size_t len;
+    if (!get_handle(env, argv[0], &c)) return throw_gs(env, GS_ERR_INVALID, "hostUnregister: bad context");
+    if (!get_bytes(env, argv[1], &host, &len)) return throw_gs(env, GS_ERR_INVALID, "hostUnregister: not a TypedArray");
+    const int rc = gs_host_unregister(c, host);
+    if (rc) return throw_gs(env, rc, "gs_host_unregister");
+    return undefined(env);
+}
+
+// readbackAsync(ctx, fb, typedArray) -> Promise: enqueues the copy of the array's byte length out
+// of the framebuffer behind the frames enqueued so far (gs_readback_start, on this thread, so in
+// call order with renderDevice) and resolves once it has landed (gs_readback_wait on the libuv
+// pool); the next frames render meanwhile.
+struct AsyncReadback {
+    gs_ctx* c = nullptr;
+    uint32_t ticket = 0;
+    int rc = 0;
+    std::string err;
+    napi_ref out_ref = nullptr;
+    napi_deferred deferred = nullptr;
+    napi_async_work work = nullptr;
+};
+
+void readback_execute(napi_env, void* data) {
+    auto* w = static_cast<AsyncReadback*>(data);
+    w->rc = gs_readback_wait(w->c, w->ticket);
+    if (w->rc) w->err = gs_last_error();
+}
+
+void readback_complete(napi_env env, napi_status, void* data) {
+    auto* w = static_cast<AsyncReadback*>(data);
+    if (w->rc == 0) {
+        napi_resolve_deferred(env, w->deferred, undefined(env));
+    } else {
+        std::string msg = "gs_readback_wait: " + w->err;
+        napi_value m, c, err;
+        napi_create_string_utf8(env, msg.c_str(), msg.size(), &m);
+        napi_create_int32(env, w->rc, &c);
+        napi_create_error(env, nullptr, m, &err);
+        napi_set_named_property(env, err, "code", c);
+        napi_reject_deferred(env, w->deferred, err);
+    }
+    if (w->out_ref) napi_delete_reference(env, w->out_ref);
+    napi_delete_async_work(env, w->work);
+    delete w;
+}
+
+napi_value ReadbackAsync(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    get_args(env, info, 3, argv);
+    gs_ctx* c;
+    void *dev, *host;
+    size_t len;
+    if (!get_handle(env, argv[0], &c) || !get_handle(env, argv[1], &dev))
+        return throw_gs(env, GS_ERR_INVALID, "readbackAsync: bad handle");
+    if (!get_bytes(env, argv[2], &host, &len)) return throw_gs(env, GS_ERR_INVALID, "readbackAsync: target must be a TypedArray");
+    auto* w = new AsyncReadback();
+    w->c = c;
+    const int rc = gs_readback_start(c, dev, host, len, &w->ticket);
+    if (rc) {
+        delete w;
+        return throw_gs(env, rc, "gs_readback_start");
+    }
+    napi_create_reference(env, argv[2], 1, &w->out_ref);  // the array stays alive until the copy lands
+    napi_value promise, name;
+    napi_create_promise(env, &w->deferred, &promise);
+    napi_create_string_utf8(env, "gs_readback", NAPI_AUTO_LENGTH, &name);
+    napi_create_async_work(env, nullptr, name, readback_execute, readback_complete, w, &w->work);
+    napi_queue_async_work(env, w->work);
+    return promise;
+}
+
 // renderDevice(ctx, scene, uniforms, W, H, opts, fb, fbBytes): enqueues the frame into the device
 // framebuffer and returns (frames in flight; errors of earlier frames are thrown here).
 napi_value RenderDevice(napi_env env, napi_callback_info info) {
@@ -657,6 +748,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"lookAt", LookAt}, {"perspective", Perspective}, {"cameraPosition", CameraPosition},
         {"cameraFromJSON", CameraFromJSON}, {"fbAlloc", FbAlloc}, {"fbFree", FbFree}, {"fbRead", FbRead},
         {"renderDevice", RenderDevice}, {"presentDevice", PresentDevice}, {"synthAos", SynthAos},
+        {"hostRegister", HostRegister}, {"hostUnregister", HostUnregister}, {"readbackAsync", ReadbackAsync},
         {"packUniforms", PackUniforms}, {"stripRows", StripRows}, {"plyParse", PlyParse}, {"encodePng", EncodePng},
     };
     for (const auto& f : fns) {

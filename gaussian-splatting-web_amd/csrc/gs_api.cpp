@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <utility>
 #include <cmath>
@@ -158,6 +159,13 @@ struct gs_ctx {
     // frame counts since gs_timings_reset (gs_stats::frames_*)
     uint32_t n_rendered = 0, n_chunked = 0, n_unsat = 0, n_seeded = 0;
     std::vector<std::pair<void*, uint64_t>> fbufs;  // gs_framebuffer_alloc'd buffers and their sizes
+    // asynchronous readback (gs_readback_start/wait): a copy stream and a ring of events
+    static constexpr int kReadbacks = 8;
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t rb_src[kReadbacks] = {};   // the context stream's frames so far (the copy's source)
+    hipEvent_t rb_done[kReadbacks] = {};  // the copy landed
+    std::atomic<uint32_t> rb_next{0};     // tickets issued
+    std::vector<void*> host_regs;         // gs_host_register'd buffers
     gs_scene* last_scene = nullptr;
     std::vector<gs_scene*> scenes;  // attached scenes; gs_ctx_destroy frees the survivors
     // A device group (gs_ctx_create with ndev > 1): one single-device member context per entry;
@@ -1321,6 +1329,8 @@ void gs_ctx_destroy(gs_ctx* c) {
             if (c->gev_entry) (void)hipEventDestroy(c->gev_entry);
             if (c->gev_gathered) (void)hipEventDestroy(c->gev_gathered);
         }
+        (void)hipSetDevice(c->members[0]->device);
+        for (void* h : c->host_regs) (void)hipHostUnregister(h);
         for (ncclComm_t m : c->comms)
             if (m) (void)ncclCommDestroy(m);
         for (gs_ctx* m : c->members) gs_ctx_destroy(m);
@@ -1330,6 +1340,15 @@ void gs_ctx_destroy(gs_ctx* c) {
     (void)hipSetDevice(c->device);
     while (!c->scenes.empty()) gs_scene_free(c->scenes.back());
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->copy_stream) {  // readbacks in flight land before their buffers are unpinned
+        (void)hipStreamSynchronize(c->copy_stream);
+        for (int k = 0; k < gs_ctx::kReadbacks; ++k) {
+            if (c->rb_src[k]) (void)hipEventDestroy(c->rb_src[k]);
+            if (c->rb_done[k]) (void)hipEventDestroy(c->rb_done[k]);
+        }
+        (void)hipStreamDestroy(c->copy_stream);
+    }
+    for (void* h : c->host_regs) (void)hipHostUnregister(h);
     for (auto& f : c->fe)
         for (auto& e : f.ev)
             if (e) (void)hipEventDestroy(e);
@@ -1704,27 +1723,92 @@ int gs_framebuffer_free(gs_ctx* c, void* dev) {
     });
 }
 
+// `bytes` from `dev` stay inside one of this context's gs_framebuffer_alloc buffers.
+static void check_fb_range(const gs_ctx* c, const void* dev, uint64_t bytes) {
+    const char* p = (const char*)dev;
+    for (const auto& e : c->fbufs) {
+        const char* b = (const char*)e.first;
+        if (p >= b && p < b + e.second) {
+            if (bytes > e.second - (uint64_t)(p - b)) throw GsError(GS_ERR_INVALID, "read past the end of the framebuffer");
+            return;
+        }
+    }
+    throw GsError(GS_ERR_INVALID, "not a framebuffer of this context (gs_framebuffer_alloc)");
+}
+
 int gs_framebuffer_read(gs_ctx* c, const void* dev, void* host, uint64_t bytes) {
     return guarded([&] {
         if (!c || !dev || !host) throw GsError(GS_ERR_INVALID, "null argument");
-        {  // a framebuffer of this context: the read stays inside its allocation
-            const char* p = (const char*)dev;
-            bool ok = false;
-            for (const auto& e : c->fbufs) {
-                const char* b = (const char*)e.first;
-                if (p >= b && p < b + e.second) {
-                    ok = bytes <= e.second - (uint64_t)(p - b);
-                    if (!ok) throw GsError(GS_ERR_INVALID, "read past the end of the framebuffer");
-                    break;
-                }
-            }
-            if (!ok) throw GsError(GS_ERR_INVALID, "not a framebuffer of this context (gs_framebuffer_alloc)");
-        }
+        check_fb_range(c, dev, bytes);
         const int rc = gs_sync(c);
         if (rc != GS_OK) throw GsError(rc, gs_last_error());
         gs_ctx* d = c->members.empty() ? c : c->members[0];
         HIPCHK(hipSetDevice(d->device));
         HIPCHK(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
+        return GS_OK;
+    });
+}
+
+int gs_host_register(gs_ctx* c, void* host, uint64_t bytes) {
+    return guarded([&] {
+        if (!c || !host || bytes == 0) throw GsError(GS_ERR_INVALID, "null ctx/host or zero bytes");
+        if (std::find(c->host_regs.begin(), c->host_regs.end(), host) != c->host_regs.end()) return GS_OK;
+        gs_ctx* d = c->members.empty() ? c : c->members[0];
+        HIPCHK(hipSetDevice(d->device));
+        HIPCHK(hipHostRegister(host, bytes, hipHostRegisterDefault));
+        c->host_regs.push_back(host);
+        return GS_OK;
+    });
+}
+
+int gs_host_unregister(gs_ctx* c, void* host) {
+    return guarded([&] {
+        if (!c || !host) throw GsError(GS_ERR_INVALID, "null argument");
+        auto it = std::find(c->host_regs.begin(), c->host_regs.end(), host);
+        if (it == c->host_regs.end()) throw GsError(GS_ERR_INVALID, "not registered (gs_host_register)");
+        gs_ctx* d = c->members.empty() ? c : c->members[0];
+        HIPCHK(hipSetDevice(d->device));
+        if (d->copy_stream) HIPCHK(hipStreamSynchronize(d->copy_stream));  // no copy still lands in it
+        HIPCHK(hipHostUnregister(host));
+        c->host_regs.erase(it);
+        return GS_OK;
+    });
+}
+
+int gs_readback_start(gs_ctx* c, const void* dev, void* host, uint64_t bytes, uint32_t* out_ticket) {
+    return guarded([&] {
+        if (!c || !dev || !host || !out_ticket) throw GsError(GS_ERR_INVALID, "null argument");
+        check_fb_range(c, dev, bytes);
+        gs_ctx* d = c->members.empty() ? c : c->members[0];
+        HIPCHK(hipSetDevice(d->device));
+        if (!d->copy_stream) {
+            HIPCHK(hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking));
+            for (int k = 0; k < gs_ctx::kReadbacks; ++k) {
+                HIPCHK(hipEventCreateWithFlags(&d->rb_src[k], hipEventDisableTiming));
+                HIPCHK(hipEventCreateWithFlags(&d->rb_done[k], hipEventDisableTiming));
+            }
+        }
+        const uint32_t t = d->rb_next.load();
+        const int k = (int)(t % gs_ctx::kReadbacks);
+        if (t >= (uint32_t)gs_ctx::kReadbacks) HIPCHK(hipEventSynchronize(d->rb_done[k]));  // ring full: the oldest first
+        HIPCHK(hipEventRecord(d->rb_src[k], d->stream));
+        HIPCHK(hipStreamWaitEvent(d->copy_stream, d->rb_src[k], 0));
+        HIPCHK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, d->copy_stream));
+        HIPCHK(hipEventRecord(d->rb_done[k], d->copy_stream));
+        d->rb_next.store(t + 1);
+        *out_ticket = t;
+        return GS_OK;
+    });
+}
+
+int gs_readback_wait(gs_ctx* c, uint32_t ticket) {
+    return guarded([&] {
+        if (!c) throw GsError(GS_ERR_INVALID, "null ctx");
+        gs_ctx* d = c->members.empty() ? c : c->members[0];
+        if (ticket >= d->rb_next.load()) throw GsError(GS_ERR_INVALID, "no such readback ticket");
+        HIPCHK(hipSetDevice(d->device));
+        // the slot may hold a later copy by now: it lands after this one (one stream, in order)
+        HIPCHK(hipEventSynchronize(d->rb_done[ticket % gs_ctx::kReadbacks]));
         return GS_OK;
     });
 }

@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "gs_abi_version", "gs_last_error", "gs_device_count", "gs_ctx_create", "gs_ctx_destroy", "gs_ctx_info",
     "gs_scene_upload", "gs_scene_free", "gs_scene_count", "gs_opts_default", "gs_strip_rows", "gs_balance_strips", "gs_ctx_strips",
     "gs_render", "gs_render_device", "gs_framebuffer_alloc", "gs_framebuffer_free", "gs_framebuffer_read",
+    "gs_host_register", "gs_host_unregister", "gs_readback_start", "gs_readback_wait",
     "gs_timings", "gs_timings_reset", "gs_sync", "gs_present",
     "gs_present_device", "gs_encode_png", "gs_look_at",
     "gs_perspective", "gs_camera_position", "gs_camera_from_json", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
@@ -121,6 +122,10 @@ def lib():
         L.gs_framebuffer_alloc.argtypes = [P, U64, ctypes.POINTER(ctypes.c_void_p)]
         L.gs_framebuffer_free.argtypes = [P, P]
         L.gs_framebuffer_read.argtypes = [P, P, P, U64]
+        L.gs_host_register.argtypes = [P, P, U64]
+        L.gs_host_unregister.argtypes = [P, P]
+        L.gs_readback_start.argtypes = [P, P, P, U64, ctypes.POINTER(ctypes.c_uint32)]
+        L.gs_readback_wait.argtypes = [P, ctypes.c_uint32]
         L.gs_timings.argtypes = [P, ctypes.POINTER(GsStats)]
         L.gs_timings_reset.argtypes = [P]
         L.gs_sync.argtypes = [P]

@@ -32,6 +32,9 @@ const now = () => Number(process.hrtime.bigint()) / 1e6;
 const FOV = 1.04719755;  // 60 degrees (src/camera.ts:4)
 
 const GS_ACCUM_FP32 = 0, GS_ACCUM_FP16_TARGET = 1, GS_OUT_RGBA_F32 = 0, GS_OUT_RGBA_F16 = 1;
+// host-readback frames in flight: the event loop's hand-off from the copy's waiting thread back
+// to the frame loop takes ~0.1 ms, so two in flight left the GPU idle between frames
+const kReadbackDepth = Number(process.env.GSPLAT_READBACK_DEPTH || 3);
 
 // ---------------------------------------------------------------------------- GpuContext
 class GpuContext {
@@ -185,6 +188,14 @@ class Renderer {
                                   options);
         this.deviceFramebuffer = null;
         this.frames = 0;
+        // host-readback frames in flight (see draw): kReadbackDepth device framebuffers, one more
+        // page-locked host array, frames delivered in order through one promise chain
+        this.devFbs = null;
+        this.hostFbs = null;
+        this.slot = 0;
+        this.inflight = 0;
+        this.waiting = null;
+        this.delivered = Promise.resolve();
         // the AoS record buffer is borrowed for this call only (copied into HBM as SoA)
         this.scene = addon().sceneUpload(context.device, gaussians.gaussiansBuffer, gaussians.numGaussians,
                                          gaussians.nShCoeffs);
@@ -196,10 +207,21 @@ class Renderer {
         if (this.destroyCallback === null) throw new Error('destroyImpl called without destroyCallback set!');
         if (this.deviceFramebuffer && this.context.device) addon().fbFree(this.context.device, this.deviceFramebuffer);
         this.deviceFramebuffer = null;
+        this.releaseReadback();
         if (this.scene && this.context.device) addon().sceneFree(this.scene);
         this.scene = null;
         this.context.destroy();
         this.destroyCallback();
+    }
+
+    // host-readback buffers: unpinned and freed (no readback in flight: see draw / animate)
+    releaseReadback() {
+        if (this.hostFbs && this.context.device)
+            for (const b of this.hostFbs) addon().hostUnregister(this.context.device, b);
+        if (this.devFbs && this.context.device)
+            for (const f of this.devFbs) addon().fbFree(this.context.device, f);
+        this.hostFbs = null;
+        this.devFbs = null;
     }
 
     // reallocate the W x H-dependent state (src/renderer.ts:293-299)
@@ -207,6 +229,7 @@ class Renderer {
         this.width = this.canvas.width;
         this.height = this.canvas.height;
         const px = this.width * this.height * 4;
+        this.releaseReadback();
         if (this.opts.deviceResident) {
             // the frame stays in HBM like the reference's framebuffer texture; readback() copies it
             if (this.deviceFramebuffer) addon().fbFree(this.context.device, this.deviceFramebuffer);
@@ -216,7 +239,16 @@ class Renderer {
             this.image = null;
             return;
         }
-        this.framebuffer = this.opts.outFormat === GS_OUT_RGBA_F16 ? new Uint16Array(px) : new Float32Array(px);
+        // host readback: like the reference's draw, a frame is submitted and the next animation
+        // frame requested without waiting for it; its copy to the host runs on a copy stream while
+        // the next frame renders (kReadbackDepth device framebuffers, one more page-locked host array)
+        const f16 = this.opts.outFormat === GS_OUT_RGBA_F16;
+        this.fbBytes = px * (f16 ? 2 : 4);
+        this.hostFbs = Array.from({length: kReadbackDepth + 1}, () => (f16 ? new Uint16Array(px) : new Float32Array(px)));
+        this.devFbs = Array.from({length: kReadbackDepth}, () => addon().fbAlloc(this.context.device, this.fbBytes));
+        for (const b of this.hostFbs) addon().hostRegister(this.context.device, b);
+        this.slot = 0;
+        this.framebuffer = this.hostFbs[0];
         this.image = this.canvas.present ? new Float32Array(px) : null;
     }
 
@@ -232,7 +264,13 @@ class Renderer {
 
     // render one frame (depth keys + sort + tile composite), then schedule nextFrameCallback
     draw(nextFrameCallback) {
-        if (this.canvas.width !== this.width || this.canvas.height !== this.height) this.resize();
+        if (this.canvas.width !== this.width || this.canvas.height !== this.height) {
+            if (this.inflight > 0) {  // resize once the frames in flight have landed
+                this.waiting = () => this.draw(nextFrameCallback);
+                return;
+            }
+            this.resize();
+        }
         if (this.opts.deviceResident) {
             // enqueue the frame (frames in flight, no readback) and go on: the reference's draw
             // submits to the GPU queue and returns the same way
@@ -248,21 +286,50 @@ class Renderer {
             raf(nextFrameCallback);
             return;
         }
-        addon().renderAsync(this.context.device, this.scene, this.uniforms, this.width, this.height, this.opts,
-                            this.framebuffer).then(() => {
-            this.frames++;
-            this.canvas.framebuffer = this.framebuffer;
-            if (this.image) {
-                addon().present(this.framebuffer, this.width, this.height, this.image);
-                this.canvas.image = this.image;
-            }
-            if (typeof this.canvas.onFrame === 'function') this.canvas.onFrame(this);
-            raf(nextFrameCallback);
-        }, (err) => {
+        // host readback, up to kReadbackDepth frames in flight: render into device framebuffer
+        // f % D, copy it out asynchronously into host array f % (D + 1), and request the next frame
+        // at once unless D are already in flight.  Frames are delivered (renderer.framebuffer,
+        // canvas.onFrame) in order, each when its copy has landed; the delivered frame's array is
+        // not written again before the next frame is delivered.
+        const D = kReadbackDepth;
+        const k = this.slot % D, h = this.slot % (D + 1);
+        this.slot = (this.slot + 1) % (D * (D + 1));
+        let copied;
+        try {
+            addon().renderDevice(this.context.device, this.scene, this.uniforms, this.width, this.height, this.opts,
+                                 this.devFbs[k], this.fbBytes);
+            copied = addon().readbackAsync(this.context.device, this.devFbs[k], this.hostFbs[h]);
+        } catch (err) {
             this.lastError = err;
             if (typeof this.canvas.onError === 'function') this.canvas.onError(err);
             raf(nextFrameCallback);
+            return;
+        }
+        const host = this.hostFbs[h];
+        this.inflight++;
+        const landed = () => {
+            this.inflight--;
+            const w = this.waiting;
+            this.waiting = null;
+            if (w) raf(w);
+        };
+        this.delivered = this.delivered.then(() => copied).then(() => {
+            this.frames++;
+            this.framebuffer = host;
+            this.canvas.framebuffer = host;
+            if (this.image) {
+                addon().present(host, this.width, this.height, this.image);
+                this.canvas.image = this.image;
+            }
+            if (typeof this.canvas.onFrame === 'function') this.canvas.onFrame(this);
+            landed();
+        }, (err) => {
+            this.lastError = err;
+            if (typeof this.canvas.onError === 'function') this.canvas.onError(err);
+            landed();
         });
+        if (this.inflight < kReadbackDepth) raf(nextFrameCallback);
+        else this.waiting = nextFrameCallback;
     }
 
     animate(forceDraw) {
@@ -273,6 +340,10 @@ class Renderer {
         if (this.fpsCounter.style) this.fpsCounter.style.display = 'block';
 
         if (this.destroyCallback !== null) {
+            if (this.inflight > 0) {  // the frames in flight land first (their buffers are freed)
+                this.waiting = () => this.animate();
+                return;
+            }
             this.destroyImpl();
             return;
         }

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3
+#define GS_ABI_VERSION 4
 
 typedef struct gs_ctx gs_ctx;
 typedef struct gs_scene gs_scene;
@@ -204,6 +204,24 @@ int gs_render_device(gs_ctx* ctx, gs_scene* scene, const void* uniforms160, int 
 int gs_framebuffer_alloc(gs_ctx* ctx, uint64_t bytes, void** out_dev);
 int gs_framebuffer_free(gs_ctx* ctx, void* dev);
 int gs_framebuffer_read(gs_ctx* ctx, const void* dev, void* host, uint64_t bytes);
+
+/* Asynchronous readback (ABI 4): the host side of the reference's frame loop, which submits a
+ * frame and requests the next animation frame without waiting for it (src/renderer.ts:301-330,
+ * :345-348), with the frame copied out to host memory.
+ * gs_host_register / gs_host_unregister: page-lock a caller's host buffer (hipHostRegister) so
+ * that copies into it run as DMA at the link's rate, asynchronously; unregister waits for the
+ * readbacks in flight.  A buffer must be unregistered before it is freed.
+ * gs_readback_start: enqueue a copy of `bytes` from a gs_framebuffer_alloc buffer (the same bounds
+ * as gs_framebuffer_read) to `host`, ordered after every frame enqueued so far on the context's
+ * own stream (gs_render_device with stream NULL), on a copy stream of its own, so the next frames
+ * render meanwhile; returns a ticket.  It does not wait: the framebuffer must not be rendered into
+ * again before the ticket's wait returns.
+ * gs_readback_wait: blocks until the ticket's copy (and every earlier one) has landed.  Safe to
+ * call from another thread than the one enqueuing frames. */
+int gs_host_register(gs_ctx* ctx, void* host, uint64_t bytes);
+int gs_host_unregister(gs_ctx* ctx, void* host);
+int gs_readback_start(gs_ctx* ctx, const void* dev, void* host, uint64_t bytes, uint32_t* out_ticket);
+int gs_readback_wait(gs_ctx* ctx, uint32_t ticket);
 
 int gs_timings(gs_ctx* ctx, gs_stats* out_stats);
 int gs_timings_reset(gs_ctx* ctx);

@@ -20,7 +20,8 @@ pytestmark = pytest.mark.skipif(not NODE or not os.path.exists(ADDON), reason="n
 EXPORTS = sorted(["abiVersion", "lastError", "deviceCount", "ctxCreate", "ctxDestroy", "sceneUpload", "sceneFree",
                   "render", "renderAsync", "timings", "timingsReset", "sync", "present", "lookAt", "perspective",
                   "cameraPosition", "cameraFromJSON", "fbAlloc", "fbFree", "fbRead", "renderDevice", "presentDevice",
-                  "synthAos", "packUniforms", "stripRows", "plyParse", "encodePng"])
+                  "synthAos", "packUniforms", "stripRows", "plyParse", "encodePng", "hostRegister",
+                  "hostUnregister", "readbackAsync"])
 
 
 def run_node(*args, timeout=120):
@@ -32,7 +33,7 @@ def run_node(*args, timeout=120):
 def test_node_host_cpu():
     out = run_node(os.path.join(ROOT, "tests", "node", "host_checks.js"), os.path.join(GOLDEN, "cameras.json"))
     assert out["exports"] == EXPORTS
-    assert out["abi"] == 3
+    assert out["abi"] == 4
     if out["deviceCount"] == 0:
         assert out["createRejected"] == "string" and out["requestRejected"] == "string"
     assert out["ctorThrows"] is True

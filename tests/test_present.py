@@ -163,3 +163,48 @@ def test_framebuffer_abi_roundtrip(gpu_ctx):
         gs.GS_ERR_INVALID
     other.free()
     assert L.gs_framebuffer_free(gpu_ctx.handle, dev) == gs.GS_OK
+
+
+@pytest.mark.gpu
+def test_async_readback(gpu_ctx):
+    """gs_host_register / gs_readback_start / gs_readback_wait: frames rendered alternately into two
+    framebuffers and copied out asynchronously (the Node Renderer's host-readback loop) equal the
+    synchronous host-output renders of the same views; bounds and tickets are checked."""
+    import ctypes
+    W, H, n = 256, 160, 30_000
+    aos = gs.synth_aos(n, 13, W, H)
+    views = [gs.orbit_uniforms(W, H, k) for k in range(6)]
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    L = gs.lib()
+    c = gpu_ctx.handle
+    nb = W * H * 16
+    devs = [ctypes.c_void_p(), ctypes.c_void_p()]
+    for d in devs:
+        assert L.gs_framebuffer_alloc(c, nb, ctypes.byref(d)) == gs.GS_OK
+    hosts = [np.zeros((H, W, 4), np.float32) for _ in range(3)]
+    for h in hosts:
+        assert L.gs_host_register(c, h.ctypes.data_as(ctypes.c_void_p), h.nbytes) == gs.GS_OK
+    tickets = []
+    for k, u in enumerate(views):
+        if k >= 2:  # framebuffer k % 2 is rendered again only after its last copy landed
+            assert L.gs_readback_wait(c, tickets[k - 2]) == gs.GS_OK
+        sc.render_device(u, W, H, devs[k % 2].value, nb)
+        t = ctypes.c_uint32()
+        assert L.gs_readback_start(c, devs[k % 2], hosts[k % 3].ctypes.data_as(ctypes.c_void_p), nb,
+                                   ctypes.byref(t)) == gs.GS_OK
+        tickets.append(t.value)
+    for k in (len(views) - 2, len(views) - 1):
+        assert L.gs_readback_wait(c, tickets[k]) == gs.GS_OK
+    ref = gs.Scene(gpu_ctx, aos, n, 16)
+    for k in range(len(views) - 3, len(views)):
+        assert np.array_equal(hosts[k % 3], ref.render(views[k], W, H)), k
+    # a copy past the framebuffer, an unknown ticket, an unregistered buffer are refused
+    assert L.gs_readback_start(c, devs[0], hosts[0].ctypes.data_as(ctypes.c_void_p), nb + 1,
+                               ctypes.byref(ctypes.c_uint32())) == gs.GS_ERR_INVALID
+    assert L.gs_readback_wait(c, 1_000_000) == gs.GS_ERR_INVALID
+    spare = np.zeros(16, np.float32)
+    assert L.gs_host_unregister(c, spare.ctypes.data_as(ctypes.c_void_p)) == gs.GS_ERR_INVALID
+    for h in hosts:
+        assert L.gs_host_unregister(c, h.ctypes.data_as(ctypes.c_void_p)) == gs.GS_OK
+    for d in devs:
+        assert L.gs_framebuffer_free(c, d) == gs.GS_OK

@@ -1,8 +1,8 @@
 'use strict';
 // Frame rate of the Node drop-in: the reference's frame loop (GpuContext.create -> new Renderer ->
 // animate/draw via the rAF shim) on the seeded synthetic scene at the bench camera, every frame
-// forced through the full path (camera marked dirty), measured in JS from the first frame's
-// callback to the last.  Two modes: deviceResident (frames stay in HBM, as the reference's
+// forced through the full path (the camera stays dirty, as a moving one: frames are requested back
+// to back), measured in JS from the fifth frame's callback to the last.  Two modes: deviceResident (frames stay in HBM, as the reference's
 // framebuffer texture; frames in flight) and host readback (renderAsync + a D2H copy per frame).
 // The device-resident mode's last frame is read back and compared with the host mode's.
 // Usage: node tools/node_fps.js <n> <seed> <W> <H> <frames>   -> one JSON line
@@ -12,7 +12,14 @@ const gs = require(path.join(__dirname, '..', 'gaussian-splatting-web_amd', 'js'
 async function run(gaussians, W, H, frames, options) {
     const a = gs.addon();
     const cam = gs.Camera.lookAt([0, 0, 0], [0, 0, -1], W, H);
+    // a camera that stays dirty until the measured frames are drawn (a moving camera, as under
+    // user input): frames are requested back to back, not each after the last one's callback
     const icam = new gs.HeadlessCamera(cam);
+    let drawn = 0;
+    icam.getCamera = function () {
+        if (++drawn >= frames + 5) this.dirty = false;
+        return this.camera;
+    };
     const context = await gs.Renderer.requestContext(gaussians, 0);
     const canvas = {width: W, height: H};
     let seen = 0, t0 = 0n, t1 = 0n;
@@ -21,8 +28,7 @@ async function run(gaussians, W, H, frames, options) {
         canvas.onFrame = (r) => {
             seen++;
             if (seen === 5) t0 = process.hrtime.bigint();  // 5 warm-up frames
-            if (seen < frames + 5) icam.setDirty();
-            else { t1 = process.hrtime.bigint(); resolve(r); }
+            if (seen >= frames + 5) { t1 = process.hrtime.bigint(); resolve(r); }
         };
     });
     const renderer = new gs.Renderer(canvas, icam, gaussians, context, null, options);
