@@ -758,19 +758,23 @@ __device__ __forceinline__ void c1_parts_body(const ProjParams& p, uint32_t blk,
     }
 }
 
-// Chunk 1, step 2: the listed partitions, one per workgroup iteration (waves take 64 consecutive
-// Gaussians).  From the cull plane, a Gaussian at or past thresh whose conservative box touches an
-// unsaturated tile is projected; the visible ones whose rect touches one get a chunk-1 slot
-// (slot_c1) with their record and colour.  The filter before project_core only skips Gaussians
-// the exact rect test after it would reject.
+// Chunk 1, step 2: the listed partitions' Gaussians, 64 consecutive ones per wave iteration, the
+// grid's waves striding over (listed partition, 64-Gaussian block) pairs (a workgroup per
+// partition walked its 16 blocks four at a time: a chain of dependent loads per block, 65 us for
+// ~1000 listed partitions under a moving camera).  From the cull plane, a Gaussian at or past
+// thresh whose conservative box touches an unsaturated tile is projected; the visible ones whose
+// rect touches one get a chunk-1 slot (slot_c1) with their record and colour.  The filter before
+// project_core only skips Gaussians the exact rect test after it would reject.
 __device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t lane = lane_id(), nl = p.ctl->c1_parts, T = frame_thresh(p);
-    for (uint32_t j = blk; j < nl; j += nblk) {
-        const uint32_t part = p.plist[j];
-        for (uint32_t r = threadIdx.x & ~63u; r < (uint32_t)kProjTile; r += blockDim.x) {
-            const uint32_t i0 = part * (uint32_t)kProjTile + r, i = i0 + lane;
+    constexpr uint32_t kBlocks = (uint32_t)kProjTile / 64u;
+    const uint32_t wpb = blockDim.x >> 6;
+    for (uint32_t v = blk * wpb + (threadIdx.x >> 6); v < nl * kBlocks; v += nblk * wpb) {
+        const uint32_t part = p.plist[v / kBlocks];
+        {
+            const uint32_t i0 = part * (uint32_t)kProjTile + (v % kBlocks) * 64u, i = i0 + lane;
             bool want = false;
             float vz, cx0, cy0, hb;
             if (i < p.n && cull_keep_box(p, p.cull[i], row_lo, row_hi, vz, cx0, cy0, hb) && sortable_key(vz) >= T) {
@@ -2818,6 +2822,9 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
     if (j >= p.n_tiles) return;
     const int tile = p.order ? (int)p.order[j] : j;
     if (p.mode == kCompSecond && p.done[tile]) return;
+#ifdef GS_C1_PRINT
+    if (tid == 0 && p.mode == kCompSecond) printf("C1T %d %u\n", tile, p.ranges[tile].y - p.ranges[tile].x);
+#endif
     const int qw = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
     const int tx0 = tx * kTile, ty0 = ty * kTile;
@@ -3125,6 +3132,10 @@ __global__ __launch_bounds__(256) void k_c1_records(ProjParams p) {
 }
 __global__ __launch_bounds__(64) void k_frame_end(Chunk1Params c) {
     __shared__ uint32_t lds[kStatShards * ((sizeof(StatShard) / 4) | 1u)];
+#ifdef GS_C1_PRINT  // diagnostics builds only: the chunk-1 workload of each frame
+    if (threadIdx.x == 0 && c.cp.ctl->not_done)
+        printf("C1F not_done %u c1_parts %u\n", c.cp.ctl->not_done, c.cp.ctl->c1_parts);
+#endif
     frame_end_body(c.cp.ctl, c.stats, c.host_ctl, c.host_seq, c.seq, lds);
 }
 

@@ -43,6 +43,11 @@ def main():
         print("blends with no hit %.3f  hits only rows 0-7 %.3f  only rows 8-15 %.3f" %
               (c[3] / c[0], c[4] / c[0], c[5] / c[0]))
         print("pixel evals inside the alpha disc (pair best) %.4g  list entries (tiles) %.4g" % (c[6], c[7]))
+        # the two waves of a tile: steps of each; a wave done early waits at the batch barriers
+        s = cn[:ntile, :, 0].astype(np.float64)
+        print("wave steps: sum %.4g  sum of per-tile max x2 %.4g (idle share %.3f)  tiles with one wave "
+              "at 0 steps %d" % (s.sum(), 2 * s.max(axis=1).sum(), 1 - s.sum() / max(1, 2 * s.max(axis=1).sum()),
+                                 int(((s[:, 0] == 0) ^ (s[:, 1] == 0)).sum())))
     # per-tile wall-clock spans of the last frame (100 MHz clock)
     tm = np.zeros((16384, 3), dtype=np.uint64)
     L.gs_diag_comp_times(tm.ctypes.data_as(ctypes.c_void_p), 16384)
