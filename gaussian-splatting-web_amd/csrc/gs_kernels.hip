@@ -911,28 +911,54 @@ __global__ __launch_bounds__(256) void k_seed_hist(ProjParams p) {
     const uint32_t nsr = (nrun + p.seed_stride - 1) / p.seed_stride;
     const float wgt = (float)p.seed_stride * 6.28318531f;
     constexpr uint32_t kRunsPerBlock = 256 / kSeedRun;
-    for (uint32_t sr = blockIdx.x * kRunsPerBlock + threadIdx.x / kSeedRun; sr < nsr; sr += gridDim.x * kRunsPerBlock) {
+    const uint32_t lane = lane_id(), lead = lane & ~(uint32_t)(kSeedRun - 1);
+    // (the loop runs whole waves: a sampled run is 16 lanes of one wave, reduced with shuffles)
+    for (uint32_t sr0 = blockIdx.x * kRunsPerBlock; sr0 < nsr; sr0 += gridDim.x * kRunsPerBlock) {
+        const uint32_t sr = sr0 + threadIdx.x / kSeedRun;
         const uint32_t i = sr * p.seed_stride * kSeedRun + threadIdx.x % kSeedRun;
-        if (i >= p.n) continue;
-        const float4 c = p.cull[i];
-        float vz, cx0, cy0, hb;
-        if (!cull_keep_box(p, c, row_lo, row_hi, vz, cx0, cy0, hb)) continue;
-        const float op = 1.0f / (1.0f + __expf(-p.geo[3 * (uint64_t)i].w));
-        const float a = p.focal / vz;
-        const float var = a * a * c.w * p.scale_mod * p.scale_mod * (1.0f / 3.0f) + 0.3f;
-        if (!(op >= 1.0f / 255.0f) || !(var < 1e12f)) continue;
-        const float r = 2.0f * sqrtf(var);
-        const float fx0 = floorf((cx0 - r) * (1.0f / kSeedCell)), fx1 = floorf((cx0 + r) * (1.0f / kSeedCell));
-        const float fy0 = floorf((cy0 - r - (float)row_lo) * (1.0f / kSeedCell));
-        const float fy1 = floorf((cy0 + r - (float)row_lo) * (1.0f / kSeedCell));
-        const float share = op * var * wgt / ((fx1 - fx0 + 1.0f) * (fy1 - fy0 + 1.0f));
-        const int x0 = (int)fmaxf(fx0, 0.0f), x1 = (int)fminf(fx1, (float)(p.seed_cx - 1));
-        const int y0 = (int)fmaxf(fy0, 0.0f), y1 = (int)fminf(fy1, (float)(p.seed_cy - 1));
-        const int b = min(max((int)(sortable_key(vz) >> kSatShift) - (int)p.seed_base, 0), kSeedBuckets - 1);
+        bool ok = sr < nsr && i < p.n;
+        float share = 0.0f;
+        int x0 = 0, x1 = -1, y0 = 0, y1 = -1, b = 0;
+        if (ok) {
+            const float4 c = p.cull[i];
+            float vz, cx0, cy0, hb;
+            ok = cull_keep_box(p, c, row_lo, row_hi, vz, cx0, cy0, hb);
+            if (ok) {
+                const float op = 1.0f / (1.0f + __expf(-p.geo[3 * (uint64_t)i].w));
+                const float a = p.focal / vz;
+                const float var = a * a * c.w * p.scale_mod * p.scale_mod * (1.0f / 3.0f) + 0.3f;
+                ok = op >= 1.0f / 255.0f && var < 1e12f;
+                if (ok) {
+                    const float r = 2.0f * sqrtf(var);
+                    const float fx0 = floorf((cx0 - r) * (1.0f / kSeedCell)), fx1 = floorf((cx0 + r) * (1.0f / kSeedCell));
+                    const float fy0 = floorf((cy0 - r - (float)row_lo) * (1.0f / kSeedCell));
+                    const float fy1 = floorf((cy0 + r - (float)row_lo) * (1.0f / kSeedCell));
+                    share = op * var * wgt / ((fx1 - fx0 + 1.0f) * (fy1 - fy0 + 1.0f));
+                    x0 = (int)fmaxf(fx0, 0.0f);
+                    x1 = (int)fminf(fx1, (float)(p.seed_cx - 1));
+                    y0 = (int)fmaxf(fy0, 0.0f);
+                    y1 = (int)fminf(fy1, (float)(p.seed_cy - 1));
+                    b = min(max((int)(sortable_key(vz) >> kSatShift) - (int)p.seed_base, 0), kSeedBuckets - 1);
+                }
+            }
+        }
+        // the run's Gaussians are neighbours (Morton order): the lanes whose cell box and depth
+        // bucket equal the run leader's add their shares once, through the leader (one set of
+        // atomics per run instead of one per Gaussian); the others add their own
+        const uint32_t kx = ok ? ((uint32_t)x0 | ((uint32_t)x1 << 16)) : 0xFFFFFFFFu;
+        const uint32_t ky = ok ? ((uint32_t)y0 | ((uint32_t)y1 << 16)) : 0xFFFFFFFFu;
+        const int lx = __shfl((int)kx, (int)lead, 64), ly = __shfl((int)ky, (int)lead, 64), lb = __shfl(b, (int)lead, 64);
+        const bool same = ok && (int)kx == lx && (int)ky == ly && b == lb;
+        float sum = same ? share : 0.0f;
+#pragma unroll
+        for (int d = kSeedRun / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+        const bool mine = ok && (!same || lane == lead);
+        const float add = same ? sum : share;
         int cells = 0;
-        for (int y = y0; y <= y1 && cells < 1024; ++y)
-            for (int x = x0; x <= x1 && cells < 1024; ++x, ++cells)
-                atomicAdd(&p.seedh[((uint64_t)y * p.seed_cx + x) * kSeedBuckets + b], share);
+        if (mine)
+            for (int y = y0; y <= y1 && cells < 1024; ++y)
+                for (int x = x0; x <= x1 && cells < 1024; ++x, ++cells)
+                    atomicAdd(&p.seedh[((uint64_t)y * p.seed_cx + x) * kSeedBuckets + b], add);
     }
 }
 
@@ -947,13 +973,22 @@ __global__ __launch_bounds__(1024) void k_seed_pick(ProjParams p) {
         const int cx = q % p.seed_cx, cy = q / p.seed_cx;
         const float px = (float)(min(kSeedCell, p.W - cx * kSeedCell) * min(kSeedCell, rows - cy * kSeedCell));
         const float need = p.seed_tau * px;
-        float* h = p.seedh + (uint64_t)q * kSeedBuckets;
+        float4* h4 = (float4*)(p.seedh + (uint64_t)q * kSeedBuckets);
+        float4 hv[kSeedBuckets / 4];
+#pragma unroll
+        for (int k = 0; k < kSeedBuckets / 4; ++k) hv[k] = h4[k];  // every load in flight at once
+#pragma unroll
+        for (int k = 0; k < kSeedBuckets / 4; ++k) h4[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // zero for the next seeded frame
         float cum = 0.0f;
         int sb = -1;
-        for (int b = 0; b < kSeedBuckets; ++b) {
-            cum += h[b];
-            h[b] = 0.0f;  // zero for the next seeded frame
-            if (sb < 0 && cum >= need) sb = b;
+#pragma unroll
+        for (int k = 0; k < kSeedBuckets / 4; ++k) {
+            const float v[4] = {hv[k].x, hv[k].y, hv[k].z, hv[k].w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                cum += v[t];
+                if (sb < 0 && cum >= need) sb = 4 * k + t;
+            }
         }
         if (sb >= 0) atomicAdd(&s_hist[sb], 1u);
     }
