@@ -198,6 +198,7 @@ struct FrameSet {
     float4* r2 = nullptr;               // per-Gaussian box of rects wider than 16 tiles
     // composite slots (slot_c0 / slot_c1): records (3 float4), (depth key, index), packed rect
     float4* crec = nullptr;
+    uint32_t* wlist = nullptr;          // [slots] wide splats of both chunks (ProjParams::wlist)
     uint2* skey = nullptr;
     uint32_t* srect = nullptr;
     uint32_t *c0 = nullptr, *c1 = nullptr;  // [parts]: slots per projection partition and chunk
@@ -768,6 +769,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.bounds = s->bounds;
     pp.orig = s->orig;
     pp.sidx = F.sidx;
+    pp.wlist = F.wlist;
     if (seeded) {
         pp.thresh = kNoSplit;
         pp.thresh_dev = &F.ctl->seed_T;
@@ -805,6 +807,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     bp.units = F.units;
     bp.rec = records(s, F);
     bp.crec = F.crec;
+    bp.wlist = F.wlist;
     bp.done = F.done;
     bp.ctl = F.ctl;
     bp.chunk = 0;
@@ -1416,6 +1419,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 HIPCHK(hipEventRecord(F.ev_out, F.stream));  // "the last frame on this set ended"
                 dev_alloc(F.r2, (size_t)std::max<uint64_t>(n, 1));
                 dev_alloc(F.crec, 3 * ((size_t)proj_parts(n) * kProjTile + 1));
+                dev_alloc(F.wlist, (size_t)proj_parts(n) * kProjTile + 1);
                 dev_alloc(F.ctl, 1);
                 dev_alloc(F.stats, kStatShards);
                 dev_alloc(F.bar, 4);
@@ -1509,6 +1513,7 @@ void gs_scene_free(gs_scene* s) {
         if (F.stream) (void)hipStreamSynchronize(F.stream);
         dev_free(F.r2);
         dev_free(F.crec);
+        dev_free(F.wlist);
         dev_free(F.ctl);
         dev_free(F.stats);
         dev_free(F.bar);

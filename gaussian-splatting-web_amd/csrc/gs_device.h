@@ -73,6 +73,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t c0_parts;            // chunk 0: projection partitions listed in ProjParams::plist0 (k_part_list)
     uint32_t seed_T;              // a seeded frame's chunk threshold (k_seed_pick; ProjParams::thresh_dev)
     uint32_t frame_T;             // the frame's chunk threshold, whichever its source (k_part_list)
+    uint32_t wl_n[2];             // wide splats listed per chunk (ProjParams::wlist: k_project, chunk-1 records)
     uint32_t sat_hist[kSatBuckets];  // tiles saturated by the end of the frame, by saturation depth
                                      // (sat_bucket; summed from the shards at the frame's end)
 };
@@ -171,6 +172,9 @@ struct ProjParams {
     const PartBound* bounds;  // [parts] (k_part_bounds)
     const uint32_t* orig;     // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx;           // [slots] storage index of each composite slot
+    // [slots] the slots of wide splats (>= kWideTiles box tiles): chunk 0's from the front,
+    // chunk 1's from the back (FrameCtl::wl_n); binning spreads them over all its workgroups
+    uint32_t* wlist;
     // chunk 1: per strip tile row, prefix counts of the tiles chunk 0 left unsaturated
     // (unsat_rows_body); rec_all: k_records dumps every visible Gaussian's record (debug)
     const uint32_t* sat;
@@ -267,7 +271,9 @@ struct BinParams {
     uint32_t heavy_len;
     uint32_t band_tiles;          // tiles per binning band (LDS counters / cursors; set by the launcher)
     uint32_t pref_words;          // LDS words of the per-partition unit prefix (set by the launcher)
-    uint32_t wide_cap;            // LDS queue of wide splats per workgroup (set by the launcher)
+    uint32_t wide_cap;            // LDS queue of wide splats per workgroup (set by the launcher; 0 with wlist)
+    const uint32_t* wlist;        // nullable: the chunk's wide splats (ProjParams::wlist), walked
+                                  // by the waves of every workgroup in turn instead of the LDS queue
 };
 
 // Per-tile sort of the tile lists (k_tile_sort): each tile's slots ordered by their sort key,

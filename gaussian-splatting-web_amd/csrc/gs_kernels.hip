@@ -23,6 +23,7 @@
 // Inter-workgroup hand-offs (the grid barrier) follow cdna_hip_programming.md Guideline 16:
 // agent-scope release / acquire, bounded spins, counters zeroed by the frame's end.
 #include <algorithm>
+#include <type_traits>
 
 #include "gs_device.h"
 
@@ -713,6 +714,19 @@ __device__ __forceinline__ bool box_tiles(const ProjParams& p, float xl, float x
     return tx0 <= tx1 && ty0 <= ty1;
 }
 
+// A wide splat's slot into the chunk's list (ProjParams::wlist: chunk 0 from the front, chunk 1
+// from the back); one counter add per wave.  Every lane of the wave calls it.
+__device__ __forceinline__ void wide_append(const ProjParams& p, int chunk, bool wide, uint32_t slot) {
+    const uint64_t b = __ballot(wide);
+    if (!b) return;
+    const uint32_t lane = lane_id();
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&p.ctl->wl_n[chunk], (uint32_t)__popcll(b));
+    base = __shfl(base, 0, 64);
+    const uint32_t j = base + (uint32_t)__popcll(b & lanemask_lt());
+    if (wide) p.wlist[chunk ? proj_parts(p.n) * (uint32_t)kProjTile - 1u - j : j] = slot;
+}
+
 // Does the tile rectangle [tx0, tx1] x [ty0, ty1] (strip tile rows, absolute) hold a tile chunk 0
 // left unsaturated?  Two reads of the row prefix counts (unsat_rows_body) per row.
 __device__ __forceinline__ bool sat_any(const ProjParams& p, uint32_t tx0, uint32_t ty0, uint32_t tx1, uint32_t ty1) {
@@ -806,13 +820,14 @@ __device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t bl
                 atomicAdd(&st->k_total, kt);
             }
             base = __shfl(base, 0, 64);
+            const uint32_t slot = slot_c1(part, base + (uint32_t)__popcll(b & lanemask_lt()));
             if (want) {
-                const uint32_t slot = slot_c1(part, base + (uint32_t)__popcll(b & lanemask_lt()));
                 store_slot(p, slot, i, p.orig[i], o);
                 float4 c = colour_of(p, i);
                 c.w = __uint_as_float(o.key);
                 p.crec[3 * (uint64_t)slot + 2] = c;
             }
+            if (p.wlist) wide_append(p, 1, want && o.ntiles >= kWideTiles, slot);
         }
     }
 }
@@ -1219,6 +1234,7 @@ __global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
         // the next unit's candidate: its load overlaps this unit's colour and stores (waiting for
         // the unit entry also drains this unit's SH loads, which are due by now)
         const uint32_t cqn = jn < L.total ? cand_of(un) : 0u;
+        if (p.wlist) wide_append(p, 0, act && vis && o.prect != kRectEmpty && o.ntiles >= kWideTiles, slot);
         if (act) {
             if (vis) {
                 store_slot(p, slot, i, oi, o);
@@ -1757,8 +1773,8 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
 // cells l, l + 64, ... of the splat's tile box (in the band), each testing its cell against the
 // ellipse's column range in the cell's tile row.  f(tile) per entry.
 template <class F>
-__device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uint32_t t_lo, uint32_t t_hi, F&& f) {
-    const uint32_t lane = lane_id();
+__device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uint32_t t_lo, uint32_t t_hi, F&& f,
+                                             uint32_t first = lane_id(), uint32_t step = 64u) {
     const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
     TileRect tr;
     rect_unpack(p, p.srect[g], p.sidx[g], tr);
@@ -1767,13 +1783,31 @@ __device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uin
     const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
     if (ya > yb) return;
     const uint32_t w = tr.x1 - tr.x0 + 1, cells = w * (yb - ya + 1);
-    for (uint32_t c = lane; c < cells; c += 64) {
+    for (uint32_t c = first; c < cells; c += step) {
         const uint32_t ty = ya + c / w, x = tr.x0 + c % w;
         uint32_t xa, xb;
         if (!ellipse_row(e, ty, xa, xb) || x < xa || x > xb) continue;
         const uint32_t t = (ty - rb) * tx + x;
         if (t < t_lo || t >= t_hi || (p.chunk == 1 && p.done[t])) continue;
         f(t);
+    }
+}
+
+// The chunk's listed wide splats (BinParams::wlist) that binning partition `part` walks: list
+// entries part, part + kBinParts, ..., each by the whole workgroup (threads over the splat's tile
+// cells), so the wide splats spread over every workgroup (a partition that held many of them
+// walked them all itself, one wave per splat: a near view's binning took 300 us).  Count and
+// emission walk the same assignment.  f(tile) or f(tile, slot) per entry.
+template <int NT, class F>
+__device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, uint32_t t_lo, uint32_t t_hi, F&& f) {
+    if (!p.wlist) return;
+    const uint32_t wn = p.ctl->wl_n[p.chunk], last = p.parts * (uint32_t)kProjTile - 1u;
+    for (uint32_t j = part; j < wn; j += kBinParts) {
+        const uint32_t g = p.chunk ? p.wlist[last - j] : p.wlist[j];
+        if constexpr (std::is_invocable_v<F, uint32_t, uint32_t>)
+            wide_entries(p, g, t_lo, t_hi, [&](uint32_t t) { f(t, g); }, threadIdx.x, (uint32_t)NT);
+        else
+            wide_entries(p, g, t_lo, t_hi, f, threadIdx.x, (uint32_t)NT);
     }
 }
 
@@ -1795,6 +1829,7 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
         if (rect_wide(tr)) {
+            if (p.wlist) continue;  // listed: walked below
             const uint32_t qi = atomicAdd(&s_nw, 1u);
             if (qi < p.wide_cap) {
                 s_wide[qi] = g;
@@ -1808,6 +1843,7 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
     const uint32_t nq = min(s_nw, p.wide_cap);
     for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64)  // wave-uniform
         wide_entries(p, s_wide[qi], t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
+    wide_listed<NT>(p, part, t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
     __syncthreads();
     uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) row[t] = s_cnt[t - t_lo];
@@ -2015,6 +2051,7 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
         if (rect_wide(tr)) {
+            if (p.wlist) continue;  // listed: walked below
             const uint32_t qi = atomicAdd(&s_nw, 1u);
             if (qi < p.wide_cap) {
                 s_wide[qi] = g;
@@ -2030,6 +2067,7 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
     __syncthreads();
     const uint32_t nq = min(s_nw, p.wide_cap);
     if (threadIdx.x == 0 && s_nw) atomicAdd(&p.ctl->wide_n[p.chunk], s_nw);  // statistics
+    if (p.wlist && part == 0 && band == 0 && threadIdx.x == 0) atomicAdd(&p.ctl->wide_n[p.chunk], p.ctl->wl_n[p.chunk]);
     for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64) {  // wave-uniform
         const uint32_t g = s_wide[qi];
         wide_entries(p, g, t_lo, t_hi, [&](uint32_t t) {
@@ -2037,6 +2075,10 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
             if (pos < cap) p.tvals[pos] = g;
         });
     }
+    wide_listed<NT>(p, part, t_lo, t_hi, [&](uint32_t t, uint32_t g) {
+        const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
+        if (pos < cap) p.tvals[pos] = g;
+    });
     __syncthreads();
 }
 
@@ -3385,7 +3427,7 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
     // wide-splat queue: larger frames hold more splats that cover many tiles (near splats at 4K);
     // a splat past the queue is walked by its own thread
     const uint32_t room = (uint32_t)(kBinLdsMaxWords - bin_lds_words(p.band_tiles, p.pref_words, 0));
-    p.wide_cap = std::min(room, std::max(kWideQueue, std::min(kWideQueueMax, p.n_tiles / 4)));
+    p.wide_cap = p.wlist ? 0u : std::min(room, std::max(kWideQueue, std::min(kWideQueueMax, p.n_tiles / 4)));
     const size_t lds = bin_lds_words(p.band_tiles, p.pref_words, p.wide_cap) * 4;
     const unsigned grid = kBinParts * bin_bands(p.n_tiles, p.band_tiles);
     if (p.units)
