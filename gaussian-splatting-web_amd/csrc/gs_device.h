@@ -29,9 +29,10 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // key of a culled Gaussian (no vis
 constexpr int kRecFloats = 16;        // 64-B projected record
 constexpr int kMaxGrid = 2048;        // persistent grids: 8 workgroups per CU
 #ifndef GS_WIDE_TILES
-#define GS_WIDE_TILES 256
+#define GS_WIDE_TILES 64
 #endif
-constexpr uint32_t kWideTiles = GS_WIDE_TILES;  // splats binding >= this many tiles: walked by whole waves
+constexpr uint32_t kWideTiles = GS_WIDE_TILES;  // splats of >= this many box tiles: listed at projection and
+                                                // walked by whole waves or workgroups in binning (wide_listed)
 constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
 constexpr int kMaxMerge = 16;           // compacted radix input: partitions per downsweep workgroup
 constexpr uint32_t kGroupParts = 32;    // radix partitions per group sum (the downsweep's offsets)

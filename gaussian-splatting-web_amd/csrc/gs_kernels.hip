@@ -1793,6 +1793,7 @@ __device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uin
     }
 }
 
+constexpr uint32_t kWaveCells = 1024;  // listed wide splats of at most this many box tiles: one wave
 // The chunk's listed wide splats (BinParams::wlist) that binning partition `part` walks: list
 // entries part, part + kBinParts, ..., each by the whole workgroup (threads over the splat's tile
 // cells), so the wide splats spread over every workgroup (a partition that held many of them
@@ -1802,12 +1803,20 @@ template <int NT, class F>
 __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, uint32_t t_lo, uint32_t t_hi, F&& f) {
     if (!p.wlist) return;
     const uint32_t wn = p.ctl->wl_n[p.chunk], last = p.parts * (uint32_t)kProjTile - 1u;
+    const uint32_t w = threadIdx.x >> 6;
+    uint32_t k = 0;  // the workgroup's list entries in turn: a splat of at most kWaveCells tile cells
+                     // goes to one wave (round-robin), a larger one to every thread of the workgroup
     for (uint32_t j = part; j < wn; j += kBinParts) {
         const uint32_t g = p.chunk ? p.wlist[last - j] : p.wlist[j];
+        TileRect tr;
+        rect_unpack(p, p.srect[g], p.sidx[g], tr);
+        const bool big = (tr.x1 - tr.x0 + 1) * (tr.y1 - tr.y0 + 1) > kWaveCells;
+        if (!big && (k++ % (NT / 64)) != w) continue;  // (wave-uniform)
+        const uint32_t first = big ? threadIdx.x : lane_id(), step = big ? (uint32_t)NT : 64u;
         if constexpr (std::is_invocable_v<F, uint32_t, uint32_t>)
-            wide_entries(p, g, t_lo, t_hi, [&](uint32_t t) { f(t, g); }, threadIdx.x, (uint32_t)NT);
+            wide_entries(p, g, t_lo, t_hi, [&](uint32_t t) { f(t, g); }, first, step);
         else
-            wide_entries(p, g, t_lo, t_hi, f, threadIdx.x, (uint32_t)NT);
+            wide_entries(p, g, t_lo, t_hi, f, first, step);
     }
 }
 
