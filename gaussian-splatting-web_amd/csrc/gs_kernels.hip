@@ -1803,20 +1803,31 @@ template <int NT, class F>
 __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, uint32_t t_lo, uint32_t t_hi, F&& f) {
     if (!p.wlist) return;
     const uint32_t wn = p.ctl->wl_n[p.chunk], last = p.parts * (uint32_t)kProjTile - 1u;
-    const uint32_t w = threadIdx.x >> 6;
-    uint32_t k = 0;  // the workgroup's list entries in turn: a splat of at most kWaveCells tile cells
-                     // goes to one wave (round-robin), a larger one to every thread of the workgroup
-    for (uint32_t j = part; j < wn; j += kBinParts) {
-        const uint32_t g = p.chunk ? p.wlist[last - j] : p.wlist[j];
-        TileRect tr;
-        rect_unpack(p, p.srect[g], p.sidx[g], tr);
-        const bool big = (tr.x1 - tr.x0 + 1) * (tr.y1 - tr.y0 + 1) > kWaveCells;
-        if (!big && (k++ % (NT / 64)) != w) continue;  // (wave-uniform)
-        const uint32_t first = big ? threadIdx.x : lane_id(), step = big ? (uint32_t)NT : 64u;
-        if constexpr (std::is_invocable_v<F, uint32_t, uint32_t>)
-            wide_entries(p, g, t_lo, t_hi, [&](uint32_t t) { f(t, g); }, first, step);
-        else
-            wide_entries(p, g, t_lo, t_hi, f, first, step);
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t share = wn > part ? (wn - part + kBinParts - 1) / kBinParts : 0u;  // entries part + i kBinParts
+    uint32_t k = 0;  // the workgroup's entries in turn: a splat of at most kWaveCells tile cells goes
+                     // to one wave (round-robin), a larger one to every thread of the workgroup
+    for (uint32_t i0 = 0; i0 < share; i0 += 64) {
+        // 64 entries' slots and tile counts loaded at once (one lane each), then broadcast
+        uint32_t g = 0, cells = 0;
+        if (i0 + lane < share) {
+            const uint32_t j = part + (i0 + lane) * kBinParts;
+            g = p.chunk ? p.wlist[last - j] : p.wlist[j];
+            TileRect tr;
+            rect_unpack(p, p.srect[g], p.sidx[g], tr);
+            cells = (tr.x1 - tr.x0 + 1) * (tr.y1 - tr.y0 + 1);
+        }
+        const uint32_t m = min(64u, share - i0);
+        for (uint32_t e = 0; e < m; ++e) {
+            const uint32_t ge = (uint32_t)__builtin_amdgcn_readlane((int)g, (int)e);
+            const bool big = (uint32_t)__builtin_amdgcn_readlane((int)cells, (int)e) > kWaveCells;
+            if (!big && (k++ % (NT / 64)) != w) continue;  // (wave-uniform)
+            const uint32_t first = big ? threadIdx.x : lane, step = big ? (uint32_t)NT : 64u;
+            if constexpr (std::is_invocable_v<F, uint32_t, uint32_t>)
+                wide_entries(p, ge, t_lo, t_hi, [&](uint32_t t) { f(t, ge); }, first, step);
+            else
+                wide_entries(p, ge, t_lo, t_hi, f, first, step);
+        }
     }
 }
 
