@@ -770,6 +770,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.orig = s->orig;
     pp.sidx = F.sidx;
     pp.wlist = F.wlist;
+    pp.wide_tiles = wide_tiles(n_tiles);
     if (seeded) {
         pp.thresh = kNoSplit;
         pp.thresh_dev = &F.ctl->seed_T;
@@ -808,6 +809,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     bp.rec = records(s, F);
     bp.crec = F.crec;
     bp.wlist = F.wlist;
+    bp.wide_tiles = pp.wide_tiles;
     bp.done = F.done;
     bp.ctl = F.ctl;
     bp.chunk = 0;
@@ -1419,7 +1421,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 HIPCHK(hipEventRecord(F.ev_out, F.stream));  // "the last frame on this set ended"
                 dev_alloc(F.r2, (size_t)std::max<uint64_t>(n, 1));
                 dev_alloc(F.crec, 3 * ((size_t)proj_parts(n) * kProjTile + 1));
-                dev_alloc(F.wlist, (size_t)proj_parts(n) * kProjTile + 1);
+                dev_alloc(F.wlist, (size_t)kWideShards * wide_shard_cap(proj_parts(n)) + 1);
                 dev_alloc(F.ctl, 1);
                 dev_alloc(F.stats, kStatShards);
                 dev_alloc(F.bar, 4);

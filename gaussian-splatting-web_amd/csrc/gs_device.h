@@ -28,11 +28,14 @@ constexpr int kHistShards = 8;        // global histograms sharded by blockIdx %
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // key of a culled Gaussian (no visible splat has it)
 constexpr int kRecFloats = 16;        // 64-B projected record
 constexpr int kMaxGrid = 2048;        // persistent grids: 8 workgroups per CU
-#ifndef GS_WIDE_TILES
-#define GS_WIDE_TILES 64
-#endif
-constexpr uint32_t kWideTiles = GS_WIDE_TILES;  // splats of >= this many box tiles: listed at projection and
-                                                // walked by whole waves or workgroups in binning (wide_listed)
+// Splats of at least wide_tiles(n_tiles) box tiles are "wide": listed at projection and walked in
+// binning by whole waves or workgroups (wide_listed).  64 at 1080p (the few workgroups whose
+// partitions met the near splats walked them all), up to 256 at 4K (there the many medium splats
+// walk faster one per thread: 4K binning 170 us at 256, 225 us at 64).
+__host__ __device__ inline uint32_t wide_tiles(int n_tiles) {
+    const int t = n_tiles / 128;
+    return (uint32_t)(t < 64 ? 64 : (t > 256 ? 256 : t));
+}
 constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
 constexpr int kMaxMerge = 16;           // compacted radix input: partitions per downsweep workgroup
 constexpr uint32_t kGroupParts = 32;    // radix partitions per group sum (the downsweep's offsets)
@@ -74,7 +77,6 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t c0_parts;            // chunk 0: projection partitions listed in ProjParams::plist0 (k_part_list)
     uint32_t seed_T;              // a seeded frame's chunk threshold (k_seed_pick; ProjParams::thresh_dev)
     uint32_t frame_T;             // the frame's chunk threshold, whichever its source (k_part_list)
-    uint32_t wl_n[2];             // wide splats listed per chunk (ProjParams::wlist: k_project, chunk-1 records)
     uint32_t sat_hist[kSatBuckets];  // tiles saturated by the end of the frame, by saturation depth
                                      // (sat_bucket; summed from the shards at the frame's end)
 };
@@ -88,6 +90,14 @@ struct FrameCtl {                 // zeroed at the start of every frame
 #define GS_STAT_SHARDS 16
 #endif
 constexpr int kStatShards = GS_STAT_SHARDS;
+// The wide-splat list (ProjParams::wlist) is sharded by projection partition (shard = partition %
+// kWideShards, each shard a region of its partitions' slot count, counter StatShard::wl_n of the
+// shard's index): a counter per shard instead of one for the frame (same-address atomics
+// serialise; at 4K one counter doubled k_project).
+constexpr uint32_t kWideShards = (uint32_t)kStatShards;
+__host__ __device__ inline uint32_t wide_shard_cap(uint32_t parts) {
+    return (parts + kWideShards - 1) / kWideShards * (uint32_t)kProjTile;
+}
 struct StatShard {
     unsigned long long k_total;
     uint32_t n_vis, key_min_inv, key_max;
@@ -95,6 +105,8 @@ struct StatShard {
     uint32_t sat_key;             // composite: max saturation key of the shard's tiles
     uint32_t sat_hist[kSatBuckets];  // composite: the shard's tiles by saturation depth
     uint32_t order_n[2];          // shards 0-7: the composite order of XCD band x (k_tile_sort)
+    uint32_t wl_n[2];             // wide splats of wide-list shard (= this shard's index) per chunk
+                                  // (ProjParams::wlist; zeroed with the shard, not summed)
 };
 
 // Bound of a projection partition (k_part_bounds, at upload): box of its finite positions,
@@ -173,9 +185,10 @@ struct ProjParams {
     const PartBound* bounds;  // [parts] (k_part_bounds)
     const uint32_t* orig;     // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx;           // [slots] storage index of each composite slot
-    // [slots] the slots of wide splats (>= kWideTiles box tiles): chunk 0's from the front,
-    // chunk 1's from the back (FrameCtl::wl_n); binning spreads them over all its workgroups
+    // [slots] the slots of wide splats (>= wide_tiles box tiles): chunk 0's from the front,
+    // chunk 1's from the back, sharded (kWideShards); binning spreads them over all its workgroups
     uint32_t* wlist;
+    uint32_t wide_tiles;      // wide_tiles(n_tiles) of the frame (strip)
     // chunk 1: per strip tile row, prefix counts of the tiles chunk 0 left unsaturated
     // (unsat_rows_body); rec_all: k_records dumps every visible Gaussian's record (debug)
     const uint32_t* sat;
@@ -273,6 +286,7 @@ struct BinParams {
     uint32_t band_tiles;          // tiles per binning band (LDS counters / cursors; set by the launcher)
     uint32_t pref_words;          // LDS words of the per-partition unit prefix (set by the launcher)
     uint32_t wide_cap;            // LDS queue of wide splats per workgroup (set by the launcher; 0 with wlist)
+    uint32_t wide_tiles;          // splats of >= this many box tiles are wide (ProjParams::wide_tiles)
     const uint32_t* wlist;        // nullable: the chunk's wide splats (ProjParams::wlist), walked
                                   // by the waves of every workgroup in turn instead of the LDS queue
 };

@@ -714,17 +714,20 @@ __device__ __forceinline__ bool box_tiles(const ProjParams& p, float xl, float x
     return tx0 <= tx1 && ty0 <= ty1;
 }
 
-// A wide splat's slot into the chunk's list (ProjParams::wlist: chunk 0 from the front, chunk 1
-// from the back); one counter add per wave.  Every lane of the wave calls it.
+// A wide splat's slot into the chunk's list (ProjParams::wlist): the shard of its partition,
+// chunk 0 from the shard region's front, chunk 1 from its back (a partition's slots of both
+// chunks fit its block, so a shard's two lists fit its region); one counter add per wave.  Every
+// lane of the wave calls it, and the wave's slots lie in one partition.
 __device__ __forceinline__ void wide_append(const ProjParams& p, int chunk, bool wide, uint32_t slot) {
     const uint64_t b = __ballot(wide);
     if (!b) return;
     const uint32_t lane = lane_id();
+    const uint32_t sh = (uint32_t)__builtin_amdgcn_readfirstlane((int)((slot / (uint32_t)kProjTile) % kWideShards));
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&p.ctl->wl_n[chunk], (uint32_t)__popcll(b));
+    if (lane == 0) base = atomicAdd(&p.stats[sh].wl_n[chunk], (uint32_t)__popcll(b));
     base = __shfl(base, 0, 64);
-    const uint32_t j = base + (uint32_t)__popcll(b & lanemask_lt());
-    if (wide) p.wlist[chunk ? proj_parts(p.n) * (uint32_t)kProjTile - 1u - j : j] = slot;
+    const uint32_t j = base + (uint32_t)__popcll(b & lanemask_lt()), cap = wide_shard_cap(proj_parts(p.n));
+    if (wide) p.wlist[(uint64_t)sh * cap + (chunk ? cap - 1u - j : j)] = slot;
 }
 
 // Does the tile rectangle [tx0, tx1] x [ty0, ty1] (strip tile rows, absolute) hold a tile chunk 0
@@ -827,7 +830,7 @@ __device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t bl
                 c.w = __uint_as_float(o.key);
                 p.crec[3 * (uint64_t)slot + 2] = c;
             }
-            if (p.wlist) wide_append(p, 1, want && o.ntiles >= kWideTiles, slot);
+            if (p.wlist) wide_append(p, 1, want && o.ntiles >= p.wide_tiles, slot);
         }
     }
 }
@@ -1234,7 +1237,7 @@ __global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
         // the next unit's candidate: its load overlaps this unit's colour and stores (waiting for
         // the unit entry also drains this unit's SH loads, which are due by now)
         const uint32_t cqn = jn < L.total ? cand_of(un) : 0u;
-        if (p.wlist) wide_append(p, 0, act && vis && o.prect != kRectEmpty && o.ntiles >= kWideTiles, slot);
+        if (p.wlist) wide_append(p, 0, act && vis && o.prect != kRectEmpty && o.ntiles >= p.wide_tiles, slot);
         if (act) {
             if (vis) {
                 store_slot(p, slot, i, oi, o);
@@ -1561,8 +1564,8 @@ __device__ __forceinline__ uint32_t tile_id(const BinParams& p, uint32_t tx, uin
     return (ty - (uint32_t)p.tile_row_begin) * (uint32_t)p.tiles_x + tx;
 }
 
-__device__ __forceinline__ bool rect_wide(const TileRect& r) {
-    return (r.x1 - r.x0 + 1) * (r.y1 - r.y0 + 1) >= kWideTiles;
+__device__ __forceinline__ bool rect_wide(const BinParams& p, const TileRect& r) {
+    return (r.x1 - r.x0 + 1) * (r.y1 - r.y0 + 1) >= p.wide_tiles;
 }
 
 // ---- exact-ish binning: the alpha >= 1/255 region of a splat is the ellipse
@@ -1802,7 +1805,11 @@ constexpr uint32_t kWaveCells = 1024;  // listed wide splats of at most this man
 template <int NT, class F>
 __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, uint32_t t_lo, uint32_t t_hi, F&& f) {
     if (!p.wlist) return;
-    const uint32_t wn = p.ctl->wl_n[p.chunk], last = p.parts * (uint32_t)kProjTile - 1u;
+    uint32_t pre[kWideShards + 1];  // the shards' lists, concatenated
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kWideShards; ++k) pre[k + 1] = pre[k] + p.stats[k].wl_n[p.chunk];
+    const uint32_t wn = pre[kWideShards], cap = wide_shard_cap(p.parts);
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     const uint32_t share = wn > part ? (wn - part + kBinParts - 1) / kBinParts : 0u;  // entries part + i kBinParts
     uint32_t k = 0;  // the workgroup's entries in turn: a splat of at most kWaveCells tile cells goes
@@ -1812,7 +1819,15 @@ __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, u
         uint32_t g = 0, cells = 0;
         if (i0 + lane < share) {
             const uint32_t j = part + (i0 + lane) * kBinParts;
-            g = p.chunk ? p.wlist[last - j] : p.wlist[j];
+            uint32_t sh = 0, base = 0;  // (selects, not an indexed array: no scratch)
+#pragma unroll
+            for (uint32_t k = 1; k < kWideShards; ++k)
+                if (j >= pre[k]) {
+                    sh = k;
+                    base = pre[k];
+                }
+            const uint32_t q = j - base;
+            g = p.wlist[(uint64_t)sh * cap + (p.chunk ? cap - 1u - q : q)];
             TileRect tr;
             rect_unpack(p, p.srect[g], p.sidx[g], tr);
             cells = (tr.x1 - tr.x0 + 1) * (tr.y1 - tr.y0 + 1);
@@ -1832,7 +1847,7 @@ __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, u
 }
 
 // Binning partition / band vb: counts of its splats' entries per tile of the band -> bmat row.
-// Wide splats (>= kWideTiles box tiles) are queued in LDS (up to wide_cap) and counted by whole
+// Wide splats (>= wide_tiles box tiles) are queued in LDS (up to wide_cap) and counted by whole
 // waves, as k_bin_emit emits them.
 template <int NT, bool LISTED>
 __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp,
@@ -1848,7 +1863,7 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
         const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
-        if (rect_wide(tr)) {
+        if (rect_wide(p, tr)) {
             if (p.wlist) continue;  // listed: walked below
             const uint32_t qi = atomicAdd(&s_nw, 1u);
             if (qi < p.wide_cap) {
@@ -2007,7 +2022,7 @@ __device__ __forceinline__ void tile_scan_body(const BinParams& p, uint32_t* s_w
 }
 
 
-// Wide splats (>= kWideTiles box tiles) are queued in LDS by the thread that meets them and
+// Wide splats (>= wide_tiles box tiles) are queued in LDS by the thread that meets them and
 // emitted row by row by whole waves (lanes over columns); the queue holds kWideQueue splats,
 // beyond that the thread emits its splat itself.
 
@@ -2070,7 +2085,7 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
         const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
         if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
-        if (rect_wide(tr)) {
+        if (rect_wide(p, tr)) {
             if (p.wlist) continue;  // listed: walked below
             const uint32_t qi = atomicAdd(&s_nw, 1u);
             if (qi < p.wide_cap) {
@@ -2087,7 +2102,8 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
     __syncthreads();
     const uint32_t nq = min(s_nw, p.wide_cap);
     if (threadIdx.x == 0 && s_nw) atomicAdd(&p.ctl->wide_n[p.chunk], s_nw);  // statistics
-    if (p.wlist && part == 0 && band == 0 && threadIdx.x == 0) atomicAdd(&p.ctl->wide_n[p.chunk], p.ctl->wl_n[p.chunk]);
+    if (p.wlist && part == 0 && band == 0 && threadIdx.x < kWideShards)
+        atomicAdd(&p.ctl->wide_n[p.chunk], p.stats[threadIdx.x].wl_n[p.chunk]);
     for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64) {  // wave-uniform
         const uint32_t g = s_wide[qi];
         wide_entries(p, g, t_lo, t_hi, [&](uint32_t t) {
