@@ -661,10 +661,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         s->hist_ok = false;
     }
     uint32_t T = s->chunk_T;
+    bool moving = false;
     {  // the statistics are a few frames old: while the camera moves, the depth at which tiles
        // saturate moves too, so the threshold gets a wider margin (1.05 x 1.10 ~ the 1.15 used for
        // every frame until round 2); a still camera keeps the tight one
-        const bool moving = std::memcmp(s->last_view, uni, sizeof(s->last_view)) != 0;
+        moving = std::memcmp(s->last_view, uni, sizeof(s->last_view)) != 0;
         std::memcpy(s->last_view, uni, sizeof(s->last_view));
         std::memcpy(s->last_campos, uni + 32, sizeof(s->last_campos));
         s->have_view = true;
@@ -836,6 +837,12 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     tsp.skey = F.skey;
     tsp.done = nullptr;
     tsp.n_tiles = n_tiles;
+    {  // lists of more than kTsBigMean entries on average (last frame; the 128-thread shape sorts rounds of 1024): most
+       // tiles would take the multi-round path (each round re-reads the whole list), so the
+       // 256-thread shape with rounds of 2048 (a moving camera at 4K: 1200 entries per tile)
+        const uint64_t k0 = s->have_last ? s->last.k_chunk[0] : 0;
+        tsp.big = n_tiles > 0 && k0 > (uint64_t)kTsBigMean * (uint64_t)n_tiles;
+    }
     CompositeParams cp{};
     cp.ranges = F.ranges;
     cp.tvals = F.tvB;
@@ -907,7 +914,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         // while the others wait at a grid barrier: the kernels beside it never wait for k_chunk1
         // and finish.  Once a recent frame left tiles unsaturated: chunk 1 as separate launches
         // at full occupancy (a kernel boundary costs less than a grid barrier), then the frame's end.
-        if (two_chunks && (seeded || (s->have_last && s->last.not_done > 0)))
+        // (a moving camera takes the launches too: its first frame that leaves tiles unsaturated
+        // after saturated ones ran chunk 1 on k_chunk1's 64 workgroups, 5.4 ms at 4K)
+        if (two_chunks && (seeded || moving || (s->have_last && s->last.not_done > 0)))
             launch_chunk1_split(c1, o.accum == GS_ACCUM_FP16_TARGET, st);
         else
             launch_chunk1(c1, c->c1_grid, o.accum == GS_ACCUM_FP16_TARGET, st);

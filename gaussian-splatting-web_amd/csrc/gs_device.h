@@ -300,7 +300,10 @@ struct TileSortParams {
     const uint2* skey;            // nullable
     const uint8_t* done;          // chunk 1: saturated tiles are skipped (nullable)
     int n_tiles;
+    int big;                      // chunk 0 with long lists: the 256-thread shape (k_tile_sort_big)
 };
+
+constexpr uint32_t kTsBigMean = 800;  // mean chunk-0 list length from which k_tile_sort_big sorts chunk 0
 
 enum CompositeMode { kCompSingle = 0, kCompFirst = 1, kCompSecond = 2 };
 

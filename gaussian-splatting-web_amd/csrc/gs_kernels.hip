@@ -3479,7 +3479,7 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
 void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return;
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
-    if (p.done)  // chunk 1: the unsaturated tiles' long lists
+    if (p.done || p.big)  // chunk 1 (the unsaturated tiles' long lists), or long chunk-0 lists
         hipLaunchKernelGGL(k_tile_sort_big, dim3(grid), dim3(TsBig::NT), 0, s, p);
     else
         hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(TsSmall::NT), 0, s, p);
