@@ -309,7 +309,10 @@ static constexpr float kMovingMargin = GS_MOVING_MARGIN;  // extra depth margin 
 static constexpr double kSplitSatFrac = GS_SPLIT_SAT_FRAC;
 // ... at this quantile of the saturated tiles' saturation depths (GS_SAT_QUANTILE overrides),
 // when the deepest saturation is more than kQuantileGain times deeper
-static constexpr float kQuantileGain = 1.5f;
+#ifndef GS_QUANTILE_GAIN
+#define GS_QUANTILE_GAIN 1.5f
+#endif
+static constexpr float kQuantileGain = GS_QUANTILE_GAIN;
 static double sat_quantile() {
     static const double q = [] {
         const char* e = std::getenv("GS_SAT_QUANTILE");
