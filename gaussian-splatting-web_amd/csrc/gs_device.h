@@ -36,7 +36,6 @@ __host__ __device__ inline uint32_t wide_tiles(int n_tiles) {
     const int t = n_tiles / 128;
     return (uint32_t)(t < 64 ? 64 : (t > 256 ? 256 : t));
 }
-constexpr int kSatMaxWords = 36864;     // summed-area table built in LDS up to this size
 constexpr int kMaxMerge = 16;           // compacted radix input: partitions per downsweep workgroup
 constexpr uint32_t kGroupParts = 32;    // radix partitions per group sum (the downsweep's offsets)
 
@@ -339,7 +338,9 @@ struct Chunk1Params {
     FrameCtl* host_ctl;
     uint32_t* host_seq;
     uint32_t seq;
+    uint32_t sat_lds_words;       // k_c1_rows: dynamic LDS of the summed-area table (0: global memory)
 };
+constexpr uint32_t kSatLdsWords = 36864;  // summed-area table of the unsaturated tiles built in LDS up to this size
 
 // launchers (gs_kernels.hip)
 void launch_bbox(const uint8_t* aos, uint64_t n, uint32_t rb, uint32_t* bbox, hipStream_t s);

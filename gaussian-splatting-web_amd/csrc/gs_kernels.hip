@@ -731,14 +731,12 @@ __device__ __forceinline__ void wide_append(const ProjParams& p, int chunk, bool
 }
 
 // Does the tile rectangle [tx0, tx1] x [ty0, ty1] (strip tile rows, absolute) hold a tile chunk 0
-// left unsaturated?  Two reads of the row prefix counts (unsat_rows_body) per row.
+// left unsaturated?  Four reads of the summed-area table (unsat_sat_body).
 __device__ __forceinline__ bool sat_any(const ProjParams& p, uint32_t tx0, uint32_t ty0, uint32_t tx1, uint32_t ty1) {
     const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
-    for (uint32_t ty = ty0; ty <= ty1; ++ty) {
-        const uint32_t* row = p.sat + (uint64_t)(ty - rb) * sw;
-        if (row[tx1 + 1] != row[tx0]) return true;
-    }
-    return false;
+    const uint32_t* a = p.sat + (uint64_t)(ty0 - rb) * sw;
+    const uint32_t* b = p.sat + (uint64_t)(ty1 + 1 - rb) * sw;
+    return (b[tx1 + 1] - b[tx0]) - (a[tx1 + 1] - a[tx0]) != 0u;
 }
 
 // Can partition b hold a chunk-1 splat: a Gaussian at or past thresh whose quad may touch a tile
@@ -2219,12 +2217,21 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
 // Row prefix counts of the tiles chunk 0 left unsaturated (done == 0): row r of the strip at
 // sat[r * (tiles_x + 1)], entry x = unsaturated tiles among the row's first x.  One wave per row,
 // the rows spread over every wave of the grid (no sequential pass).
-__device__ __forceinline__ void unsat_rows_body(const uint8_t* __restrict__ done, int tiles_x, int rows,
-                                                uint32_t* __restrict__ sat) {
-    const uint32_t sw = (uint32_t)tiles_x + 1, lane = lane_id();
-    const uint32_t wpb = blockDim.x / 64, wave = blockIdx.x * wpb + (threadIdx.x >> 6);
-    for (uint32_t r = wave; r < (uint32_t)rows; r += gridDim.x * wpb) {
-        uint32_t* row = sat + (uint64_t)r * sw;
+// Summed-area table of the tiles chunk 0 left unsaturated, by one workgroup: sat[r][x] (r <=
+// rows, x <= tiles_x, row and column 0 zero) = unsaturated tiles in strip rows < r and columns <
+// x, so any tile rectangle is tested with four reads (sat_any).  Row prefixes by ballots (one
+// wave per row), then the column prefix (one wave per column, a wave scan per 64 rows), in LDS
+// when the table fits `lds_words` (1080p: 8 K words, 4K: 33 K), else in global memory.  (A per-row prefix with a loop over the rectangle's rows made
+// the partition test of chunk 1 walk up to 68 rows per partition.)
+__device__ __forceinline__ void unsat_sat_body(const uint8_t* __restrict__ done, int tiles_x, int rows,
+                                               uint32_t* __restrict__ sat, uint32_t* lds, uint32_t lds_words) {
+    const uint32_t sw = (uint32_t)tiles_x + 1, lane = lane_id(), nt = blockDim.x;
+    const uint32_t words = ((uint32_t)rows + 1) * sw;
+    const bool in_lds = words <= lds_words;
+    uint32_t* t = in_lds ? lds : sat;
+    for (uint32_t x = threadIdx.x; x < sw; x += nt) t[x] = 0;  // row 0
+    for (uint32_t r = threadIdx.x >> 6; r < (uint32_t)rows; r += nt >> 6) {
+        uint32_t* row = t + (uint64_t)(r + 1) * sw;
         uint32_t run = 0;
         if (lane == 0) row[0] = 0;
         for (int x0 = 0; x0 < tiles_x; x0 += 64) {
@@ -2234,6 +2241,21 @@ __device__ __forceinline__ void unsat_rows_body(const uint8_t* __restrict__ done
             if (x < tiles_x) row[x + 1] = run + __popcll(b & ((lanemask_lt() << 1) | 1ull));
             run += __popcll(b);
         }
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x >> 6; x < sw; x += nt >> 6) {  // column prefix: a wave per column,
+        uint32_t carry = 0;                                       // lanes over 64 rows at a time
+        for (uint32_t r0 = 1; r0 <= (uint32_t)rows; r0 += 64) {
+            const uint32_t r = r0 + lane;
+            const uint32_t v = r <= (uint32_t)rows ? t[(uint64_t)r * sw + x] : 0u;
+            const uint32_t incl = wave_incl_scan(v) + carry;
+            if (r <= (uint32_t)rows) t[(uint64_t)r * sw + x] = incl;
+            carry = (uint32_t)__shfl((int)incl, 63, 64);
+        }
+    }
+    if (in_lds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < words; i += nt) sat[i] = lds[i];
     }
 }
 
@@ -3177,7 +3199,7 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     FrameCtl* ctl = c.cp.ctl;
     const uint32_t G = gridDim.x, b = blockIdx.x;
     C1_MARK(0);
-    unsat_rows_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat);
+    if (b == 0) unsat_sat_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat, (uint32_t*)lds, (uint32_t)(kChunk1Lds / 4));
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(1);
     c1_parts_body(c.pp, b, G);
@@ -3231,9 +3253,10 @@ __global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
 // frame did): the phases of chunk1_phases at full occupancy with a kernel boundary (~1.5 us) in
 // place of each grid barrier; every launch returns at once when chunk 0 saturated every tile.
 // Binning, per-tile sort and composite are the chunk-0 kernels with chunk-1 parameters.
-__global__ __launch_bounds__(256) void k_c1_rows(Chunk1Params c) {
+__global__ __launch_bounds__(1024) void k_c1_rows(Chunk1Params c) {
+    extern __shared__ uint32_t sat_lds[];
     if (c.cp.ctl->not_done == 0) return;
-    unsat_rows_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat);
+    unsat_sat_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat, sat_lds, c.sat_lds_words);
 }
 __global__ __launch_bounds__(256) void k_c1_parts(ProjParams p) {
     if (p.ctl->not_done == 0) return;
@@ -3504,8 +3527,12 @@ int chunk1_occupancy() {
 }
 void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
     if (c.two_chunks && c.cp.n_tiles > 0) {
-        const unsigned rows_grid = (unsigned)((c.bp.rows + 3) / 4);
-        hipLaunchKernelGGL(k_c1_rows, dim3(rows_grid), dim3(256), 0, s, c);
+        static const bool lds_ok = hipFuncSetAttribute((const void*)k_c1_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(kSatLdsWords * 4)) == hipSuccess;
+        Chunk1Params cr = c;
+        const uint32_t words = (uint32_t)(c.bp.rows + 1) * (uint32_t)(c.bp.tiles_x + 1);
+        cr.sat_lds_words = lds_ok && words <= kSatLdsWords ? words : 0u;  // else the column pass in global memory
+        hipLaunchKernelGGL(k_c1_rows, dim3(1), dim3(1024), (size_t)cr.sat_lds_words * 4, s, cr);
         const unsigned parts = proj_parts(c.pp.n);
         hipLaunchKernelGGL(k_c1_parts, dim3(std::max(1u, (parts + 255) / 256)), dim3(256), 0, s, c.pp);
         hipLaunchKernelGGL(k_c1_records, dim3(kMaxGrid), dim3(256), 0, s, c.pp);
