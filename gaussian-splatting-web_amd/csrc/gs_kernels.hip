@@ -2977,6 +2977,7 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
         cr = st.x; cg = st.y; cb = st.z;
         if (FP16_TARGET) ca = st.w; else T = st.w;
     }
+    if (!FP16_TARGET && !in) T = -1.0f;  // FP32: the pixel test reads liveness from T (as k_composite)
     bool live = in && (FP16_TARGET ? ca < 1.0f : T >= t_min);
     bool wave_live = __any(live);
 
@@ -3040,7 +3041,10 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
         const float qd = __builtin_fmaf(u, u, v * v);
         const float e = l2op - qd;
         const float a = __builtin_amdgcn_exp2f(e);
-        const bool hit = live && fmaxf(fabsf(u), fabsf(v)) <= L && a >= amin;
+        // FP32: one sign, z = min(L - max(|u|,|v|), a - amin, T - t_min) >= 0, each difference exact
+        // in sign (k_composite's test, bit for bit the box, alpha and liveness tests)
+        const bool hit = FP16_TARGET ? live && fmaxf(fabsf(u), fabsf(v)) <= L && a >= amin
+                                     : fminf(fminf(L - fmaxf(fabsf(u), fabsf(v)), a - amin), T - t_min) >= 0.0f;
         if (FP16_TARGET) {
 #pragma clang fp contract(off)
             if (hit) {
@@ -3057,7 +3061,7 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
             cg = __builtin_fmaf(kg, s, cg);
             cb = __builtin_fmaf(kb, s, cb);
             T = T - s;
-            live = live && T >= t_min;
+            live = T >= t_min;  // (pixels off the image: T = -1)
         }
     };
     if (tid == 0) s_sat = 0;
