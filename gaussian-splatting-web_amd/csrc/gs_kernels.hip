@@ -2056,15 +2056,28 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
                 if (i < w) base += s_tmp[i];
                 tot += s_tmp[i];
             }
+            // A thread's ipt = 8 cursors are contiguous: written as two 16-B words when they lie
+            // inside the band and 16-B aligned (lane stride 8 words in single stores is an
+            // 8-way LDS bank conflict), one by one at the band's ends.
+            const uint32_t tf = t0 + (uint32_t)tid * ipt;
+            const bool whole = tf >= t_lo && tf + ipt <= t_hi && ((tf - t_lo) & 3u) == 0;
+            uint32_t cur[ipt];
 #pragma unroll
             for (int k = 0; k < ipt; ++k) {
-                const uint32_t t = t0 + (uint32_t)tid * ipt + k;
+                const uint32_t t = tf + k;
+                cur[k] = 0;
                 if (t >= t_lo && t < t_hi) {
                     const uint32_t bb = min(base, cap);
-                    s_cur[t - t_lo] = bb + row[t];
+                    cur[k] = bb + row[t];
+                    if (!whole) s_cur[t - t_lo] = cur[k];
                     if (part == 0) p.ranges[t] = make_uint2(bb, min(base + v[k], cap));
                 }
                 base += v[k];
+            }
+            if (whole) {
+                uint4* d = reinterpret_cast<uint4*>(s_cur + (tf - t_lo));
+                d[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
+                d[1] = make_uint4(cur[4], cur[5], cur[6], cur[7]);
             }
             carry += tot;
             __syncthreads();
@@ -2289,8 +2302,8 @@ template <class C>
 struct TsSharedT {
     unsigned long long k[C::Cap];
     uint32_t v[C::Cap];
-    uint32_t cnt[C::Buckets];
-    uint32_t start[C::Buckets];
+    alignas(16) uint32_t cnt[C::Buckets];    // a thread's per = Buckets / NT = 4 counters are one
+    alignas(16) uint32_t start[C::Buckets];  // 16-B word (ds_read/write_b128, no stride-4 conflicts)
     unsigned long long red[8];
     uint32_t tmp[8];
 };
@@ -2350,22 +2363,14 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
         }
     }
     __syncthreads();
-    constexpr int per = kTsBuckets / kTsThreads;
-    uint32_t c[per], sum = 0, big = 0;
-#pragma unroll
-    for (int q = 0; q < per; ++q) {
-        c[q] = S.cnt[per * tid + q];
-        sum += c[q];
-        big = max(big, c[q]);
-    }
+    static_assert(kTsBuckets / kTsThreads == 4, "a thread's bucket counters are one uint4");
+    const uint4 c4 = reinterpret_cast<const uint4*>(S.cnt)[tid];
+    const uint32_t sum = c4.x + c4.y + c4.z + c4.w, big = max(max(c4.x, c4.y), max(c4.z, c4.w));
     uint32_t total;
-    uint32_t b = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
-#pragma unroll
-    for (int q = 0; q < per; ++q) {
-        S.start[per * tid + q] = b;
-        S.cnt[per * tid + q] = b;  // scatter cursor
-        b += c[q];
-    }
+    const uint32_t b = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
+    const uint4 st = make_uint4(b, b + c4.x, b + c4.x + c4.y, b + c4.x + c4.y + c4.z);
+    reinterpret_cast<uint4*>(S.start)[tid] = st;
+    reinterpret_cast<uint4*>(S.cnt)[tid] = st;  // scatter cursor
     const bool heavy = __syncthreads_or(big > kTsHeavy);
 #pragma unroll
     for (int j = 0; j < kTsIpt; ++j) {
@@ -2478,12 +2483,10 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
                     if (key >= lo && key - lo <= span) atomicAdd(&S.cnt[(uint32_t)((key - lo) >> s)], 1u);
                 }
                 __syncthreads();
-                uint32_t c[perb], sum = 0;
-#pragma unroll
-                for (int q = 0; q < perb; ++q) {
-                    c[q] = S.cnt[perb * tid + q];
-                    sum += c[q];
-                }
+                static_assert(perb == 4, "a thread's bucket counters are one uint4");
+                const uint4 c4 = reinterpret_cast<const uint4*>(S.cnt)[tid];
+                const uint32_t c[perb] = {c4.x, c4.y, c4.z, c4.w};
+                const uint32_t sum = c4.x + c4.y + c4.z + c4.w;
                 uint32_t total;
                 uint32_t run = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
                 uint32_t fit = 0;
