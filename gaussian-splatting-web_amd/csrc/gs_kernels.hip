@@ -2302,8 +2302,9 @@ template <class C>
 struct TsSharedT {
     unsigned long long k[C::Cap];
     uint32_t v[C::Cap];
-    alignas(16) uint32_t cnt[C::Buckets];    // a thread's per = Buckets / NT = 4 counters are one
-    alignas(16) uint32_t start[C::Buckets];  // 16-B word (ds_read/write_b128, no stride-4 conflicts)
+    alignas(16) uint32_t cnt[C::Buckets];  // a thread's per = Buckets / NT = 4 counters are one 16-B
+                                           // word (ds_read/write_b128, no stride-4 conflicts); after
+                                           // the scatter cnt[b] is bucket b's end = bucket b+1's start
     unsigned long long red[8];
     uint32_t tmp[8];
 };
@@ -2369,7 +2370,6 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
     uint32_t total;
     const uint32_t b = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
     const uint4 st = make_uint4(b, b + c4.x, b + c4.x + c4.y, b + c4.x + c4.y + c4.z);
-    reinterpret_cast<uint4*>(S.start)[tid] = st;
     reinterpret_cast<uint4*>(S.cnt)[tid] = st;  // scatter cursor
     const bool heavy = __syncthreads_or(big > kTsHeavy);
 #pragma unroll
@@ -2385,7 +2385,7 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
 #pragma unroll
         for (int j = 0; j < kTsIpt; ++j) {
             if (j * kTsThreads + tid < (int)n) {
-                const uint32_t b0 = S.start[bk[j]], b1 = bk[j] + 1 < kTsBuckets ? S.start[bk[j] + 1] : n;
+                const uint32_t b0 = bk[j] ? S.cnt[bk[j] - 1] : 0u, b1 = S.cnt[bk[j]];  // bucket bk's [start, end)
                 uint32_t r = b0;
                 for (uint32_t q = b0; q < b1; ++q) r += S.k[q] < k[j] ? 1u : 0u;
                 out[r] = v[j];
