@@ -2377,7 +2377,7 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
         if (j * kTsThreads + tid < (int)n) {
             const uint32_t pos = atomicAdd(&S.cnt[bk[j]], 1u);
             S.k[pos] = k[j];
-            S.v[pos] = v[j];
+            if (heavy) S.v[pos] = v[j];  // the count ranking writes v from registers
         }
     }
     __syncthreads();
