@@ -2335,7 +2335,7 @@ __device__ __forceinline__ void block_minmax64(unsigned long long& mn, unsigned 
         mn = min(mn, s[i]);
         mx = max(mx, s[4 + i]);
     }
-    __syncthreads();
+    // no trailing barrier: the per-tile sort writes s again only after several more barriers
 }
 
 template <class C>
@@ -2351,9 +2351,7 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
     constexpr int kTsThreads = C::NT, kTsIpt = C::IPT;
     constexpr uint32_t kTsBuckets = C::Buckets;
     const int tid = threadIdx.x;
-    const int s = ts_shift<C>(kmax - kmin);
-    for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;
-    __syncthreads();
+    const int s = ts_shift<C>(kmax - kmin);  // S.cnt was zeroed by the caller before block_minmax64's barrier
     uint32_t bk[kTsIpt];
 #pragma unroll
     for (int j = 0; j < kTsIpt; ++j) {
@@ -2455,6 +2453,7 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
                 mx = max(mx, k[j]);
             }
         }
+        for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;  // (ts_segment's counters)
         block_minmax64<kTsThreads>(mn, mx, S.red);
         ts_segment<C>(S, k, v, L, mn, mx, out);
         return;
@@ -2530,7 +2529,8 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
                 mx = max(mx, k[j]);
             }
         }
-        block_minmax64<kTsThreads>(mn, mx, S.red);  // (its barriers order the LDS reads before ts_segment)
+        for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;  // (ts_segment's counters)
+        block_minmax64<kTsThreads>(mn, mx, S.red);  // (its barrier orders the LDS reads before ts_segment)
         ts_segment<C>(S, k, v, nc, mn, mx, out + done_n);
         done_n += nc;
         lo = hi;
