@@ -2442,12 +2442,14 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
     if (L <= kTsCap) {
         unsigned long long mn = ~0ull, mx = 0ull;
 #pragma unroll
-        for (int j = 0; j < kTsIpt; ++j) {
+        for (int j = 0; j < kTsIpt; ++j) {  // every list load in flight before the first key gather
             const uint32_t i = j * kTsThreads + tid;
+            v[j] = i < L ? in[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kTsIpt; ++j) {
             k[j] = 0ull;
-            v[j] = 0u;
-            if (i < L) {
-                v[j] = in[i];
+            if (j * kTsThreads + tid < L) {
                 k[j] = ts_key(p, v[j]);
                 mn = min(mn, k[j]);
                 mx = max(mx, k[j]);
