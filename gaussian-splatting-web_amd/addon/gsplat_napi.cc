@@ -237,11 +237,16 @@ napi_value parse_render(napi_env env, napi_value* argv, RenderArgs* a) {
         if (!get_bytes(env, argv[6], &a->out, &a->out_len))
             return throw_gs(env, GS_ERR_INVALID, "render: out must be a TypedArray or null");
         int row0 = 0, rows = a->H;
-        if (a->opts.tile_row_end > 0)
-            rows = std::min(16 * a->opts.tile_row_end, a->H) - 16 * a->opts.tile_row_begin;
-        else if (a->opts.strip_count > 1)
-            gs_strip_rows(a->H, a->opts.strip_index, a->opts.strip_count, &row0, &rows);
-        const size_t need = (size_t)rows * (size_t)a->W * (a->opts.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
+        bool sized = a->W > 0 && a->H > 0;  // a bad size or range: gs_render reports it, not the size check
+        if (a->opts.tile_row_end > 0 || a->opts.tile_row_begin != 0) {
+            const int TR = (a->H + 15) / 16;
+            sized = sized && a->opts.strip_count == 1 && a->opts.tile_row_begin >= 0 &&
+                    a->opts.tile_row_begin < a->opts.tile_row_end && a->opts.tile_row_end <= TR;
+            if (sized) rows = std::min(16 * a->opts.tile_row_end, a->H) - 16 * a->opts.tile_row_begin;
+        } else if (a->opts.strip_count > 1) {
+            sized = sized && gs_strip_rows(a->H, a->opts.strip_index, a->opts.strip_count, &row0, &rows) == GS_OK;
+        }
+        const size_t need = sized ? (size_t)rows * (size_t)a->W * (a->opts.out_format == GS_OUT_RGBA_F16 ? 8 : 16) : 0;
         if (a->out_len < need) return throw_gs(env, GS_ERR_INVALID, "render: out buffer too small");
     }
     return undefined(env);

@@ -15,11 +15,15 @@
 #include <algorithm>
 #include <atomic>
 #include <array>
+#include <chrono>
 #include <utility>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <memory>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -138,6 +142,33 @@ uint32_t scaled_threshold(uint32_t k, float factor) {
     return t >= kNoSplit - 1 ? kNoSplit : t + 1;
 }
 
+// A device group's member g >= 1 enqueues its strip from a host thread of its own, so a group
+// frame costs the caller about one strip's enqueue instead of G of them (G = 8
+// members enqueued one after another took ~270-400 us of host time, more than one GPU's frame).
+// Hand-off: the caller posts a job number; the worker spins on it for up to kSpinNs after its last
+// job (a frame loop never sleeps) and then blocks on a condition variable; the caller spins until
+// every worker has finished enqueueing (its own strip runs meanwhile), then enqueues the gather.
+struct GroupWorker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<uint32_t> posted{0};    // jobs posted by the caller
+    std::atomic<uint32_t> finished{0};  // jobs the worker finished (rc / msg valid)
+    std::atomic<bool> sleeping{false};
+    std::atomic<bool> quit{false};
+    void (*fn)(void*, int) = nullptr;   // the job: fn(arg, member), set before `posted` moves
+    void* arg = nullptr;
+    int member = 0;
+    int rc = 0;
+    std::string msg;
+    int64_t t_start = 0, t_end = 0;  // the last job's start and end (steady clock, ns; GS_GROUP_TRACE)
+    static constexpr int64_t kSpinNs = 2000000;  // 2 ms
+};
+
+static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 }  // namespace
 
 struct gs_ctx {
@@ -185,6 +216,9 @@ struct gs_ctx {
     std::vector<int> gbounds;          // tile-row boundaries of the members' strips (G + 1), K-balanced
     int gH = 0;                        // the image height gbounds were made for
     uint32_t gframe = 0;               // frames since gbounds were (re)made
+    std::vector<std::unique_ptr<GroupWorker>> workers;  // [member] (g >= 1): its enqueue thread
+    bool group_peer_copy = false;      // GS_GROUP_PEER_COPY=1 at creation: members on device 0 peer-copy
+                                       // their strips too (tests of that path on a one-GPU box)
 };
 
 // Everything one frame writes.  kFrameSets sets, used by frames in turn, each with its own stream
@@ -839,6 +873,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     tsp.out = F.tvB;
     tsp.skey = F.skey;
     tsp.done = nullptr;
+    tsp.scratch = F.bmat;  // kBinParts (256) words per tile, dead once the emission has read them
     tsp.n_tiles = n_tiles;
     {  // lists of more than kTsBigMean entries on average (last frame; the 128-thread shape sorts rounds of 1024): most
        // tiles would take the multi-round path (each round re-reads the whole list), so the
@@ -1088,15 +1123,7 @@ static void quirk_prepare(gs_scene* s, const float* uni, hipStream_t st) {
     s->qdraw = r.second;
 }
 
-// A device group's frame (gs_ctx::members): member g renders tile rows [gbounds[g], gbounds[g+1])
-// of the image -- member 0 straight into `out` (device 0, H rows), member g >= 1 into one of its two
-// strip buffers -- and the strips travel to member 0 only: RCCL send/receive pairs over the
-// communicators of ncclCommInitAll (distinct devices, xGMI), or peer copies (a list that repeats a
-// device: the one-GPU tests).  The transfers run on the members' gather streams, so member g's
-// next frame renders into its other buffer while this frame's strip is sent.  The strips are
-// K-balanced: every kRebalanceFrames frames the boundaries move so that each member's binned
-// entries (plus a per-tile cost) are equal (balance_bounds).  Enqueue only: the image is complete
-// on device 0 in stream order of st0.
+// Group strips are K-balanced (render_group): every kRebalanceFrames frames the boundaries move.
 constexpr uint32_t kRebalanceFrames = 8;
 constexpr double kTileCost = 32.0;  // a tile's fixed cost in binned-entry units (its scan, sort and composite start)
 
@@ -1112,14 +1139,223 @@ static void rebalance_group(gs_ctx* c, gs_scene* s, int W, int TR) {
     }
     std::vector<int> nb(G + 1);
     balance_bounds(G, TR, c->gbounds.data(), cost.data(), nb.data());
+    // a member whose strip grows may bin more entries than its tile lists hold: grow them ahead
+    // (each old strip's entries spread evenly over its rows; 1.5x headroom), instead of letting the
+    // first frame on the new strips overflow and fail
+    for (int g = 0; g < G; ++g) {
+        double est = 0.0;
+        for (int j = 0; j < G; ++j) {
+            const int r0 = std::max(nb[g], c->gbounds[j]), r1 = std::min(nb[g + 1], c->gbounds[j + 1]);
+            const int rows = c->gbounds[j + 1] - c->gbounds[j];
+            if (r1 > r0 && rows > 0) est += (double)s->members[j]->last.k_total * (r1 - r0) / rows;
+        }
+        gs_scene* m = s->members[g];
+        const uint64_t want = (uint64_t)(1.5 * est);
+        bool grow = false;
+        for (const FrameSet& F : m->fs) grow = grow || want > F.kcap;
+        if (!grow) continue;
+        HIPCHK(hipSetDevice(c->members[g]->device));
+        for (FrameSet& F : m->fs) ensure_tile_capacity(F, want);  // (hipFree waits for the frames using them)
+    }
     c->gbounds = nb;
 }
 
+// ---- the group's enqueue threads
+static void worker_loop(GroupWorker* w, int device) {
+    (void)hipSetDevice(device);
+    uint32_t seen = 0;
+    for (;;) {
+        uint32_t p = w->posted.load(std::memory_order_acquire);
+        if (p == seen) {  // spin a while, then sleep until the next post
+            const auto t0 = std::chrono::steady_clock::now();
+            while ((p = w->posted.load(std::memory_order_acquire)) == seen) {
+                __builtin_ia32_pause();
+                if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() >
+                    GroupWorker::kSpinNs)
+                    break;
+            }
+            if (p == seen) {
+                std::unique_lock<std::mutex> lk(w->mu);
+                w->sleeping.store(true);  // (seq_cst, paired with post_job's load: no lost wake-up)
+                w->cv.wait(lk, [&] { return w->quit.load() || w->posted.load() != seen; });
+                w->sleeping.store(false);
+                p = w->posted.load(std::memory_order_acquire);
+            }
+        }
+        if (w->quit.load()) return;
+        seen = p;
+        w->rc = GS_OK;
+        w->msg.clear();
+        w->t_start = now_ns();
+        try {
+            w->fn(w->arg, w->member);
+        } catch (const GsError& e) {
+            w->rc = e.code;
+            w->msg = e.what();
+        } catch (const std::bad_alloc&) {
+            w->rc = GS_ERR_OOM;
+            w->msg = "host allocation failed";
+        } catch (const std::exception& e) {
+            w->rc = GS_ERR_INTERNAL;
+            w->msg = e.what();
+        } catch (...) {
+            w->rc = GS_ERR_INTERNAL;
+            w->msg = "unknown exception";
+        }
+        w->t_end = now_ns();
+        w->finished.store(p, std::memory_order_release);
+    }
+}
+
+static void post_job(GroupWorker* w, void (*fn)(void*, int), void* arg, int member) {
+    w->fn = fn;
+    w->arg = arg;
+    w->member = member;
+    w->posted.fetch_add(1);  // seq_cst: ordered against the worker's `sleeping` store
+    if (w->sleeping.load()) {
+        { std::lock_guard<std::mutex> lk(w->mu); }  // the worker is inside cv.wait (or has left it)
+        w->cv.notify_one();
+    }
+}
+
+// Wait for the worker's last posted job; its error, if any, as (code, message).
+static void join_job(GroupWorker* w, int& rc, std::string& msg) {
+    const uint32_t want = w->posted.load();
+    while (w->finished.load(std::memory_order_acquire) != want) __builtin_ia32_pause();
+    if (w->rc != GS_OK && rc == GS_OK) {
+        rc = w->rc;
+        msg = w->msg;
+    }
+}
+
+static void start_workers(gs_ctx* c) {
+    c->workers.resize(c->members.size());
+    for (size_t g = 1; g < c->members.size(); ++g) {
+        c->workers[g].reset(new GroupWorker());
+        GroupWorker* w = c->workers[g].get();
+        c->workers[g]->th = std::thread(worker_loop, w, c->members[g]->device);
+    }
+}
+
+static void stop_workers(gs_ctx* c) {
+    for (auto& w : c->workers) {
+        if (!w) continue;
+        {
+            std::lock_guard<std::mutex> lk(w->mu);
+            w->quit.store(true);
+            w->posted.fetch_add(1);  // a spinning worker sees a post, then quit
+        }
+        w->cv.notify_one();
+        if (w->th.joinable()) w->th.join();
+    }
+    c->workers.clear();
+}
+
+// One group frame as the members see it (on the caller's stack while render_group runs).
+struct GroupFrame {
+    gs_ctx* c;
+    gs_scene* s;
+    const float* uni;
+    int W, H;
+    gs_opts o;
+    void* out;
+    hipStream_t st0;
+    size_t row_bytes;
+    int buf;
+    std::atomic<bool> m0_enqueued{false};  // member 0's frame is on st0: the members' strips may be waited for there
+};
+
+// How member g's strip reaches the image on device 0.
+enum GroupPath {
+    kGroupDirect = 0,  // member 0, or a member on device 0: it renders straight into its rows of the image
+    kGroupRccl = 1,    // distinct devices: an RCCL send of the strip buffer to member 0
+    kGroupPeer = 2     // another device without RCCL (a list that repeats devices), or forced: a peer copy
+};
+static int group_path(const gs_ctx* c, int g) {
+    if (g == 0) return kGroupDirect;
+    if (!c->comms.empty()) return kGroupRccl;
+    return c->members[g]->device == c->members[0]->device && !c->group_peer_copy ? kGroupDirect : kGroupPeer;
+}
+
+// Member g's part of a group frame, enqueued from its own thread: render its strip -- into its
+// rows of the image (direct), or into its strip buffer `buf` -- and start the strip's way to
+// device 0: an RCCL send or a peer copy on its gather stream, each recording gev_sent[g][buf]
+// ("the strip is in the image / the buffer is free again").
+static void group_member(void* arg, int g) {
+    const GroupFrame& f = *(const GroupFrame*)arg;
+    gs_ctx* c = f.c;
+    const int tb = c->gbounds[g], te = c->gbounds[g + 1];
+    if (tb >= te) return;
+    gs_ctx* m = c->members[g];
+    HIPCHK(hipSetDevice(m->device));
+    gs_opts og = f.o;
+    og.strip_index = 0;
+    og.strip_count = 1;
+    og.tile_row_begin = tb;
+    og.tile_row_end = te;
+    char* img = (char*)f.out + (size_t)tb * kTile * f.row_bytes;
+    const int path = group_path(c, g);
+    if (g == 0) {
+        render_frame(m, f.s->members[0], f.uni, f.W, f.H, og, img, f.st0);
+        return;
+    }
+    // st0 (the caller's stream) waits for this strip behind member 0's frame (so that member 0's
+    // kernels do not wait for it); from this thread, so the caller does not issue G - 1 waits
+    auto st0_waits = [&](hipEvent_t e) {
+        while (!f.m0_enqueued.load(std::memory_order_acquire)) __builtin_ia32_pause();
+        HIPCHK(hipSetDevice(c->members[0]->device));
+        HIPCHK(hipStreamWaitEvent(f.st0, e, 0));
+    };
+    if (path == kGroupDirect) {  // device 0's rows, after the caller's earlier work on the image
+        HIPCHK(hipStreamWaitEvent(m->stream, c->gev_entry, 0));
+        render_frame(m, f.s->members[g], f.uni, f.W, f.H, og, img, m->stream);
+        HIPCHK(hipEventRecord(c->gev_sent[g][f.buf], m->stream));
+        st0_waits(c->gev_sent[g][f.buf]);
+        return;
+    }
+    const size_t need = (size_t)f.H * f.row_bytes;  // any strip fits: the bounds move
+    if (c->gbuf_bytes[g] < need) {
+        HIPCHK(hipDeviceSynchronize());
+        for (void*& p : c->gbuf[g]) {
+            if (p) HIPCHK(hipFree(p));
+            p = nullptr;
+        }
+        c->gbuf_bytes[g] = 0;
+        for (void*& p : c->gbuf[g]) HIPCHK(hipMalloc(&p, need));
+        c->gbuf_bytes[g] = need;
+    }
+    void* dst = c->gbuf[g][f.buf];
+    HIPCHK(hipStreamWaitEvent(m->stream, c->gev_sent[g][f.buf], 0));  // frame f - 2's transfer of it
+    render_frame(m, f.s->members[g], f.uni, f.W, f.H, og, dst, m->stream);
+    HIPCHK(hipEventRecord(c->gev_rendered[g], m->stream));
+    HIPCHK(hipStreamWaitEvent(c->gstream[g], c->gev_rendered[g], 0));
+    const size_t bytes = (size_t)(std::min(te * kTile, f.H) - tb * kTile) * f.row_bytes;
+    if (path == kGroupRccl) {  // member 0's receive is queued by the caller (render_group)
+        const ncclResult_t r = ncclSend(dst, bytes, ncclUint8, 0, c->comms[g], c->gstream[g]);
+        if (r != ncclSuccess) throw GsError(GS_ERR_HIP, std::string("ncclSend: ") + ncclGetErrorString(r));
+    } else {  // peer copy into the image, after the caller's earlier work on it (gev_entry)
+        HIPCHK(hipStreamWaitEvent(c->gstream[g], c->gev_entry, 0));
+        HIPCHK(hipMemcpyPeerAsync(img, c->members[0]->device, dst, m->device, bytes, c->gstream[g]));
+    }
+    HIPCHK(hipEventRecord(c->gev_sent[g][f.buf], c->gstream[g]));
+    if (path == kGroupPeer) st0_waits(c->gev_sent[g][f.buf]);  // (RCCL: st0 waits for member 0's receives)
+}
+
+// A device group's frame (gs_ctx::members): member g renders tile rows [gbounds[g], gbounds[g+1])
+// of the image, every member at once -- member 0 on the caller's thread, member g >= 1 from its own
+// enqueue thread (GroupWorker).  Member 0, and members on device 0, render straight into their rows
+// of `out`; a member on another device renders into one of two strip buffers there
+// (double-buffered: its next frame renders into the other while this one travels) and sends it to
+// device 0 on its gather stream -- RCCL send/receive pairs over the communicators of
+// ncclCommInitAll (distinct devices, xGMI; the caller queues member 0's receives while the members
+// render), or a peer copy (a list that repeats devices).  The strips are K-balanced: every
+// kRebalanceFrames frames the boundaries move so that each member's binned entries (plus a
+// per-tile cost) are equal (balance_bounds).  Enqueue only: the image is complete on device 0 in
+// stream order of st0.
 static void render_group(gs_ctx* c, gs_scene* s, const float* uni, int W, int H, const gs_opts& o, void* out,
                          hipStream_t st0) {
     const int G = (int)c->members.size();
     const int TR = (H + kTile - 1) / kTile;
-    const size_t row_bytes = (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16);
     if (c->gH != H || (int)c->gbounds.size() != G + 1) {  // even strips until statistics arrive
         c->gbounds.assign(G + 1, 0);
         for (int g = 0; g <= G; ++g) c->gbounds[g] = (int)((int64_t)g * TR / G);
@@ -1128,78 +1364,82 @@ static void render_group(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     } else if (++c->gframe % kRebalanceFrames == 0) {
         rebalance_group(c, s, W, TR);
     }
-    const int buf = (int)(c->gframe & 1u);
-    auto stream_of = [&](int g) { return g == 0 ? st0 : c->members[g]->stream; };
+    if (c->workers.size() != (size_t)G) start_workers(c);
+    GroupFrame f{c, s, uni, W, H, o, out, st0, (size_t)W * (o.out_format == GS_OUT_RGBA_F16 ? 8 : 16),
+                 (int)(c->gframe & 1u), {false}};
     const int dev0 = c->members[0]->device;
-    // the transfers into `out` start after the caller's earlier work on it
+    const bool rccl = !c->comms.empty();
+    // the strips land in `out` after the caller's earlier work on it
     HIPCHK(hipSetDevice(dev0));
     HIPCHK(hipEventRecord(c->gev_entry, st0));
-    HIPCHK(hipStreamWaitEvent(c->gstream[0], c->gev_entry, 0));
-    for (int g = 0; g < G; ++g) {
-        const int tb = c->gbounds[g], te = c->gbounds[g + 1];
-        if (tb >= te) continue;
-        gs_ctx* m = c->members[g];
-        HIPCHK(hipSetDevice(m->device));
-        gs_opts og = o;
-        og.strip_index = 0;
-        og.strip_count = 1;
-        og.tile_row_begin = tb;
-        og.tile_row_end = te;
-        void* dst = (char*)out + (size_t)tb * kTile * row_bytes;
-        if (g > 0) {
-            const size_t need = (size_t)H * row_bytes;  // any strip fits: the bounds move
-            if (c->gbuf_bytes[g] < need) {
-                HIPCHK(hipDeviceSynchronize());
-                for (void*& p : c->gbuf[g]) {
-                    if (p) HIPCHK(hipFree(p));
-                    p = nullptr;
-                }
-                c->gbuf_bytes[g] = 0;
-                for (void*& p : c->gbuf[g]) HIPCHK(hipMalloc(&p, need));
-                c->gbuf_bytes[g] = need;
+    static const bool serial = [] {  // GS_GROUP_SERIAL=1: every member from the caller's thread (A/B)
+        const char* e = std::getenv("GS_GROUP_SERIAL");
+        return e && e[0] == '1';
+    }();
+    static const int trace = [] {  // GS_GROUP_TRACE=1: per-member enqueue times to stderr every 200 frames; 2: every frame
+        const char* e = std::getenv("GS_GROUP_TRACE");
+        return e ? std::atoi(e) : 0;
+    }();
+    const int64_t t_post = trace ? now_ns() : 0;
+    if (!serial)
+        for (int g = 1; g < G; ++g) post_job(c->workers[g].get(), group_member, &f, g);
+    int rc = GS_OK;
+    std::string msg;
+    try {
+        if (rccl) {  // member 0's receives, queued while the members render (ordered per peer by frame)
+            HIPCHK(hipStreamWaitEvent(c->gstream[0], c->gev_entry, 0));
+            ncclResult_t r = ncclGroupStart();
+            for (int g = 1; g < G && r == ncclSuccess; ++g) {
+                const int tb = c->gbounds[g], te = c->gbounds[g + 1];
+                if (tb >= te) continue;
+                const size_t bytes = (size_t)(std::min(te * kTile, H) - tb * kTile) * f.row_bytes;
+                r = ncclRecv((char*)out + (size_t)tb * kTile * f.row_bytes, bytes, ncclUint8, g, c->comms[0], c->gstream[0]);
             }
-            dst = c->gbuf[g][buf];
-            HIPCHK(hipStreamWaitEvent(stream_of(g), c->gev_sent[g][buf], 0));  // frame f - 2's send of it
+            const ncclResult_t r2 = ncclGroupEnd();
+            if (r != ncclSuccess || r2 != ncclSuccess)
+                throw GsError(GS_ERR_HIP, std::string("ncclRecv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+            HIPCHK(hipEventRecord(c->gev_gathered, c->gstream[0]));
         }
-        render_frame(m, s->members[g], uni, W, H, og, dst, stream_of(g));
-        if (g > 0) HIPCHK(hipEventRecord(c->gev_rendered[g], stream_of(g)));
+        group_member(&f, 0);
+        f.m0_enqueued.store(true, std::memory_order_release);
+        if (serial)
+            for (int g = 1; g < G; ++g) group_member(&f, g);
+    } catch (const GsError& e) {
+        rc = e.code;
+        msg = e.what();
+    } catch (const std::exception& e) {
+        rc = GS_ERR_INTERNAL;
+        msg = e.what();
+    } catch (...) {
+        rc = GS_ERR_INTERNAL;
+        msg = "unknown exception";
     }
-    if (!c->comms.empty()) {
-        for (int g = 1; g < G; ++g) {
-            HIPCHK(hipSetDevice(c->members[g]->device));
-            HIPCHK(hipStreamWaitEvent(c->gstream[g], c->gev_rendered[g], 0));
-        }
-        ncclResult_t r = ncclGroupStart();
-        for (int g = 1; g < G && r == ncclSuccess; ++g) {
-            const int tb = c->gbounds[g], te = c->gbounds[g + 1];
-            if (tb >= te) continue;
-            const size_t bytes = (size_t)(std::min(te * kTile, H) - tb * kTile) * row_bytes;
-            r = ncclSend(c->gbuf[g][buf], bytes, ncclUint8, 0, c->comms[g], c->gstream[g]);
-            if (r == ncclSuccess)
-                r = ncclRecv((char*)out + (size_t)tb * kTile * row_bytes, bytes, ncclUint8, g, c->comms[0], c->gstream[0]);
-        }
-        const ncclResult_t r2 = ncclGroupEnd();
-        if (r != ncclSuccess || r2 != ncclSuccess)
-            throw GsError(GS_ERR_HIP, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-        for (int g = 1; g < G; ++g) {
-            HIPCHK(hipSetDevice(c->members[g]->device));
-            HIPCHK(hipEventRecord(c->gev_sent[g][buf], c->gstream[g]));
-        }
-    } else {
-        HIPCHK(hipSetDevice(dev0));
-        for (int g = 1; g < G; ++g) {
-            const int tb = c->gbounds[g], te = c->gbounds[g + 1];
-            if (tb >= te) continue;
-            const size_t bytes = (size_t)(std::min(te * kTile, H) - tb * kTile) * row_bytes;
-            HIPCHK(hipStreamWaitEvent(c->gstream[0], c->gev_rendered[g], 0));
-            HIPCHK(hipMemcpyPeerAsync((char*)out + (size_t)tb * kTile * row_bytes, dev0, c->gbuf[g][buf],
-                                      c->members[g]->device, bytes, c->gstream[0]));
-            HIPCHK(hipEventRecord(c->gev_sent[g][buf], c->gstream[0]));
-        }
-    }
+    f.m0_enqueued.store(true, std::memory_order_release);  // (also after an error: the members finish)
+    const int64_t t_m0 = trace ? now_ns() : 0;
+    if (!serial)
+        for (int g = 1; g < G; ++g) join_job(c->workers[g].get(), rc, msg);  // (every job ends before f does)
     HIPCHK(hipSetDevice(dev0));
-    HIPCHK(hipEventRecord(c->gev_gathered, c->gstream[0]));
-    HIPCHK(hipStreamWaitEvent(st0, c->gev_gathered, 0));
+    if (rc != GS_OK) throw GsError(rc, msg);
+    if (rccl) HIPCHK(hipStreamWaitEvent(st0, c->gev_gathered, 0));
+    if (trace && !serial) {
+        static std::vector<double> acc;
+        static int frames = 0;
+        acc.resize(3 * G + 1, 0.0);
+        acc[0] += (t_m0 - t_post) * 1e-3;
+        for (int g = 1; g < G; ++g) {
+            acc[3 * g] += (c->workers[g]->t_start - t_post) * 1e-3;
+            acc[3 * g + 1] += (c->workers[g]->t_end - c->workers[g]->t_start) * 1e-3;
+        }
+        acc[3 * G] += (now_ns() - t_post) * 1e-3;
+        if (++frames == (trace == 2 ? 1 : 200)) {
+            std::fprintf(stderr, "group trace (mean us over %d frames): member 0 %.1f; call %.1f;", frames, acc[0] / frames,
+                         acc[3 * G] / frames);
+            for (int g = 1; g < G; ++g) std::fprintf(stderr, " m%d start +%.1f run %.1f;", g, acc[3 * g] / frames, acc[3 * g + 1] / frames);
+            std::fprintf(stderr, "\n");
+            std::fill(acc.begin(), acc.end(), 0.0);
+            frames = 0;
+        }
+    }
     c->last_scene = s;
 }
 
@@ -1263,6 +1503,10 @@ int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
                     throw GsError(GS_ERR_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
                 }
             }
+            {
+                const char* e = std::getenv("GS_GROUP_PEER_COPY");
+                c->group_peer_copy = e && e[0] == '1';
+            }
             c->gbuf.assign(ndev, {nullptr, nullptr});
             c->gbuf_bytes.assign(ndev, 0);
             c->gstream.assign(ndev, nullptr);
@@ -1274,17 +1518,24 @@ int gs_ctx_create(const int* devices, int ndev, gs_ctx** out) {
                 HIPCHK(hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking));
                 HIPCHK(hipEventCreateWithFlags(&c->gev_rendered[g], hipEventDisableTiming));
                 if (g == 0) {
-                    HIPCHK(hipEventCreateWithFlags(&c->gev_entry, hipEventDisableTiming));
+                    const bool one_dev = std::all_of(devices, devices + ndev, [&](int d) { return d == devices[0]; });
+                    HIPCHK(hipEventCreateWithFlags(&c->gev_entry, one_dev ? hipEventDisableTiming | hipEventDisableSystemFence
+                                                                          : hipEventDisableTiming));
                     HIPCHK(hipEventCreateWithFlags(&c->gev_gathered, hipEventDisableTiming));
                 }
             }
-            for (int g = 1; g < ndev; ++g)  // recorded where the strip is sent: member g's gather
-                for (hipEvent_t& e : c->gev_sent[g]) {  // stream (RCCL) or device 0's (peer copies)
-                    const int d = rccl ? devices[g] : devices[0];
-                    HIPCHK(hipSetDevice(d));
-                    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                    HIPCHK(hipEventRecord(e, c->gstream[rccl ? g : 0]));  // "the buffer is free"
+            (void)rccl;
+            // events that order work on device 0 only need no system-scope fence (its cache
+            // write-back would delay the waiting stream); those waited on across devices keep it
+            for (int g = 1; g < ndev; ++g)  // recorded where the strip is sent: member g's gather stream
+                for (hipEvent_t& e : c->gev_sent[g]) {
+                    HIPCHK(hipSetDevice(devices[g]));
+                    const unsigned fl = devices[g] == devices[0] ? hipEventDisableTiming | hipEventDisableSystemFence
+                                                                 : hipEventDisableTiming;
+                    HIPCHK(hipEventCreateWithFlags(&e, fl));
+                    HIPCHK(hipEventRecord(e, c->gstream[g]));  // "the buffer is free"
                 }
+            start_workers(c);
         } catch (...) {
             gs_ctx_destroy(c);
             throw;
@@ -1325,6 +1576,7 @@ static gs_ctx* create_single(int dev) {
 void gs_ctx_destroy(gs_ctx* c) {
     if (!c) return;
     if (!c->members.empty()) {
+        stop_workers(c);
         while (!c->scenes.empty()) gs_scene_free(c->scenes.back());
         for (size_t g = 0; g < c->members.size(); ++g) {
             (void)hipSetDevice(c->members[g]->device);
@@ -1621,8 +1873,18 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
         if (!out_dev) throw GsError(GS_ERR_INVALID, "null output");
         if (out_bytes < out_bytes_for(W, H, o)) throw GsError(GS_ERR_INVALID, "output buffer too small");
         if (!c->members.empty()) {  // the image (H rows) into out_dev on the first device
+            // every member's pending error is handled (capacities grown) before the first is reported
+            int rc = GS_OK;
+            std::string msg;
             for (gs_scene* m : s->members)
-                if (m->pending_err & (kErrOverflow | kErrBarrier)) check_frame_errors(m);  // (sets m's device)
+                if (m->pending_err & (kErrOverflow | kErrBarrier)) {
+                    const int r = guarded([&] { check_frame_errors(m); return GS_OK; });  // (sets m's device)
+                    if (r != GS_OK && rc == GS_OK) {
+                        rc = r;
+                        msg = gs_last_error();
+                    }
+                }
+            if (rc != GS_OK) throw GsError(rc, msg);
             gs_ctx* m0 = c->members[0];
             HIPCHK(hipSetDevice(m0->device));
             hipStream_t st0 = stream ? (hipStream_t)stream : m0->stream;
@@ -1835,11 +2097,17 @@ int gs_readback_wait(gs_ctx* c, uint32_t ticket) {
 int gs_sync(gs_ctx* c) {
     return guarded([&] {
         if (!c) throw GsError(GS_ERR_INVALID, "null ctx");
-        if (!c->members.empty()) {
+        if (!c->members.empty()) {  // every member synchronised and its errors handled; the first reported
+            int rc = GS_OK;
+            std::string msg;
             for (gs_ctx* m : c->members) {
-                const int rc = gs_sync(m);
-                if (rc != GS_OK) throw GsError(rc, gs_last_error());
+                const int r = gs_sync(m);
+                if (r != GS_OK && rc == GS_OK) {
+                    rc = r;
+                    msg = gs_last_error();
+                }
             }
+            if (rc != GS_OK) throw GsError(rc, msg);
             return GS_OK;
         }
         HIPCHK(hipSetDevice(c->device));
@@ -1871,7 +2139,7 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
                 a.k_chunk1 += m.k_chunk1;
                 a.wide_chunk0 += m.wide_chunk0;
                 a.wide_chunk1 += m.wide_chunk1;
-                a.frames_unsat += m.frames_unsat;
+                a.frames_unsat = std::max(a.frames_unsat, m.frames_unsat);  // frames, not strips (as below)
                 a.frames_chunked = std::max(a.frames_chunked, m.frames_chunked);
                 a.frames_seeded = std::max(a.frames_seeded, m.frames_seeded);
                 a.tile_row_end = std::max(a.tile_row_end, m.tile_row_end);

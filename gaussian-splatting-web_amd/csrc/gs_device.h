@@ -294,10 +294,11 @@ struct BinParams {
 // key(g) = g (slots are depth ranks) or, with skey, (skey[g].x << 32) | skey[g].y.
 struct TileSortParams {
     const uint2* ranges;          // [n_tiles]
-    const uint32_t* in;           // unordered lists (k_bin_emit / k_bin_wide)
+    uint32_t* in;                 // unordered lists (k_bin_emit); scratch of ts_long once it has read them
     uint32_t* out;                // the same lists, each in ascending key order
     const uint2* skey;            // nullable
     const uint8_t* done;          // chunk 1: saturated tiles are skipped (nullable)
+    uint32_t* scratch;            // [n_tiles][256] long lists' bucket ends (the binning's bmat, dead by then)
     int n_tiles;
     int big;                      // chunk 0 with long lists: the 256-thread shape (k_tile_sort_big)
 };

@@ -920,6 +920,8 @@ __device__ __forceinline__ float key_depth(uint32_t k) {  // the float a depth k
     return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : (k ^ 0x80000001u));
 }
 
+constexpr int kSeedMaxCells = 4096;  // cell atomics per sampled Gaussian at most
+
 __global__ __launch_bounds__(256) void k_seed_hist(ProjParams p) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
@@ -970,11 +972,17 @@ __global__ __launch_bounds__(256) void k_seed_hist(ProjParams p) {
         for (int d = kSeedRun / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
         const bool mine = ok && (!same || lane == lead);
         const float add = same ? sum : share;
-        int cells = 0;
-        if (mine)
-            for (int y = y0; y <= y1 && cells < 1024; ++y)
-                for (int x = x0; x <= x1 && cells < 1024; ++x, ++cells)
-                    atomicAdd(&p.seedh[((uint64_t)y * p.seed_cx + x) * kSeedBuckets + b], add);
+        if (mine) {
+            // every cell of the box (a 4K frame has 2040); a box of more than kSeedMaxCells cells
+            // (larger frames) visits every sy-th row, each visited row taking the mass of the rows
+            // it stands for, so the mass the splat adds is its whole share either way
+            const int nx = x1 - x0 + 1, ny = y1 - y0 + 1;
+            const int sy = max(1, (nx * ny + kSeedMaxCells - 1) / kSeedMaxCells);
+            const float addr = add * (float)ny / (float)((ny + sy - 1) / sy);
+            for (int y = y0; y <= y1; y += sy)
+                for (int x = x0; x <= x1; ++x)
+                    atomicAdd(&p.seedh[((uint64_t)y * p.seed_cx + x) * kSeedBuckets + b], addr);
+        }
     }
 }
 
@@ -2419,48 +2427,41 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
     __syncthreads();
 }
 
+// Sort the n <= C::Cap (key, slot) pairs staged in S.k / S.v (after a barrier) into out[0, n).
 template <class C>
-__device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t vb, TsSharedT<C>& S) {
-    constexpr int kTsThreads = C::NT, kTsIpt = C::IPT;
-    constexpr uint32_t kTsCap = C::Cap, kTsBuckets = C::Buckets;
-    const int per = (p.n_tiles + 7) >> 3;  // XCD-banded, as k_composite
-    const int tile = (int)(vb & 7) * per + (int)(vb >> 3);
-    if (tile >= p.n_tiles) return;
-    if (p.done && p.done[tile]) return;
-    const uint2 range = p.ranges[tile];
-    const uint32_t L = range.y - range.x;
-    if (L == 0) return;
-    const uint32_t* __restrict__ in = p.in + range.x;
-    uint32_t* __restrict__ out = p.out + range.x;
+__device__ __forceinline__ void ts_lds_round(TsSharedT<C>& S, uint32_t n, uint32_t* __restrict__ out) {
     const int tid = threadIdx.x;
-    unsigned long long k[kTsIpt];
-    uint32_t v[kTsIpt];
-    if (L == 1) {
-        if (tid == 0) out[0] = in[0];
-        return;
-    }
-    if (L <= kTsCap) {
-        unsigned long long mn = ~0ull, mx = 0ull;
+    unsigned long long k[C::IPT];
+    uint32_t v[C::IPT];
+    unsigned long long mn = ~0ull, mx = 0ull;
 #pragma unroll
-        for (int j = 0; j < kTsIpt; ++j) {  // every list load in flight before the first key gather
-            const uint32_t i = j * kTsThreads + tid;
-            v[j] = i < L ? in[i] : 0u;
+    for (int j = 0; j < C::IPT; ++j) {
+        const uint32_t i = j * C::NT + tid;
+        k[j] = 0ull;
+        v[j] = 0u;
+        if (i < n) {
+            k[j] = S.k[i];
+            v[j] = S.v[i];
+            mn = min(mn, k[j]);
+            mx = max(mx, k[j]);
         }
-#pragma unroll
-        for (int j = 0; j < kTsIpt; ++j) {
-            k[j] = 0ull;
-            if (j * kTsThreads + tid < L) {
-                k[j] = ts_key(p, v[j]);
-                mn = min(mn, k[j]);
-                mx = max(mx, k[j]);
-            }
-        }
-        for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;  // (ts_segment's counters)
-        block_minmax64<kTsThreads>(mn, mx, S.red);
-        ts_segment<C>(S, k, v, L, mn, mx, out);
-        return;
     }
-    // long list: rounds of <= kTsCap consecutive keys
+    for (uint32_t b = tid; b < C::Buckets; b += C::NT) S.cnt[b] = 0;  // (ts_segment's counters)
+    block_minmax64<C::NT>(mn, mx, S.red);  // (its barrier orders the LDS reads before ts_segment)
+    ts_segment<C>(S, k, v, n, mn, mx, out);
+}
+
+// A list of L > C::Cap entries in rounds of <= C::Cap consecutive keys: per round, a bucket
+// histogram of the keys not yet done picks the round's upper bound, the round's elements are
+// gathered into LDS and sorted (ts_segment).  Every round re-reads the whole list, so this is
+// O(L^2 / Cap): ts_long uses it only for one bucket of more than Cap entries (keys packed in a
+// narrow range).  in and out are distinct.
+template <class C>
+__device__ void ts_rounds(const TileSortParams& p, TsSharedT<C>& S, const uint32_t* __restrict__ in,
+                          uint32_t* __restrict__ out, uint32_t L) {
+    constexpr int kTsThreads = C::NT;
+    constexpr uint32_t kTsCap = C::Cap, kTsBuckets = C::Buckets;
+    const int tid = threadIdx.x;
     unsigned long long kmin = ~0ull, kmax = 0ull;
     for (uint32_t i = tid; i < L; i += kTsThreads) {
         const unsigned long long key = ts_key(p, in[i]);
@@ -2518,25 +2519,171 @@ __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t
         }
         __syncthreads();
         const uint32_t nc = S.tmp[4];
+        ts_lds_round<C>(S, nc, out + done_n);
+        done_n += nc;
+        lo = hi;
+    }
+}
+
+
+// A list of L > C::Cap entries (a long list: a tile of a frame whose tiles do not saturate, or chunk
+// 1's), in time linear in L (the rounds of ts_rounds re-read the whole list each, so
+// a one-chunk 50 M / 4K frame spent 8.2 ms in this kernel):
+//   1. the key range; 2. a histogram of 256 buckets of equal key width over it; 3. their starts;
+//   4. a counting scatter of the slots into `out`, grouped by bucket (unordered within one);
+//   5. runs of consecutive buckets of <= C::Cap entries in all, each loaded from `out`, sorted in
+//      LDS (ts_segment) and written back in place.  A single bucket of more than C::Cap entries
+//      is copied to `in` (free once the scatter has read it) and sorted by ts_rounds into `out`.
+// Four reads of the list and its keys per entry, one write of the scatter and one of the sort.
+constexpr int kTsLongBB = 8;
+constexpr uint32_t kTsLongBuckets = 1u << kTsLongBB;
+__device__ __forceinline__ unsigned long long uniform64(unsigned long long x) {
+    return ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+template <class C>
+__device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                        uint32_t L, uint32_t* __restrict__ ends) {  // ends: kTsLongBuckets words of global scratch
+    constexpr int NT = C::NT;
+    constexpr uint32_t Cap = C::Cap;
+    constexpr int PB = (int)kTsLongBuckets / NT;  // buckets per thread (consecutive)
+    static_assert(PB >= 1 && kTsLongBuckets % NT == 0 && kTsLongBuckets <= C::Buckets, "long-list buckets");
+    const int tid = threadIdx.x;
+    unsigned long long kmin = ~0ull, kmax = 0ull;
+    for (uint32_t i = tid; i < L; i += NT) {
+        const unsigned long long key = ts_key(p, in[i]);
+        kmin = min(kmin, key);
+        kmax = max(kmax, key);
+    }
+    for (uint32_t b = tid; b < kTsLongBuckets; b += NT) S.cnt[b] = 0;
+    block_minmax64<NT>(kmin, kmax, S.red);  // (its barrier also orders the zeroed counters)
+    kmin = uniform64(kmin);  // (block-uniform values in scalar registers: the rounds below hold
+    kmax = uniform64(kmax);  // the full set of a round's keys in vector registers)
+    const unsigned long long span = kmax - kmin;
+    const int sh = __builtin_amdgcn_readfirstlane(span == 0 ? 0 : max(0, 64 - (int)__clzll(span) - kTsLongBB));
+    for (uint32_t i = tid; i < L; i += NT)
+        atomicAdd(&S.cnt[(uint32_t)((ts_key(p, in[i]) - kmin) >> sh)], 1u);
+    __syncthreads();
+    {
+        uint32_t c[PB], sum = 0;
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+            c[q] = S.cnt[tid * PB + q];
+            sum += c[q];
+        }
+        uint32_t total;
+        uint32_t run = block_excl_scan<NT>(sum, S.tmp, &total);  // (its barriers order the reads above)
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+            S.cnt[tid * PB + q] = run;  // scatter cursor = the bucket's start
+            run += c[q];
+            ends[tid * PB + q] = run;   // (the rounds read them back: registers would spill)
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < L; i += NT) {
+        const uint32_t g = in[i];
+        const uint32_t pos = atomicAdd(&S.cnt[(uint32_t)((ts_key(p, g) - kmin) >> sh)], 1u);
+        out[pos] = g;
+    }
+    __syncthreads();  // (the scatter's stores are visible to the workgroup: one CU, one L1)
+    uint32_t pos0 = 0;
+    bool heavy = false;
+    while (pos0 < L) {
+        // m = buckets whose end is <= pos0 + Cap (a prefix: the ends ascend); this round is
+        // [pos0, end[m - 1]), or bucket m alone when it holds more than Cap entries
+        const uint32_t lim = pos0 + Cap;
+        uint32_t end[PB], mine = 0;
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+            end[q] = ends[tid * PB + q];
+            mine += end[q] <= lim ? 1u : 0u;
+        }
+        uint32_t m;
+        block_excl_scan<NT>(mine, S.tmp, &m);
+        m = __builtin_amdgcn_readfirstlane(m);
+        // the owner of bucket m - 1 (m >= 1) publishes its end; of bucket m, its end (a heavy bucket)
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+            const uint32_t b = (uint32_t)(tid * PB + q);
+            if (m >= 1 && b == m - 1) S.tmp[5] = end[q];
+            if (b == m) S.tmp[6] = end[q];
+        }
+        if (m == 0 && tid == 0) S.tmp[5] = 0;
+        __syncthreads();
+        uint32_t pos1 = __builtin_amdgcn_readfirstlane(S.tmp[5]);
+        const uint32_t heavy_end = __builtin_amdgcn_readfirstlane(S.tmp[6]);
+        if (pos1 > pos0) {  // one round: staged in LDS, sorted, written back in place
+            const uint32_t n = pos1 - pos0;
+            for (uint32_t i = tid; i < n; i += NT) {
+                const uint32_t g = out[pos0 + i];
+                S.k[i] = ts_key(p, g);
+                S.v[i] = g;
+            }
+            __syncthreads();
+            ts_lds_round<C>(S, n, out + pos0);  // (ends with a barrier)
+        } else {  // bucket m holds more than Cap entries: left for the pass below
+            pos1 = heavy_end;
+            heavy = true;
+        }
+        pos0 = pos1;
+    }
+    if (!heavy) return;
+    // the buckets of more than Cap entries, one at a time: copied to `in`, sorted by ts_rounds
+    for (uint32_t b = 0; b < kTsLongBuckets; ++b) {
+        const uint32_t e0 = __builtin_amdgcn_readfirstlane(b ? ends[b - 1] : 0u);
+        const uint32_t e1 = __builtin_amdgcn_readfirstlane(ends[b]);
+        if (e1 - e0 <= Cap) continue;
+        for (uint32_t i = e0 + tid; i < e1; i += NT) in[i] = out[i];
+        __syncthreads();
+        ts_rounds<C>(p, S, in + e0, out + e0, e1 - e0);
+        __syncthreads();
+    }
+}
+
+template <class C>
+__device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t vb, TsSharedT<C>& S) {
+    constexpr int kTsThreads = C::NT, kTsIpt = C::IPT;
+    constexpr uint32_t kTsCap = C::Cap, kTsBuckets = C::Buckets;
+    const int per = (p.n_tiles + 7) >> 3;  // XCD-banded, as k_composite
+    const int tile = (int)(vb & 7) * per + (int)(vb >> 3);
+    if (tile >= p.n_tiles) return;
+    if (p.done && p.done[tile]) return;
+    const uint2 range = p.ranges[tile];
+    const uint32_t L = range.y - range.x;
+    if (L == 0) return;
+    const uint32_t* __restrict__ in = p.in + range.x;
+    uint32_t* __restrict__ out = p.out + range.x;
+    const int tid = threadIdx.x;
+    unsigned long long k[kTsIpt];
+    uint32_t v[kTsIpt];
+    if (L == 1) {
+        if (tid == 0) out[0] = in[0];
+        return;
+    }
+    if (L <= kTsCap) {
         unsigned long long mn = ~0ull, mx = 0ull;
 #pragma unroll
-        for (int j = 0; j < kTsIpt; ++j) {
+        for (int j = 0; j < kTsIpt; ++j) {  // every list load in flight before the first key gather
             const uint32_t i = j * kTsThreads + tid;
+            v[j] = i < L ? in[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kTsIpt; ++j) {
             k[j] = 0ull;
-            v[j] = 0u;
-            if (i < nc) {
-                k[j] = S.k[i];
-                v[j] = S.v[i];
+            if (j * kTsThreads + tid < L) {
+                k[j] = ts_key(p, v[j]);
                 mn = min(mn, k[j]);
                 mx = max(mx, k[j]);
             }
         }
         for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;  // (ts_segment's counters)
-        block_minmax64<kTsThreads>(mn, mx, S.red);  // (its barrier orders the LDS reads before ts_segment)
-        ts_segment<C>(S, k, v, nc, mn, mx, out + done_n);
-        done_n += nc;
-        lo = hi;
+        block_minmax64<kTsThreads>(mn, mx, S.red);
+        ts_segment<C>(S, k, v, L, mn, mx, out);
+        return;
     }
+    ts_long<C>(p, S, p.in + range.x, out, L, p.scratch + (size_t)tile * kTsLongBuckets);
 }
 
 __global__ __launch_bounds__(TsSmall::NT, 5) void k_tile_sort(TileSortParams p) {

@@ -243,6 +243,19 @@ def synth_aos(n, seed, W=1920, H=1080):
     return out
 
 
+SPARSE_LOGIT_SHIFT = 4.0
+
+
+def synth_aos_sparse(n, seed, W=1920, H=1080):
+    """SURVEY §8d's generator with every opacity logit shifted by -SPARSE_LOGIT_SHIFT (logit ~ N(-4, 2)):
+    a scene whose tiles do not saturate (at bench_uniforms, 6.1 M Gaussians at 1920x1080, no 16x16
+    tile reaches T < 1e-4), so every frame renders every visible splat as one chunk -- the regime
+    of a real capture's sky or background."""
+    a = synth_aos(n, seed, W, H)
+    a.reshape(n, 80)[:, 12] -= np.float32(SPARSE_LOGIT_SHIFT)
+    return a
+
+
 def parse_ply(data):
     """PackedGaussians(arrayBuffer) (src/ply.ts): .ply bytes -> (AoS records as uint8, info dict)."""
     buf = np.frombuffer(bytes(data), np.uint8)

@@ -34,7 +34,9 @@ const FOV = 1.04719755;  // 60 degrees (src/camera.ts:4)
 const GS_ACCUM_FP32 = 0, GS_ACCUM_FP16_TARGET = 1, GS_OUT_RGBA_F32 = 0, GS_OUT_RGBA_F16 = 1;
 // host-readback frames in flight: the event loop's hand-off from the copy's waiting thread back
 // to the frame loop takes ~0.1 ms, so two in flight left the GPU idle between frames
-const kReadbackDepth = Number(process.env.GSPLAT_READBACK_DEPTH || 3);
+// (GSPLAT_READBACK_DEPTH overrides; clamped to [1, 7]: the C library's readback ring holds 8
+// copies, gs_ctx::kReadbacks, and a deeper frame loop would wait on a slot a newer copy reused)
+const kReadbackDepth = Math.min(7, Math.max(1, parseInt(process.env.GSPLAT_READBACK_DEPTH, 10) || 3));
 
 // ---------------------------------------------------------------------------- GpuContext
 class GpuContext {
@@ -45,7 +47,9 @@ class GpuContext {
     }
 
     // deviceIndex: one HIP device, or an array of devices (a device group: the frame is split into
-    // row strips, one per device, gathered with one RCCL all-gather; the image lands on the first)
+    // K-balanced row strips, one per device, and each strip is sent to the first device -- RCCL
+    // send/receive pairs over distinct devices, peer copies when the list repeats one -- where the
+    // image lands)
     static async create(deviceIndex = 0) {
         let n = 0;
         try {

@@ -25,7 +25,7 @@ import numpy as np
 import pytest
 
 import oracle_py as orc
-from test_gpu_parity import image_close_fp32
+from test_gpu_parity import image_close_fp32, webgpu_bar
 
 pytestmark = pytest.mark.gpu
 
@@ -95,6 +95,7 @@ def test_bench_static_sequence(gpu_ctx, bench_scene):
         assert np.array_equal(_bits(im), _bits(one)), "static frame %d differs from its one-chunk render" % k
     ost = _vs_oracle(aos, N3, u, W, H, imgs[-1], "bench_static_last")
     assert n_vis == ost["n_vis"]
+    webgpu_bar(imgs[-1], aos, N3, 16, u, W, H, name="bench_static_last_webgpu")
 
 
 @pytest.mark.timeout(600)
@@ -122,6 +123,7 @@ def test_bench_orbit_sequence(gpu_ctx, bench_scene):
         assert np.array_equal(_bits(im), _bits(one)), "orbit frame %d differs from its one-chunk render" % k
     for k in (15, 45):  # the yaw extremes (+-25 deg): part of the screen off the scene
         _vs_oracle(aos, N3, views[k], W, H, imgs[k], "bench_orbit_%d" % k)
+        webgpu_bar(imgs[k], aos, N3, 16, views[k], W, H, name="bench_orbit_%d_webgpu" % k)
 
 
 @pytest.mark.timeout(600)
@@ -146,6 +148,40 @@ def test_bench_cold_sequence(gpu_ctx, bench_scene):
         assert np.array_equal(_bits(im), _bits(one)), "cold frame %d (view %d) differs from one chunk" % (k, k % 4)
     for k in (1, 3):  # from inside the scene; moved and turned
         _vs_oracle(aos, N3, views[k], W, H, imgs[k], "bench_cold_%d" % k)
+
+
+@pytest.mark.timeout(600)
+def test_bench_sparse_sequence(gpu_ctx):
+    """bench.py's `sparse` scene (gs.synth_aos_sparse: opacity logit ~ N(-4, 2), no tile saturates):
+    8 frames in flight, each bit-identical to its one-chunk render and to a frame forced into two
+    chunks (chunk 1 then composites every tile, its long lists sorted by ts_long); the last frame
+    against the fp32 oracle and the WebGPU stand-in (fp16-target oracle)."""
+    W, H, n = W3, H3, N3
+    aos = gs.synth_aos_sparse(n, 6, W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    u = gs.bench_uniforms(W, H)
+    head = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=2)
+    bufs = [gs.DeviceBuffer(W * H * 8) for _ in range(8)]
+    gpu_ctx.timings_reset()
+    imgs = _frames(sc, gpu_ctx, [u] * 8, W, H, head, bufs)
+    st = gpu_ctx.timings()
+    for b in bufs:
+        b.free()
+    assert st["frames_rendered"] == 8
+    # fewer than 20 % of the tiles saturate (alpha = 1 in f16 at every pixel), so after the seeded
+    # first frames (no history) every frame is one chunk
+    a = imgs[-1][:H // 16 * 16, :W // 16 * 16, 3].reshape(H // 16, 16, W // 16, 16)
+    assert (a == 1.0).all(axis=(1, 3)).mean() < 0.2
+    assert st["frames_chunked"] <= 3 and st["chunk_fraction"] == 1.0, st
+    one = _one_chunk(sc, u, W, H)
+    split = sc.render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, chunk_fraction=0.25))
+    assert gpu_ctx.timings()["k_chunk1"] > 0
+    assert np.array_equal(_bits(split), _bits(one)), "sparse frame split into two chunks differs"
+    for k, im in enumerate(imgs):
+        assert np.array_equal(_bits(im), _bits(one)), "sparse frame %d differs from its one-chunk render" % k
+    _vs_oracle(aos, n, u, W, H, imgs[-1], "bench_sparse_last")
+    webgpu_bar(imgs[-1], aos, n, 16, u, W, H, name="bench_sparse_webgpu")
+    sc.close()
 
 
 @pytest.mark.timeout(900)

@@ -16,7 +16,7 @@ import pytest
 
 import oracle_py as orc
 from conftest import camera, load_scene
-from test_gpu_parity import image_close_fp16, image_close_fp32
+from test_gpu_parity import image_close_fp16, image_close_fp32, webgpu_bar
 
 pytestmark = pytest.mark.gpu
 
@@ -39,6 +39,9 @@ def test_config1_pc_short_1280x720(gpu_ctx, cam):
     ref16, _ = orc.render(aos, n, nsh, u, W, H, accum=1, t_min=0.0)
     r = image_close_fp16(img16.astype(np.float32), ref16)
     assert r[2], r
+    # the bench's timed mode (fp32 accumulation, t_min 1e-4, f16 out) against the WebGPU stand-in
+    imgb = sc.render(u, W, H, gs.make_opts(t_min=1e-4, out_format=gs.GS_OUT_RGBA_F16))
+    webgpu_bar(imgb, aos, n, nsh, u, W, H, name="pc_short_720_bench_" + cam)
 
 
 @pytest.mark.timeout(300)
@@ -61,6 +64,10 @@ def test_config3_6m_1080p_full_frame(gpu_ctx):
     ref16, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=1, t_min=1e-4)
     r = image_close_fp16(img16.astype(np.float32), ref16)
     assert r[2], r
+    # the mode bench.py times (fp32 accumulation, t_min 1e-4, f16 out) against the WebGPU
+    # stand-in (fp16-target oracle, no cutoff)
+    imgb = sc.render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16))
+    webgpu_bar(imgb, aos, n, 16, u, W, H, name="cfg3_6m_bench")
 
 
 @pytest.mark.timeout(600)

@@ -87,8 +87,82 @@ def test_group_arguments():
         assert e.value.code == gs.GS_ERR_UNSUPPORTED
 
 
+def _group_burst_and_error(devices, gather):
+    """A group's render_device burst of 20 frames in flight on a top-heavy scene (two rebalances of
+    the strips, both strip buffers of every member alternating), every frame bit-identical to the
+    single-device frame; then a frame error (tile-list overflow on huge splats) reported by a later
+    call, and clean, bit-identical frames after it.  Each member enqueues from its own host thread."""
+    W, H, n = 640, 480, 150_000
+    aos = _top_heavy_scene(n, 11, W, H)
+    F16 = gs.GS_OUT_RGBA_F16
+    views = [gs.orbit_uniforms(W, H, k) for k in range(0, 40, 2)]
+    with gs.Context(0) as ctx:
+        one = gs.Scene(ctx, aos, n, 16)
+        refs = [one.render(u, W, H, gs.make_opts(out_format=F16)) for u in views]
+    with gs.Context(devices) as gc:
+        assert gc.info() == (len(devices), gather)
+        sc = gs.Scene(gc, aos, n, 16)
+        bufs = [gs.DeviceBuffer(H * W * 8) for _ in range(len(views))]
+        for u, b in zip(views, bufs):
+            sc.render_device(u, W, H, b.ptr.value, b.nbytes, None, gs.make_opts(out_format=F16))
+        gc.sync()
+        assert gc.timings()["frames_rendered"] >= len(views)
+        for k, b in enumerate(bufs):
+            got = np.empty((H, W, 4), np.float16)
+            b.to_host(got)
+            assert np.array_equal(got.view(np.uint16), refs[k].view(np.uint16)), (k, gc.strips())
+        # an induced frame error: every splat's quad covers the screen, so every member's tile
+        # lists overflow (12 000 x 1200 tiles; a member starts with ~1 M entries of capacity)
+        m = 12000
+        big = gs.synth_aos(m, 41, W, H).reshape(m, 80)
+        big[:, 4:7] = np.abs(big[:, 2:3]) * 2.0
+        big[:, 12] = 0.0
+        bsc = gs.Scene(gc, big.reshape(-1), m, 16)
+        u = gs.bench_uniforms(W, H)
+        o = gs.make_opts(out_format=F16, chunk_fraction=1.0)
+        errors = []
+        for _ in range(4):
+            try:
+                bsc.render_device(u, W, H, bufs[0].ptr.value, bufs[0].nbytes, None, o)
+            except gs.GsError as e:
+                errors.append(str(e))
+        try:
+            gc.sync()
+        except gs.GsError as e:
+            errors.append(str(e))
+        assert errors and all("capacity" in e for e in errors), errors
+        with gs.Context(0) as ctx:
+            want = gs.Scene(ctx, big.reshape(-1), m, 16).render(u, W, H, o)
+        for b in bufs[:3]:
+            bsc.render_device(u, W, H, b.ptr.value, b.nbytes, None, o)
+        gc.sync()
+        for b in bufs[:3]:
+            got = np.empty((H, W, 4), np.float16)
+            b.to_host(got)
+            assert np.array_equal(got.view(np.uint16), want.view(np.uint16))
+        # and the first scene renders on after the error
+        sc.render_device(views[3], W, H, bufs[0].ptr.value, bufs[0].nbytes, None, gs.make_opts(out_format=F16))
+        gc.sync()
+        got = np.empty((H, W, 4), np.float16)
+        bufs[0].to_host(got)
+        assert np.array_equal(got.view(np.uint16), refs[3].view(np.uint16))
+        for b in bufs:
+            b.free()
+
+
+@pytest.mark.parametrize("peer", [False, True])
+def test_group_burst_and_frame_error_one_device(peer, monkeypatch):
+    """The burst / frame-error sequence on a group that repeats device 0: its members render
+    straight into their rows of the image, or (GS_GROUP_PEER_COPY=1) into strip buffers that are
+    peer-copied into it -- the path of members on another device without RCCL."""
+    if peer:
+        monkeypatch.setenv("GS_GROUP_PEER_COPY", "1")
+    _group_burst_and_error([0, 0, 0, 0], "peer_copy")
+
+
 def test_group_distinct_devices_use_rccl():
-    """With two or more GPUs the group gathers with RCCL (not reachable on a one-GPU box)."""
+    """With two or more GPUs the group gathers with RCCL (not reachable on a one-GPU box): a
+    synchronous frame, then the burst / frame-error sequence over every device of the box (up to 8)."""
     if gs.device_count() < 2:
         pytest.skip("one GPU")
     W, H, n = 640, 480, 100_000
@@ -99,6 +173,7 @@ def test_group_distinct_devices_use_rccl():
         a = gs.Scene(ctx, aos, n, 16).render(u, W, H)
         b = gs.Scene(gc, aos, n, 16).render(u, W, H)
         assert np.array_equal(a, b)
+    _group_burst_and_error(list(range(min(8, gs.device_count()))), "rccl")
 
 
 def test_chunk1_grid_is_resident(gpu_ctx):

@@ -183,6 +183,40 @@ def test_tile_order_with_equal_keys(gpu_ctx, depths):
     assert r[2], r
 
 
+@pytest.mark.parametrize("plane_frac", [0.0, 0.7])
+def test_tile_order_long_lists(gpu_ctx, plane_frac):
+    """Tile lists of thousands of entries (a faint scene: ~3500 per tile), longer than one sorting
+    round: ts_long (bucket scatter, then runs of buckets sorted in place) -- and, with 70 % of the
+    Gaussians on one depth plane, a bucket of more than a round of keys, which ts_long hands to
+    ts_rounds.  The first frame sorts with the 128-thread shape (rounds of 1024), the second with
+    the 256-thread shape (its last frame's lists averaged > 800 entries; rounds of 2048).  Every
+    tile's list must be the stable global order restricted to the tile."""
+    W, H, n = 320, 240, 800_000
+    rng = np.random.default_rng(5)
+    aos = gs.synth_aos(n, 81, W, H).reshape(n, 80)
+    aos[:, 12] -= 4.0  # faint: long lists, nothing saturates
+    if plane_frac:
+        m = rng.random(n) < plane_frac
+        d = -aos[m, 2]
+        aos[m, 0] *= np.float32(8.0) / d
+        aos[m, 1] *= np.float32(8.0) / d
+        aos[m, 2] = -8.0
+    aos = aos.reshape(-1)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    sp = orc.project(aos.view(np.uint8), n, 16, u, W, H)
+    imgs = []
+    for _ in range(2):
+        imgs.append(sc.render(u, W, H, gs.make_opts(chunk_fraction=1.0, t_min=0.0)))
+        rg, en = check_tile_lists(sc, sp, W, H, full_sets=False)
+        lens = rg[:, 1] - rg[:, 0]
+        assert lens.max() > 2048 and np.median(lens) > 1024, (lens.max(), np.median(lens))
+    assert np.array_equal(imgs[0], imgs[1])
+    ref, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=0.0)
+    r = image_close_fp32(imgs[0], ref, name="long_lists_%g" % plane_frac)
+    assert r[2], r
+
+
 # ------------------------------------------------------------------------------- ref_quirks
 def test_keyed_slots_rule():
     assert orc.keyed_slots(62) == 62 and orc.keyed_slots(100) == 96 and orc.keyed_slots(1003) == 1000

@@ -48,6 +48,17 @@ def image_close_fp16(img, ref):
     return mse, good, mse < 1e-5 and good >= 0.999
 
 
+def webgpu_bar(img16, aos, n, nsh, u, W, H, name=None):
+    """The north star's bar for the mode bench.py times (fp32 accumulation, t_min 1e-4, f16 out)
+    against the declared WebGPU stand-in: the oracle's rgba16float-target mode with no cutoff
+    (src/simple_render.ts:455-471 "under" blend, :499-505 rgba16float target): per-pixel MSE < 1e-5
+    over RGBA and >= 99.9 % of pixels within 2e-2 (image_close_fp16)."""
+    ref16, _ = orc.render(np.ascontiguousarray(aos).view(np.uint8), n, nsh, u, W, H, accum=1, t_min=0.0)
+    r = image_close_fp16(np.asarray(img16).astype(np.float32), ref16)
+    assert r[2], (name, r)
+    return r
+
+
 # ------------------------------------------------------------------------------- sort
 @pytest.mark.parametrize("n", [1, 7, 100, 4095, 4096, 4097, 65536 + 13, 1_000_003])
 def test_sort_pairs_exact(gpu_ctx, n):
