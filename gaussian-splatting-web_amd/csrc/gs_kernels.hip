@@ -2315,7 +2315,21 @@ struct TsSharedT {
                                            // the scatter cnt[b] is bucket b's end = bucket b+1's start
     unsigned long long red[8];
     uint32_t tmp[8];
+    uint32_t any[C::NT / 64];              // block_any's per-wave flags
 };
+
+// A workgroup-wide OR with a barrier (as __syncthreads_or, whose library form reads the 3-D
+// work-item ids and so kept two more values live through the sort: scratch spills).
+template <int NT>
+__device__ __forceinline__ bool block_any(bool v, uint32_t* s) {
+    const bool w = __any(v);
+    if (lane_id() == 0) s[threadIdx.x >> 6] = w ? 1u : 0u;
+    __syncthreads();
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) r |= s[i];
+    return r != 0;  // (no trailing barrier: a caller that writes s again before its next barrier
+}                   // alternates between two flag arrays)
 using TsShared = TsSharedT<TsBig>;
 
 __device__ __forceinline__ unsigned long long ts_key(const TileSortParams& p, uint32_t g) {
@@ -2377,7 +2391,7 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
     const uint32_t b = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
     const uint4 st = make_uint4(b, b + c4.x, b + c4.x + c4.y, b + c4.x + c4.y + c4.z);
     reinterpret_cast<uint4*>(S.cnt)[tid] = st;  // scatter cursor
-    const bool heavy = __syncthreads_or(big > kTsHeavy);
+    const bool heavy = block_any<kTsThreads>(big > kTsHeavy, S.any);
 #pragma unroll
     for (int j = 0; j < kTsIpt; ++j) {
         if (j * kTsThreads + tid < (int)n) {
@@ -2779,6 +2793,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                                                        // producing wave, tail: the null record)
     __shared__ uint32_t sN[2][2][kBands][2];           // per half, band, producing wave: list length
     __shared__ uint32_t s_sat;                    // depth key of the splat that saturated the last wave
+    __shared__ uint32_t s_any[3][2];              // block_any flags: batches by parity, the tile's end
     const int tid = threadIdx.x;
     if (p.mode == kCompSecond && p.done[tile]) return;
 #ifdef GS_COMP_DIAG
@@ -3017,7 +3032,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
             }
         }
         if (b + 1 < nb) park(cur ^ 1);
-        if (__syncthreads_count(wave_live) == 0) break;
+        if (!block_any<128>(wave_live, s_any[b & 1])) break;
     }
 #ifdef GS_COMP_DIAG
     if (lane == 0 && tile < 16384)
@@ -3037,7 +3052,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         g_comp_time[tile][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
     }
 #endif
-    const bool tile_done = __syncthreads_count(live0 || live1) == 0;
+    const bool tile_done = !block_any<128>(live0 || live1, s_any[2]);
     if (tile_done && tid == 0 && n > 0) {  // saturation statistics for the chunk controller
         StatShard* sh = p.stats + tile % kStatShards;
         atomicAdd(&sh->sat_hist[sat_bucket(s_sat, p.sat_base)], 1u);
@@ -3095,6 +3110,7 @@ struct CompQShared {
     uint16_t sL[2][4][kCompBatchQ];  // per quarter: LDS byte offsets of the records in sR, segment = producing wave
     uint32_t sN[2][4][4];           // per quarter, per producing wave: list length
     uint32_t s_sat;
+    uint32_t any[3][4];             // block_any flags: batches by parity, the tile's end
 };
 
 template <bool FP16_TARGET>
@@ -3254,9 +3270,9 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
             }
         }
         if (b + 1 < nb) park(cur ^ 1);
-        if (__syncthreads_count(wave_live) == 0) break;
+        if (!block_any<256>(wave_live, S.any[b & 1])) break;
     }
-    const bool tile_done = __syncthreads_count(live) == 0;
+    const bool tile_done = !block_any<256>(live, S.any[2]);
     if (tile_done && tid == 0 && n > 0) {
         StatShard* sh = p.stats + tile % kStatShards;
         atomicAdd(&sh->sat_hist[sat_bucket(s_sat, p.sat_base)], 1u);
