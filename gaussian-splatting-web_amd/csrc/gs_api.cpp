@@ -316,6 +316,11 @@ struct gs_scene {
 };
 
 static constexpr size_t kHistWords = kHistShards * 256;
+// A diagnostics switch read once from the environment ("1" = on).
+static bool gs_env_flag(const char* name) {
+    const char* e = std::getenv(name);
+    return e && e[0] == '1';
+}
 // Largest scene for which the reference's init-sort dispatch is valid: max(N/8, 8) workgroups
 // <= 65535 (src/renderer.ts:306; beyond it WebGPU rejects the dispatch and no key is written).
 static constexpr uint64_t kQuirkMaxN = 65535ull * 8;
@@ -677,7 +682,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     // events measure that stage alone.
     const hipStream_t cst = st;
     st = F.stream;
-    HIPCHK(hipStreamWaitEvent(st, F.ev_out, 0));  // the set's last frame ended (normally long ago)
+    {  // the set's last frame ended (normally long ago: then the host skips the wait, ~3 us of enqueue)
+        const hipError_t q = hipEventQuery(F.ev_out);
+        if (q == hipErrorNotReady) HIPCHK(hipStreamWaitEvent(st, F.ev_out, 0));
+        else HIPCHK(q);
+    }
     if (o.timing == 1) HIPCHK(hipStreamWaitEvent(st, s->fs[s->last_fs].ev_out, 0));
     collect_stats(s, false);
     const int slot = s->stat_cur;  // this frame's statistics slot
@@ -809,6 +818,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.sidx = F.sidx;
     pp.wlist = F.wlist;
     pp.wide_tiles = wide_tiles(n_tiles);
+    static const bool no_fuse = gs_env_flag("GS_NO_FUSE_PARTS");  // (A/B)
+    pp.fuse_parts = n_tiles <= kDeepTiles && !no_fuse ? 1 : 0;
     if (seeded) {
         pp.thresh = kNoSplit;
         pp.thresh_dev = &F.ctl->seed_T;
