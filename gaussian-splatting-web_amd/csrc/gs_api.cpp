@@ -316,11 +316,7 @@ struct gs_scene {
 };
 
 static constexpr size_t kHistWords = kHistShards * 256;
-// A diagnostics switch read once from the environment ("1" = on).
-static bool gs_env_flag(const char* name) {
-    const char* e = std::getenv(name);
-    return e && e[0] == '1';
-}
+
 // Largest scene for which the reference's init-sort dispatch is valid: max(N/8, 8) workgroups
 // <= 65535 (src/renderer.ts:306; beyond it WebGPU rejects the dispatch and no key is written).
 static constexpr uint64_t kQuirkMaxN = 65535ull * 8;
@@ -818,8 +814,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.sidx = F.sidx;
     pp.wlist = F.wlist;
     pp.wide_tiles = wide_tiles(n_tiles);
-    static const bool no_fuse = gs_env_flag("GS_NO_FUSE_PARTS");  // (A/B)
-    pp.fuse_parts = n_tiles <= kDeepTiles && !no_fuse ? 1 : 0;
     if (seeded) {
         pp.thresh = kNoSplit;
         pp.thresh_dev = &F.ctl->seed_T;

@@ -206,7 +206,6 @@ struct ProjParams {
     uint32_t seed_base;       // depth bucket 0 = keys from (seed_base << kSatShift): the near plane
     int seed_cx, seed_cy;     // coarse cells (kSeedCell px) across the frame / strip
     float seed_tau;           // alpha mass per pixel taken as saturation
-    int fuse_parts;           // small frames: k_cull tests the partitions itself (no k_part_list)
 };
 
 // Coarse depth estimate of a seeded frame: sampled Gaussians' alpha mass op * 2 pi sigma^2 by

@@ -1040,12 +1040,6 @@ __global__ __launch_bounds__(1024) void k_seed_pick(ProjParams p) {
     }
 }
 
-// FUSED (small frames: row strips): the partition test of k_part_list in the same launch -- every
-// workgroup tests the partitions blockIdx.x, + gridDim.x, ... itself (interleaved, so the
-// partitions a strip keeps, which cluster in Morton order, spread over the workgroups), one
-// launch fewer on a strip frame's chain.  Full frames keep k_part_list (a compacted list gives
-// the cull's workgroups equal shares of the surviving partitions).
-template <bool FUSED>
 __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
     __shared__ unsigned long long s_mask[kProjRounds][kProjThreads / 64];
@@ -1058,19 +1052,11 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = proj_parts(p.n), ucap = unit_shard_cap(parts);
     KT_MARK(0, 0, 0);
-    const uint32_t nl = FUSED ? parts : p.ctl->c0_parts;  // the partitions k_part_list kept
+    const uint32_t nl = p.ctl->c0_parts;  // the partitions k_part_list kept
     const uint32_t T = frame_thresh(p);
-    if (FUSED && blockIdx.x == 0 && tid == 0) p.ctl->frame_T = T;
     uint32_t kt_items = 0;
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
-        const uint32_t part = FUSED ? j : p.plist0[j];
-        if (FUSED) {  // (k_part_list's test and zeroing; uniform over the workgroup)
-            if (tid == 0) p.c1[part] = 0;
-            if (!part_maybe(p, p.bounds[part], row_lo, row_hi, T)) {
-                if (tid == 0) p.c0[part] = 0;
-                continue;
-            }
-        }
+        const uint32_t part = p.plist0[j];
         if (kt_items++ == 0) KT_MARK(0, 1, part);
         const uint32_t p0 = part * kProjTile;
         float4 c[kProjRounds];
@@ -3615,13 +3601,9 @@ void launch_project(const ProjParams& p, hipStream_t s) {
 #ifndef GS_PROJ_GRID
 #define GS_PROJ_GRID 1536
 #endif
+    hipLaunchKernelGGL(k_part_list, dim3((parts + 255) / 256), dim3(256), 0, s, p);
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(GS_CULL_GRID, parts));
-    if (p.fuse_parts) {
-        hipLaunchKernelGGL(k_cull<true>, dim3(grid), dim3(kProjThreads), 0, s, p);
-    } else {
-        hipLaunchKernelGGL(k_part_list, dim3((parts + 255) / 256), dim3(256), 0, s, p);
-        hipLaunchKernelGGL(k_cull<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
-    }
+    hipLaunchKernelGGL(k_cull, dim3(grid), dim3(kProjThreads), 0, s, p);
     const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(GS_PROJ_GRID, (uint64_t)parts * kProjRounds));
     if (p.shq == 12)
         hipLaunchKernelGGL(k_project<true>, dim3(ugrid), dim3(kProjThreads), 0, s, p);
