@@ -120,7 +120,7 @@ def cpu_baseline(aos, n, W, H, u, budget_s=10.0, max_frames=10):
                                                                        time.perf_counter() - t_all)}
 
 
-def node_fps(n, seed, W, H, frames=100):
+def node_fps(n, seed, W, H, frames=300):
     """The Node drop-in's frame rate (tools/node_fps.js: the reference's Renderer frame loop through
     the N-API addon, same scene and camera; device-resident frames and host readback), or None
     when node or the addon is absent."""

@@ -8,6 +8,10 @@
 // Usage: node tools/node_fps.js <n> <seed> <W> <H> <frames>   -> one JSON line
 const path = require('path');
 const gs = require(path.join(__dirname, '..', 'gaussian-splatting-web_amd', 'js'));
+// warm-up frames before timing: the chunk controller's statistics reach the host a few frames
+// late, so the first frames of a scene run with a seeded or a stale split (with 5 warm-up frames
+// and 100 timed ones the Node line read ~0.43 ms per frame against ~0.30 ms at steady state)
+const kWarm = 20;
 
 async function run(gaussians, W, H, frames, options) {
     const a = gs.addon();
@@ -17,7 +21,7 @@ async function run(gaussians, W, H, frames, options) {
     const icam = new gs.HeadlessCamera(cam);
     let drawn = 0;
     icam.getCamera = function () {
-        if (++drawn >= frames + 5) this.dirty = false;
+        if (++drawn >= frames + kWarm) this.dirty = false;
         return this.camera;
     };
     const context = await gs.Renderer.requestContext(gaussians, 0);
@@ -27,8 +31,8 @@ async function run(gaussians, W, H, frames, options) {
         canvas.onError = reject;
         canvas.onFrame = (r) => {
             seen++;
-            if (seen === 5) t0 = process.hrtime.bigint();  // 5 warm-up frames
-            if (seen >= frames + 5) { t1 = process.hrtime.bigint(); resolve(r); }
+            if (seen === kWarm) t0 = process.hrtime.bigint();  // warm-up frames (bench.py's count)
+            if (seen >= frames + kWarm) { t1 = process.hrtime.bigint(); resolve(r); }
         };
     });
     const renderer = new gs.Renderer(canvas, icam, gaussians, context, null, options);
