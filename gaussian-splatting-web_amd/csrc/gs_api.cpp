@@ -253,6 +253,7 @@ struct FrameSet {
     uint32_t* bmat = nullptr;           // [kBinParts][n_tiles] binning partition counts / offsets
     uint32_t* tbase = nullptr;          // [n_tiles] tile totals, then list begins
     uint8_t* done = nullptr;
+    uint32_t* c1tiles = nullptr;  // chunk 1: the tiles chunk 0 left unsaturated, compact
     uint32_t* sat = nullptr;            // (strip rows + 1) x (tiles_x + 1), then the bitmask
     size_t sat_cap = 0;
     int tiles_cap = 0;
@@ -375,12 +376,14 @@ static void ensure_tiles(FrameSet& F, int n_tiles) {
     if (n_tiles <= F.tiles_cap && F.ranges) return;
     dev_free(F.ranges);
     dev_free(F.done);
+    dev_free(F.c1tiles);
     dev_free(F.bmat);
     dev_free(F.tbase);
     dev_free(F.order);
     dev_alloc(F.ranges, (size_t)n_tiles);
     dev_alloc(F.order, (size_t)n_tiles);
     dev_alloc(F.done, (size_t)n_tiles);
+    dev_alloc(F.c1tiles, (size_t)n_tiles);
     dev_alloc(F.bmat, (size_t)kBinParts * n_tiles);
     dev_alloc(F.tbase, (size_t)n_tiles);
     F.tiles_cap = n_tiles;
@@ -901,6 +904,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     cp.mode = two_chunks ? kCompFirst : kCompSingle;
     cp.state = F.state;
     cp.done = F.done;
+    cp.c1tiles = two_chunks ? F.c1tiles : nullptr;
     cp.ctl = F.ctl;
     cp.stats = F.stats;
     cp.sat_base = s->have_krange ? (s->key_lo >> kSatShift) : 0u;
@@ -938,6 +942,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.bp.order = nullptr;
         c1.tp = tsp;
         c1.tp.done = F.done;
+        c1.tp.c1tiles = cp.c1tiles;
+        c1.tp.c1_n = &F.ctl->not_done;
         c1.cp = cp;
         c1.cp.mode = kCompSecond;
         c1.cp.order = nullptr;
@@ -1803,6 +1809,7 @@ void gs_scene_free(gs_scene* s) {
         dev_free(F.tbase);
         dev_free(F.order);
         dev_free(F.done);
+        dev_free(F.c1tiles);
         dev_free(F.sat);
         dev_free(F.state);
         dev_free(F.seedh);

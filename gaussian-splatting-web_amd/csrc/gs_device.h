@@ -301,6 +301,10 @@ struct TileSortParams {
     uint32_t* scratch;            // [n_tiles][256] long lists' bucket ends (the binning's bmat, dead by then)
     int n_tiles;
     int big;                      // chunk 0 with long lists: the 256-thread shape (k_tile_sort_big)
+    // chunk 1: the tiles chunk 0 left unsaturated, a compact list (CompositeParams::c1tiles) of
+    // *c1_n entries; the launch walks it instead of every tile (nullable)
+    const uint32_t* c1tiles;
+    const uint32_t* c1_n;
 };
 
 constexpr uint32_t kTsBigMean = 800;  // mean chunk-0 list length from which k_tile_sort_big sorts chunk 0
@@ -323,6 +327,9 @@ struct CompositeParams {
     uint32_t sat_base;            // sat_bucket's base
     void* out;                    // rows_padded x W pixels
     int out_f16;
+    // the tiles chunk 0 leaves unsaturated: appended by the first pass (kCompFirst, position = its
+    // FrameCtl::not_done ticket) and walked by chunk 1's per-tile sort and composite (kCompSecond)
+    uint32_t* c1tiles;
 };
 
 struct Chunk1Params {

@@ -2657,13 +2657,29 @@ __device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __re
 }
 
 template <class C>
+__device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const int tile, TsSharedT<C>& S);
+
+// Workgroup item vb -> tile: XCD-banded as k_composite, or the compact list of chunk 1's tiles
+// (c1tiles set).
+template <class C>
 __device__ __forceinline__ void tile_sort_body(const TileSortParams& p, uint32_t vb, TsSharedT<C>& S) {
+    int tile;
+    if (C::NT == TsBig::NT && p.c1tiles) {  // (chunk 1 runs k_tile_sort_big only)
+        if (vb >= *p.c1_n) return;
+        tile = __builtin_amdgcn_readfirstlane((int)p.c1tiles[vb]);
+    } else {
+        const int per = (p.n_tiles + 7) >> 3;
+        tile = (int)(vb & 7) * per + (int)(vb >> 3);
+        if (tile >= p.n_tiles) return;
+        if (p.done && p.done[tile]) return;
+    }
+    tile_sort_tile<C>(p, tile, S);  // one inlined copy
+}
+
+template <class C>
+__device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const int tile, TsSharedT<C>& S) {
     constexpr int kTsThreads = C::NT, kTsIpt = C::IPT;
     constexpr uint32_t kTsCap = C::Cap, kTsBuckets = C::Buckets;
-    const int per = (p.n_tiles + 7) >> 3;  // XCD-banded, as k_composite
-    const int tile = (int)(vb & 7) * per + (int)(vb >> 3);
-    if (tile >= p.n_tiles) return;
-    if (p.done && p.done[tile]) return;
     const uint2 range = p.ranges[tile];
     const uint32_t L = range.y - range.x;
     if (L == 0) return;
@@ -2706,6 +2722,8 @@ __global__ __launch_bounds__(TsSmall::NT, 5) void k_tile_sort(TileSortParams p) 
 }
 __global__ __launch_bounds__(TsBig::NT, 4) void k_tile_sort_big(TileSortParams p) {
     __shared__ TsSharedT<TsBig> S;
+    // (chunk 1: workgroup j takes entry j of the compact tile list, the rest return at once; a
+    // grid-stride loop over the list would spill: the sort body is at the 128-VGPR bound)
     tile_sort_body<TsBig>(p, blockIdx.x, S);
 }
 
@@ -3064,7 +3082,8 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
             if (in1) p.state[pix_late(1)] = make_float4(cr.y, cg.y, cb.y, FP16_TARGET ? ca.y : T.y);
             if (tid == 0) {
                 p.done[tile] = 0;
-                atomicAdd(&p.ctl->not_done, 1u);
+                const uint32_t at = atomicAdd(&p.ctl->not_done, 1u);
+                if (p.c1tiles) p.c1tiles[at] = (uint32_t)tile;  // chunk 1's tile list
             }
             return;
         }
@@ -3114,17 +3133,33 @@ struct CompQShared {
 };
 
 template <bool FP16_TARGET>
+__device__ __forceinline__ void composite_q_tile(const CompositeParams& p, const int tile, CompQShared& S);
+
+// Workgroup item vb -> tile: XCD-banded (through the tile order when set), or chunk 1's compact
+// list of the tiles chunk 0 left unsaturated (kCompSecond with c1tiles).
+template <bool FP16_TARGET>
 __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint32_t vb, CompQShared& S) {
+    int tile;
+    if (p.mode == kCompSecond && p.c1tiles) {
+        if (vb >= p.ctl->not_done) return;
+        tile = __builtin_amdgcn_readfirstlane((int)p.c1tiles[vb]);
+    } else {
+        const int per = (p.n_tiles + 7) >> 3;
+        const int j = (int)(vb & 7) * per + (int)(vb >> 3);  // XCD band, position
+        if (j >= p.n_tiles) return;
+        tile = p.order ? (int)p.order[j] : j;
+        if (p.mode == kCompSecond && p.done[tile]) return;
+    }
+    composite_q_tile<FP16_TARGET>(p, tile, S);  // one inlined copy
+}
+
+template <bool FP16_TARGET>
+__device__ __forceinline__ void composite_q_tile(const CompositeParams& p, const int tile, CompQShared& S) {
     auto& sR = S.sR;
     auto& sL = S.sL;
     auto& sN = S.sN;
     uint32_t& s_sat = S.s_sat;
     const int tid = threadIdx.x;
-    const int per = (p.n_tiles + 7) >> 3;
-    const int j = (int)(vb & 7) * per + (int)(vb >> 3);  // XCD band, position
-    if (j >= p.n_tiles) return;
-    const int tile = p.order ? (int)p.order[j] : j;
-    if (p.mode == kCompSecond && p.done[tile]) return;
 #ifdef GS_C1_PRINT
     if (tid == 0 && p.mode == kCompSecond) printf("C1T %d %u\n", tile, p.ranges[tile].y - p.ranges[tile].x);
 #endif
@@ -3283,7 +3318,8 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
             if (in) p.state[pix] = make_float4(cr, cg, cb, FP16_TARGET ? ca : T);
             if (tid == 0) {
                 p.done[tile] = 0;
-                atomicAdd(&p.ctl->not_done, 1u);
+                const uint32_t at = atomicAdd(&p.ctl->not_done, 1u);
+                if (p.c1tiles) p.c1tiles[at] = (uint32_t)tile;  // chunk 1's tile list
             }
             return;
         }
@@ -3399,7 +3435,8 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     for (uint32_t vb = b; vb < nbin; vb += G) bin_emit_body<256, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(7);
-    const uint32_t ntb = 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
+    // (chunk 1's tiles: the compact list when the first pass kept one, else every tile)
+    const uint32_t ntb = c.cp.c1tiles ? ctl->not_done : 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
     for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body<TsBig>(c.tp, vb, *(TsShared*)lds);
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(8);
@@ -3710,7 +3747,8 @@ void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
         hipLaunchKernelGGL(k_c1_records, dim3(kMaxGrid), dim3(256), 0, s, c.pp);
         launch_bin(c.bp, s);
         launch_tile_sort(c.tp, s);
-        // the unsaturated tiles only, each with a long list: 4 waves per tile at any frame size
+        // the unsaturated tiles only, each with a long list: 4 waves per tile at any frame size;
+        // workgroup j takes entry j of the compact tile list (c1tiles), the rest return at once
         const unsigned grid = 8u * (unsigned)((c.cp.n_tiles + 7) / 8);
         if (accum_fp16)
             hipLaunchKernelGGL(k_composite_q<true>, dim3(grid), dim3(256), 0, s, c.cp);
