@@ -887,7 +887,10 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
        // tiles would take the multi-round path (each round re-reads the whole list), so the
        // 256-thread shape with rounds of 2048 (a moving camera at 4K: 1200 entries per tile)
         const uint64_t k0 = s->have_last ? s->last.k_chunk[0] : 0;
-        tsp.big = n_tiles > 0 && k0 > (uint64_t)kTsBigMean * (uint64_t)n_tiles;
+        tsp.big = n_tiles <= 0                                       ? 0
+                  : k0 > (uint64_t)kTsHugeMean * (uint64_t)n_tiles ? 2
+                  : k0 > (uint64_t)kTsBigMean * (uint64_t)n_tiles  ? 1
+                                                                   : 0;
     }
     CompositeParams cp{};
     cp.ranges = F.ranges;

@@ -300,7 +300,8 @@ struct TileSortParams {
     const uint8_t* done;          // chunk 1: saturated tiles are skipped (nullable)
     uint32_t* scratch;            // [n_tiles][256] long lists' bucket ends (the binning's bmat, dead by then)
     int n_tiles;
-    int big;                      // chunk 0 with long lists: the 256-thread shape (k_tile_sort_big)
+    int big;                      // chunk 0 with long lists: 1 = the 256-thread shape (k_tile_sort_big),
+                                  // 2 = the 1024-thread shape (k_tile_sort_huge: lists of <= 8192 in LDS)
     // chunk 1: the tiles chunk 0 left unsaturated, a compact list (CompositeParams::c1tiles) of
     // *c1_n entries; the launch walks it instead of every tile (nullable)
     const uint32_t* c1tiles;
@@ -308,6 +309,7 @@ struct TileSortParams {
 };
 
 constexpr uint32_t kTsBigMean = 800;  // mean chunk-0 list length from which k_tile_sort_big sorts chunk 0
+constexpr uint32_t kTsHugeMean = 3000;  // ... and k_tile_sort_huge
 
 enum CompositeMode { kCompSingle = 0, kCompFirst = 1, kCompSecond = 2 };
 

@@ -2304,6 +2304,9 @@ struct TsCfg {
 };
 using TsBig = TsCfg<256, 8, 10>;
 using TsSmall = TsCfg<128, 8, 9>;
+// Lists of a few thousand entries (a one-chunk frame at 4K: ~6300 per tile): the whole list in
+// LDS (112 KB, one workgroup per CU), one gather of the keys instead of ts_long's four passes.
+using TsHuge = TsCfg<1024, 8, 12>;
 constexpr uint32_t kTsHeavy = 64;  // largest bucket ranked by counting
 
 template <class C>
@@ -2313,8 +2316,9 @@ struct TsSharedT {
     alignas(16) uint32_t cnt[C::Buckets];  // a thread's per = Buckets / NT = 4 counters are one 16-B
                                            // word (ds_read/write_b128, no stride-4 conflicts); after
                                            // the scatter cnt[b] is bucket b's end = bucket b+1's start
-    unsigned long long red[8];
-    uint32_t tmp[8];
+    unsigned long long red[2 * (C::NT / 64)];  // block_minmax64's per-wave min | max
+    uint32_t tmp[C::NT / 64];              // block_excl_scan's per-wave totals
+    uint32_t misc[4];                      // ts_rounds' gather cursor, ts_long's round bounds
     uint32_t any[C::NT / 64];              // block_any's per-wave flags
 };
 
@@ -2344,18 +2348,19 @@ __device__ __forceinline__ void block_minmax64(unsigned long long& mn, unsigned 
         mn = min(mn, (unsigned long long)__shfl_xor(mn, d, 64));
         mx = max(mx, (unsigned long long)__shfl_xor(mx, d, 64));
     }
+    constexpr int NW = NT / 64;
     const int w = threadIdx.x >> 6;
     if (lane_id() == 0) {
         s[w] = mn;
-        s[4 + w] = mx;
+        s[NW + w] = mx;
     }
     __syncthreads();
     mn = s[0];
-    mx = s[4];
+    mx = s[NW];
 #pragma unroll
-    for (int i = 1; i < NT / 64; ++i) {
+    for (int i = 1; i < NW; ++i) {
         mn = min(mn, s[i]);
-        mx = max(mx, s[4 + i]);
+        mx = max(mx, s[NW + i]);
     }
     // no trailing barrier: the per-tile sort writes s again only after several more barriers
 }
@@ -2465,6 +2470,30 @@ __device__ __forceinline__ void ts_lds_round(TsSharedT<C>& S, uint32_t n, uint32
     ts_segment<C>(S, k, v, n, mn, mx, out);
 }
 
+constexpr int kTsLongU = 4;
+// f(i, list[i], key of list[i]) for every i < n, kTsLongU entries per thread in flight.
+template <int NT, class F>
+__device__ __forceinline__ void ts_long_pass(const TileSortParams& p, const uint32_t* __restrict__ list, uint32_t n, F&& f) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t base = 0; base < n; base += NT * kTsLongU) {
+        uint32_t g[kTsLongU];
+        unsigned long long key[kTsLongU];
+#pragma unroll
+        for (int u = 0; u < kTsLongU; ++u) {
+            const uint32_t i = base + u * NT + tid;
+            g[u] = i < n ? list[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kTsLongU; ++u)
+            if (base + u * NT + tid < n) key[u] = ts_key(p, g[u]);
+#pragma unroll
+        for (int u = 0; u < kTsLongU; ++u) {
+            const uint32_t i = base + u * NT + tid;
+            if (i < n) f(i, g[u], key[u]);
+        }
+    }
+}
+
 // A list of L > C::Cap entries in rounds of <= C::Cap consecutive keys: per round, a bucket
 // histogram of the keys not yet done picks the round's upper bound, the round's elements are
 // gathered into LDS and sorted (ts_segment).  Every round re-reads the whole list, so this is
@@ -2477,11 +2506,10 @@ __device__ void ts_rounds(const TileSortParams& p, TsSharedT<C>& S, const uint32
     constexpr uint32_t kTsCap = C::Cap, kTsBuckets = C::Buckets;
     const int tid = threadIdx.x;
     unsigned long long kmin = ~0ull, kmax = 0ull;
-    for (uint32_t i = tid; i < L; i += kTsThreads) {
-        const unsigned long long key = ts_key(p, in[i]);
+    ts_long_pass<kTsThreads>(p, in, L, [&](uint32_t, uint32_t, unsigned long long key) {
         kmin = min(kmin, key);
         kmax = max(kmax, key);
-    }
+    });
     block_minmax64<kTsThreads>(kmin, kmax, S.red);
     unsigned long long lo = kmin, hi = 0ull;
     uint32_t done_n = 0;
@@ -2494,10 +2522,9 @@ __device__ void ts_rounds(const TileSortParams& p, TsSharedT<C>& S, const uint32
                 const int s = ts_shift<C>(span);
                 for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;
                 __syncthreads();
-                for (uint32_t i = tid; i < L; i += kTsThreads) {
-                    const unsigned long long key = ts_key(p, in[i]);
+                ts_long_pass<kTsThreads>(p, in, L, [&](uint32_t, uint32_t, unsigned long long key) {
                     if (key >= lo && key - lo <= span) atomicAdd(&S.cnt[(uint32_t)((key - lo) >> s)], 1u);
-                }
+                });
                 __syncthreads();
                 static_assert(perb == 4, "a thread's bucket counters are one uint4");
                 const uint4 c4 = reinterpret_cast<const uint4*>(S.cnt)[tid];
@@ -2520,19 +2547,17 @@ __device__ void ts_rounds(const TileSortParams& p, TsSharedT<C>& S, const uint32
                 span = (1ull << s) - 1ull;  // the first bucket alone overflows: narrow to it (s > 0)
             }
         }
-        if (tid == 0) S.tmp[4] = 0;
+        if (tid == 0) S.misc[0] = 0;
         __syncthreads();
-        for (uint32_t i = tid; i < L; i += kTsThreads) {
-            const uint32_t g = in[i];
-            const unsigned long long key = ts_key(p, g);
+        ts_long_pass<kTsThreads>(p, in, L, [&](uint32_t, uint32_t g, unsigned long long key) {
             if (key >= lo && (!bounded || key < hi)) {
-                const uint32_t pos = atomicAdd(&S.tmp[4], 1u);
+                const uint32_t pos = atomicAdd(&S.misc[0], 1u);
                 S.k[pos] = key;
                 S.v[pos] = g;
             }
-        }
+        });
         __syncthreads();
-        const uint32_t nc = S.tmp[4];
+        const uint32_t nc = S.misc[0];
         ts_lds_round<C>(S, nc, out + done_n);
         done_n += nc;
         lo = hi;
@@ -2556,6 +2581,22 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long x) {
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
+#ifdef GS_TS_TIME  // diagnostics builds only (make diag DIAGFLAGS=-DGS_TS_TIME): ts_long's phases
+__device__ unsigned long long g_ts_time[8];  // cycles summed over tiles: minmax, hist, scan, scatter, rounds, heavy; tiles; entries
+#define TS_T(i)                                                                        \
+    do {                                                                               \
+        if (threadIdx.x == 0) {                                                        \
+            const unsigned long long t_ = clock64();                                   \
+            atomicAdd(&g_ts_time[(i) - 1], t_ - ts_t0);                                \
+            ts_t0 = t_;                                                                \
+        }                                                                              \
+    } while (0)
+#else
+#define TS_T(i) \
+    do {        \
+    } while (0)
+#endif
+
 template <class C>
 __device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                         uint32_t L, uint32_t* __restrict__ ends) {  // ends: kTsLongBuckets words of global scratch
@@ -2564,21 +2605,33 @@ __device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __re
     constexpr int PB = (int)kTsLongBuckets / NT;  // buckets per thread (consecutive)
     static_assert(PB >= 1 && kTsLongBuckets % NT == 0 && kTsLongBuckets <= C::Buckets, "long-list buckets");
     const int tid = threadIdx.x;
+#ifdef GS_TS_TIME
+    unsigned long long ts_t0 = clock64();
+    if (tid == 0) {
+        atomicAdd(&g_ts_time[6], 1ull);
+        atomicAdd(&g_ts_time[7], (unsigned long long)L);
+    }
+#endif
     unsigned long long kmin = ~0ull, kmax = 0ull;
-    for (uint32_t i = tid; i < L; i += NT) {
-        const unsigned long long key = ts_key(p, in[i]);
+    // The passes over the list are gathers behind list loads (latency-bound, VERDICT r03 item 5:
+    // one entry in flight per thread kept the waves 85 % waiting): kTsLongU entries per thread
+    // per step, every list load issued before the first key gather.
+    ts_long_pass<NT>(p, in, L, [&](uint32_t, uint32_t, unsigned long long key) {
         kmin = min(kmin, key);
         kmax = max(kmax, key);
-    }
+    });
     for (uint32_t b = tid; b < kTsLongBuckets; b += NT) S.cnt[b] = 0;
     block_minmax64<NT>(kmin, kmax, S.red);  // (its barrier also orders the zeroed counters)
     kmin = uniform64(kmin);  // (block-uniform values in scalar registers: the rounds below hold
     kmax = uniform64(kmax);  // the full set of a round's keys in vector registers)
+    TS_T(1);
     const unsigned long long span = kmax - kmin;
     const int sh = __builtin_amdgcn_readfirstlane(span == 0 ? 0 : max(0, 64 - (int)__clzll(span) - kTsLongBB));
-    for (uint32_t i = tid; i < L; i += NT)
-        atomicAdd(&S.cnt[(uint32_t)((ts_key(p, in[i]) - kmin) >> sh)], 1u);
+    ts_long_pass<NT>(p, in, L, [&](uint32_t, uint32_t, unsigned long long key) {
+        atomicAdd(&S.cnt[(uint32_t)((key - kmin) >> sh)], 1u);
+    });
     __syncthreads();
+    TS_T(2);
     {
         uint32_t c[PB], sum = 0;
 #pragma unroll
@@ -2596,12 +2649,12 @@ __device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __re
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < L; i += NT) {
-        const uint32_t g = in[i];
-        const uint32_t pos = atomicAdd(&S.cnt[(uint32_t)((ts_key(p, g) - kmin) >> sh)], 1u);
-        out[pos] = g;
-    }
+    TS_T(3);
+    ts_long_pass<NT>(p, in, L, [&](uint32_t, uint32_t g, unsigned long long key) {
+        out[atomicAdd(&S.cnt[(uint32_t)((key - kmin) >> sh)], 1u)] = g;
+    });
     __syncthreads();  // (the scatter's stores are visible to the workgroup: one CU, one L1)
+    TS_T(4);
     uint32_t pos0 = 0;
     bool heavy = false;
     while (pos0 < L) {
@@ -2621,20 +2674,19 @@ __device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __re
 #pragma unroll
         for (int q = 0; q < PB; ++q) {
             const uint32_t b = (uint32_t)(tid * PB + q);
-            if (m >= 1 && b == m - 1) S.tmp[5] = end[q];
-            if (b == m) S.tmp[6] = end[q];
+            if (m >= 1 && b == m - 1) S.misc[1] = end[q];
+            if (b == m) S.misc[2] = end[q];
         }
-        if (m == 0 && tid == 0) S.tmp[5] = 0;
+        if (m == 0 && tid == 0) S.misc[1] = 0;
         __syncthreads();
-        uint32_t pos1 = __builtin_amdgcn_readfirstlane(S.tmp[5]);
-        const uint32_t heavy_end = __builtin_amdgcn_readfirstlane(S.tmp[6]);
+        uint32_t pos1 = __builtin_amdgcn_readfirstlane(S.misc[1]);
+        const uint32_t heavy_end = __builtin_amdgcn_readfirstlane(S.misc[2]);
         if (pos1 > pos0) {  // one round: staged in LDS, sorted, written back in place
             const uint32_t n = pos1 - pos0;
-            for (uint32_t i = tid; i < n; i += NT) {
-                const uint32_t g = out[pos0 + i];
-                S.k[i] = ts_key(p, g);
+            ts_long_pass<NT>(p, out + pos0, n, [&](uint32_t i, uint32_t g, unsigned long long key) {
+                S.k[i] = key;
                 S.v[i] = g;
-            }
+            });
             __syncthreads();
             ts_lds_round<C>(S, n, out + pos0);  // (ends with a barrier)
         } else {  // bucket m holds more than Cap entries: left for the pass below
@@ -2643,6 +2695,7 @@ __device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __re
         }
         pos0 = pos1;
     }
+    TS_T(5);
     if (!heavy) return;
     // the buckets of more than Cap entries, one at a time: copied to `in`, sorted by ts_rounds
     for (uint32_t b = 0; b < kTsLongBuckets; ++b) {
@@ -2654,6 +2707,7 @@ __device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __re
         ts_rounds<C>(p, S, in + e0, out + e0, e1 - e0);
         __syncthreads();
     }
+    TS_T(6);
 }
 
 template <class C>
@@ -2713,12 +2767,21 @@ __device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const in
         ts_segment<C>(S, k, v, L, mn, mx, out);
         return;
     }
-    ts_long<C>(p, S, p.in + range.x, out, L, p.scratch + (size_t)tile * kTsLongBuckets);
+    // k_tile_sort_huge: a list past 8192 in rounds of 8192 (ts_long at 1024 threads would spill;
+    // the shape runs when lists average 3000-odd entries, so few are that long)
+    if constexpr (C::NT > TsBig::NT)
+        ts_rounds<C>(p, S, in, out, L);
+    else
+        ts_long<C>(p, S, p.in + range.x, out, L, p.scratch + (size_t)tile * kTsLongBuckets);
 }
 
 __global__ __launch_bounds__(TsSmall::NT, 5) void k_tile_sort(TileSortParams p) {
     __shared__ TsSharedT<TsSmall> S;
     tile_sort_body<TsSmall>(p, blockIdx.x, S);
+}
+__global__ __launch_bounds__(TsHuge::NT, 1) void k_tile_sort_huge(TileSortParams p) {
+    __shared__ TsSharedT<TsHuge> S;
+    tile_sort_body<TsHuge>(p, blockIdx.x, S);
 }
 __global__ __launch_bounds__(TsBig::NT, 4) void k_tile_sort_big(TileSortParams p) {
     __shared__ TsSharedT<TsBig> S;
@@ -2745,6 +2808,16 @@ __global__ __launch_bounds__(TsBig::NT, 4) void k_tile_sort_big(TileSortParams p
 // Chunked frames: mode kCompFirst marks saturated tiles done (and writes them out) and parks the
 // per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
 constexpr int kCompBatch = 128;
+#ifndef GS_COMP_BFI
+#define GS_COMP_BFI 1
+#endif
+// z >= 0 ? a : 0 for z != -0, without a lane mask (inline asm: the compiler folds the and-with-
+// sign-shift form back into compare + select)
+__device__ __forceinline__ float sel_nonneg(float z, float a) {
+    float r;
+    asm("v_ashrrev_i32 %0, 31, %1\n\tv_bfi_b32 %0, %0, 0, %2" : "=&v"(r) : "v"(z), "v"(a));
+    return r;
+}
 #if defined(GS_COMP_STATS) || defined(GS_COMP_TIME)
 #define GS_COMP_DIAG 1
 #endif
@@ -2993,7 +3066,14 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         } else {
 #pragma clang fp contract(off)
             // (no contraction: T - am T must not become one fma, k_composite_q rounds it twice)
+#if GS_COMP_BFI
+            // am = z >= 0 ? a : 0 from z's sign bit (z is never -0: each difference is +0 when
+            // exact), as two plain VALU ops: the compare + select form writes VCC and reads it
+            // back as a lane mask, which costs two wait states per pixel (s_nop 1)
+            const f2 am = {sel_nonneg(z0, a0), sel_nonneg(z1, a1)};
+#else
             const f2 am = {hit0 ? a0 : 0.0f, hit1 ? a1 : 0.0f};
+#endif
             const f2 s2 = am * T;  // = hit ? a T : 0 (T is finite and >= 0)
             cr = __builtin_elementwise_fma((f2)kr, s2, cr);
             cg = __builtin_elementwise_fma((f2)kg, s2, cg);
@@ -3711,7 +3791,9 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
 void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return;
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
-    if (p.done || p.big)  // chunk 1 (the unsaturated tiles' long lists), or long chunk-0 lists
+    if (p.big == 2 && !p.done)  // chunk-0 lists of thousands (one-chunk frames at 4K)
+        hipLaunchKernelGGL(k_tile_sort_huge, dim3(grid), dim3(TsHuge::NT), 0, s, p);
+    else if (p.done || p.big)  // chunk 1 (the unsaturated tiles' long lists), or long chunk-0 lists
         hipLaunchKernelGGL(k_tile_sort_big, dim3(grid), dim3(TsBig::NT), 0, s, p);
     else
         hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(TsSmall::NT), 0, s, p);
@@ -3789,6 +3871,13 @@ extern "C" int gs_diag_kt(unsigned long long* out) {  // out: 2 x 8192 x 6
 }
 extern "C" int gs_diag_fe(unsigned long long* out) {  // out: 8
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_fe), sizeof(gs::g_fe)) == hipSuccess ? 0 : -1;
+}
+#endif
+#ifdef GS_TS_TIME
+extern "C" int gs_diag_ts_time(unsigned long long* out) {  // out: 8 (read and zeroed)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_ts_time), 64) != hipSuccess) return -1;
+    const unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_ts_time), z, 64) == hipSuccess ? 0 : -1;
 }
 #endif
 #ifdef GS_COMP_DIAG

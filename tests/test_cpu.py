@@ -283,7 +283,7 @@ def test_kernel_resources_no_scratch():
     from kernel_resources import kernel_resources
     res = kernel_resources(lib)
     frame = ["k_cull", "k_project<true>", "k_project<false>", "k_bin_count<true>", "k_bin_count<false>",
-             "k_bin_colscan", "k_bin_emit<true>", "k_bin_emit<false>", "k_tile_sort", "k_tile_sort_big", "k_composite<false>",
+             "k_bin_colscan", "k_bin_emit<true>", "k_bin_emit<false>", "k_tile_sort", "k_tile_sort_big", "k_tile_sort_huge", "k_composite<false>",
              "k_composite<true>", "k_composite_q<false>", "k_composite_q<true>", "k_chunk1<false>", "k_chunk1<true>",
              "k_c1_rows", "k_c1_parts", "k_c1_records", "k_frame_end"]
     for k in frame:

@@ -183,15 +183,18 @@ def test_tile_order_with_equal_keys(gpu_ctx, depths):
     assert r[2], r
 
 
-@pytest.mark.parametrize("plane_frac", [0.0, 0.7])
-def test_tile_order_long_lists(gpu_ctx, plane_frac):
-    """Tile lists of thousands of entries (a faint scene: ~3500 per tile), longer than one sorting
-    round: ts_long (bucket scatter, then runs of buckets sorted in place) -- and, with 70 % of the
-    Gaussians on one depth plane, a bucket of more than a round of keys, which ts_long hands to
-    ts_rounds.  The first frame sorts with the 128-thread shape (rounds of 1024), the second with
-    the 256-thread shape (its last frame's lists averaged > 800 entries; rounds of 2048).  Every
-    tile's list must be the stable global order restricted to the tile."""
-    W, H, n = 320, 240, 800_000
+@pytest.mark.parametrize("n,plane_frac", [(800_000, 0.0), (800_000, 0.7), (1_600_000, 0.0), (1_600_000, 0.7),
+                                          (3_200_000, 0.0)])
+def test_tile_order_long_lists(gpu_ctx, n, plane_frac):
+    """Tile lists of thousands of entries (a faint scene: ~2100, ~4100 or ~8300 per tile), longer
+    than one sorting round.  The first frame sorts with the 128-thread shape (rounds of 1024:
+    ts_long, a bucket scatter then runs of buckets sorted in place); the second with the shape its
+    last frame's mean list length picks: the 256-thread shape (mean > 800; ts_long in rounds of
+    2048) at 800 K, the 1024-thread shape (mean > 3000; a list of <= 8192 sorted whole in LDS,
+    longer ones by ts_rounds in rounds of 8192) at 1.6 M and 3.2 M.  With 70 % of the Gaussians on one
+    depth plane, ts_long meets buckets of more than a round of keys, which it hands to ts_rounds.
+    Every tile's list must be the stable global order restricted to the tile."""
+    W, H = 320, 240
     rng = np.random.default_rng(5)
     aos = gs.synth_aos(n, 81, W, H).reshape(n, 80)
     aos[:, 12] -= 4.0  # faint: long lists, nothing saturates
@@ -211,6 +214,8 @@ def test_tile_order_long_lists(gpu_ctx, plane_frac):
         rg, en = check_tile_lists(sc, sp, W, H, full_sets=False)
         lens = rg[:, 1] - rg[:, 0]
         assert lens.max() > 2048 and np.median(lens) > 1024, (lens.max(), np.median(lens))
+        if n >= 3_200_000:
+            assert lens.max() > 8192, lens.max()  # the 1024-thread shape's multi-round lists
     assert np.array_equal(imgs[0], imgs[1])
     ref, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=0.0)
     r = image_close_fp32(imgs[0], ref, name="long_lists_%g" % plane_frac)
