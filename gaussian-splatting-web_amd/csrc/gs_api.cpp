@@ -110,7 +110,10 @@ constexpr int kFrameSets = GS_FRAME_SETS;
 constexpr int kSetStreams = GS_SET_STREAMS;  // distinct streams of the frame sets
 constexpr int kStatSlots = 8;
 static_assert(kStatSlots >= kFrameSets && kStatSlots * 4 <= 64, "statistics slots (h_seq: 64 B)");
-constexpr int kDeepTiles = 1536;  // frames of at most this many tiles keep kFrameSets in flight
+#ifndef GS_DEEP_TILES
+#define GS_DEEP_TILES 1536
+#endif
+constexpr int kDeepTiles = GS_DEEP_TILES;  // frames of at most this many tiles keep kFrameSets in flight
 
 struct FrameEvents {
     hipEvent_t ev[EV_COUNT] = {};

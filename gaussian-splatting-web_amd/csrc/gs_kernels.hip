@@ -2370,6 +2370,24 @@ __device__ __forceinline__ int ts_shift(unsigned long long span) {
     return span == 0 ? 0 : max(0, 64 - (int)__clzll(span) - C::BB);
 }
 
+#ifdef GS_TS_TIME  // diagnostics builds only (make diag DIAGFLAGS=-DGS_TS_TIME): the long-list phases
+// cycles summed over tiles.  ts_long: minmax, hist, scan, scatter, rounds, heavy; the 1024-thread
+// shape's one-round lists: load + gather, minmax, count, scan + scatter, rank + write; then tiles, entries
+__device__ unsigned long long g_ts_time[8];
+#define TS_T(i)                                                                        \
+    do {                                                                               \
+        if (threadIdx.x == 0) {                                                        \
+            const unsigned long long t_ = clock64();                                   \
+            atomicAdd(&g_ts_time[(i) - 1], t_ - ts_t0);                                \
+            ts_t0 = t_;                                                                \
+        }                                                                              \
+    } while (0)
+#else
+#define TS_T(i) \
+    do {        \
+    } while (0)
+#endif
+
 // Sort n <= C::Cap elements held in registers (element j * NT + tid of k/v) with keys in
 // [kmin, kmax]; out[rank] = value.
 template <class C>
@@ -2378,6 +2396,10 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
     constexpr int kTsThreads = C::NT, kTsIpt = C::IPT;
     constexpr uint32_t kTsBuckets = C::Buckets;
     const int tid = threadIdx.x;
+#ifdef GS_TS_TIME
+    constexpr bool kT = C::NT > 256;  // the 1024-thread shape's phases
+    unsigned long long ts_t0 = clock64();
+#endif
     const int s = ts_shift<C>(kmax - kmin);  // S.cnt was zeroed by the caller before block_minmax64's barrier
     uint32_t bk[kTsIpt];
 #pragma unroll
@@ -2389,6 +2411,9 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
         }
     }
     __syncthreads();
+#ifdef GS_TS_TIME
+    if (kT) TS_T(3);
+#endif
     static_assert(kTsBuckets / kTsThreads == 4, "a thread's bucket counters are one uint4");
     const uint4 c4 = reinterpret_cast<const uint4*>(S.cnt)[tid];
     const uint32_t sum = c4.x + c4.y + c4.z + c4.w, big = max(max(c4.x, c4.y), max(c4.z, c4.w));
@@ -2406,6 +2431,9 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
         }
     }
     __syncthreads();
+#ifdef GS_TS_TIME
+    if (kT) TS_T(4);
+#endif
     if (!heavy) {
 #pragma unroll
         for (int j = 0; j < kTsIpt; ++j) {
@@ -2444,6 +2472,9 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
         for (uint32_t i = tid; i < n; i += kTsThreads) out[i] = S.v[i];
     }
     __syncthreads();
+#ifdef GS_TS_TIME
+    if (kT) TS_T(5);
+#endif
 }
 
 // Sort the n <= C::Cap (key, slot) pairs staged in S.k / S.v (after a barrier) into out[0, n).
@@ -2581,21 +2612,6 @@ __device__ __forceinline__ unsigned long long uniform64(unsigned long long x) {
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
-#ifdef GS_TS_TIME  // diagnostics builds only (make diag DIAGFLAGS=-DGS_TS_TIME): ts_long's phases
-__device__ unsigned long long g_ts_time[8];  // cycles summed over tiles: minmax, hist, scan, scatter, rounds, heavy; tiles; entries
-#define TS_T(i)                                                                        \
-    do {                                                                               \
-        if (threadIdx.x == 0) {                                                        \
-            const unsigned long long t_ = clock64();                                   \
-            atomicAdd(&g_ts_time[(i) - 1], t_ - ts_t0);                                \
-            ts_t0 = t_;                                                                \
-        }                                                                              \
-    } while (0)
-#else
-#define TS_T(i) \
-    do {        \
-    } while (0)
-#endif
 
 template <class C>
 __device__ void ts_long(const TileSortParams& p, TsSharedT<C>& S, uint32_t* __restrict__ in, uint32_t* __restrict__ out,
@@ -2747,6 +2763,14 @@ __device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const in
         return;
     }
     if (L <= kTsCap) {
+#ifdef GS_TS_TIME
+        constexpr bool kT = C::NT > 256;
+        unsigned long long ts_t0 = clock64();
+        if (kT && tid == 0) {
+            atomicAdd(&g_ts_time[6], 1ull);
+            atomicAdd(&g_ts_time[7], (unsigned long long)L);
+        }
+#endif
         unsigned long long mn = ~0ull, mx = 0ull;
 #pragma unroll
         for (int j = 0; j < kTsIpt; ++j) {  // every list load in flight before the first key gather
@@ -2762,8 +2786,17 @@ __device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const in
                 mx = max(mx, k[j]);
             }
         }
+#ifdef GS_TS_TIME
+        if (kT) {
+            __syncthreads();  // (diagnostics: every wave's gathers landed)
+            TS_T(1);
+        }
+#endif
         for (uint32_t b = tid; b < kTsBuckets; b += kTsThreads) S.cnt[b] = 0;  // (ts_segment's counters)
         block_minmax64<kTsThreads>(mn, mx, S.red);
+#ifdef GS_TS_TIME
+        if (kT) TS_T(2);
+#endif
         ts_segment<C>(S, k, v, L, mn, mx, out);
         return;
     }
@@ -2808,16 +2841,7 @@ __global__ __launch_bounds__(TsBig::NT, 4) void k_tile_sort_big(TileSortParams p
 // Chunked frames: mode kCompFirst marks saturated tiles done (and writes them out) and parks the
 // per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
 constexpr int kCompBatch = 128;
-#ifndef GS_COMP_BFI
-#define GS_COMP_BFI 1
-#endif
-// z >= 0 ? a : 0 for z != -0, without a lane mask (inline asm: the compiler folds the and-with-
-// sign-shift form back into compare + select)
-__device__ __forceinline__ float sel_nonneg(float z, float a) {
-    float r;
-    asm("v_ashrrev_i32 %0, 31, %1\n\tv_bfi_b32 %0, %0, 0, %2" : "=&v"(r) : "v"(z), "v"(a));
-    return r;
-}
+
 #if defined(GS_COMP_STATS) || defined(GS_COMP_TIME)
 #define GS_COMP_DIAG 1
 #endif
@@ -3066,14 +3090,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         } else {
 #pragma clang fp contract(off)
             // (no contraction: T - am T must not become one fma, k_composite_q rounds it twice)
-#if GS_COMP_BFI
-            // am = z >= 0 ? a : 0 from z's sign bit (z is never -0: each difference is +0 when
-            // exact), as two plain VALU ops: the compare + select form writes VCC and reads it
-            // back as a lane mask, which costs two wait states per pixel (s_nop 1)
-            const f2 am = {sel_nonneg(z0, a0), sel_nonneg(z1, a1)};
-#else
             const f2 am = {hit0 ? a0 : 0.0f, hit1 ? a1 : 0.0f};
-#endif
             const f2 s2 = am * T;  // = hit ? a T : 0 (T is finite and >= 0)
             cr = __builtin_elementwise_fma((f2)kr, s2, cr);
             cg = __builtin_elementwise_fma((f2)kg, s2, cg);

@@ -67,6 +67,28 @@ def main():
     print("  tiles with a heavy bucket: %d; entries in heavy buckets %d; ts_rounds entry reads %d (%.2f x K)" %
           (heavy_tiles, heavy_entries, rounds_cost, rounds_cost / max(1, K)))
     print("  largest heavy buckets (bucket, list, tile):", worst[:8])
+    # the 1024-thread shape's count ranking (lists <= 8192, 4096 buckets of equal width over the
+    # tile's key range): element i = j * 1024 + t is ranked by a loop over its bucket, so a wave's
+    # step j costs the largest bucket among its 64 lanes
+    samp = long_[:: max(1, len(long_) // 400)]
+    mean_b, mean_wmax = [], []
+    for t in samp:
+        k = key64[rg[t, 0]:rg[t, 1]]
+        if len(k) > 8192:
+            continue
+        kmin, kmax = int(k.min()), int(k.max())
+        span = kmax - kmin
+        sh = 0 if span == 0 else max(0, span.bit_length() - 12)
+        b = ((k - np.uint64(kmin)) >> np.uint64(sh)).astype(np.int64)
+        cnt = np.bincount(b, minlength=4096)
+        sz = cnt[b]
+        mean_b.append(sz.mean())
+        pad = np.zeros(8192, np.int64)
+        pad[:len(sz)] = sz
+        mean_wmax.append(pad.reshape(8, 16, 64).max(axis=2).sum() / (8 * 16))
+    if mean_b:
+        print("  1024-thread ranking over %d tiles: mean bucket of an element %.2f; mean wave-step cost %.2f" %
+              (len(mean_b), float(np.mean(mean_b)), float(np.mean(mean_wmax))))
     # per-tile work if one workgroup streams ~ 6 reads per entry: the longest lists
     top = np.argsort(L)[::-1][:8]
     print("  longest lists (tile, L):", [(int(t), int(L[t])) for t in top])

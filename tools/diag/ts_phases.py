@@ -13,6 +13,8 @@ sys.path.insert(0, os.path.join(ROOT, "gaussian-splatting-web_amd"))
 import gsplat_amd as gs  # noqa: E402
 
 PHASES = ("minmax", "histogram", "scan", "scatter", "rounds", "heavy buckets")
+# the 1024-thread shape (k_tile_sort_huge) on lists of one round
+PHASES_HUGE = ("load + gather", "minmax", "count", "scan + scatter", "rank + write", "-")
 
 
 def main():
@@ -45,7 +47,8 @@ def main():
     tot = sum(cnt[:6])
     print("%s: %d long lists, %d entries over %d frames; %.0f cycles per tile" %
           (which, cnt[6], cnt[7], frames, tot / max(1, cnt[6])))
-    for i, name in enumerate(PHASES):
+    names = PHASES_HUGE if os.environ.get("HUGE") == "1" else PHASES
+    for i, name in enumerate(names):
         print("  %-14s %5.1f %%  %8.0f cycles/tile  %6.2f cycles/entry" %
               (name, 100.0 * cnt[i] / max(1, tot), cnt[i] / max(1, cnt[6]), cnt[i] / max(1, cnt[7])))
 
