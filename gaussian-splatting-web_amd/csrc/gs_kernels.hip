@@ -2305,15 +2305,17 @@ struct TsCfg {
 using TsBig = TsCfg<256, 8, 10>;
 using TsSmall = TsCfg<128, 8, 9>;
 // Lists of a few thousand entries (a one-chunk frame at 4K: ~6300 per tile): the whole list in
-// LDS (112 KB, one workgroup per CU), one gather of the keys instead of ts_long's four passes.
-using TsHuge = TsCfg<1024, 8, 12>;
+// LDS (128 KB, one workgroup per CU), one gather of the keys instead of ts_long's four passes;
+// 8192 buckets (a thread's eight counters, two 16-B words): a bucket holds ~3 of a tile's keys at
+// 4096, and the count ranking loops over the bucket (sort 1.62 -> 1.56 ms at 50 M / 4K).
+using TsHuge = TsCfg<1024, 8, 13>;
 constexpr uint32_t kTsHeavy = 64;  // largest bucket ranked by counting
 
 template <class C>
 struct TsSharedT {
     unsigned long long k[C::Cap];
     uint32_t v[C::Cap];
-    alignas(16) uint32_t cnt[C::Buckets];  // a thread's per = Buckets / NT = 4 counters are one 16-B
+    alignas(16) uint32_t cnt[C::Buckets];  // a thread's per = Buckets / NT = 4 (8) counters are one (two) 16-B
                                            // word (ds_read/write_b128, no stride-4 conflicts); after
                                            // the scatter cnt[b] is bucket b's end = bucket b+1's start
     unsigned long long red[2 * (C::NT / 64)];  // block_minmax64's per-wave min | max
@@ -2414,13 +2416,25 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
 #ifdef GS_TS_TIME
     if (kT) TS_T(3);
 #endif
-    static_assert(kTsBuckets / kTsThreads == 4, "a thread's bucket counters are one uint4");
-    const uint4 c4 = reinterpret_cast<const uint4*>(S.cnt)[tid];
-    const uint32_t sum = c4.x + c4.y + c4.z + c4.w, big = max(max(c4.x, c4.y), max(c4.z, c4.w));
+    // a thread's PB consecutive bucket counters as PB / 4 16-B LDS words
+    constexpr int PB = (int)(kTsBuckets / kTsThreads), PQ = PB / 4;
+    static_assert(PB % 4 == 0, "a thread's bucket counters are whole uint4s");
+    uint4 c4[PQ];
+    uint32_t sum = 0, big = 0;
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+        c4[q] = reinterpret_cast<const uint4*>(S.cnt)[tid * PQ + q];
+        sum += c4[q].x + c4[q].y + c4[q].z + c4[q].w;
+        big = max(big, max(max(c4[q].x, c4[q].y), max(c4[q].z, c4[q].w)));
+    }
     uint32_t total;
-    const uint32_t b = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
-    const uint4 st = make_uint4(b, b + c4.x, b + c4.x + c4.y, b + c4.x + c4.y + c4.z);
-    reinterpret_cast<uint4*>(S.cnt)[tid] = st;  // scatter cursor
+    uint32_t b = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {  // scatter cursors
+        const uint4 st = make_uint4(b, b + c4[q].x, b + c4[q].x + c4[q].y, b + c4[q].x + c4[q].y + c4[q].z);
+        reinterpret_cast<uint4*>(S.cnt)[tid * PQ + q] = st;
+        b += c4[q].x + c4[q].y + c4[q].z + c4[q].w;
+    }
     const bool heavy = block_any<kTsThreads>(big > kTsHeavy, S.any);
 #pragma unroll
     for (int j = 0; j < kTsIpt; ++j) {
@@ -2557,10 +2571,17 @@ __device__ void ts_rounds(const TileSortParams& p, TsSharedT<C>& S, const uint32
                     if (key >= lo && key - lo <= span) atomicAdd(&S.cnt[(uint32_t)((key - lo) >> s)], 1u);
                 });
                 __syncthreads();
-                static_assert(perb == 4, "a thread's bucket counters are one uint4");
-                const uint4 c4 = reinterpret_cast<const uint4*>(S.cnt)[tid];
-                const uint32_t c[perb] = {c4.x, c4.y, c4.z, c4.w};
-                const uint32_t sum = c4.x + c4.y + c4.z + c4.w;
+                static_assert(perb % 4 == 0, "a thread's bucket counters are whole uint4s");
+                uint32_t c[perb], sum = 0;
+#pragma unroll
+                for (int q = 0; q < perb / 4; ++q) {
+                    const uint4 c4 = reinterpret_cast<const uint4*>(S.cnt)[tid * (perb / 4) + q];
+                    c[4 * q] = c4.x;
+                    c[4 * q + 1] = c4.y;
+                    c[4 * q + 2] = c4.z;
+                    c[4 * q + 3] = c4.w;
+                    sum += c4.x + c4.y + c4.z + c4.w;
+                }
                 uint32_t total;
                 uint32_t run = block_excl_scan<kTsThreads>(sum, S.tmp, &total);
                 uint32_t fit = 0;

@@ -1,9 +1,10 @@
 #!/bin/bash
 # GPU box: PMC passes over one-chunk frames (tools/diag/onechunk_probe.py), for the long-list
-# per-tile sort.  Usage: bash tools/gpu_sortpmc.sh TAG [cfg4|sparse]
+# per-tile sort.  Usage: bash tools/gpu_sortpmc.sh TAG [cfg4|sparse] [kernel]
 set -o pipefail
 TAG=${1:-sp}
 W=${2:-cfg4}
+K=${3:-k_tile_sort_huge}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -22,5 +23,5 @@ run sq2 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CY
 run fetch FETCH_SIZE || exit 1
 run write WRITE_SIZE || exit 1
 python3 tools/pmc_summary.py $OUT > $OUT/pmc.txt
-grep -A 20 "k_tile_sort_big" $OUT/pmc.txt | head -20 || true
+grep -A 18 "^$K\$" $OUT/pmc.txt || true
 echo done
