@@ -337,7 +337,7 @@ static constexpr int kDepthSortIpt = 8;
 #endif
 static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
 #ifndef GS_MOVING_MARGIN
-#define GS_MOVING_MARGIN 1.10f
+#define GS_MOVING_MARGIN 1.05f
 #endif
 static constexpr float kMovingMargin = GS_MOVING_MARGIN;  // extra depth margin while the view changes
 // split the visible splats into two chunks when at least this share of the tiles saturated in the
@@ -711,8 +711,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     uint32_t T = s->chunk_T;
     bool moving = false;
     {  // the statistics are a few frames old: while the camera moves, the depth at which tiles
-       // saturate moves too, so the threshold gets a wider margin (1.05 x 1.10 ~ the 1.15 used for
-       // every frame until round 2); a still camera keeps the tight one
+       // saturate moves too, so the threshold gets a wider margin (1.05 x kMovingMargin; 1.05 x 1.05
+       // measured best over 1080p and 4K orbits, tools/gpu_margin_sweep.sh); a still camera keeps the
+       // tight one
         moving = std::memcmp(s->last_view, uni, sizeof(s->last_view)) != 0;
         std::memcpy(s->last_view, uni, sizeof(s->last_view));
         std::memcpy(s->last_campos, uni + 32, sizeof(s->last_campos));
