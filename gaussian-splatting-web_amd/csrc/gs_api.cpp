@@ -330,14 +330,15 @@ static constexpr int kMaxGroup = 64;  // devices per context
 // radix partition size of gs_debug_sort_pairs (items per thread x 256)
 static constexpr int kDepthSortIpt = 8;
 // chunk-0 threshold: the farthest saturation key of the last frame, its depth scaled by this
-// (bench scene: 1.15 -> 1.05 is 2766 -> 2915 fps static; the orbit camera 2083 -> 2017, the
-// tiles that saturate later than the margin finish in chunk 1)
+// (bench scene: 1.15 -> 1.05 was 2766 -> 2915 fps static, 1.05 -> 1.01 3262 -> 3318 and at
+// 50 M / 4K 1511 -> 1655; a moving camera multiplies in kMovingMargin, and the tiles that
+// saturate later than the margin finish in chunk 1)
 #ifndef GS_CHUNK_MARGIN
-#define GS_CHUNK_MARGIN 1.05f
+#define GS_CHUNK_MARGIN 1.01f
 #endif
 static constexpr float kChunkMargin = GS_CHUNK_MARGIN;
 #ifndef GS_MOVING_MARGIN
-#define GS_MOVING_MARGIN 1.05f
+#define GS_MOVING_MARGIN 1.09f
 #endif
 static constexpr float kMovingMargin = GS_MOVING_MARGIN;  // extra depth margin while the view changes
 // split the visible splats into two chunks when at least this share of the tiles saturated in the
@@ -711,9 +712,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     uint32_t T = s->chunk_T;
     bool moving = false;
     {  // the statistics are a few frames old: while the camera moves, the depth at which tiles
-       // saturate moves too, so the threshold gets a wider margin (1.05 x kMovingMargin; 1.05 x 1.05
-       // measured best over 1080p and 4K orbits, tools/gpu_margin_sweep.sh); a still camera keeps the
-       // tight one
+       // saturate moves too, so the threshold gets a wider margin (kChunkMargin x kMovingMargin
+       // ~ 1.10 measured best over 1080p and 4K orbits, tools/gpu_margin_sweep.sh); a still camera
+       // keeps the tight one
         moving = std::memcmp(s->last_view, uni, sizeof(s->last_view)) != 0;
         std::memcpy(s->last_view, uni, sizeof(s->last_view));
         std::memcpy(s->last_campos, uni + 32, sizeof(s->last_campos));
