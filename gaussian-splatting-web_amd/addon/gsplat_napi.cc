@@ -515,6 +515,8 @@ napi_value Timings(napi_env env, napi_callback_info info) {
     put("framesUnsat", st.frames_unsat);
     put("framesSeeded", st.frames_seeded);
     put("chunkDepth", st.chunk_depth);
+    put("listMax", st.list_max);
+    put("tilesLong", st.tiles_long);
     return o;
 }
 

@@ -165,7 +165,15 @@ struct GroupWorker {
     int rc = 0;
     std::string msg;
     int64_t t_start = 0, t_end = 0;  // the last job's start and end (steady clock, ns; GS_GROUP_TRACE)
-    static constexpr int64_t kSpinNs = 2000000;  // 2 ms
+    int64_t t_post_last = 0;         // when the last job was posted (steady clock, ns)
+    std::atomic<int64_t> gap_ns{kSpinNs};  // running mean of the time between posts
+    // After a job the worker waits for the next post: it pause-spins for kPauseNs, then yields its
+    // core while it polls (another runnable thread, e.g. Node's event loop, gets the core), up to
+    // min(kSpinNs, 2 x the mean time between posts) -- a frame loop's next post arrives well within
+    // it -- and then sleeps on the condition variable.  (Round 4 pause-spun the full 2 ms: a G = 8
+    // group above ~500 fps kept seven host cores at 100 %)
+    static constexpr int64_t kSpinNs = 2000000;   // 2 ms
+    static constexpr int64_t kPauseNs = 20000;    // 20 us
 };
 
 static int64_t now_ns() {
@@ -897,6 +905,13 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
                   : k0 > (uint64_t)kTsBigMean * (uint64_t)n_tiles  ? 1
                                                                    : 0;
     }
+    tsp.stats = F.stats;
+    if (tsp.big == 2) {  // lists past one 8192-entry LDS round: the linear long-list path (256 threads);
+                         // c1tiles is free until the composite appends chunk 1's tiles to it
+        tsp.long_tiles = F.c1tiles;
+        tsp.long_n = &F.ctl->long_n;
+        tsp.long_grid = (uint32_t)std::min<uint64_t>((uint64_t)n_tiles, F.kcap / 8193u + 1u);
+    }
     CompositeParams cp{};
     cp.ranges = F.ranges;
     cp.tvals = F.tvB;
@@ -1185,13 +1200,16 @@ static void worker_loop(GroupWorker* w, int device) {
     uint32_t seen = 0;
     for (;;) {
         uint32_t p = w->posted.load(std::memory_order_acquire);
-        if (p == seen) {  // spin a while, then sleep until the next post
-            const auto t0 = std::chrono::steady_clock::now();
+        if (p == seen) {  // spin a while (pause, then yield), then sleep until the next post
+            const int64_t t0 = now_ns();
+            const int64_t window = std::min<int64_t>(GroupWorker::kSpinNs, 2 * w->gap_ns.load(std::memory_order_relaxed));
             while ((p = w->posted.load(std::memory_order_acquire)) == seen) {
-                __builtin_ia32_pause();
-                if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() >
-                    GroupWorker::kSpinNs)
-                    break;
+                const int64_t dt = now_ns() - t0;
+                if (dt > window) break;
+                if (dt < GroupWorker::kPauseNs)
+                    __builtin_ia32_pause();
+                else
+                    std::this_thread::yield();
             }
             if (p == seen) {
                 std::unique_lock<std::mutex> lk(w->mu);
@@ -1227,6 +1245,12 @@ static void worker_loop(GroupWorker* w, int device) {
 }
 
 static void post_job(GroupWorker* w, void (*fn)(void*, int), void* arg, int member) {
+    const int64_t t = now_ns();
+    if (w->t_post_last) {  // running mean of the time between posts (the worker's spin window)
+        const int64_t g = std::min<int64_t>(t - w->t_post_last, GroupWorker::kSpinNs);
+        w->gap_ns.store((w->gap_ns.load(std::memory_order_relaxed) * 7 + g) / 8, std::memory_order_relaxed);
+    }
+    w->t_post_last = t;
     w->fn = fn;
     w->arg = arg;
     w->member = member;
@@ -1240,7 +1264,13 @@ static void post_job(GroupWorker* w, void (*fn)(void*, int), void* arg, int memb
 // Wait for the worker's last posted job; its error, if any, as (code, message).
 static void join_job(GroupWorker* w, int& rc, std::string& msg) {
     const uint32_t want = w->posted.load();
-    while (w->finished.load(std::memory_order_acquire) != want) __builtin_ia32_pause();
+    const int64_t t0 = now_ns();
+    while (w->finished.load(std::memory_order_acquire) != want) {
+        if (now_ns() - t0 < GroupWorker::kPauseNs)
+            __builtin_ia32_pause();
+        else
+            std::this_thread::yield();
+    }
     if (w->rc != GS_OK && rc == GS_OK) {
         rc = w->rc;
         msg = w->msg;
@@ -1296,6 +1326,22 @@ static int group_path(const gs_ctx* c, int g) {
     return c->members[g]->device == c->members[0]->device && !c->group_peer_copy ? kGroupDirect : kGroupPeer;
 }
 
+// Member g's two strip buffers on its device, at least `need` bytes each (any strip fits: the
+// bounds move).
+static void ensure_group_buffers(gs_ctx* c, int g, size_t need) {
+    if (c->gbuf_bytes[g] >= need) return;
+    gs_ctx* m = c->members[g];
+    HIPCHK(hipSetDevice(m->device));
+    HIPCHK(hipDeviceSynchronize());
+    for (void*& p : c->gbuf[g]) {
+        if (p) HIPCHK(hipFree(p));
+        p = nullptr;
+    }
+    c->gbuf_bytes[g] = 0;
+    for (void*& p : c->gbuf[g]) HIPCHK(hipMalloc(&p, need));
+    c->gbuf_bytes[g] = need;
+}
+
 // Member g's part of a group frame, enqueued from its own thread: render its strip -- into its
 // rows of the image (direct), or into its strip buffer `buf` -- and start the strip's way to
 // device 0: an RCCL send or a peer copy on its gather stream, each recording gev_sent[g][buf]
@@ -1332,27 +1378,36 @@ static void group_member(void* arg, int g) {
         st0_waits(c->gev_sent[g][f.buf]);
         return;
     }
-    const size_t need = (size_t)f.H * f.row_bytes;  // any strip fits: the bounds move
-    if (c->gbuf_bytes[g] < need) {
-        HIPCHK(hipDeviceSynchronize());
-        for (void*& p : c->gbuf[g]) {
-            if (p) HIPCHK(hipFree(p));
-            p = nullptr;
-        }
-        c->gbuf_bytes[g] = 0;
-        for (void*& p : c->gbuf[g]) HIPCHK(hipMalloc(&p, need));
-        c->gbuf_bytes[g] = need;
-    }
+    if (path == kGroupPeer) ensure_group_buffers(c, g, (size_t)f.H * f.row_bytes);  // (RCCL: by the caller)
     void* dst = c->gbuf[g][f.buf];
+    const size_t bytes = (size_t)(std::min(te * kTile, f.H) - tb * kTile) * f.row_bytes;
+    if (path == kGroupRccl) {
+        // Member 0's receive of this strip is already queued (render_group): it must get its send
+        // whatever happens here, or device 0's gather stream waits forever / pairs the next
+        // frame's send with this frame's receive.  On a failed render the (stale)
+        // strip buffer is still sent, then the error goes to the caller.
+        std::string err;
+        int code = GS_OK;
+        try {
+            HIPCHK(hipStreamWaitEvent(m->stream, c->gev_sent[g][f.buf], 0));  // frame f - 2's transfer of it
+            render_frame(m, f.s->members[g], f.uni, f.W, f.H, og, dst, m->stream);
+        } catch (const GsError& e) {
+            code = e.code;
+            err = e.what();
+        }
+        (void)hipEventRecord(c->gev_rendered[g], m->stream);
+        (void)hipStreamWaitEvent(c->gstream[g], c->gev_rendered[g], 0);
+        const ncclResult_t r = ncclSend(dst, bytes, ncclUint8, 0, c->comms[g], c->gstream[g]);
+        HIPCHK(hipEventRecord(c->gev_sent[g][f.buf], c->gstream[g]));
+        if (code != GS_OK) throw GsError(code, err);
+        if (r != ncclSuccess) throw GsError(GS_ERR_HIP, std::string("ncclSend: ") + ncclGetErrorString(r));
+        return;
+    }
     HIPCHK(hipStreamWaitEvent(m->stream, c->gev_sent[g][f.buf], 0));  // frame f - 2's transfer of it
     render_frame(m, f.s->members[g], f.uni, f.W, f.H, og, dst, m->stream);
     HIPCHK(hipEventRecord(c->gev_rendered[g], m->stream));
     HIPCHK(hipStreamWaitEvent(c->gstream[g], c->gev_rendered[g], 0));
-    const size_t bytes = (size_t)(std::min(te * kTile, f.H) - tb * kTile) * f.row_bytes;
-    if (path == kGroupRccl) {  // member 0's receive is queued by the caller (render_group)
-        const ncclResult_t r = ncclSend(dst, bytes, ncclUint8, 0, c->comms[g], c->gstream[g]);
-        if (r != ncclSuccess) throw GsError(GS_ERR_HIP, std::string("ncclSend: ") + ncclGetErrorString(r));
-    } else {  // peer copy into the image, after the caller's earlier work on it (gev_entry)
+    {  // peer copy into the image, after the caller's earlier work on it (gev_entry)
         HIPCHK(hipStreamWaitEvent(c->gstream[g], c->gev_entry, 0));
         HIPCHK(hipMemcpyPeerAsync(img, c->members[0]->device, dst, m->device, bytes, c->gstream[g]));
     }
@@ -1391,10 +1446,17 @@ static void render_group(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     // the strips land in `out` after the caller's earlier work on it
     HIPCHK(hipSetDevice(dev0));
     HIPCHK(hipEventRecord(c->gev_entry, st0));
-    static const bool serial = [] {  // GS_GROUP_SERIAL=1: every member from the caller's thread (A/B)
+    static const bool serial_env = [] {  // GS_GROUP_SERIAL=1: every member from the caller's thread (A/B)
         const char* e = std::getenv("GS_GROUP_SERIAL");
         return e && e[0] == '1';
     }();
+    // (not with RCCL: member 0's receives are queued before the sends, and one thread issuing both
+    // could block in the first connection setup -- ADVICE r04)
+    const bool serial = serial_env && !rccl;
+    if (rccl) {  // every strip buffer exists before any receive is queued (each receive gets its send)
+        for (int g = 1; g < G; ++g) ensure_group_buffers(c, g, (size_t)H * f.row_bytes);
+        HIPCHK(hipSetDevice(dev0));
+    }
     static const int trace = [] {  // GS_GROUP_TRACE=1: per-member enqueue times to stderr every 200 frames; 2: every frame
         const char* e = std::getenv("GS_GROUP_TRACE");
         return e ? std::atoi(e) : 0;
@@ -2163,6 +2225,8 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
                 a.frames_chunked = std::max(a.frames_chunked, m.frames_chunked);
                 a.frames_seeded = std::max(a.frames_seeded, m.frames_seeded);
                 a.tile_row_end = std::max(a.tile_row_end, m.tile_row_end);
+                a.list_max = std::max(a.list_max, m.list_max);
+                a.tiles_long += m.tiles_long;
                 for (float* f : {&a.ms_total, &a.ms_project, &a.ms_sort, &a.ms_bin, &a.ms_tile_sort, &a.ms_ranges,
                                  &a.ms_composite, &a.ms_other}) {
                     const float v = *(const float*)((const char*)&m + ((const char*)f - (const char*)&a));
@@ -2189,6 +2253,8 @@ int gs_timings(gs_ctx* c, gs_stats* out) {
             st.wide_chunk1 = l.wide_n[1];
             st.chunk_fraction = l.n_vis ? (float)l.n_chunk[0] / (float)l.n_vis : 0.0f;
             st.chunk_depth = l.frame_T == kNoSplit ? 0.0f : std::fabs(key_to_float(l.frame_T));
+            st.list_max = l.list_max;
+            st.tiles_long = l.long_n;
         }
         st.frames = (int32_t)c->comp_frames;
         for (gs_scene* s : c->scenes) collect_stats(s, false);

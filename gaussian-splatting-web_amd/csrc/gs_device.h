@@ -78,6 +78,8 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t frame_T;             // the frame's chunk threshold, whichever its source (k_part_list)
     uint32_t sat_hist[kSatBuckets];  // tiles saturated by the end of the frame, by saturation depth
                                      // (sat_bucket; summed from the shards at the frame's end)
+    uint32_t list_max;            // longest tile list of the frame (either chunk) when > kListMaxMin, else 0
+    uint32_t long_n;              // tiles the 1024-thread sort shape left to the long-list pass (TileSortParams::long_tiles)
 };
 
 // Per-frame counters that many workgroups add to, sharded so that no address takes more than a
@@ -106,7 +108,9 @@ struct StatShard {
     uint32_t order_n[2];          // shards 0-7: the composite order of XCD band x (k_tile_sort)
     uint32_t wl_n[2];             // wide splats of wide-list shard (= this shard's index) per chunk
                                   // (ProjParams::wlist; zeroed with the shard, not summed)
+    uint32_t list_max;            // k_tile_sort: longest list of the shard's tiles (only lists > kListMaxMin)
 };
+constexpr uint32_t kListMaxMin = 1024;  // shorter lists do not report their length (one atomic per long list)
 
 // Bound of a projection partition (k_part_bounds, at upload): box of its finite positions,
 // largest ||R(q) diag(s)||_F^2, count of finite positions.
@@ -306,6 +310,14 @@ struct TileSortParams {
     // *c1_n entries; the launch walks it instead of every tile (nullable)
     const uint32_t* c1tiles;
     const uint32_t* c1_n;
+    // the 1024-thread shape (big == 2) sorts lists of <= 8192 entries in one LDS round; a longer
+    // list's tile is appended here (count FrameCtl::long_n) and sorted afterwards by the 256-thread
+    // shape's linear long-list path (launch_tile_sort's second launch) instead of in rounds that
+    // each re-read the list (O(L^2 / 8192))
+    uint32_t* long_tiles;
+    uint32_t* long_n;             // &FrameCtl::long_n
+    StatShard* stats;             // nullable: list_max
+    uint32_t long_grid;           // workgroups of the long-list launch (>= the lists that can exceed 8192)
 };
 
 constexpr uint32_t kTsBigMean = 800;  // mean chunk-0 list length from which k_tile_sort_big sorts chunk 0

@@ -2200,6 +2200,10 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
         for (uint32_t j = 0; j < kStatShards; ++j)
             kt += (unsigned long long)lds[j * kStride] | ((unsigned long long)lds[j * kStride + 1] << 32);
         ctl->k_total = kt;
+    } else if (lane == offsetof(StatShard, list_max) / 4) {
+        uint32_t a = 0;
+        for (uint32_t j = 0; j < kStatShards; ++j) a = max(a, lds[j * kStride + lane]);
+        ctl->list_max = a;
     } else if (lane >= 2 && lane < 8 + kSatBuckets) {
         const bool is_max = lane == 3 || lane == 4 || lane == 7;  // key_min_inv, key_max, sat_key
         uint32_t a = 0;
@@ -2774,9 +2778,16 @@ __device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const in
     const uint2 range = p.ranges[tile];
     const uint32_t L = range.y - range.x;
     if (L == 0) return;
+    const int tid = threadIdx.x;
+    if (L > kListMaxMin && tid == 0 && p.stats) atomicMax(&p.stats[tile % kStatShards].list_max, L);
+    if constexpr (C::NT > TsBig::NT) {
+        if (L > kTsCap && p.long_tiles) {  // left to the long-list launch (ts_long at 256 threads)
+            if (tid == 0) p.long_tiles[atomicAdd(p.long_n, 1u)] = (uint32_t)tile;
+            return;
+        }
+    }
     const uint32_t* __restrict__ in = p.in + range.x;
     uint32_t* __restrict__ out = p.out + range.x;
-    const int tid = threadIdx.x;
     unsigned long long k[kTsIpt];
     uint32_t v[kTsIpt];
     if (L == 1) {
@@ -2821,8 +2832,8 @@ __device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const in
         ts_segment<C>(S, k, v, L, mn, mx, out);
         return;
     }
-    // k_tile_sort_huge: a list past 8192 in rounds of 8192 (ts_long at 1024 threads would spill;
-    // the shape runs when lists average 3000-odd entries, so few are that long)
+    // k_tile_sort_huge without a long-list launch: a list past 8192 in rounds of 8192 (ts_long at
+    // 1024 threads would spill)
     if constexpr (C::NT > TsBig::NT)
         ts_rounds<C>(p, S, in, out, L);
     else
@@ -3829,9 +3840,17 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
 void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return;
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);
-    if (p.big == 2 && !p.done)  // chunk-0 lists of thousands (one-chunk frames at 4K)
+    if (p.big == 2 && !p.done) {  // chunk-0 lists of thousands (one-chunk frames at 4K)
         hipLaunchKernelGGL(k_tile_sort_huge, dim3(grid), dim3(TsHuge::NT), 0, s, p);
-    else if (p.done || p.big)  // chunk 1 (the unsaturated tiles' long lists), or long chunk-0 lists
+        if (p.long_tiles && p.long_n && p.long_grid) {  // the lists past one LDS round: linear, 256 threads
+            TileSortParams q = p;
+            q.c1tiles = p.long_tiles;
+            q.c1_n = p.long_n;
+            q.long_tiles = nullptr;
+            q.stats = nullptr;
+            hipLaunchKernelGGL(k_tile_sort_big, dim3(std::min<uint32_t>(p.long_grid, grid)), dim3(TsBig::NT), 0, s, q);
+        }
+    } else if (p.done || p.big)  // chunk 1 (the unsaturated tiles' long lists), or long chunk-0 lists
         hipLaunchKernelGGL(k_tile_sort_big, dim3(grid), dim3(TsBig::NT), 0, s, p);
     else
         hipLaunchKernelGGL(k_tile_sort, dim3(grid), dim3(TsSmall::NT), 0, s, p);

@@ -68,7 +68,7 @@ class GsStats(ctypes.Structure):
                 ("wide_chunk0", ctypes.c_uint32), ("wide_chunk1", ctypes.c_uint32),
                 ("frames_rendered", ctypes.c_uint32), ("frames_chunked", ctypes.c_uint32),
                 ("frames_unsat", ctypes.c_uint32), ("frames_seeded", ctypes.c_uint32),
-                ("chunk_depth", ctypes.c_float)]
+                ("chunk_depth", ctypes.c_float), ("list_max", ctypes.c_uint32), ("tiles_long", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

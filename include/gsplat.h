@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4
+#define GS_ABI_VERSION 5
 
 typedef struct gs_ctx gs_ctx;
 typedef struct gs_scene gs_scene;
@@ -126,6 +126,11 @@ typedef struct gs_stats {
     uint32_t frames_seeded;    /* ... whose split depth came from the frame's own coarse depth
                                   estimate (no usable history: a first frame or a camera cut) */
     float chunk_depth;         /* |view depth| of the last frame's chunk split (0: one chunk) */
+    /* ABI 5: */
+    uint32_t list_max;         /* longest tile list of the last frame, either chunk (0 when none is
+                                  longer than 1024 entries) */
+    uint32_t tiles_long;       /* tiles whose list outgrew the 1024-thread sort shape's one LDS
+                                  round (8192 entries) and went to the linear long-list sort */
 } gs_stats;
 
 /* ---- library / device ---------------------------------------------------------------------- */

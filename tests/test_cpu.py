@@ -258,7 +258,7 @@ def test_abi_exports_every_declared_symbol():
     L = gs.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert L.gs_abi_version() == 4
+    assert L.gs_abi_version() == 5
 
 
 def test_abi_rejects_without_device():

@@ -222,6 +222,47 @@ def test_tile_order_long_lists(gpu_ctx, n, plane_frac):
     assert r[2], r
 
 
+def test_tile_order_long_tail(gpu_ctx):
+    """A few tiles of 20 K+ entries among lists of ~4 K: the
+    second frame takes the 1024-thread shape (the last frame's mean list > 3000), which sorts a
+    list of <= 8192 entries in one LDS round and hands every longer one to the linear long-list
+    pass (ts_long at 256 threads, FrameCtl::long_n) instead of rounds of 8192 that each re-read
+    the list.  Orders must equal the stable global order restricted to each tile; the frame's
+    statistics report the longest list and the tiles sent to the long-list pass."""
+    W, H, n = 320, 240, 1_600_000
+    rng = np.random.default_rng(11)
+    aos = gs.synth_aos(n, 83, W, H).reshape(n, 80)
+    aos[:, 12] -= 4.0  # faint: long lists, nothing saturates
+    # a dense cluster: 120 K Gaussians within ~16 px of the image centre at depth 6-10
+    m = rng.choice(n, 120_000, replace=False)
+    d = rng.uniform(6.0, 10.0, m.size).astype(np.float32)
+    t = np.float32(np.tan(np.pi / 6))
+    aos[m, 0] = rng.uniform(-0.1, 0.1, m.size).astype(np.float32) * d * t * np.float32(W / H)
+    aos[m, 1] = rng.uniform(-0.1, 0.1, m.size).astype(np.float32) * d * t
+    aos[m, 2] = -d
+    aos = aos.reshape(-1)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    sp = orc.project(aos.view(np.uint8), n, 16, u, W, H)
+    imgs = []
+    for f in range(3):
+        gpu_ctx.timings_reset()
+        imgs.append(sc.render(u, W, H, gs.make_opts(chunk_fraction=1.0, t_min=0.0)))
+        rg, en = check_tile_lists(sc, sp, W, H, full_sets=False)
+        lens = (rg[:, 1] - rg[:, 0]).astype(np.int64)
+        assert lens.max() > 20_000 and np.median(lens) > 3000, (lens.max(), np.median(lens))
+        assert 0 < (lens > 8192).sum() <= 16, (lens > 8192).sum()
+        gpu_ctx.sync()
+        st = gpu_ctx.timings()
+        assert st["list_max"] == lens.max(), (st["list_max"], lens.max())
+        if f >= 1:  # the 1024-thread shape: every list past one round went to the long-list pass
+            assert st["tiles_long"] == (lens > 8192).sum(), (st["tiles_long"], (lens > 8192).sum())
+    assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[1], imgs[2])
+    ref, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=0, t_min=0.0)
+    r = image_close_fp32(imgs[1], ref, name="long_tail")
+    assert r[2], r
+
+
 # ------------------------------------------------------------------------------- ref_quirks
 def test_keyed_slots_rule():
     assert orc.keyed_slots(62) == 62 and orc.keyed_slots(100) == 96 and orc.keyed_slots(1003) == 1000

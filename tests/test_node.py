@@ -33,7 +33,7 @@ def run_node(*args, timeout=120):
 def test_node_host_cpu():
     out = run_node(os.path.join(ROOT, "tests", "node", "host_checks.js"), os.path.join(GOLDEN, "cameras.json"))
     assert out["exports"] == EXPORTS
-    assert out["abi"] == 4
+    assert out["abi"] == 5
     if out["deviceCount"] == 0:
         assert out["createRejected"] == "string" and out["requestRejected"] == "string"
     assert out["ctorThrows"] is True

@@ -21,7 +21,8 @@ def main():
     L = ctypes.CDLL(gs.LIB_PATH)
     import numpy as np
     buf = gs.DeviceBuffer(H * W * 8)
-    o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=2)
+    G, g = int(os.environ.get("G", 1)), int(os.environ.get("STRIP", 0))
+    o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=2, strip_index=g, strip_count=G)
     for _ in range(4):
         sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
     ctx.sync()
@@ -32,6 +33,10 @@ def main():
     ctx.sync()
     print("composite (HIP events) %.1f us per frame" % (ctx.timings()["ms_composite"] * 1e3))
     ntile = ((W + 15) // 16) * ((H + 15) // 16)
+    if G > 1:  # the strip's tiles (local tile ids)
+        from gsplat_amd.strips import strip_geometry
+        ntile = ((W + 15) // 16) * (strip_geometry(H, g, G)[1] // 16)
+        H = strip_geometry(H, g, G)[1]
     cn = np.zeros((16384, 2, 8), dtype=np.uint64)
     L.gs_diag_comp_counters(cn.ctypes.data_as(ctypes.c_void_p), 16384)
     c = cn[:ntile].sum(axis=(0, 1)).astype(np.float64)  # the last frame

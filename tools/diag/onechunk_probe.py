@@ -40,8 +40,9 @@ def main():
             ctx.sync()
             t.append(time.perf_counter() - t0)
         st = ctx.timings()
-        print("%s one-chunk frame: mean %.3f ms min %.3f ms; n_vis %d k_binned %d" %
-              (which, 1e3 * sum(t) / len(t), 1e3 * min(t), st["n_vis"], st["k_entries"]), flush=True)
+        print("%s one-chunk frame: mean %.3f ms min %.3f ms; n_vis %d k_binned %d; longest list %d, "
+              "tiles to the long-list pass %d" % (which, 1e3 * sum(t) / len(t), 1e3 * min(t), st["n_vis"],
+                                                  st["k_entries"], st["list_max"], st["tiles_long"]), flush=True)
         buf.free()
         sc.close()
 
