@@ -176,6 +176,10 @@ def main():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the latency / orbit / stage loops")
+    ap.add_argument("--list-split", type=int, default=0, choices=(0, 1),
+                    help="gs_opts.list_split: one serial chain per tile (0, default: bit-identical across "
+                         "chunk splits, strips and groups) or long tile lists of frames with few tiles over "
+                         "several wave pairs (1)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -211,8 +215,8 @@ def main():
     # timed loop: HIP events around the composite only (timing=2; an event record costs the stream a
     # few microseconds); a separate shorter loop with events between every stage (timing=1) gives
     # the stage breakdown
-    opts_head = gs.make_opts(strip_index=rank, strip_count=world, timing=2, out_format=gs.GS_OUT_RGBA_F16)
-    opts_stage = gs.make_opts(strip_index=rank, strip_count=world, timing=1, out_format=gs.GS_OUT_RGBA_F16)
+    opts_head = gs.make_opts(strip_index=rank, strip_count=world, list_split=args.list_split, timing=2, out_format=gs.GS_OUT_RGBA_F16)
+    opts_stage = gs.make_opts(strip_index=rank, strip_count=world, list_split=args.list_split, timing=1, out_format=gs.GS_OUT_RGBA_F16)
     cur = {"opts": opts_head}
     strip_bytes = rows_padded * W * 8
     if launched:
@@ -273,7 +277,7 @@ def main():
     extra = {}
     if not args.no_extra:
         # median single-frame time of 50 frames (each frame waited for, no overlap)
-        cur["opts"] = gs.make_opts(strip_index=rank, strip_count=world, out_format=gs.GS_OUT_RGBA_F16)
+        cur["opts"] = gs.make_opts(strip_index=rank, strip_count=world, list_split=args.list_split, out_format=gs.GS_OUT_RGBA_F16)
         lat = []
         for _ in range(50):
             t0 = time.perf_counter()
@@ -367,7 +371,7 @@ def main():
         sparse.close()
     # one untimed one-chunk frame for the exact visible count and K of SURVEY 8d's byte model
     # (with a chunk split the pipeline never projects the splats past it)
-    cur["opts"] = gs.make_opts(strip_index=rank, strip_count=world, chunk_fraction=1.0,
+    cur["opts"] = gs.make_opts(strip_index=rank, strip_count=world, list_split=args.list_split, chunk_fraction=1.0,
                                out_format=gs.GS_OUT_RGBA_F16)
     frame()
     sync()
@@ -422,7 +426,7 @@ def main():
                         seed, "; bicycle PLY absent" if args.config == 3 else ""),
             "config": {"workload": "configs[%d]: %d Gaussians (SH deg 3) at %dx%d, lookAt([0,0,0],[0,0,-1]) "
                                    "perspective(60deg,W/H,0.03,1000)" % (args.config, N, W, H),
-                       "n_gaussians": N, "width": W, "height": H,
+                       "n_gaussians": N, "width": W, "height": H, "list_split": args.list_split,
                        "parallelism": "row-strips x%d + all-gather" % world if world > 1 else "single GPU"},
             # per-stage HIP-event times from the separate timing=1 loop (events between stages add
             # ~20 us to its frame), except ms_composite, timed live in the headline loop:

@@ -910,7 +910,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
                          // c1tiles is free until the composite appends chunk 1's tiles to it
         tsp.long_tiles = F.c1tiles;
         tsp.long_n = &F.ctl->long_n;
-        tsp.long_grid = (uint32_t)std::min<uint64_t>((uint64_t)n_tiles, F.kcap / 8193u + 1u);
+        tsp.long_grid = (uint32_t)std::min(n_tiles, 2 * c->num_cus);
     }
     CompositeParams cp{};
     cp.ranges = F.ranges;
@@ -934,6 +934,10 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     s->stat_base[slot] = cp.sat_base;
     cp.out = out;
     cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
+    const bool split = o.list_split != 0 && o.accum != GS_ACCUM_FP16_TARGET;
+    // chunk 0: as many wave pairs per tile as keep every tile resident (a function of the frame's
+    // size only, so a view renders the same whatever came before it)
+    cp.seg = split ? composite_seg(n_tiles, c->num_cus) : 1;
     mark(EV_DSORT_0);
     launch_bin(bp, st);
     mark(EV_BIN_0);
@@ -970,9 +974,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.cp = cp;
         c1.cp.mode = kCompSecond;
         c1.cp.order = nullptr;
+        c1.cp.seg = split ? 4 : 1;  // chunk 1: a few tiles with long lists (launch_chunk1_split)
         c1.sat = F.sat;
         c1.bar = F.bar;
         c1.spin_ticks = c->spin_ticks;
+        c1.cus = c->num_cus;
         c1.two_chunks = two_chunks ? 1 : 0;
         const uint32_t q = s->seq_next++;
         s->stat_want[slot] = q;

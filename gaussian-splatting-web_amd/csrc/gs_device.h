@@ -317,7 +317,7 @@ struct TileSortParams {
     uint32_t* long_tiles;
     uint32_t* long_n;             // &FrameCtl::long_n
     StatShard* stats;             // nullable: list_max
-    uint32_t long_grid;           // workgroups of the long-list launch (>= the lists that can exceed 8192)
+    uint32_t long_grid;           // workgroups of the long-list launch (k_tile_sort_list strides the list)
 };
 
 constexpr uint32_t kTsBigMean = 800;  // mean chunk-0 list length from which k_tile_sort_big sorts chunk 0
@@ -344,7 +344,16 @@ struct CompositeParams {
     // the tiles chunk 0 leaves unsaturated: appended by the first pass (kCompFirst, position = its
     // FrameCtl::not_done ticket) and walked by chunk 1's per-tile sort and composite (kCompSecond)
     uint32_t* c1tiles;
+    int seg;                      // wave pairs per tile (the list split, composite_tile's SEG): 1, 2 or 4
 };
+// Wave pairs per tile for a chunk-0 composite of n_tiles tiles on `cus` CUs (gs_opts.list_split):
+// as many as keep every tile resident at once (a SEG-pair workgroup stages SEG x 14.5 KB in LDS:
+// 10 / 5 / 2 workgroups per CU for 1 / 2 / 4 pairs), 1 when the frame fills the device anyway.
+__host__ __device__ inline int composite_seg(int n_tiles, int cus) {
+    if (n_tiles <= 2 * cus) return 4;
+    if (n_tiles <= 5 * cus) return 2;
+    return 1;
+}
 
 struct Chunk1Params {
     ProjParams pp;                // chunk-1 slots (pp.sat = the unsaturated-tile row prefixes)
@@ -361,6 +370,7 @@ struct Chunk1Params {
     uint32_t* host_seq;
     uint32_t seq;
     uint32_t sat_lds_words;       // k_c1_rows: dynamic LDS of the summed-area table (0: global memory)
+    int cus;                      // the device's CUs (grids that stride chunk 1's compact tile list)
 };
 constexpr uint32_t kSatLdsWords = 36864;  // summed-area table of the unsaturated tiles built in LDS up to this size
 

@@ -2854,6 +2854,17 @@ __global__ __launch_bounds__(TsBig::NT, 4) void k_tile_sort_big(TileSortParams p
     // grid-stride loop over the list would spill: the sort body is at the 128-VGPR bound)
     tile_sort_body<TsBig>(p, blockIdx.x, S);
 }
+// The same over a compact tile list (chunk 1's unsaturated tiles, the huge shape's long lists)
+// with a grid of a few workgroups per CU striding it: one workgroup per possible entry cost a
+// full grid of mostly empty workgroups (8160 at 1080p: ~25 us of dispatch for tens of tiles).
+__global__ __launch_bounds__(TsBig::NT, 2) void k_tile_sort_list(TileSortParams p) {
+    __shared__ TsSharedT<TsBig> S;
+    const uint32_t nl = *p.c1_n;
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
+        tile_sort_tile<TsBig>(p, __builtin_amdgcn_readfirstlane((int)p.c1tiles[j]), S);
+        __syncthreads();
+    }
+}
 
 // ============================================================================ k_composite
 // Workgroup = one 16x16 tile, 2 waves; wave h owns the 8-wide column half h, and each lane owns
@@ -2874,8 +2885,19 @@ __global__ __launch_bounds__(TsBig::NT, 4) void k_tile_sort_big(TileSortParams p
 // per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
 constexpr int kCompBatch = 128;
 
+#if defined(GS_COMP_PHASE) && !defined(GS_COMP_TIME)
+#define GS_COMP_TIME 1
+#endif
 #if defined(GS_COMP_STATS) || defined(GS_COMP_TIME)
 #define GS_COMP_DIAG 1
+#endif
+#ifdef GS_COMP_PHASE  // diagnostics: per-wave shader cycles in g_comp_cnt[tile][wave][0..4]:
+                      // first batch (load, park, barrier), walks, parks, barriers, gathers
+#define CP_T0(v) const unsigned long long v = clock64()
+#define CP_ADD(i, v) (dg[i] += clock64() - v)
+#else
+#define CP_T0(v) do { } while (0)
+#define CP_ADD(i, v) do { } while (0)
 #endif
 #ifdef GS_COMP_DIAG
 // diagnostics builds only (make diag): counters of k_composite's per-wave blends (GS_COMP_STATS),
@@ -2929,24 +2951,43 @@ __device__ __forceinline__ void band_lane(int l, int& band, int& idx) {
 // distinct addresses per wave cost what one broadcast address does: a step costs what a step over
 // one half-tile list did, and a splat that reaches only one quarter no longer costs a whole step
 // of the wave (max(|top|, |bottom|) steps instead of |top u bottom|).
-template <bool FP16_TARGET>
+// List split (SEG > 1, round 5): a workgroup of SEG wave pairs composites one tile; pair s walks
+// the s-th of nseg = clamp(n / kSegMin, 1, SEG) equal, contiguous segments of the tile's list
+// (a function of the list only: run-to-run deterministic) with its own staging, pair 0 from the
+// tile's incoming state and pair s > 0 from (C = 0, T = 1); afterwards pair 0 merges in list
+// order, C += T C_s, T *= T_s while T >= t_min.  A pair stops once its own pixels' T < t_min, so
+// after the tile's true saturation point a later pair may still add contributions the one-chain
+// walk would skip: each is below t_min x colour.  The image therefore meets the fp32 oracle's bar
+// (and the WebGPU stand-in's) but is not bit-identical to the one-chain walk (SEG = 1, or any tile
+// whose list is shorter than 2 kSegMin, which is).  It divides a tile's serial chain -- what a
+// frame with fewer tiles than the chip holds at once (a row strip, chunk 1's unsaturated tiles)
+// is bound by -- by nseg.  FP16_TARGET (rgba16float rounding after every blend) has no such
+// merge: SEG is 1 there.
+constexpr uint32_t kSegMin = 96;  // shortest segment worth a pair of waves
+
+template <bool FP16_TARGET, int SEG>
 __device__ __forceinline__ void composite_tile(const CompositeParams& p, const int tile) {
+    static_assert(SEG == 1 || (!FP16_TARGET && (SEG == 2 || SEG == 4)), "list split: fp32 accumulation, 2 or 4 pairs");
+    constexpr int NT = 128 * SEG;
     // staged record per batch entry: [0] c0u, c0v, a, b  [1] c, d, log2(op), slot (bits)
     // [2] r, g, b, -   with u = a lx + b ly + c0u, v = c lx + d ly + c0v in tile-local pixels;
     // entry kCompBatch of buffer 1 is the null record (log2 op = -inf: alpha 0, nothing blended)
-    __shared__ float4 sR[2][kCompBatch + 1][3];
-    __shared__ uint16_t sL[2][2][kBands][kCompBatch];  // per half, per row band: LDS byte offsets
-                                                       // of the staged records in sR (segment =
-                                                       // producing wave, tail: the null record)
-    __shared__ uint32_t sN[2][2][kBands][2];           // per half, band, producing wave: list length
-    __shared__ uint32_t s_sat;                    // depth key of the splat that saturated the last wave
-    __shared__ uint32_t s_any[3][2];              // block_any flags: batches by parity, the tile's end
+    __shared__ float4 sR[SEG][2][kCompBatch + 1][3];
+    __shared__ uint16_t sL[SEG][2][2][kBands][kCompBatch];  // per half, per row band: LDS byte offsets
+                                                            // of the staged records in sR (segment =
+                                                            // producing wave, tail: the null record)
+    __shared__ uint32_t sN[SEG][2][2][kBands][2];           // per half, band, producing wave: list length
+    __shared__ uint32_t s_sat[SEG];               // depth key of the splat that saturated the pair's last wave
+    __shared__ uint32_t s_any[3][2 * SEG];        // block_any flags: batches by parity, the tile's end
+    __shared__ uint32_t s_qsat;                   // SEG > 1: the segment in which the merged tile saturated
     const int tid = threadIdx.x;
     if (p.mode == kCompSecond && p.done[tile]) return;
 #ifdef GS_COMP_DIAG
     const unsigned long long t_begin = wall_clock64();
 #endif
-    const int h = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int sg = SEG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 7) : 0;  // the pair's segment
+    const int ptid = SEG > 1 ? (tid & 127) : tid;                            // thread within the pair
+    const int h = __builtin_amdgcn_readfirstlane(ptid >> 6), lane = tid & 63;
     int qr, m;  // the lane's row band and its position in the band (band_lane)
     band_lane(lane, qr, m);
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x + p.tile_row_begin;
@@ -2955,11 +2996,23 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     const bool in0 = px < p.W && py < p.H, in1 = px < p.W && py + 1 < p.H;
     const float lx = (float)(px - tx0) + 0.5f;  // tile-local pixel centres
     const f2 ly = {(float)(py - ty0) + 0.5f, (float)(py - ty0) + 1.5f};
-    const uint2 range = p.ranges[tile];
+    const uint2 range0 = p.ranges[tile];
+    // the pair's segment of the list (the whole list when SEG = 1)
+    uint32_t nseg = 1;
+    uint2 range = range0;
+    if (SEG > 1) {
+        const uint32_t nall = range0.y - range0.x;
+        nseg = min((uint32_t)SEG, max(1u, nall / kSegMin));
+        nseg = __builtin_amdgcn_readfirstlane(nseg);
+        const uint32_t s = min((uint32_t)sg, nseg);
+        range.x = range0.x + (uint32_t)(((uint64_t)nall * s) / nseg);
+        range.y = sg < (int)nseg ? range0.x + (uint32_t)(((uint64_t)nall * (s + 1)) / nseg) : range.x;
+    }
     const float4* __restrict__ rec = p.rec;
     const uint32_t* __restrict__ tvals = p.tvals;
     const float L = 2.0f * kSqrtLog2e, amin = 1.0f / 255.0f, t_min = p.t_min;
-    constexpr uint32_t kNullOff = (uint32_t)((kCompBatch + 1 + kCompBatch) * 3 * 16);  // sR[1][kCompBatch]
+    // sR[sg][1][kCompBatch]
+    const uint32_t kNullOff = (uint32_t)((((sg * 2 + 1) * (kCompBatch + 1)) + kCompBatch) * 3 * 16);
     // the lane's pixel coordinates, recomputed where needed after the blend loop from the lane id
     // (mbcnt: not folded into the values computed before the loop, so none of them is held
     // across it — held, they were spilled)
@@ -2983,7 +3036,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 #ifdef GS_COMP_DIAG
     unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    if (p.mode == kCompSecond) {
+    if (p.mode == kCompSecond && sg == 0) {  // (pairs s > 0 start their segment from C = 0, T = 1)
         if (in0) {
             const float4 st = p.state[pix_of(0)];
             cr.x = st.x; cg.x = st.y; cb.x = st.z;
@@ -3004,7 +3057,9 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     bool wave_live = __any(live0 || live1);
 
     const uint32_t n = range.y - range.x;
-    const uint32_t nb = (n + kCompBatch - 1) / kCompBatch;
+    // batches: the longest segment's (every pair runs the same barriers)
+    const uint32_t nmax = SEG > 1 ? (range0.y - range0.x + nseg - 1) / nseg : n;
+    const uint32_t nb = (nmax + kCompBatch - 1) / kCompBatch;
     float4 ga, gb;  // the next batch's records in flight: geometry only (colour at park time)
     uint32_t gs_ = 0;
     bool gv = false;
@@ -3012,11 +3067,11 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     // b + 1 do not wait for a tile-list load first
     uint32_t sl_next = 0;
     auto load_slots = [&](uint32_t batch) {
-        const uint32_t e = range.x + batch * kCompBatch + tid;
+        const uint32_t e = range.x + batch * kCompBatch + ptid;
         if (e < range.y) sl_next = tvals[e];
     };
     auto gather = [&](uint32_t batch) {
-        const uint32_t e = range.x + batch * kCompBatch + tid;
+        const uint32_t e = range.x + batch * kCompBatch + ptid;
         gv = e < range.y;
         if (gv) {
             gs_ = sl_next;
@@ -3035,9 +3090,9 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         // staged as [b, a, d, c] [r, c0u, g, c0v] [b, log2 op, slot, key]: every value a packed
         // op broadcasts sits in the low half of an aligned register pair (no moves in the blend;
         // log2 op is broadcast from a high half by op_sel)
-        sR[buf][tid][0] = make_float4(ga.w, ga.z, gb.y, gb.x);
-        sR[buf][tid][1] = make_float4(gc.x, c0u, gc.y, c0v);
-        sR[buf][tid][2] = make_float4(gc.z, gb.z, __uint_as_float(gs_), gc.w);
+        sR[sg][buf][ptid][0] = make_float4(ga.w, ga.z, gb.y, gb.x);
+        sR[sg][buf][ptid][1] = make_float4(gc.x, c0u, gc.y, c0v);
+        sR[sg][buf][ptid][2] = make_float4(gc.z, gb.z, __uint_as_float(gs_), gc.w);
         // the splat's pixel columns within each quarter's 8 rows (ellipse; the binning's margins),
         // against both column halves: 4 lists, each compacted per producing wave by a ballot; the
         // slots past a list's end hold the null record
@@ -3055,14 +3110,14 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                 const bool hit = cols && (int)ul <= qx + 7 && (int)uh >= qx;
                 const uint64_t b = __ballot(hit);
                 const uint32_t cnt = (uint32_t)__popcll(b);
-                uint16_t* Lq = &sL[buf][hx][hy][h * 64];
-                if (hit) Lq[__popcll(b & lanemask_lt())] = (uint16_t)(((buf * (kCompBatch + 1) + tid) * 3) * 16);
+                uint16_t* Lq = &sL[sg][buf][hx][hy][h * 64];
+                if (hit) Lq[__popcll(b & lanemask_lt())] = (uint16_t)((((sg * 2 + buf) * (kCompBatch + 1) + ptid) * 3) * 16);
                 if ((uint32_t)lane >= cnt) Lq[lane] = (uint16_t)kNullOff;
-                if (lane == 0) sN[buf][hx][hy][h] = cnt;
+                if (lane == 0) sN[sg][buf][hx][hy][h] = cnt;
             }
         }
     };
-    const char* const sRb = (const char*)&sR[0][0][0];
+    const char* const sRb = (const char*)&sR[0][0][0][0];
     auto blend = [&](uint32_t off) {
         const float4 A = *(const float4*)(sRb + off);
         const float4 B = *(const float4*)(sRb + off + 16);
@@ -3135,26 +3190,37 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 #ifdef GS_COMP_DIAG
     if (tid == 0) dg[7] = n;
 #endif
-    if (tid == 0) s_sat = 0;
-    if (tid < 3) sR[1][kCompBatch][tid] = make_float4(0.0f, tid == 2 ? -INFINITY : 0.0f, 0.0f, 0.0f);
+    if (ptid == 0) s_sat[sg] = 0;
+    if (ptid < 3) sR[sg][1][kCompBatch][ptid] = make_float4(0.0f, ptid == 2 ? -INFINITY : 0.0f, 0.0f, 0.0f);
+#ifdef GS_COMP_PHASE
+    const unsigned long long cp_start = clock64();
+#endif
     if (nb > 0) {
         load_slots(0);
         gather(0);
         park(0);
     }
     __syncthreads();
+#ifdef GS_COMP_PHASE
+    dg[0] += clock64() - cp_start;
+#endif
     for (uint32_t b = 0; b < nb; ++b) {
         const int cur = b & 1;
-        if (b + 1 < nb) gather(b + 1);  // in flight while this batch is blended
+        {
+            CP_T0(cg0);
+            if (b + 1 < nb) gather(b + 1);  // in flight while this batch is blended
+            CP_ADD(4, cg0);
+        }
+        CP_T0(cw0);
         if (wave_live) {
             for (int seg = 0; seg < 2 && wave_live; ++seg) {
                 // both quarters' lists of this producing wave, in lockstep (the shorter one's tail
                 // is the null record)
-                uint32_t cmax = sN[cur][h][0][seg];
+                uint32_t cmax = sN[sg][cur][h][0][seg];
 #pragma unroll
-                for (int bb = 1; bb < kBands; ++bb) cmax = max(cmax, sN[cur][h][bb][seg]);
+                for (int bb = 1; bb < kBands; ++bb) cmax = max(cmax, sN[sg][cur][h][bb][seg]);
                 const int cnt = (int)cmax;
-                const uint16_t* list = &sL[cur][h][qr][seg * 64];  // this lane's band
+                const uint16_t* list = &sL[sg][cur][h][qr][seg * 64];  // this lane's band
                 int k = 0;
                 for (; k + 3 < cnt; k += 4) {  // saturation checked every 4 steps
                     const uint32_t o3 = list[k + 3];
@@ -3164,7 +3230,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                     blend(o3);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (m == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + o3 + 44));
+                        if (m == 0) atomicMax(&s_sat[sg], *(const uint32_t*)(sRb + o3 + 44));
                         break;
                     }
                 }
@@ -3173,21 +3239,29 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                     blend(ok);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (m == 0) atomicMax(&s_sat, *(const uint32_t*)(sRb + ok + 44));
+                        if (m == 0) atomicMax(&s_sat[sg], *(const uint32_t*)(sRb + ok + 44));
                     }
                 }
             }
         }
-        if (b + 1 < nb) park(cur ^ 1);
-        if (!block_any<128>(wave_live, s_any[b & 1])) break;
+        CP_ADD(1, cw0);
+        {
+            CP_T0(cp0);
+            if (b + 1 < nb) park(cur ^ 1);
+            CP_ADD(2, cp0);
+        }
+        CP_T0(cb0);
+        const bool go_on = block_any<NT>(wave_live, s_any[b & 1]);
+        CP_ADD(3, cb0);
+        if (!go_on) break;
     }
 #ifdef GS_COMP_DIAG
-    if (lane == 0 && tile < 16384)
+    if (sg == 0 && lane == 0 && tile < 16384)
         for (int i = 0; i < 8; ++i) g_comp_cnt[tile][h][i] = dg[i];
     __shared__ uint32_t s_blends;
     if (tid == 0) s_blends = 0;
     __syncthreads();
-    if (lane == 0) atomicAdd(&s_blends, (uint32_t)dg[0]);
+    if (lane == 0 && sg == 0) atomicAdd(&s_blends, (uint32_t)dg[0]);
     __syncthreads();
     if (tid == 0 && tile < 16384) {
         uint32_t hw;
@@ -3199,11 +3273,55 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
         g_comp_time[tile][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
     }
 #endif
-    const bool tile_done = !block_any<128>(live0 || live1, s_any[2]);
-    if (tile_done && tid == 0 && n > 0) {  // saturation statistics for the chunk controller
+    if (SEG > 1 && nseg > 1) {
+        // the segments' (C, T) through LDS (each pair's own staging area, dead now), merged by
+        // pair 0 in list order
+        f2* sM = (f2*)&sR[sg][0][0][0];  // [4][128]: r, g, b, T of the pair's pixel pairs
+        __syncthreads();                  // (every pair's walk has read its staging area)
+        if (sg > 0 && sg < (int)nseg) {
+            sM[0 * 128 + ptid] = cr;
+            sM[1 * 128 + ptid] = cg;
+            sM[2 * 128 + ptid] = cb;
+            sM[3 * 128 + ptid] = T;
+            if (ptid == 0 && s_sat[sg] == 0 && n > 0)  // never saturated alone: its last splat's key
+                s_sat[sg] = __float_as_uint(rec[3 * (uint64_t)tvals[range.y - 1] + 2].w);
+        }
+        if (tid == 0) s_qsat = 0;
+        __syncthreads();
+        if (sg == 0) {
+            int q0 = 0, q1 = 0;  // the segment in which each pixel's merged T fell below t_min
+            for (uint32_t q = 1; q < nseg; ++q) {
+                const f2* mq = (const f2*)&sR[q][0][0][0];
+                const f2 qr_ = mq[0 * 128 + ptid], qg = mq[1 * 128 + ptid], qb = mq[2 * 128 + ptid];
+                const f2 qt = mq[3 * 128 + ptid];
+                if (T.x >= t_min) {
+                    cr.x = __builtin_fmaf(T.x, qr_.x, cr.x);
+                    cg.x = __builtin_fmaf(T.x, qg.x, cg.x);
+                    cb.x = __builtin_fmaf(T.x, qb.x, cb.x);
+                    T.x = T.x * qt.x;
+                    if (T.x < t_min) q0 = (int)q;
+                }
+                if (T.y >= t_min) {
+                    cr.y = __builtin_fmaf(T.y, qr_.y, cr.y);
+                    cg.y = __builtin_fmaf(T.y, qg.y, cg.y);
+                    cb.y = __builtin_fmaf(T.y, qb.y, cb.y);
+                    T.y = T.y * qt.y;
+                    if (T.y < t_min) q1 = (int)q;
+                }
+            }
+            live0 = T.x >= t_min;
+            live1 = T.y >= t_min;
+            const int qm = max(q0, q1);
+            if (qm > 0) atomicMax(&s_qsat, (uint32_t)qm);
+        }
+    }
+    const bool tile_done = !block_any<NT>(sg == 0 && (live0 || live1), s_any[2]);
+    if (SEG > 1 && sg != 0) return;
+    if (tile_done && tid == 0 && range0.y > range0.x) {  // saturation statistics for the chunk controller
+        const uint32_t key = SEG > 1 && nseg > 1 ? s_sat[s_qsat] : s_sat[0];
         StatShard* sh = p.stats + tile % kStatShards;
-        atomicAdd(&sh->sat_hist[sat_bucket(s_sat, p.sat_base)], 1u);
-        atomicMax(&sh->sat_key, s_sat);
+        atomicAdd(&sh->sat_hist[sat_bucket(key, p.sat_base)], 1u);
+        atomicMax(&sh->sat_key, key);
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {  // park the pixels for chunk 1
@@ -3239,11 +3357,22 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 // tiles, 2560 resident workgroups; the last partly filled round costs ~25 % of the span): a
 // resident grid with per-band ticket counters (278 us), an equal static share per workgroup
 // (285 us) and one ticket counter for all bands (352 us) were all slower than this (230 us).
-template <bool FP16_TARGET>
-__global__ __launch_bounds__(128, GS_COMP_WAVES) void k_composite(CompositeParams p) {
+template <bool FP16_TARGET, int SEG>
+__global__ __launch_bounds__(128 * SEG, SEG == 1 ? GS_COMP_WAVES : (SEG == 2 ? 5 : 2)) void k_composite(CompositeParams p) {
     const int per = (p.n_tiles + 7) >> 3;
     const int j = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // XCD band, position
-    if (j < p.n_tiles) composite_tile<FP16_TARGET>(p, p.order ? (int)p.order[j] : j);
+    if (j < p.n_tiles) composite_tile<FP16_TARGET, SEG>(p, p.order ? (int)p.order[j] : j);
+}
+
+// Chunk 1 (kCompSecond): workgroup j takes entry j of the compact list of the tiles chunk 0 left
+// unsaturated; the rest return at once.  (A grid of a few workgroups per CU striding the list was
+// slower: orbit frames' chunk-1 composite 69 -> 87 us, k_composite_q 71 -> 100 us; up to ~2600
+// tiles are listed, most with few chunk-1 entries, and a strided workgroup walks its share of
+// them one after another.)
+template <bool FP16_TARGET, int SEG>
+__global__ __launch_bounds__(128 * SEG, 2) void k_composite_c1(CompositeParams p) {
+    if (blockIdx.x >= p.ctl->not_done) return;
+    composite_tile<FP16_TARGET, SEG>(p, __builtin_amdgcn_readfirstlane((int)p.c1tiles[blockIdx.x]));
 }
 
 // Quarter variant for frames with few tiles (row strips): 4 waves per tile, wave q owns the 8x8
@@ -3848,7 +3977,7 @@ void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
             q.c1_n = p.long_n;
             q.long_tiles = nullptr;
             q.stats = nullptr;
-            hipLaunchKernelGGL(k_tile_sort_big, dim3(std::min<uint32_t>(p.long_grid, grid)), dim3(TsBig::NT), 0, s, q);
+            hipLaunchKernelGGL(k_tile_sort_list, dim3(std::min<uint32_t>(p.long_grid, grid)), dim3(TsBig::NT), 0, s, q);
         }
     } else if (p.done || p.big)  // chunk 1 (the unsaturated tiles' long lists), or long chunk-0 lists
         hipLaunchKernelGGL(k_tile_sort_big, dim3(grid), dim3(TsBig::NT), 0, s, p);
@@ -3888,11 +4017,14 @@ void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
         launch_tile_sort(c.tp, s);
         // the unsaturated tiles only, each with a long list: 4 waves per tile at any frame size;
         // workgroup j takes entry j of the compact tile list (c1tiles), the rest return at once
-        const unsigned grid = 8u * (unsigned)((c.cp.n_tiles + 7) / 8);
+        // (list split: the 4-pair half-tile kernel, the long lists cut into segments)
+        const unsigned cgrid = 8u * (unsigned)((c.cp.n_tiles + 7) / 8);
         if (accum_fp16)
-            hipLaunchKernelGGL(k_composite_q<true>, dim3(grid), dim3(256), 0, s, c.cp);
+            hipLaunchKernelGGL(k_composite_q<true>, dim3(cgrid), dim3(256), 0, s, c.cp);
+        else if (c.cp.seg > 1)
+            hipLaunchKernelGGL((k_composite_c1<false, 4>), dim3(cgrid), dim3(512), 0, s, c.cp);
         else
-            hipLaunchKernelGGL(k_composite_q<false>, dim3(grid), dim3(256), 0, s, c.cp);
+            hipLaunchKernelGGL(k_composite_q<false>, dim3(cgrid), dim3(256), 0, s, c.cp);
     }
     hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, c);
 }
@@ -3904,14 +4036,14 @@ void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
             hipLaunchKernelGGL(k_composite_q<true>, dim3(grid), dim3(256), 0, s, p);
         else
             hipLaunchKernelGGL(k_composite_q<false>, dim3(grid), dim3(256), 0, s, p);
+    } else if (accum_fp16) {
+        hipLaunchKernelGGL((k_composite<true, 1>), dim3(grid), dim3(128), 0, s, p);
+    } else if (p.seg >= 4) {
+        hipLaunchKernelGGL((k_composite<false, 4>), dim3(grid), dim3(512), 0, s, p);
+    } else if (p.seg == 2) {
+        hipLaunchKernelGGL((k_composite<false, 2>), dim3(grid), dim3(256), 0, s, p);
     } else {
-#ifndef GS_COMP_DYN_LDS
-#define GS_COMP_DYN_LDS 0
-#endif
-        if (accum_fp16)
-            hipLaunchKernelGGL(k_composite<true>, dim3(grid), dim3(128), GS_COMP_DYN_LDS, s, p);
-        else
-            hipLaunchKernelGGL(k_composite<false>, dim3(grid), dim3(128), GS_COMP_DYN_LDS, s, p);
+        hipLaunchKernelGGL((k_composite<false, 1>), dim3(grid), dim3(128), 0, s, p);
     }
 }
 

@@ -51,7 +51,7 @@ class GsOpts(ctypes.Structure):
                 ("ref_quirks", ctypes.c_int32), ("strip_index", ctypes.c_int32),
                 ("strip_count", ctypes.c_int32), ("timing", ctypes.c_int32),
                 ("chunk_fraction", ctypes.c_float), ("tile_row_begin", ctypes.c_int32),
-                ("tile_row_end", ctypes.c_int32)]
+                ("tile_row_end", ctypes.c_int32), ("list_split", ctypes.c_int32)]
 
 
 class GsStats(ctypes.Structure):
@@ -312,13 +312,15 @@ def device_count():
 
 
 def make_opts(accum=GS_ACCUM_FP32, out_format=GS_OUT_RGBA_F32, t_min=1e-4, strip_index=0, strip_count=1,
-              timing=0, ref_quirks=0, chunk_fraction=0.0, tile_rows=None):
-    """gs_opts; tile_rows = (begin, end): an explicit strip of tile rows [begin, end)."""
+              timing=0, ref_quirks=0, chunk_fraction=0.0, tile_rows=None, list_split=0):
+    """gs_opts; tile_rows = (begin, end): an explicit strip of tile rows [begin, end); list_split = 1:
+    long tile lists of frames with few tiles split over wave pairs (gs_opts.list_split)."""
     o = GsOpts()
     lib().gs_opts_default(ctypes.byref(o))
     o.accum, o.out_format, o.t_min = accum, out_format, t_min
     o.strip_index, o.strip_count, o.timing, o.ref_quirks = strip_index, strip_count, timing, ref_quirks
     o.chunk_fraction = chunk_fraction
+    o.list_split = list_split
     if tile_rows is not None:
         o.tile_row_begin, o.tile_row_end = int(tile_rows[0]), int(tile_rows[1])
     return o

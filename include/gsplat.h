@@ -94,6 +94,15 @@ typedef struct gs_opts {
        [16*tile_row_begin, min(16*tile_row_end, H)), no padding.  K-balanced strips: gs_balance_strips. */
     int32_t tile_row_begin;
     int32_t tile_row_end;
+    /* (ABI 5) list split: 0 (default) = every tile's depth-ordered list is one serial chain of
+       blends; the image is then bit-identical whatever the chunk split, the strips or the device
+       group.  1 = in frames with fewer tiles than the device holds at once (row strips, chunk 1's
+       unsaturated tiles under a moving camera) a long tile list is cut into up to 4 contiguous
+       segments blended by separate wave pairs and merged in list order (C += T C_s, T *= T_s):
+       within the fp32 oracle bar and run-to-run deterministic, not bit-identical to 0 (a
+       segment may add contributions below t_min x colour after the tile's saturation point).
+       accum = GS_ACCUM_FP16_TARGET ignores it. */
+    int32_t list_split;
 } gs_opts;
 
 typedef struct gs_stats {

@@ -127,6 +127,37 @@ def test_bench_orbit_sequence(gpu_ctx, bench_scene):
 
 
 @pytest.mark.timeout(600)
+def test_bench_orbit_sequence_list_split(gpu_ctx, bench_scene):
+    """bench.py's orbit with the list split (gs_opts.list_split = 1, as bench.py renders its
+    orbit, cold and sparse lines and strips): chunk 1's long lists of the unsaturated tiles are cut
+    over 4 wave pairs.  Not bit-identical to the one-chunk render (tests/test_gpu_split.py); every
+    frame within 2e-3 of it (f16), the yaw extremes against the oracle and the WebGPU stand-in."""
+    aos, sc = bench_scene
+    W, H = W3, H3
+    u = gs.bench_uniforms(W, H)
+    head = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=2, list_split=1)
+    views = [gs.orbit_uniforms(W, H, k) for k in range(60)]
+    warm = [gs.DeviceBuffer(W * H * 8)]
+    _frames(sc, gpu_ctx, [u] * 5, W, H, head, warm * 5)
+    _frames(sc, gpu_ctx, views[:5], W, H, head, warm * 5)
+    bufs = [gs.DeviceBuffer(W * H * 8) for _ in range(60)]
+    gpu_ctx.timings_reset()
+    imgs = _frames(sc, gpu_ctx, views, W, H, head, bufs)
+    st = gpu_ctx.timings()
+    for b in bufs + warm:
+        b.free()
+    assert st["frames_unsat"] > 0, st
+    worst = 0.0
+    for k in range(0, 60, 5):
+        one = _one_chunk(sc, views[k], W, H)
+        worst = max(worst, float(np.abs(imgs[k].astype(np.float32) - one.astype(np.float32)).max()))
+    assert worst < 2e-3, worst
+    for k in (15, 45):
+        _vs_oracle(aos, N3, views[k], W, H, imgs[k], "bench_orbit_split_%d" % k)
+        webgpu_bar(imgs[k], aos, N3, 16, views[k], W, H, name="bench_orbit_split_%d_webgpu" % k)
+
+
+@pytest.mark.timeout(600)
 def test_bench_cold_sequence(gpu_ctx, bench_scene):
     aos, sc = bench_scene
     W, H = W3, H3

@@ -13,8 +13,8 @@ import gsplat_amd as gs  # noqa: E402
 
 
 def main():
-    N, W, H = int(os.environ.get("N", 6_100_000)), 1920, 1080
-    aos = gs.synth_aos(N, 6, W, H)
+    N, W, H = int(os.environ.get("N", 6_100_000)), int(os.environ.get("W", 1920)), int(os.environ.get("H", 1080))
+    aos = gs.synth_aos(N, int(os.environ.get("SEED", 6)), W, H)
     u = gs.bench_uniforms(W, H)
     ctx = gs.Context(0)
     sc = gs.Scene(ctx, aos, N, 16)
@@ -22,7 +22,8 @@ def main():
     import numpy as np
     buf = gs.DeviceBuffer(H * W * 8)
     G, g = int(os.environ.get("G", 1)), int(os.environ.get("STRIP", 0))
-    o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=2, strip_index=g, strip_count=G)
+    o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=2, strip_index=g, strip_count=G,
+                     list_split=int(os.environ.get("LIST_SPLIT", "0")))
     for _ in range(4):
         sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
     ctx.sync()
@@ -39,7 +40,16 @@ def main():
         H = strip_geometry(H, g, G)[1]
     cn = np.zeros((16384, 2, 8), dtype=np.uint64)
     L.gs_diag_comp_counters(cn.ctypes.data_as(ctypes.c_void_p), 16384)
+    ntile = min(ntile, 16384)
     c = cn[:ntile].sum(axis=(0, 1)).astype(np.float64)  # the last frame
+    if os.environ.get("PHASE"):  # GS_COMP_PHASE build: per-wave shader cycles by phase
+        ph = cn[:ntile, :, :5].astype(np.float64)
+        tot = ph.sum(axis=2)
+        names = ["first batch", "walks", "parks", "barriers", "gathers"]
+        print("phase kcycles per wave (mean over waves): " +
+              "  ".join("%s %.2f (%.0f%%)" % (nm, ph[:, :, i].mean() / 1e3, 100 * ph[:, :, i].sum() / tot.sum())
+                        for i, nm in enumerate(names)) + "  total %.2f" % (tot.mean() / 1e3))
+        c[0] = 0  # (the counters are not blend statistics)
     if c[0] > 0:
         px = 64 * 2 * c[0]
         print("wave blends/frame %.4g  pixel evals %.4g" % (c[0], px))

@@ -24,7 +24,8 @@ def main():
     modes = [("adaptive", 0.0, 0), ("one_chunk", 1.0, 0), ("adaptive_staged", 0.0, 1), ("one_chunk_staged", 1.0, 1)]
     only = os.environ.get("MODE")  # one mode only (e.g. under rocprofv3)
     for name, cf, timing in [m for m in modes if not only or m[0] == only]:
-        o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, chunk_fraction=cf, timing=timing)
+        o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, chunk_fraction=cf, timing=timing,
+                         list_split=int(os.environ.get("LIST_SPLIT", "0")))
         for k in range(5):
             sc.render_device(uo[k], W, H, buf.ptr.value, buf.nbytes, None, o)
         ctx.sync()

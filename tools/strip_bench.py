@@ -30,7 +30,7 @@ def main():
             if only is not None and g != only:
                 continue
             o = gs.make_opts(strip_index=g, strip_count=G, timing=int(os.environ.get("TIMING", "1")),
-                             out_format=gs.GS_OUT_RGBA_F16)
+                             out_format=gs.GS_OUT_RGBA_F16, list_split=int(os.environ.get("LIST_SPLIT", "0")))
             # warm-up: the scene's chunk controller was last fed another strip's statistics,
             # which reach the host up to 8 frames late
             for _ in range(int(os.environ.get("WARMUP", 20))):
