@@ -287,6 +287,7 @@ struct gs_scene {
     int last_fs = 0;                    // the set of the last frame
     uint32_t* orig = nullptr;           // [n] reference index of each storage slot (Morton order)
     PartBound* bounds = nullptr;        // [parts] partition bounds (upload)
+    PartBound* bbounds = nullptr;       // [ceil(n / kCullBlock)] block bounds (upload)
     ProjParams last_pp{};               // the last frame's projection (k_records for the debug dump)
     int last_tiles = 0;                 // tiles of the last frame's strip
     // asynchronous frame statistics (chunk controller, capacity): the frame's end (k_chunk1) stores FrameCtl into
@@ -826,6 +827,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.units = F.units;
     pp.plist0 = F.plist0;
     pp.bounds = s->bounds;
+    pp.bbounds = s->bbounds;
     pp.orig = s->orig;
     pp.sidx = F.sidx;
     pp.wlist = F.wlist;
@@ -846,6 +848,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         pp.cull = s->qcull;
         pp.sh = s->qshade;
         pp.bounds = s->qbounds;
+        pp.bbounds = nullptr;  // (the draw-ordered copy has partition bounds only)
         pp.orig = s->qorig;
         pp.key_zero = 1;
     }
@@ -1755,6 +1758,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
             dev_alloc(s->shade, (size_t)sh_quads(n_sh) * std::max<uint64_t>(n, 1));
             dev_alloc(s->cull, (size_t)std::max<uint64_t>(n, 1));
             dev_alloc(s->bounds, (size_t)proj_parts(n) + 1);
+            dev_alloc(s->bbounds, (size_t)((n + kCullBlock - 1) / kCullBlock) + 1);
             dev_alloc(s->orig, (size_t)n + 1);
             for (int k = 0; k < kFrameSets; ++k) {
                 FrameSet& F = s->fs[k];
@@ -1784,7 +1788,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                 dev_alloc(F.c0, (size_t)proj_parts(n) + 1);
                 dev_alloc(F.c1, (size_t)proj_parts(n) + 1);
                 dev_alloc(F.units, (size_t)kUnitShards * unit_shard_cap(proj_parts(n)) + 1);
-                dev_alloc(F.plist, (size_t)proj_parts(n) + 1);
+                dev_alloc(F.plist, (size_t)std::max<uint64_t>(proj_parts(n), (n + kCullBlock - 1) / kCullBlock) + 1);
                 dev_alloc(F.plist0, (size_t)proj_parts(n) + 1);
                 dev_alloc(F.cand, nslots);
                 dev_alloc(F.sidx, nslots);
@@ -1818,6 +1822,7 @@ int gs_scene_upload(gs_ctx* c, const void* aos, uint64_t n, int n_sh, gs_scene**
                     const auto r = device_sort_pairs(kA, vA, kB, vB, n, 0, 32, st);
                     launch_transpose(tmp, n, n_sh, r.second, s->geo, s->shade, s->cull, s->orig, st);
                     launch_part_bounds(s->cull, n, s->bounds, st);
+                    launch_block_bounds(s->cull, n, s->bbounds, st);
                     HIPCHK(hipGetLastError());
                     HIPCHK(hipStreamSynchronize(st));
                 } catch (...) {
@@ -1895,6 +1900,7 @@ void gs_scene_free(gs_scene* s) {
     for (int k = 0; k < kSetStreams; ++k)  // (sets past kSetStreams share these)
         if (s->fs[k].stream) (void)hipStreamDestroy(s->fs[k].stream);
     dev_free(s->bounds);
+    dev_free(s->bbounds);
     dev_free(s->orig);
     dev_free(s->qk); dev_free(s->qv); dev_free(s->qK); dev_free(s->qV); dev_free(s->qK2); dev_free(s->qV2);
     dev_free(s->qinv); dev_free(s->qgeo); dev_free(s->qshade); dev_free(s->qcull); dev_free(s->qorig);

@@ -18,6 +18,8 @@ constexpr int kSortThreads = 256;     // 4 waves
 constexpr int kSortIPT = 16;          // items per thread
 constexpr int kProjTile = 1024;       // projection partition: bounds, candidates, slot block
 constexpr int kProjRounds = kProjTile / kProjThreads;  // work units (rounds of kProjThreads) per partition
+constexpr int kCullBlock = 64;        // storage slots per block bound (one wave's cull planes)
+constexpr float kCullFaint = -1.0f;   // cull plane w of a Gaussian whose opacity is below 1/255
 constexpr int kUnitShards = 8;        // the frame's work-unit list, sharded (FrameCtl::unit_n)
 constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per radix partition
 constexpr int kBinThreads = 1024;     // binning workgroup (one partition of the chunk's ranks)
@@ -72,7 +74,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t key_max;             // largest depth key of a visible splat (project)
     uint32_t sat_key;             // depth key of the farthest splat a tile saturated at (the frame's end, k_chunk1)
     uint32_t unit_n[kUnitShards]; // chunk-0 work units per shard (k_cull; see ProjParams::units)
-    uint32_t c1_parts;            // chunk 1: projection partitions listed in ProjParams::plist (k_chunk1)
+    uint32_t c1_parts;            // chunk 1: items listed in ProjParams::plist: 64-slot blocks (partitions without block bounds)
     uint32_t c0_parts;            // chunk 0: projection partitions listed in ProjParams::plist0 (k_part_list)
     uint32_t seed_T;              // a seeded frame's chunk threshold (k_seed_pick; ProjParams::thresh_dev)
     uint32_t frame_T;             // the frame's chunk threshold, whichever its source (k_part_list)
@@ -186,6 +188,7 @@ struct ProjParams {
     uint16_t* cand;           // [parts * kProjTile] chunk-0 candidates: offsets in the partition (k_cull)
     uint32_t* units;          // [kUnitShards][unit_shard_cap] the non-empty chunk-0 work units (k_cull)
     const PartBound* bounds;  // [parts] (k_part_bounds)
+    const PartBound* bbounds; // [ceil(n / kCullBlock)] (k_block_bounds), nullable
     const uint32_t* orig;     // [n] reference index of each storage slot (Morton order)
     uint32_t* sidx;           // [slots] storage index of each composite slot
     // [slots] the slots of wide splats (>= wide_tiles box tiles): chunk 0's from the front,
@@ -381,6 +384,7 @@ void launch_morton(const uint8_t* aos, uint64_t n, uint32_t rb, const uint32_t* 
 void launch_transpose(const uint8_t* aos, uint64_t n, int n_sh, const uint32_t* perm, float4* geo, float4* shade,
                       float4* cull, uint32_t* orig, hipStream_t s);
 void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s);
+void launch_block_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s);
 // ref_quirks (src/renderer.ts:306): the init-sort pass's (key, value) slots and the draw-ordered
 // scene copy (see k_quirk_keys / k_quirk_gather)
 void launch_inverse(const uint32_t* orig, uint64_t n, uint32_t* inv, hipStream_t s);

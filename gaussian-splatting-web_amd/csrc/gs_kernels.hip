@@ -164,6 +164,13 @@ __global__ __launch_bounds__(256) void k_morton(const uint8_t* __restrict__ aos,
 }
 
 // Storage slot i from reference record perm[i] (or i): geometry record, cull plane, shading block.
+// sigmoid (src/simple_render.ts:118-125), as the projection evaluates it
+__device__ __forceinline__ float sigmoid_ref(float logit) {
+    if (logit >= 0.0f) return 1.0f / (1.0f + expf(-logit));
+    const float e = expf(logit);
+    return e / (1.0f + e);
+}
+
 __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ aos, uint64_t n,
                                                    int n_sh, const uint32_t* __restrict__ perm,
                                                    float4* __restrict__ geo, float4* __restrict__ shade,
@@ -187,7 +194,12 @@ __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ a
         const float t = (r00 * r00 + r10 * r10 + r20 * r20) * r[4] * r[4] +
                         (r01 * r01 + r11 * r11 + r21 * r21) * r[5] * r[5] +
                         (r02 * r02 + r12 * r12 + r22 * r22) * r[6] * r[6];
-        cull[i] = make_float4(r[0], r[1], r[2], t * 1.0001f);
+        // a Gaussian whose opacity is below 1/255 (or NaN) is never visible (every fragment's
+        // alpha <= op is discarded, src/simple_render.ts:169-200; project_core's op test): its
+        // cull plane is marked (w = -1) and every cull rejects it before loading more (a faint
+        // scene: logit ~ N(-4, 2) has 22 % of them)
+        const bool faint = !(sigmoid_ref(r[12]) >= 1.0f / 255.0f);
+        cull[i] = make_float4(r[0], r[1], r[2], faint ? kCullFaint : t * 1.0001f);
     }
     const uint32_t q = sh_quads(n_sh);  // SH coefficients sh[k][c] at 3k + c, packed
     float v[4 * 12];
@@ -204,6 +216,49 @@ __global__ __launch_bounds__(256) void k_transpose(const uint8_t* __restrict__ a
         if (t < q) o[t] = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
 }
 
+// Per block of kCullBlock (64) consecutive storage slots, one wave each: the same bound as
+// k_part_bounds' (box of the finite positions, largest ||R(q) diag(s)||_F^2, finite count).  The
+// partition bound decides whether a partition is visited at all; inside a visited partition a
+// wave tests its block's bound before loading its 64 cull planes (a strip's partitions straddle
+// its edges, chunk 1's partitions reach an unsaturated tile with a few of their blocks).
+__global__ __launch_bounds__(256) void k_block_bounds(const float4* __restrict__ cull, uint64_t n,
+                                                      PartBound* __restrict__ out) {
+    const uint64_t blk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t i = blk * kCullBlock + (threadIdx.x & 63);
+    if (blk * kCullBlock >= n) return;
+    uint32_t lo[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, hi[3] = {0u, 0u, 0u}, trs = 0u, fin = 0u;
+    if (i < n) {
+        const float4 c = cull[i];
+        if (isfinite(c.x) && isfinite(c.y) && isfinite(c.z) && !(c.w < 0.0f)) {  // (kCullFaint)
+            const float v[3] = {c.x, c.y, c.z};
+#pragma unroll
+            for (int d = 0; d < 3; ++d) lo[d] = hi[d] = f2ord(v[d]);
+            trs = f2ord(c.w != c.w ? INFINITY : c.w);
+            fin = 1;
+        }
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = min(lo[d], (uint32_t)__shfl_xor((int)lo[d], s, 64));
+            hi[d] = max(hi[d], (uint32_t)__shfl_xor((int)hi[d], s, 64));
+        }
+        trs = max(trs, (uint32_t)__shfl_xor((int)trs, s, 64));
+        fin += (uint32_t)__shfl_xor((int)fin, s, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        PartBound b;
+        for (int d = 0; d < 3; ++d) {
+            b.lo[d] = ord2f(lo[d]);
+            b.hi[d] = ord2f(hi[d]);
+        }
+        b.trs = fin ? ord2f(trs) : 0.0f;
+        b.nfin = fin;
+        out[blk] = b;
+    }
+}
+
 // Per projection partition (kProjTile consecutive storage slots): the box of its finite
 // positions, the largest ||R(q) diag(s)||_F^2 (NaN counts as infinite) and its count of finite
 // positions (zero: nothing in it can be visible).
@@ -218,7 +273,7 @@ __global__ __launch_bounds__(256) void k_part_bounds(const float4* __restrict__ 
         const uint64_t i = p0 + k;
         if (i >= n) break;
         const float4 c = cull[i];
-        if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z))) continue;
+        if (!(isfinite(c.x) && isfinite(c.y) && isfinite(c.z)) || c.w < 0.0f) continue;  // (kCullFaint)
         const float v[3] = {c.x, c.y, c.z};
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
@@ -361,6 +416,7 @@ __device__ __forceinline__ bool cull_keep_box(const ProjParams& p, float4 c, int
 #pragma clang fp contract(off)
     const float x = c.x, y = c.y, z = c.z;
     vz0 = ((p.V[2] * x + p.V[6] * y) + p.V[10] * z) + p.V[14] * 1.0f;  // = project_footprint's vz
+    if (c.w < 0.0f) return false;  // kCullFaint: opacity below 1/255 (a NaN bound stays conservative)
     const float cw = ((p.PV[3] * x + p.PV[7] * y) + p.PV[11] * z) + p.PV[15] * 1.0f;
     const float cz = ((p.PV[2] * x + p.PV[6] * y) + p.PV[10] * z) + p.PV[14] * 1.0f;
     if (!((cw > 0.0f) && (cz >= 0.0f) && (cz <= cw))) return false;  // :230 + near/far (exact)
@@ -439,14 +495,7 @@ __device__ __forceinline__ bool project_core_g(const ProjParams& p, uint32_t i, 
         Footprint f;
         project_footprint(p, x, y, z, sx, sy, sz, qx, qy, qz, qw, vz, clip, f);
         bool vis = (clip.w > 0.0f) && (clip.z >= 0.0f) && (clip.z <= clip.w);  // :230, near/far clip
-        // sigmoid (:118-125)
-        float op;
-        if (logit >= 0.0f) {
-            op = 1.0f / (1.0f + expf(-logit));
-        } else {
-            const float e = expf(logit);
-            op = e / (1.0f + e);
-        }
+        const float op = sigmoid_ref(logit);
         vis = vis && (op >= 1.0f / 255.0f);  // alpha <= op: below 1/255 every fragment is discarded
         vis = vis && isfinite(f.cx) && isfinite(f.cy) && isfinite(f.e1x) && isfinite(f.e1y) &&
               isfinite(f.e2x) && isfinite(f.e2y);
@@ -759,11 +808,18 @@ __device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b, uint32_t 
 // Chunk 1, step 1: every thread of the grid tests partitions (part_maybe_c1 against the row
 // prefix counts of the unsaturated tiles); the ones that may hold a chunk-1 splat are appended to plist (one
 // counter add per wave; list order does not matter: a partition's chunk-1 slots are its own).
+// With block bounds (p.bbounds) the list holds 64-slot blocks instead of partitions: a partition
+// that reaches an unsaturated tile mostly does so with a few of its 16 blocks (orbit frames list
+// ~1000-2000 partitions at the scene's edge, next to ~2300 empty off-scene tiles).
+__device__ __forceinline__ uint32_t c1_items(const ProjParams& p) {
+    return p.bbounds ? (uint32_t)((p.n + kCullBlock - 1) / kCullBlock) : proj_parts(p.n);
+}
 __device__ __forceinline__ void c1_parts_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
-    const uint32_t parts = proj_parts(p.n), lane = lane_id(), T = frame_thresh(p);
+    const uint32_t parts = c1_items(p), lane = lane_id(), T = frame_thresh(p);
+    const PartBound* bnd = p.bbounds ? p.bbounds : p.bounds;
     for (uint32_t q0 = blk * blockDim.x + (threadIdx.x & ~63u); q0 < parts; q0 += nblk * blockDim.x) {
         const uint32_t q = q0 + lane;
-        const bool want = q < parts && part_maybe_c1(p, p.bounds[q], T);
+        const bool want = q < parts && part_maybe_c1(p, bnd[q], T);
         const uint64_t b = __ballot(want);
         if (!b) continue;
         uint32_t base = 0;
@@ -784,12 +840,14 @@ __device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t bl
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t lane = lane_id(), nl = p.ctl->c1_parts, T = frame_thresh(p);
-    constexpr uint32_t kBlocks = (uint32_t)kProjTile / 64u;
+    const uint32_t kBlocks = p.bbounds ? 1u : (uint32_t)kProjTile / 64u;  // waves per listed item
     const uint32_t wpb = blockDim.x >> 6;
     for (uint32_t v = blk * wpb + (threadIdx.x >> 6); v < nl * kBlocks; v += nblk * wpb) {
-        const uint32_t part = p.plist[v / kBlocks];
+        const uint32_t i0 = p.bbounds ? p.plist[v] * (uint32_t)kCullBlock
+                                      : p.plist[v / kBlocks] * (uint32_t)kProjTile + (v % kBlocks) * 64u;
+        const uint32_t part = i0 / (uint32_t)kProjTile;
         {
-            const uint32_t i0 = part * (uint32_t)kProjTile + (v % kBlocks) * 64u, i = i0 + lane;
+            const uint32_t i = i0 + lane;
             bool want = false;
             float vz, cx0, cy0, hb;
             if (i < p.n && cull_keep_box(p, p.cull[i], row_lo, row_hi, vz, cx0, cy0, hb) && sortable_key(vz) >= T) {
@@ -3870,6 +3928,11 @@ void launch_part_bounds(const float4* cull, uint64_t n, PartBound* out, hipStrea
     if (!n) return;
     hipLaunchKernelGGL(k_part_bounds, dim3(proj_parts(n)), dim3(256), 0, s, cull, n, out);
 }
+void launch_block_bounds(const float4* cull, uint64_t n, PartBound* out, hipStream_t s) {
+    if (!n) return;
+    const uint64_t blocks = (n + kCullBlock - 1) / kCullBlock;
+    hipLaunchKernelGGL(k_block_bounds, dim3((unsigned)((blocks + 3) / 4)), dim3(256), 0, s, cull, n, out);
+}
 void launch_inverse(const uint32_t* orig, uint64_t n, uint32_t* inv, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(k_inverse, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, orig, n, inv);
@@ -4011,7 +4074,8 @@ void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
         cr.sat_lds_words = lds_ok && words <= kSatLdsWords ? words : 0u;  // else the column pass in global memory
         hipLaunchKernelGGL(k_c1_rows, dim3(1), dim3(1024), (size_t)cr.sat_lds_words * 4, s, cr);
         const unsigned parts = proj_parts(c.pp.n);
-        hipLaunchKernelGGL(k_c1_parts, dim3(std::max(1u, (parts + 255) / 256)), dim3(256), 0, s, c.pp);
+        const unsigned items = c.pp.bbounds ? (unsigned)((c.pp.n + kCullBlock - 1) / kCullBlock) : parts;
+        hipLaunchKernelGGL(k_c1_parts, dim3(std::max(1u, (items + 255) / 256)), dim3(256), 0, s, c.pp);
         hipLaunchKernelGGL(k_c1_records, dim3(kMaxGrid), dim3(256), 0, s, c.pp);
         launch_bin(c.bp, s);
         launch_tile_sort(c.tp, s);
