@@ -941,6 +941,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     // chunk 0: as many wave pairs per tile as keep every tile resident (a function of the frame's
     // size only, so a view renders the same whatever came before it)
     cp.seg = split ? composite_seg(n_tiles, c->num_cus) : 1;
+    {  // row bands (image-invariant): 4 when the last frame left most tiles unsaturated
+        uint32_t sat_tiles = 0;
+        for (int k = 0; k < kSatBuckets; ++k) sat_tiles += s->last.sat_hist[k];
+        cp.bands = s->have_last && 2u * sat_tiles < (uint32_t)n_tiles ? 4 : 2;
+    }
     mark(EV_DSORT_0);
     launch_bin(bp, st);
     mark(EV_BIN_0);

@@ -91,3 +91,22 @@ def test_split_strips_1080p(gpu_ctx, G):
     for name, im in (("chunked", img), ("one_chunk", again)):
         r = image_close_fp32(im, ref, name="split_strips_%d_%s" % (G, name))
         assert r[2], (name, r)
+
+
+@pytest.mark.parametrize("accum", [0, 1])
+def test_row_bands_do_not_change_the_image(gpu_ctx, accum):
+    """CompositeParams::bands: a frame after one whose tiles mostly did not saturate walks 8x4 row
+    bands (4 per wave) instead of 8x8 quarters.  Each pixel still sees its list in order and a
+    splat left off its band's list adds exactly zero, so the image is bit-identical: the first
+    frame (no history: 2 bands) against the next ones (4 bands), in both accumulation modes."""
+    W, H, n = 320, 240, 300_000
+    aos = _scene(n, 95, W, H, -4.0)
+    u = gs.bench_uniforms(W, H)
+    sc = gs.Scene(gpu_ctx, aos, n, 16)
+    o = gs.make_opts(accum=accum, t_min=1e-4 if accum == 0 else 0.0)
+    imgs = [sc.render(u, W, H, o) for _ in range(3)]
+    assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[1], imgs[2])
+    ref, _ = orc.render(aos.view(np.uint8), n, 16, u, W, H, accum=accum, t_min=1e-4 if accum == 0 else 0.0)
+    from test_gpu_parity import image_close_fp16
+    r = image_close_fp32(imgs[2], ref, name="bands4") if accum == 0 else image_close_fp16(imgs[2], ref)
+    assert r[2], r

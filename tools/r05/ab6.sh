@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU box: -m gpu suite, bench A/B (working tree vs lib/ab variants), G=1/8 strips at 1080p and
+# 50 M / 4K, and the strip frames with device-memory kernel arguments off (HIP_FORCE_DEV_KERNARG=0).
+set -o pipefail
+TAG=${1:-ab6}; VARS=${2:-prev}; REPS=${3:-2}
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+export TMPDIR=/tmp
+if [ -z "$NOTEST" ]; then
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+fi
+B=$PWD/gaussian-splatting-web_amd/lib/libgsplat.so
+lib() { if [ "$1" = base ]; then echo $B; else echo $PWD/gaussian-splatting-web_amd/lib/ab/libgsplat_$1.so; fi; }
+for r in $(seq $REPS); do
+for v in base $VARS; do
+  GSPLAT_LIB=$(lib $v) timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 > $OUT/b_${v}_$r.log 2>&1 || { tail -5 $OUT/b_${v}_$r.log; exit 1; }
+  python3 -c "import json; d=json.loads(open('$OUT/b_${v}_$r.log').read().strip().splitlines()[-1]); print('%-6s fps %.1f orbit %.1f cold %.1f sparse %.1f (comp %.1f)' % ('$v', d['fps'], d['orbit']['fps'], d['cold']['fps'], d['sparse']['fps'], d['sparse']['ms_composite']*1e3), {k: round(v*1e3,1) for k,v in d['stages_ms'].items()})"
+done
+done
+for kv in 1 0; do
+  HIP_FORCE_DEV_KERNARG=$kv GS=1,8 TIMING=2 timeout -k 10 200 python -u tools/strip_bench.py 2>&1 | sed -e "s/(p0.000 s0.000 b0.000 t0.000 /(/g;s/^/kernarg$kv 1080p /"
+done
+for kv in 1 0; do
+  HIP_FORCE_DEV_KERNARG=$kv N=50000000 W=3840 H=2160 SEED=50 GS=1,8 TIMING=2 WARMUP=10 timeout -k 10 400 python -u tools/strip_bench.py 2>&1 | sed -e "s/(p0.000 s0.000 b0.000 t0.000 /(/g;s/^/kernarg$kv 4k /"
+done
+GS=1,8 timeout -k 10 300 python -u tools/diag/strip_stages.py 2>&1 | tee $OUT/stages1080.txt
+N=50000000 W=3840 H=2160 SEED=50 GS=1,8 timeout -k 10 500 python -u tools/diag/strip_stages.py 2>&1 | tee $OUT/stages4k.txt
+echo done
