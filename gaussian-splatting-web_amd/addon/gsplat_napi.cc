@@ -118,6 +118,7 @@ void read_opts(napi_env env, napi_value o, gs_opts* opts) {
     opts->chunk_fraction = (float)field("chunkFraction", opts->chunk_fraction);
     opts->tile_row_begin = (int32_t)field("tileRowBegin", opts->tile_row_begin);
     opts->tile_row_end = (int32_t)field("tileRowEnd", opts->tile_row_end);
+    opts->list_split = (int32_t)field("listSplit", opts->list_split);
 }
 
 // ---- library / device --------------------------------------------------------------------

@@ -13,6 +13,8 @@ export interface RenderOptions {
     stripCount?: number;
     timing?: number;
     chunkFraction?: number;  // 0 = adaptive
+    refQuirks?: number;      // 1: the reference's init-sort truncation (INTEGRATION.md section 5)
+    listSplit?: number;      // 1: long tile lists in parallel segments (fp32-oracle bar, not bit-identical)
     deviceResident?: boolean;  // frames stay in HBM (renderDevice); Renderer.readback() copies one out
 }
 
