@@ -1113,16 +1113,55 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     const uint32_t nl = p.ctl->c0_parts;  // the partitions k_part_list kept
     const uint32_t T = frame_thresh(p);
     uint32_t kt_items = 0;
-    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
-        const uint32_t part = p.plist0[j];
+    // Software-pipelined over the workgroup's partitions: the next partition's cull planes are
+    // loaded when this one starts (two register sets) and the list entry of the one after it, so
+    // the loads are in flight while this partition is tested; the barriers wait for LDS only (a
+    // __syncthreads would drain the loads too).  Slots past n read the last plane and list
+    // positions past the end the last entry: no branch around a load (its zero fill would wait for it).
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    auto load_planes = [&](uint32_t part, float4 (&c)[kProjRounds]) {
+        const uint32_t p0 = part * kProjTile;
+#pragma unroll
+        for (int it = 0; it < kProjRounds; ++it) c[it] = p.cull[min(p0 + it * kProjThreads + tid, p.n - 1u)];
+    };
+    // the workgroup's partitions (list entries blockIdx.x + k gridDim.x) into LDS at once
+    __shared__ uint32_t s_part[128];
+    const uint32_t nmine = nl > blockIdx.x ? (nl - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u;
+    for (uint32_t k = tid; k < min(nmine, 128u); k += kProjThreads) s_part[k] = p.plist0[blockIdx.x + k * gridDim.x];
+    lds_barrier();
+    auto part_at = [&](uint32_t k) { return k < 128u ? s_part[k] : p.plist0[blockIdx.x + k * gridDim.x]; };
+    // the workgroup's work units: all in shard blockIdx.x % kUnitShards (the grid is a multiple of
+    // kUnitShards or one partition per workgroup, so a shard holds the units of the list positions
+    // j == shard (mod kUnitShards): at most unit_shard_cap of them, as sharding by partition did)
+    constexpr uint32_t kCullUnitsLds = 512;
+    __shared__ uint32_t s_units[kCullUnitsLds];
+    __shared__ uint32_t s_nu, s_pos;
+    if (tid == 0) s_nu = 0;
+    lds_barrier();
+    const uint32_t ush = blockIdx.x % kUnitShards;
+    auto flush_units = [&] {  // (after a barrier: every thread reads s_nu)
+        const uint32_t nu = s_nu;
+        if (!nu) return;
+        if (tid == 0) s_pos = atomicAdd(&p.ctl->unit_n[ush], nu);
+        lds_barrier();
+        for (uint32_t r = tid; r < nu; r += kProjThreads) p.units[(uint64_t)ush * ucap + s_pos + r] = s_units[r];
+        lds_barrier();
+        if (tid == 0) s_nu = 0;
+        lds_barrier();
+    };
+    float4 ca[kProjRounds], cb[kProjRounds];  // ping-pong: no register moves between partitions
+    uint32_t k = 0;
+    uint32_t part = 0;
+    if (nmine) {
+        part = part_at(0);
+        load_planes(part, ca);
+    }
+    // one partition: its planes in c, the next one's loaded into cn
+    auto step = [&](float4 (&c)[kProjRounds], float4 (&cn)[kProjRounds]) {
+        const uint32_t part_next = k + 1 < nmine ? part_at(k + 1) : part;
+        load_planes(part_next, cn);  // (past the last: this partition again, unused)
         if (kt_items++ == 0) KT_MARK(0, 1, part);
         const uint32_t p0 = part * kProjTile;
-        float4 c[kProjRounds];
-#pragma unroll
-        for (int it = 0; it < kProjRounds; ++it) {
-            const uint32_t i = p0 + it * kProjThreads + tid;
-            c[it] = i < p.n ? p.cull[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
         uint32_t cand = 0;  // bit it: slot p0 + it * kProjThreads + tid is a candidate
 #pragma unroll
         for (int it = 0; it < kProjRounds; ++it) {
@@ -1142,7 +1181,7 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
             const uint64_t bb = __ballot(cd);
             if (lane == 0) s_mask[it][w] = bb;
         }
-        __syncthreads();
+        lds_barrier();
         if (tid < 64) {  // exclusive prefix of the (round, wave) ballots: index order
             constexpr int nb = kProjRounds * (kProjThreads / 64);
             const uint32_t cnt = tid < nb ? __popcll(s_mask[tid / (kProjThreads / 64)][tid % (kProjThreads / 64)]) : 0u;
@@ -1150,7 +1189,7 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
             if (tid < nb) s_base[tid / (kProjThreads / 64)][tid % (kProjThreads / 64)] = incl - cnt;
             if (tid == 63) s_total = incl;
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int it = 0; it < kProjRounds; ++it) {
             const uint64_t bb = s_mask[it][w];
@@ -1159,16 +1198,25 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
         if (tid == 0) {
             const uint32_t tot = s_total;
             p.c0[part] = tot;
-            if (tot) {  // the partition's work units into the frame's list (shard by partition)
-                const uint32_t nu = (tot + kProjThreads - 1) / kProjThreads, sh = part % kUnitShards;
-                const uint32_t pos = atomicAdd(&p.ctl->unit_n[sh], nu);
-                for (uint32_t r = 0; r < nu; ++r)
-                    p.units[(uint64_t)sh * ucap + pos + r] =
-                        (part * kProjRounds + r) | ((min(tot - r * kProjThreads, (uint32_t)kProjThreads) - 1u) << 20);
-            }
+            // the partition's work units, gathered in LDS and appended to the frame's list once per
+            // workgroup below (a returning atomic per partition on eight shared counters serialised
+            // the one-chunk 50 M frame's cull: 49 K of them)
+            const uint32_t nu = (tot + kProjThreads - 1) / kProjThreads;
+            for (uint32_t r = 0; r < nu; ++r)
+                s_units[s_nu + r] = (part * kProjRounds + r) | ((min(tot - r * kProjThreads, (uint32_t)kProjThreads) - 1u) << 20);
+            s_nu += nu;
         }
-        __syncthreads();
+        lds_barrier();  // (s_mask, s_base and s_total are rewritten by the next partition)
+        if (s_nu > kCullUnitsLds - kProjRounds) flush_units();  // (room for one more partition's units)
+        part = part_next;
+        ++k;
+    };
+    while (k < nmine) {
+        step(ca, cb);
+        if (k >= nmine) break;
+        step(cb, ca);
     }
+    flush_units();
     if (my_vis) {
         atomicAdd(&s_vis, my_vis);
         atomicMax(&s_kmin_inv, my_kmin_inv);
