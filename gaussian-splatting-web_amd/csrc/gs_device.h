@@ -295,6 +295,8 @@ struct BinParams {
     uint32_t wide_tiles;          // splats of >= this many box tiles are wide (ProjParams::wide_tiles)
     const uint32_t* wlist;        // nullable: the chunk's wide splats (ProjParams::wlist), walked
                                   // by the waves of every workgroup in turn instead of the LDS queue
+    uint32_t uid_lds;             // 1: the partition's unit entries cached in LDS after the unit
+                                  // prefix (set by the launcher when it fits; chunk 0 only)
 };
 
 // Per-tile sort of the tile lists (k_tile_sort): each tile's slots ordered by their sort key,

@@ -1812,6 +1812,7 @@ __device__ uint32_t bin_slots(const BinParams& p, const UnitList& L, uint32_t b,
     const uint32_t m = min(bin_units(L, b), kBinMaxUnits);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     constexpr int per = kBinMaxUnits / NT;
+    uint32_t* s_uid = LISTED && p.uid_lds ? s_pref + p.pref_words : nullptr;  // (bin_slot reads them)
     uint32_t c[per], sum = 0;
 #pragma unroll
     for (int k = 0; k < per; ++k) {
@@ -1821,6 +1822,7 @@ __device__ uint32_t bin_slots(const BinParams& p, const UnitList& L, uint32_t b,
             const uint32_t u = unit_at(L, b + j * kBinParts);
             if (LISTED) {
                 c[k] = unit_count(u);
+                if (s_uid) s_uid[j] = u;
             } else {
                 const uint32_t part = u / kProjRounds, r0 = (u % kProjRounds) * kProjThreads;
                 const uint32_t cn = p.cnt[part];
@@ -1856,7 +1858,9 @@ __device__ __forceinline__ uint32_t bin_slot(const BinParams& p, const UnitList&
         const uint32_t mid = (lo + hi) >> 1;
         if (s_pref[mid] <= r) lo = mid; else hi = mid;
     }
-    const uint32_t u = unit_id(unit_at(L, b + lo * kBinParts)), part = u / kProjRounds;
+    // (the unit entry from LDS when bin_slots cached it: no global round trip per slot)
+    const uint32_t u = unit_id(p.uid_lds && L.units ? s_pref[p.pref_words + lo] : unit_at(L, b + lo * kBinParts)),
+                   part = u / kProjRounds;
     const uint32_t q = (u % kProjRounds) * kProjThreads + (r - s_pref[lo]);
     return p.chunk ? slot_c1(part, q) : slot_c0(part, q);
 }
@@ -1958,6 +1962,44 @@ __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, u
     }
 }
 
+// The slots of binning partition `part` in rank order r = threadIdx.x, + NT, ...: f(g, packed
+// rect, storage index, record quads 0 and 1) per slot, each slot's words loaded one slot ahead
+// (two register sets, no moves), so a thread's next slot is in flight while it walks the current
+// one (the one-chunk 50 M / 4K frame's binning holds ~160 slots per thread at one workgroup per CU).
+// Records are loaded for every slot (holes included: valid memory, unused).
+template <int NT, class F>
+__device__ __forceinline__ void bin_walk(const BinParams& p, const UnitList& L, uint32_t part, const uint32_t* s_pref,
+                                         uint32_t total, F&& f) {
+    struct In {
+        uint32_t g, pr, sj;
+        float4 q0, q1;
+    };
+    auto fetch = [&](uint32_t r, In& s) {
+        s.g = bin_slot(p, L, part, s_pref, r);
+        s.pr = p.srect[s.g];
+        s.sj = p.sidx[s.g];
+        const float4* q = p.crec + 3 * (uint64_t)s.g;
+        s.q0 = q[0];
+        s.q1 = q[1];
+    };
+    uint32_t r = threadIdx.x;
+    if (r >= total) return;
+    In a, b;
+    fetch(r, a);
+    auto step = [&](In& cur, In& nxt) {
+        const uint32_t rn = r + NT;
+        fetch(min(rn, total - 1u), nxt);  // (past the end: the last slot again, unused)
+        f(cur.g, cur.pr, cur.sj, cur.q0, cur.q1);
+        r = rn;
+    };
+    for (;;) {
+        step(a, b);
+        if (r >= total) break;
+        step(b, a);
+        if (r >= total) break;
+    }
+}
+
 // Binning partition / band vb: counts of its splats' entries per tile of the band -> bmat row.
 // Wide splats (>= wide_tiles box tiles) are queued in LDS (up to wide_cap) and counted by whole
 // waves, as k_bin_emit emits them.
@@ -1971,21 +2013,19 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
     if (threadIdx.x == 0) s_nw = 0;
     const UnitList L = bin_unit_list(p);
     const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
-    for (uint32_t r = threadIdx.x; r < total; r += NT) {
-        const uint32_t g = bin_slot(p, L, part, s_pref, r);
+    bin_walk<NT>(p, L, part, s_pref, total, [&](uint32_t g, uint32_t pr, uint32_t sj, float4 q0, float4 q1) {
         TileRect tr;
-        if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
+        if (!rect_unpack(p, pr, sj, tr)) return;
         if (rect_wide(p, tr)) {
-            if (p.wlist) continue;  // listed: walked below
+            if (p.wlist) return;  // listed: walked below
             const uint32_t qi = atomicAdd(&s_nw, 1u);
             if (qi < p.wide_cap) {
                 s_wide[qi] = g;
-                continue;
+                return;
             }
         }
-        const float4* q = p.crec + 3 * (uint64_t)g;
-        splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
-    }
+        splat_entries(p, tr, ellipse_of(q0, q1), t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
+    });
     __syncthreads();
     const uint32_t nq = min(s_nw, p.wide_cap);
     for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64)  // wave-uniform
@@ -2013,7 +2053,7 @@ template <bool LISTED>  // LISTED: chunk 0 (k_cull's unit list); else chunk 1 (e
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     uint32_t* s_cnt = bin_lds();
     uint32_t* s_pref = s_cnt + p.band_tiles;
-    uint32_t* s_tmp = s_pref + p.pref_words;
+    uint32_t* s_tmp = s_pref + p.pref_words * (p.uid_lds ? 2u : 1u);  // (then the unit entries)
     uint32_t* s_wide = s_tmp + kBinThreads / 64;
     uint32_t* s_nw = s_wide + p.wide_cap;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
@@ -2206,6 +2246,8 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
     if (threadIdx.x == 0) s_nw = 0;
     const UnitList L = bin_unit_list(p);
     const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
+    // (not bin_walk: with the slot prefetch the emission ran slower, 1.60 -> 1.68 ms at the one-chunk
+    // 50 M / 4K frame: its scattered list stores, not its slot loads, bound it)
     for (uint32_t r = threadIdx.x; r < total; r += NT) {
         const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
@@ -2224,6 +2266,7 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
             if (pos < cap) p.tvals[pos] = g;
         });
     }
+
     __syncthreads();
     const uint32_t nq = min(s_nw, p.wide_cap);
     if (threadIdx.x == 0 && s_nw) atomicAdd(&p.ctl->wide_n[p.chunk], s_nw);  // statistics
@@ -2247,7 +2290,7 @@ template <bool LISTED>
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     uint32_t* s_cur = bin_lds();
     uint32_t* s_pref = s_cur + p.band_tiles;
-    uint32_t* s_tmp = s_pref + p.pref_words;
+    uint32_t* s_tmp = s_pref + p.pref_words * (p.uid_lds ? 2u : 1u);  // (then the unit entries)
     uint32_t* s_wide = s_tmp + kBinThreads / 64;
     uint32_t* s_nw = s_wide + p.wide_cap;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;
@@ -4065,9 +4108,12 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
     p.pref_words = std::min<uint32_t>(kBinMaxUnits, (p.parts * (uint32_t)kProjRounds + kBinParts - 1) / kBinParts) + 1;
     // wide-splat queue: larger frames hold more splats that cover many tiles (near splats at 4K);
     // a splat past the queue is walked by its own thread
-    const uint32_t room = (uint32_t)(kBinLdsMaxWords - bin_lds_words(p.band_tiles, p.pref_words, 0));
+    // the unit entries cached in LDS beside their prefix when that leaves the minimum wide queue
+    p.uid_lds = p.units && bin_lds_words(p.band_tiles, 2 * p.pref_words, kWideQueue) <= kBinLdsMaxWords ? 1u : 0u;
+    const uint32_t pw = p.pref_words * (p.uid_lds ? 2u : 1u);
+    const uint32_t room = (uint32_t)(kBinLdsMaxWords - bin_lds_words(p.band_tiles, pw, 0));
     p.wide_cap = p.wlist ? 0u : std::min(room, std::max(kWideQueue, std::min(kWideQueueMax, p.n_tiles / 4)));
-    const size_t lds = bin_lds_words(p.band_tiles, p.pref_words, p.wide_cap) * 4;
+    const size_t lds = bin_lds_words(p.band_tiles, pw, p.wide_cap) * 4;
     const unsigned grid = kBinParts * bin_bands(p.n_tiles, p.band_tiles);
     if (p.units)
         hipLaunchKernelGGL(k_bin_count<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
@@ -4103,6 +4149,7 @@ void launch_chunk1(const Chunk1Params& c0, int grid, int accum_fp16, hipStream_t
     c.bp.band_tiles = kBandTiles;
     c.bp.pref_words = kBinMaxUnits + 1;
     c.bp.wide_cap = kWideQueue;
+    c.bp.uid_lds = 0;  // (static LDS sized without the entries)
     if (accum_fp16)
         hipLaunchKernelGGL(k_chunk1<true>, dim3(grid), dim3(256), 0, s, c);
     else
