@@ -1879,6 +1879,22 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
         xa = max(xa, tr.x0);
         xb = min(xb, tr.x1);
         const uint32_t t0 = (ty - rb) * tx;
+        if (p.chunk == 0) {  // the row's run clipped to the band, then four entries at a time (their
+                             // counter atomics independent, in flight together: one-chunk 50 M / 4K
+                             // count 0.87 -> 0.77 ms)
+            xa = max(xa, t_lo > t0 ? t_lo - t0 : 0u);
+            if (t_hi <= t0) continue;
+            xb = min(xb, t_hi - 1u - t0);
+            uint32_t x = xa;
+            for (; x + 3u <= xb; x += 4u) {
+                f(t0 + x);
+                f(t0 + x + 1u);
+                f(t0 + x + 2u);
+                f(t0 + x + 3u);
+            }
+            for (; x <= xb; ++x) f(t0 + x);
+            continue;
+        }
         for (uint32_t x = xa; x <= xb; ++x) {
             const uint32_t t = t0 + x;
             if (t < t_lo || t >= t_hi) continue;
