@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-rank frame time of the row-strip split, measured one strip at a time on one GPU (the
 8-GPU run itself is the driver's): for G in 1, 2, 4, 8, every strip's mean frame time and stage
-times; the slowest strip bounds the G-GPU frame (plus the all-gather)."""
+times; the slowest strip bounds the G-GPU frame (plus the all-gather).  Env: N, W, H, SEED, GS,
+STRIP, TIMING (0: no events; 1: every stage; 2: the composite only), WARMUP, FRAMES (timed)."""
 import os
 import sys
 import time
@@ -37,11 +38,12 @@ def main():
                 sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
             ctx.sync()
             ctx.timings_reset()
+            nf = int(os.environ.get("FRAMES", 30))
             t0 = time.perf_counter()
-            for _ in range(30):
+            for _ in range(nf):
                 sc.render_device(u, W, H, buf.ptr.value, buf.nbytes, None, o)
             ctx.sync()
-            ms = (time.perf_counter() - t0) / 30 * 1e3
+            ms = (time.perf_counter() - t0) / nf * 1e3
             st = ctx.timings()
             worst = max(worst, ms)
             line.append("%d:%.3f(p%.3f s%.3f b%.3f t%.3f c%.3f)" % (g, ms, st["ms_project"], st["ms_sort"],
