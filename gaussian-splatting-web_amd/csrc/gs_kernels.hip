@@ -2080,15 +2080,17 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
 // total into tbase.  The prefix runs XCD-major: partition p is emitted by workgroup p (and
 // p + kBinParts ...) on XCD p % 8, so ordering the partitions (p % 8, p / 8) gives every XCD one
 // contiguous sub-range of each tile's list and its L2 merges the scattered 4-B stores into whole
-// lines.  Workgroup = 64 tiles x 4 waves; wave w sums ordered partitions [64 w, 64 w + 64).
+// lines.  Workgroup = 64 tiles x NW waves; wave w sums ordered partitions [w R, w R + R),
+// R = kBinParts / NW (k_bin_colscan: 8 waves of 32 rows; k_chunk1's 256-thread phase: 4 of 64).
 constexpr int kColTiles = 64;
-constexpr int kColRows = kBinParts / 4;
 static_assert(kBinParts % 8 == 0, "binning partitions must split evenly over the 8 XCDs");
 __device__ __forceinline__ uint32_t colscan_part(uint32_t q) {  // q-th partition in XCD-major order
     return (q % (kBinParts / 8)) * 8 + q / (kBinParts / 8);
 }
 
+template <int NW>
 __device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, uint32_t (*s_sum)[kColTiles]) {
+    constexpr int kColRows = kBinParts / NW;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t = vb * kColTiles + lane;
     const bool ok = t < p.n_tiles;
@@ -2108,9 +2110,9 @@ __device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, ui
             p.bmat[(uint64_t)colscan_part(w * kColRows + k) * p.n_tiles + t] = run;
             run += v[k];
         }
-        if (w == 3) p.tbase[t] = run;
+        if (w == NW - 1) p.tbase[t] = run;
     }
-    if (w == 3 && p.order) {  // the composite's tile order (chunk 0)
+    if (w == NW - 1 && p.order) {  // the composite's tile order (chunk 0)
         // XCD band x = tiles [x per, x per + per) is composited by the workgroups on XCD x in order;
         // its tiles with more than heavy_len entries go first (counter order_n[0] of shard x), the
         // rest from the band's end (order_n[1]), so the longest lists do not start in the last,
@@ -2138,10 +2140,10 @@ __device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, ui
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_bin_colscan(BinParams p) {
-    __shared__ uint32_t s_sum[4][kColTiles];
+__global__ __launch_bounds__(512) void k_bin_colscan(BinParams p) {
+    __shared__ uint32_t s_sum[8][kColTiles];
     if (p.chunk == 1 && p.ctl->not_done == 0) return;
-    colscan_body(p, blockIdx.x, s_sum);
+    colscan_body<8>(p, blockIdx.x, s_sum);
 }
 
 // One workgroup: exclusive scan of the tile totals in tile order -> ranges [begin, end) and
@@ -3851,7 +3853,7 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(4);
     const uint32_t ncol = (c.bp.n_tiles + kColTiles - 1) / kColTiles;
-    for (uint32_t vb = b; vb < ncol; vb += G) colscan_body(c.bp, vb, (uint32_t(*)[kColTiles])lds);
+    for (uint32_t vb = b; vb < ncol; vb += G) colscan_body<4>(c.bp, vb, (uint32_t(*)[kColTiles])lds);
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(5);
     if (b == 0) tile_scan_body<256>(c.bp, s_a);
@@ -4135,7 +4137,7 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
         hipLaunchKernelGGL(k_bin_count<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
     else
         hipLaunchKernelGGL(k_bin_count<false>, dim3(grid), dim3(kBinThreads), lds, s, p);
-    hipLaunchKernelGGL(k_bin_colscan, dim3((p.n_tiles + kColTiles - 1) / kColTiles), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_bin_colscan, dim3((p.n_tiles + kColTiles - 1) / kColTiles), dim3(512), 0, s, p);
     if (p.units)  // each workgroup scans the tile totals itself
         hipLaunchKernelGGL(k_bin_emit<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
     else
