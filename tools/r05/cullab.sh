@@ -19,7 +19,7 @@ for v in base $VARS; do
 for w in sparse cfg4; do
   (cd /tmp && GSPLAT_LIB=$(lib $v) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/${v}_$w -o run -- python3 $R/tools/diag/onechunk_probe.py $w 5 > $R/$OUT/${v}_$w.log 2>&1) || { tail -30 $OUT/${v}_$w.log; exit 1; }
   echo "$v $(grep 'one-chunk' $OUT/${v}_$w.log | cut -c1-60)"
-  python3 tools/kstats.py $OUT/${v}_$w/run_kernel_stats.csv 6 | grep -E "k_cull|k_project|k_bin|k_tile_sort|k_composite" | sed -e "s/^/   /"
+  python3 tools/kstats.py $OUT/${v}_$w/run_kernel_stats.csv 6 | grep -E "k_tile_sort|k_bin_emit" | sed -e "s/^/   /"
 done
 done
 echo done
