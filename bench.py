@@ -174,6 +174,9 @@ def main():
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--prewarm", type=float, default=0.2,
+                    help="seconds of untimed frames before the --warmup frames (the GPU's clocks and the "
+                         "scene's first frames after its upload settle; 0: none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the latency / orbit / stage loops")
     ap.add_argument("--list-split", type=int, default=0, choices=(0, 1),
@@ -253,6 +256,14 @@ def main():
         def sync():
             ctx.sync()
 
+    # untimed: at least `prewarm` seconds of frames, then the W warmup frames (20 timed frames right
+    # after the scene's upload and 5 warmup frames ran ~5 % below the steady rate:
+    # tools/r05/benchsteps.sh)
+    n_prewarm = 0
+    t_pre = time.perf_counter()
+    while time.perf_counter() - t_pre < args.prewarm:
+        frame()
+        n_prewarm += 1
     for _ in range(args.warmup):
         frame()
     sync()
@@ -427,6 +438,7 @@ def main():
             "config": {"workload": "configs[%d]: %d Gaussians (SH deg 3) at %dx%d, lookAt([0,0,0],[0,0,-1]) "
                                    "perspective(60deg,W/H,0.03,1000)" % (args.config, N, W, H),
                        "n_gaussians": N, "width": W, "height": H, "list_split": args.list_split,
+                       "prewarm": {"seconds": args.prewarm, "frames": n_prewarm},
                        "parallelism": "row-strips x%d + all-gather" % world if world > 1 else "single GPU"},
             # per-stage HIP-event times from the separate timing=1 loop (events between stages add
             # ~20 us to its frame), except ms_composite, timed live in the headline loop:
