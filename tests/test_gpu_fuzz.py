@@ -69,3 +69,32 @@ def test_randomized_frames(gpu_ctx, case):
     r = image_close_fp32(ls, ref, name=tag + "_ls")
     assert r[2], (tag, "list_split", r)
     assert np.array_equal(sc.render(u, W, H, gs.make_opts(list_split=1)), ls), (tag, "list_split determinism")
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_randomized_fp16_modes(gpu_ctx, case):
+    """The rgba16float-target accumulation (the reference's blend, rounded after every splat)
+    against the oracle's fp16-target mode (image_close_fp16), with strips bit-identical to the
+    full frame; and the bench's mode (fp32 accumulation, t_min 1e-4, f16 out) against the WebGPU
+    stand-in's bar (webgpu_bar)."""
+    from test_gpu_parity import image_close_fp16, webgpu_bar
+    W, H, n, nsh, shift, cam, k, G, frac = draw_case(500 + case)
+    tag = "fuzz16_%d_%dx%d_n%d_sh%d_s%g_%s%d" % (case, W, H, n, nsh, shift, cam, k)
+    full = gs.synth_aos(n, 700 + case, W, H).reshape(n, 80)
+    full[:, 12] += np.float32(shift)
+    rec = np.ascontiguousarray(full[:, : 16 + 4 * nsh]).reshape(-1)
+    sc = gs.Scene(gpu_ctx, rec, n, nsh)
+    u = uniforms(cam, W, H, k)
+    o16 = dict(accum=gs.GS_ACCUM_FP16_TARGET, t_min=0.0)
+    img = sc.render(u, W, H, gs.make_opts(**o16))
+    ref, st = orc.render(rec.view(np.uint8), n, nsh, u, W, H, accum=1, t_min=0.0)
+    r = image_close_fp16(img, ref)
+    assert r[2], (tag, r)
+    parts = [sc.render(u, W, H, gs.make_opts(strip_index=g, strip_count=G, **o16)) for g in range(G)]
+    assert np.array_equal(np.concatenate(parts, axis=0)[:H], img), (tag, "fp16-target strips", G)
+    # the visible set, exact (one pass over every rank: a chunked frame projects only the ranks
+    # that can still reach an unsaturated tile)
+    sc.render(u, W, H, gs.make_opts(chunk_fraction=1.0, timing=1))
+    assert gpu_ctx.timings()["n_vis"] == st["n_vis"], tag
+    bench_mode = sc.render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16))
+    webgpu_bar(bench_mode, rec, n, nsh, u, W, H, name=tag)
