@@ -104,8 +104,12 @@ constexpr int kFrameSets = GS_FRAME_SETS;
 // frame kFrameSets back to enqueue the next one (the sets' reuse is ordered on the device).  With
 // kFrameSets slots the host blocked every third row-strip frame for the one three back
 // (G = 8 strip: enqueue p50 34 us, p90 280 us, so at most ~1.5 frames ran on the GPU at once).
+// Two streams for the three sets (set k on stream k % 2): sets 0 and 2 are never in flight
+// together on the device's chains anyway, and one stream fewer maps the caller's stream and the
+// sets onto the four hardware queues with less sharing (round 5, tools/r05/ss.sh, five
+// alternating runs: bench +0.2..1.3 %, sparse scene 1035-1062 -> 1057-1086 fps, strips equal).
 #ifndef GS_SET_STREAMS
-#define GS_SET_STREAMS kFrameSets
+#define GS_SET_STREAMS 2
 #endif
 constexpr int kSetStreams = GS_SET_STREAMS;  // distinct streams of the frame sets
 constexpr int kStatSlots = 8;
