@@ -93,10 +93,8 @@ enum {
 };
 enum { ST_TOTAL, ST_PROJECT, ST_SORT, ST_BIN, ST_TSORT, ST_RANGES, ST_COMPOSITE, ST_COUNT };
 
-// Four sets on two streams (late round 5, tools/r05/ss.sh: bench +1.3 %, sparse scene +2 %, the
-// 1080p / 4K G = 8 strip bounds +2-4 % against three sets; two sets lost 5 % under a moving camera)
 #ifndef GS_FRAME_SETS
-#define GS_FRAME_SETS 4
+#define GS_FRAME_SETS 3
 #endif
 // Frames in flight: per-frame buffers (FrameSet), statistics slots and timing events rotate over
 // this many frames; frame f reuses frame f - kFrameSets's set once that frame has ended.
@@ -106,13 +104,8 @@ constexpr int kFrameSets = GS_FRAME_SETS;
 // frame kFrameSets back to enqueue the next one (the sets' reuse is ordered on the device).  With
 // kFrameSets slots the host blocked every third row-strip frame for the one three back
 // (G = 8 strip: enqueue p50 34 us, p90 280 us, so at most ~1.5 frames ran on the GPU at once).
-// Two streams for the sets (set k on stream k % 2): consecutive frames alternate streams, and
-// one stream per set mapped the caller's stream and the sets onto the box's four hardware queues
-// with more sharing (round 5, tools/r05/ss.sh, three sets: five alternating runs, bench
-// +0.2..1.3 %, sparse scene 1035-1062 -> 1057-1086 fps, strips equal; one stream for every set
-// serialised the chains: bench -4 %, G = 8 strip 0.081 -> 0.097 ms).
 #ifndef GS_SET_STREAMS
-#define GS_SET_STREAMS 2
+#define GS_SET_STREAMS kFrameSets
 #endif
 constexpr int kSetStreams = GS_SET_STREAMS;  // distinct streams of the frame sets
 constexpr int kStatSlots = 8;
@@ -690,11 +683,9 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     const int TX = (W + kTile - 1) / kTile;
     const int n_tiles = TX * (tr_end - tr_begin);
     FrameSet& F = s->fs[s->cur_fs];
-    {  // frames in flight: kFrameSets (four) for small frames (row strips: latency-bound kernels,
-       // so a later frame's early kernels fill the GPU; measured G=8 strip 0.156 -> 0.144 ms with a
-       // third), two for large ones (a third only adds contention: 448 -> 461 us at the bench
-       // configuration).  With four sets on two streams consecutive frames always alternate
-       // streams (three sets put frames 3k+2 and 3k+3 on one stream, one chain behind the other)
+    {  // frames in flight: three for small frames (row strips: latency-bound kernels, so a third
+       // frame's early kernels fill the GPU; measured G=8 strip 0.156 -> 0.144 ms), two for large
+       // ones (a third only adds contention: 448 -> 461 us at the bench configuration)
         const int depth = n_tiles <= kDeepTiles ? kFrameSets : 2;
         if (depth < kFrameSets) HIPCHK(hipEventSynchronize(s->fs[(s->cur_fs + kFrameSets - depth) % kFrameSets].ev_out));
     }
