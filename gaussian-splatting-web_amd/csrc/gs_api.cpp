@@ -413,7 +413,10 @@ static void ensure_seed(FrameSet& F, size_t words) {
     if (words <= F.seed_cap && F.seedh) return;
     dev_free(F.seedh);
     dev_alloc(F.seedh, words);
-    HIPCHK(hipMemset(F.seedh, 0, words * sizeof(float)));  // k_seed_pick re-zeroes what it read
+    // zeroed on the set's stream, ahead of the k_seed_hist that reads it (a plain hipMemset runs
+    // on the null stream, which does not order against the non-blocking set streams);
+    // k_seed_pick re-zeroes what it read
+    HIPCHK(hipMemsetAsync(F.seedh, 0, words * sizeof(float), F.stream));
     F.seed_cap = words;
 }
 
