@@ -263,6 +263,7 @@ struct FrameSet {
     uint2* ranges = nullptr;
     uint32_t* bmat = nullptr;           // [kBinParts][n_tiles] binning partition counts / offsets
     uint32_t* tbase = nullptr;          // [n_tiles] tile totals, then list begins
+    uint2* bchk = nullptr;              // [bin_chk_words(n_tiles)] binning's count checksums
     uint8_t* done = nullptr;
     uint32_t* c1tiles = nullptr;  // chunk 1: the tiles chunk 0 left unsaturated, compact
     uint32_t* sat = nullptr;            // (strip rows + 1) x (tiles_x + 1), then the bitmask
@@ -392,8 +393,10 @@ static void ensure_tiles(FrameSet& F, int n_tiles) {
     dev_free(F.c1tiles);
     dev_free(F.bmat);
     dev_free(F.tbase);
+    dev_free(F.bchk);
     dev_free(F.order);
     dev_alloc(F.ranges, (size_t)n_tiles);
+    dev_alloc(F.bchk, (size_t)bin_chk_words((uint32_t)n_tiles));
     dev_alloc(F.order, (size_t)n_tiles);
     dev_alloc(F.done, (size_t)n_tiles);
     dev_alloc(F.c1tiles, (size_t)n_tiles);
@@ -885,6 +888,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     bp.n_tiles = (uint32_t)n_tiles;
     bp.bmat = F.bmat;
     bp.tbase = F.tbase;
+    bp.bchk = F.bchk;
     bp.tvals = F.tvA;
     bp.rows = tr_end - tr_begin;
     bp.order = F.order;
@@ -1089,6 +1093,8 @@ static void check_frame_errors(gs_scene* s) {
         for (FrameSet& F : s->fs) HIPCHK(hipMemset(F.bar, 0, 16));
         throw GsError(GS_ERR_DEVICE_FAULT, "chunk-1 grid barrier timed out (workgroups not co-resident)");
     }
+    if (e & kErrBinning)  // a wrong tile list (count and emission disagreed): never a valid image
+        throw GsError(GS_ERR_DEVICE_FAULT, "binning invariant violated: a tile's emitted entries differ from its count");
     if (e & kErrOverflow) {
         grow_after_overflow(s);
         throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded; capacity grown, render again");
@@ -1896,6 +1902,7 @@ void gs_scene_free(gs_scene* s) {
         dev_free(F.ranges);
         dev_free(F.bmat);
         dev_free(F.tbase);
+        dev_free(F.bchk);
         dev_free(F.order);
         dev_free(F.done);
         dev_free(F.c1tiles);
@@ -1979,7 +1986,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
             int rc = GS_OK;
             std::string msg;
             for (gs_scene* m : s->members)
-                if (m->pending_err & (kErrOverflow | kErrBarrier)) {
+                if (m->pending_err & (kErrOverflow | kErrBarrier | kErrBinning)) {
                     const int r = guarded([&] { check_frame_errors(m); return GS_OK; });  // (sets m's device)
                     if (r != GS_OK && rc == GS_OK) {
                         rc = r;
@@ -1994,7 +2001,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
             return GS_OK;
         }
         HIPCHK(hipSetDevice(c->device));
-        if (s->pending_err & (kErrOverflow | kErrBarrier)) check_frame_errors(s);
+        if (s->pending_err & (kErrOverflow | kErrBarrier | kErrBinning)) check_frame_errors(s);
         hipStream_t st = stream ? (hipStream_t)stream : c->stream;
         render_frame(c, s, (const float*)uni, W, H, o, out_dev, st);
         return GS_OK;
@@ -2043,7 +2050,7 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
                     HIPCHK(hipDeviceSynchronize());
                     gs_scene* m = s->members[g];
                     collect_stats(m, true);
-                    if (m->pending_err & kErrBarrier) check_frame_errors(m);
+                    if (m->pending_err & (kErrBarrier | kErrBinning)) check_frame_errors(m);
                     if (m->pending_err & kErrOverflow) {
                         overflow = true;
                         m->pending_err = 0;
@@ -2064,7 +2071,7 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
             render_frame(c, s, (const float*)uni, W, H, o, c->d_out, c->stream);
             HIPCHK(hipStreamSynchronize(c->stream));
             collect_stats(s, true);
-            if (s->pending_err & kErrBarrier) check_frame_errors(s);
+            if (s->pending_err & (kErrBarrier | kErrBinning)) check_frame_errors(s);
             if (!(s->pending_err & kErrOverflow)) break;
             s->pending_err = 0;
             if (attempt >= 2) throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded");
@@ -2529,6 +2536,62 @@ int gs_debug_tile_lists(gs_ctx* c, gs_scene* s, uint32_t* out_ranges, uint64_t r
             out_entries[2 * e] = qd.empty() ? sk[g].x : sk[g].y;
             out_entries[2 * e + 1] = qd.empty() ? sk[g].y : qd[sk[g].y];
         }
+        return GS_OK;
+    });
+}
+
+int gs_debug_tile_list_check(gs_ctx* c, gs_scene* s, uint64_t out[5]) {
+    return guarded([&] {
+        if (c && !c->members.empty()) throw GsError(GS_ERR_UNSUPPORTED, "debug exports take a single-device context");
+        if (!c || !s || !out) throw GsError(GS_ERR_INVALID, "null argument");
+        if (!s->have_frame) throw GsError(GS_ERR_INVALID, "no frame rendered yet");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipDeviceSynchronize());
+        collect_stats(s, true);
+        if (s->last.n_chunk[1] > 0)
+            throw GsError(GS_ERR_UNSUPPORTED, "tile lists of a two-chunk frame (render with chunk_fraction >= 1)");
+        const FrameSet& F = s->fs[s->last_fs];
+        const int nt = std::max(s->last_tiles, 0);
+        std::vector<uint2> rg((size_t)std::max(nt, 1));
+        if (nt > 0) HIPCHK(hipMemcpy(rg.data(), F.ranges, (size_t)nt * sizeof(uint2), hipMemcpyDeviceToHost));
+        uint64_t total = 0;
+        for (int t = 0; t < nt; ++t) total = std::max<uint64_t>(total, rg[t].y);
+        std::vector<uint32_t> tv(total);
+        if (total) HIPCHK(hipMemcpy(tv.data(), F.tvB, total * 4, hipMemcpyDeviceToHost));
+        const size_t ns = (size_t)proj_parts(s->n) * kProjTile;
+        std::vector<uint2> sk(std::max<size_t>(ns, 1));
+        std::vector<uint32_t> sr(std::max<size_t>(ns, 1));
+        if (ns) {
+            HIPCHK(hipMemcpy(sk.data(), F.skey, ns * sizeof(uint2), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(sr.data(), F.srect, ns * 4, hipMemcpyDeviceToHost));
+        }
+        uint64_t dup = 0, order = 0, gaps = 0, bad = 0, prev_end = 0;
+        std::vector<uint32_t> idx;
+        for (int t = 0; t < nt; ++t) {
+            const uint64_t b = rg[t].x, e = rg[t].y;
+            if (b != prev_end || e < b) ++gaps;
+            prev_end = e;
+            idx.clear();
+            uint64_t last = 0;
+            for (uint64_t j = b; j < e && j < total; ++j) {
+                const uint32_t g = tv[j];
+                if (g >= ns || sr[g] == kRectHole || sr[g] == kRectEmpty) {
+                    ++bad;
+                    continue;
+                }
+                const uint64_t k = ((uint64_t)sk[g].x << 32) | sk[g].y;
+                if (j > b && k <= last) ++order;
+                last = k;
+                idx.push_back(sk[g].y);
+            }
+            std::sort(idx.begin(), idx.end());
+            for (size_t j = 1; j < idx.size(); ++j) dup += idx[j] == idx[j - 1] ? 1u : 0u;
+        }
+        out[0] = total;
+        out[1] = dup;
+        out[2] = order;
+        out[3] = gaps;
+        out[4] = bad;
         return GS_OK;
     });
 }

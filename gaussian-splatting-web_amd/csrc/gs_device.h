@@ -51,6 +51,8 @@ constexpr uint32_t kRectHole = 0xFFFFFFFDu;   // a composite slot whose candidat
 // Device-side error bits (FrameCtl::err); a nonzero word fails the frame.
 constexpr uint32_t kErrOverflow = 1u;
 constexpr uint32_t kErrBarrier = 2u;   // a grid barrier of k_chunk1 timed out
+constexpr uint32_t kErrBinning = 4u;   // a binning workgroup emitted other entries than it counted
+                                       // (k_bin_emit's check of BinParams::bchk): a tile list is wrong
 
 // Saturation-depth histogram: tile saturated at depth key k -> bucket (k >> 21) - base, clamped to
 // [0, kSatBuckets): quarter-octave buckets of depth from the last frame's nearest visible splat
@@ -297,7 +299,16 @@ struct BinParams {
                                   // by the waves of every workgroup in turn instead of the LDS queue
     uint32_t uid_lds;             // 1: the partition's unit entries cached in LDS after the unit
                                   // prefix (set by the launcher when it fits; chunk 0 only)
+    // [bin_chk_words(n_tiles)] per binning workgroup (partition, band): checksums of the entries
+    // k_bin_count counted per tile (sum of counts, sum of count x bin_hash(tile)); k_bin_emit
+    // compares the entries it emitted with them and sets kErrBinning on a difference
+    uint2* bchk;
 };
+// Binning workgroups of a chunk at most (the launches' bands of up to kBandTilesMax tiles and
+// k_chunk1's of kBandTiles): the size of BinParams::bchk.
+__host__ __device__ inline uint32_t bin_chk_words(uint32_t n_tiles) {
+    return (uint32_t)kBinParts * ((n_tiles + kBandTiles - 1) / kBandTiles + 1);
+}
 
 // Per-tile sort of the tile lists (k_tile_sort): each tile's slots ordered by their sort key,
 // key(g) = g (slots are depth ranks) or, with skey, (skey[g].x << 32) | skey[g].y.

@@ -22,6 +22,8 @@
 //
 // Inter-workgroup hand-offs (the grid barrier) follow cdna_hip_programming.md Guideline 16:
 // agent-scope release / acquire, bounded spins, counters zeroed by the frame's end.
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <type_traits>
 
@@ -1685,8 +1687,19 @@ __device__ __forceinline__ bool rect_wide(const BinParams& p, const TileRect& r)
 // (the quad's |u|,|v| <= 2 only removes pixels from it).  It is convex, so in every tile row the
 // tiles holding one of its pixel centres form one contiguous column range, computed in closed
 // form below and widened (log2 margin, 0.02 px + relative) so that no pixel the composite would
-// blend is ever dropped.  Count, emission and the wide path call the same functions, so their
-// entry counts agree exactly.
+// blend is ever dropped.  Count, emission and the wide path call the same functions, and those
+// functions are compiled without floating-point contraction: with hipcc's default (fusion left to
+// the backend) each inlined copy could fuse a different mul + add into an FMA, so the count
+// (inside bin_walk), the emission loop and wide_entries rounded one column bound differently and
+// a splat's entry could be counted in a tile it was not emitted into -- one list position left
+// stale (a duplicate of an older frame's entry) and the splat missing.
+// With every operation rounded on its own, every copy computes the same bits, so a tile's count
+// and its entries agree exactly; k_bin_emit checks that (bin_chk, kErrBinning).
+#ifndef GS_BIN_CONTRACT_FAST  // (diagnostics builds only: the round-5 code generation, for the A/B)
+#define GS_BIN_NO_CONTRACT _Pragma("clang fp contract(off)")
+#else
+#define GS_BIN_NO_CONTRACT
+#endif
 struct Ellipse {
     float cx, cy, m00, m01, det, l, hy, dys, xm, rm00;  // xm: x margin; rm00 = 1 / m00
     uint32_t px0, px1;                             // pixel box columns
@@ -1699,6 +1712,7 @@ __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 __device__ __forceinline__ Ellipse ellipse_of(const float4 q0, const float4 q1) {
+    GS_BIN_NO_CONTRACT
     Ellipse e;
     const float ax = q0.z, ay = q0.w, bx = q1.x, by = q1.y;
     const uint32_t bbx = __float_as_uint(q1.w);
@@ -1728,6 +1742,7 @@ __device__ __forceinline__ Ellipse ellipse_of(const float4 q0, const float4 q1) 
 // dy0 / dy1: the band's first and last pixel-row centres minus the ellipse centre's y.
 __device__ __forceinline__ bool ellipse_cols_dy(const Ellipse& e, float dy0, float dy1, uint32_t& pl_,
                                                 uint32_t& ph_) {
+    GS_BIN_NO_CONTRACT
     if (!e.ok) {
         pl_ = e.px0;
         ph_ = e.px1;
@@ -1756,6 +1771,7 @@ __device__ __forceinline__ bool ellipse_cols_dy(const Ellipse& e, float dy0, flo
 
 __device__ __forceinline__ bool ellipse_cols_band(const Ellipse& e, uint32_t y0, uint32_t y1, uint32_t& pl_,
                                                   uint32_t& ph_) {  // pixel rows y0 .. y1
+    GS_BIN_NO_CONTRACT
     return ellipse_cols_dy(e, (float)y0 + 0.5f - e.cy, (float)y1 + 0.5f - e.cy, pl_, ph_);
 }
 
@@ -2016,6 +2032,21 @@ __device__ __forceinline__ void bin_walk(const BinParams& p, const UnitList& L, 
     }
 }
 
+// The count/emission invariant (kErrBinning): per binning workgroup, the entries it counted and
+// the entries it emitted, both as (sum over its tiles of n_t, sum of n_t * bin_hash(t)) mod 2^32.
+// Equal sums mean equal per-tile counts unless two or more tiles differ in a way that cancels in
+// both: a net change shows in the first, one entry moved between tiles a and b in the second
+// ((a - b) * odd != 0 mod 2^32).  s_chk: two LDS words, zeroed before the walk.
+__device__ __forceinline__ uint32_t bin_hash(uint32_t t) { return t * 0x9E3779B1u + 0x7F4A7C15u; }
+__device__ __forceinline__ void bin_chk_add(uint32_t* s_chk, uint32_t a, uint32_t b) {  // whole waves
+    a = wave_incl_scan(a);
+    b = wave_incl_scan(b);
+    if (lane_id() == 63) {
+        atomicAdd(&s_chk[0], a);
+        atomicAdd(&s_chk[1], b);
+    }
+}
+
 // Binning partition / band vb: counts of its splats' entries per tile of the band -> bmat row.
 // Wide splats (>= wide_tiles box tiles) are queued in LDS (up to wide_cap) and counted by whole
 // waves, as k_bin_emit emits them.
@@ -2023,10 +2054,15 @@ template <int NT, bool LISTED>
 __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp,
                                                uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
+    uint32_t* s_chk = s_nw_p + 1;
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * p.band_tiles, t_hi = min(p.n_tiles, t_lo + p.band_tiles);
     for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += NT) s_cnt[t] = 0;
-    if (threadIdx.x == 0) s_nw = 0;
+    if (threadIdx.x == 0) {
+        s_nw = 0;
+        s_chk[0] = 0;
+        s_chk[1] = 0;
+    }
     const UnitList L = bin_unit_list(p);
     const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
     bin_walk<NT>(p, L, part, s_pref, total, [&](uint32_t g, uint32_t pr, uint32_t sj, float4 q0, float4 q1) {
@@ -2049,8 +2085,16 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
     wide_listed<NT>(p, part, t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
     __syncthreads();
     uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
-    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) row[t] = s_cnt[t - t_lo];
+    uint32_t c1 = 0, c2 = 0;
+    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) {
+        const uint32_t c = s_cnt[t - t_lo];
+        row[t] = c;
+        c1 += c;
+        c2 += c * bin_hash(t);
+    }
+    bin_chk_add(s_chk, c1, c2);
     __syncthreads();
+    if (threadIdx.x == 0) p.bchk[vb] = make_uint2(s_chk[0], s_chk[1]);
 }
 
 // The binning launches size their LDS to the frame: band_tiles counters (one band up to
@@ -2062,7 +2106,7 @@ __device__ __forceinline__ uint32_t* bin_lds() {
     return dyn_lds;
 }
 __host__ __device__ inline size_t bin_lds_words(uint32_t band_tiles, uint32_t pref_words, uint32_t wide_cap) {
-    return (size_t)band_tiles + pref_words + kBinThreads / 64 + wide_cap + 1;
+    return (size_t)band_tiles + pref_words + kBinThreads / 64 + wide_cap + 3;  // (s_nw, s_chk[2])
 }
 
 template <bool LISTED>  // LISTED: chunk 0 (k_cull's unit list); else chunk 1 (every unit, counts from c1)
@@ -2204,10 +2248,12 @@ template <int NT, bool SCAN, bool LISTED>
 __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, uint32_t* s_pref, uint32_t* s_tmp,
                               uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
+    uint32_t* s_chk = s_nw_p + 1;
     const uint32_t part = vb % kBinParts, band = vb / kBinParts;
     const uint32_t t_lo = band * p.band_tiles, t_hi = min(p.n_tiles, t_lo + p.band_tiles);
     const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     const uint32_t cap = p.capacity;
+    uint32_t d1 = 0, d2 = 0;  // minus the thread's start cursors (the checksum of bin_chk_add)
     if (SCAN) {
         constexpr int nw = NT / 64, ipt = 8;
         const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -2241,6 +2287,8 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
                 if (t >= t_lo && t < t_hi) {
                     const uint32_t bb = min(base, cap);
                     cur[k] = bb + row[t];
+                    d1 -= cur[k];
+                    d2 -= cur[k] * bin_hash(t);
                     if (!whole) s_cur[t - t_lo] = cur[k];
                     if (part == 0) p.ranges[t] = make_uint2(bb, min(base + v[k], cap));
                 }
@@ -2259,9 +2307,18 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
             if (carry > cap) atomicOr(&p.ctl->err, kErrOverflow);
         }
     } else {
-        for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) s_cur[t - t_lo] = p.tbase[t] + row[t];
+        for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) {
+            const uint32_t c = p.tbase[t] + row[t];
+            s_cur[t - t_lo] = c;
+            d1 -= c;
+            d2 -= c * bin_hash(t);
+        }
     }
-    if (threadIdx.x == 0) s_nw = 0;
+    if (threadIdx.x == 0) {
+        s_nw = 0;
+        s_chk[0] = 0;
+        s_chk[1] = 0;
+    }
     const UnitList L = bin_unit_list(p);
     const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
     // (not bin_walk: with the slot prefetch the emission ran slower, 1.60 -> 1.68 ms at the one-chunk
@@ -2302,6 +2359,18 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
         if (pos < cap) p.tvals[pos] = g;
     });
     __syncthreads();
+    // the invariant: every cursor advanced by exactly the tile's count (end - start = n_t)
+    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) {
+        const uint32_t c = s_cur[t - t_lo];
+        d1 += c;
+        d2 += c * bin_hash(t);
+    }
+    bin_chk_add(s_chk, d1, d2);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint2 want = p.bchk[vb];
+        if (want.x != s_chk[0] || want.y != s_chk[1]) atomicOr(&p.ctl->err, kErrBinning);
+    }
 }
 
 template <bool LISTED>
@@ -3816,7 +3885,7 @@ __device__ __forceinline__ void grid_sync(uint32_t* bar, FrameCtl* ctl, uint64_t
     __syncthreads();
 }
 
-constexpr size_t kBinLdsWords = kBandTiles + (kBinMaxUnits + 1) + 4 + kWideQueue + 1;
+constexpr size_t kBinLdsWords = kBandTiles + (kBinMaxUnits + 1) + 4 + kWideQueue + 3;  // (s_nw, s_chk[2])
 constexpr size_t kChunk1Lds = std::max(std::max(kBinLdsWords * 4, sizeof(TsShared)), sizeof(CompQShared));
 
 #ifdef GS_C1_TIME
@@ -4133,6 +4202,10 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
     p.wide_cap = p.wlist ? 0u : std::min(room, std::max(kWideQueue, std::min(kWideQueueMax, p.n_tiles / 4)));
     const size_t lds = bin_lds_words(p.band_tiles, pw, p.wide_cap) * 4;
     const unsigned grid = kBinParts * bin_bands(p.n_tiles, p.band_tiles);
+    if (!p.bchk || grid > bin_chk_words(p.n_tiles)) {
+        std::fprintf(stderr, "gsplat: launch_bin without room for its %u workgroups' checksums\n", grid);
+        std::abort();
+    }
     if (p.units)
         hipLaunchKernelGGL(k_bin_count<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
     else

@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "gs_present_device", "gs_encode_png", "gs_look_at",
     "gs_perspective", "gs_camera_position", "gs_camera_from_json", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
     "gs_debug_chunk1_grid", "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records", "gs_debug_last_slots",
-    "gs_debug_tile_lists",
+    "gs_debug_tile_lists", "gs_debug_tile_list_check",
 )
 
 
@@ -145,6 +145,7 @@ def lib():
         L.gs_debug_last_records.argtypes = [P, P, P, U64]
         L.gs_debug_last_slots.argtypes = [P, P, P, U64, ctypes.POINTER(U64)]
         L.gs_debug_tile_lists.argtypes = [P, P, P, U64, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.gs_debug_tile_list_check.argtypes = [P, P, P]
         _lib = L
     return _lib
 
@@ -477,6 +478,15 @@ class Scene:
         _check(lib().gs_debug_tile_lists(self.ctx.handle, self.handle, _ptr(rg), nt.value, _ptr(en), ne.value,
                                          ctypes.byref(nt), ctypes.byref(ne)))
         return rg, en
+
+    def tile_list_check(self):
+        """Structural check of the last one-chunk frame's tile lists (gs_debug_tile_list_check): dict
+        of entries, dup (a (tile, Gaussian) pair listed twice), order (adjacent entries not strictly
+        ascending by (key, index)), gaps (a list not starting where the previous one ends), bad
+        (an entry that is not a visible splat's slot).  A correct frame has all but entries 0."""
+        out = (ctypes.c_uint64 * 5)()
+        _check(lib().gs_debug_tile_list_check(self.ctx.handle, self.handle, out))
+        return dict(zip(("entries", "dup", "order", "gaps", "bad"), (int(v) for v in out)))
 
     def last_records(self):
         out = np.empty((self.n, 16), np.float32)

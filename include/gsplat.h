@@ -334,6 +334,14 @@ int gs_debug_last_slots(gs_ctx* ctx, gs_scene* scene, uint32_t* out16, uint64_t 
 int gs_debug_tile_lists(gs_ctx* ctx, gs_scene* scene, uint32_t* out_ranges, uint64_t ranges_capacity,
                         uint32_t* out_entries, uint64_t entries_capacity, uint64_t* out_tiles,
                         uint64_t* out_entries_n);
+/* Structural check of the last frame's tile lists (one-chunk frames only), on the host, at any
+ * frame size: out[0] = entries, out[1] = (tile, Gaussian) pairs listed more than once, out[2] =
+ * adjacent entries of a tile not in strictly ascending (depth key, reference index) order, out[3]
+ * = tiles whose list does not begin where the previous tile's ends, out[4] = entries holding a
+ * slot that is not a visible splat of the frame (a hole or past the slot space).  A correct
+ * frame has out[1..4] == 0; the reference draws every Gaussian at most once per frame
+ * (drawIndexed(6, N), src/simple_render.ts:525-534) and blends in stable depth order. */
+int gs_debug_tile_list_check(gs_ctx* ctx, gs_scene* scene, uint64_t out[5]);
 
 #ifdef __cplusplus
 }
