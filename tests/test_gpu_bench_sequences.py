@@ -44,8 +44,20 @@ def _frames(sc, ctx, views, W, H, opts, bufs):
     return [b.to_host(np.empty((H, W, 4), np.float16)) for b in bufs[:len(views)]]
 
 
-def _one_chunk(sc, u, W, H):
-    return sc.render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, chunk_fraction=1.0))
+def _one_chunk(sc, u, W, H, check=True):
+    """The view as one chunk (the comparison render); check: its tile lists structurally sound
+    (gs_debug_tile_list_check: no (tile, Gaussian) pair twice, strictly ascending (key, index),
+    contiguous ranges, only visible splats' slots).  Every frame, chunked or not, is also checked
+    on the device by the binning invariant (kErrBinning: the render raises on a violation)."""
+    img = sc.render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, chunk_fraction=1.0))
+    if check:
+        _assert_lists_sound(sc)
+    return img
+
+
+def _assert_lists_sound(sc):
+    chk = sc.tile_list_check()
+    assert chk["entries"] > 0 and chk["dup"] == 0 and chk["order"] == 0 and chk["gaps"] == 0 and chk["bad"] == 0, chk
 
 
 def _bits(img):
@@ -128,8 +140,8 @@ def test_bench_orbit_sequence(gpu_ctx, bench_scene):
 
 @pytest.mark.timeout(600)
 def test_bench_orbit_sequence_list_split(gpu_ctx, bench_scene):
-    """bench.py's orbit with the list split (gs_opts.list_split = 1, as bench.py renders its
-    orbit, cold and sparse lines and strips): chunk 1's long lists of the unsaturated tiles are cut
+    """bench.py's orbit with the list split (gs_opts.list_split = 1: bench.py's --list-split 1; its
+    default, and every number it reports by default, is 0): chunk 1's long lists of the unsaturated tiles are cut
     over 4 wave pairs.  Not bit-identical to the one-chunk render (tests/test_gpu_split.py); every
     frame within 2e-3 of it (f16), the yaw extremes against the oracle and the WebGPU stand-in."""
     aos, sc = bench_scene
@@ -179,6 +191,40 @@ def test_bench_cold_sequence(gpu_ctx, bench_scene):
         assert np.array_equal(_bits(im), _bits(one)), "cold frame %d (view %d) differs from one chunk" % (k, k % 4)
     for k in (1, 3):  # from inside the scene; moved and turned
         _vs_oracle(aos, N3, views[k], W, H, imgs[k], "bench_cold_%d" % k)
+
+
+@pytest.mark.timeout(600)
+def test_bench_tile_lists_sound(gpu_ctx, bench_scene):
+    """Round-5 bug regression: cold view 3 of the bench scene rendered as one chunk
+    three times in a row -- tile (26, 47)'s list had one Gaussian counted but never emitted, so one
+    list position kept an older frame's entry (a duplicate, out of order; 1792 entries instead of
+    1791).  Cause: the binning's ellipse math was contracted into FMAs differently in the count and
+    the emission.  Every render must raise no kErrBinning, pass the structural check, list 1791
+    entries in that tile and be bit-identical to the first; then forced chunk splits of the view
+    (tools/diag/split_sweep.py's fractions) bit-identical to it; then the other cold views and the
+    orbit's yaw extremes, three renders each, structurally sound."""
+    aos, sc = bench_scene
+    W, H = W3, H3
+    tile = 47 * ((W + 15) // 16) + 26
+    u = gs.cold_uniforms(W, H, 3)
+    first = None
+    for rep in range(3):
+        img = _one_chunk(sc, u, W, H)
+        rg, en = sc.tile_lists()
+        lst = en[rg[tile, 0]:rg[tile, 1]]
+        assert len(lst) == 1791, (rep, len(lst))
+        assert len(np.unique(lst[:, 1])) == len(lst)
+        k64 = (lst[:, 0].astype(np.uint64) << np.uint64(32)) | lst[:, 1].astype(np.uint64)
+        assert np.all(k64[1:] > k64[:-1]), "tile list not strictly ascending"
+        if first is None:
+            first = img
+        assert np.array_equal(_bits(img), _bits(first)), "one-chunk render %d of cold view 3 differs" % rep
+    for f in (0.29, 0.48, 0.67):
+        img = sc.render(u, W, H, gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, chunk_fraction=f))
+        assert np.array_equal(_bits(img), _bits(first)), "cold view 3 split at %.2f differs from one chunk" % f
+    for v in [gs.cold_uniforms(W, H, k) for k in (0, 1, 2)] + [gs.orbit_uniforms(W, H, k) for k in (15, 45)]:
+        for rep in range(3):
+            _one_chunk(sc, v, W, H)
 
 
 @pytest.mark.timeout(600)
@@ -236,7 +282,7 @@ def test_orbit_50m_4k(gpu_ctx):
         b.free()
     assert st["frames_chunked"] >= 8, st
     for k, im in enumerate(imgs):
-        assert np.array_equal(_bits(im), _bits(_one_chunk(sc, views[k], W, H))), "4K orbit frame %d" % k
+        assert np.array_equal(_bits(im), _bits(_one_chunk(sc, views[k], W, H, check=k == 0))), "4K orbit frame %d" % k
     # camera cuts at 4K: seeded frames
     views = [gs.cold_uniforms(W, H, k) for k in range(4)]
     bufs = [gs.DeviceBuffer(W * H * 8) for _ in range(4)]
@@ -247,5 +293,5 @@ def test_orbit_50m_4k(gpu_ctx):
         b.free()
     assert st["frames_seeded"] >= 3, st
     for k, im in enumerate(imgs):
-        assert np.array_equal(_bits(im), _bits(_one_chunk(sc, views[k], W, H))), "4K cold frame %d" % k
+        assert np.array_equal(_bits(im), _bits(_one_chunk(sc, views[k], W, H, check=k == 3))), "4K cold frame %d" % k
     sc.close()
