@@ -1093,6 +1093,10 @@ static void check_frame_errors(gs_scene* s) {
         for (FrameSet& F : s->fs) HIPCHK(hipMemset(F.bar, 0, 16));
         throw GsError(GS_ERR_DEVICE_FAULT, "chunk-1 grid barrier timed out (workgroups not co-resident)");
     }
+    if (e & kErrState) {  // frame state the frame did not write: every set starts clean again
+        for (FrameSet& F : s->fs) F.meta_clean = false;
+        throw GsError(GS_ERR_DEVICE_FAULT, "frame state out of range (a unit, partition or wide-splat count past its list)");
+    }
     if (e & kErrBinning)  // a wrong tile list (count and emission disagreed): never a valid image
         throw GsError(GS_ERR_DEVICE_FAULT, "binning invariant violated: a tile's emitted entries differ from its count");
     if (e & kErrOverflow) {
@@ -1986,7 +1990,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
             int rc = GS_OK;
             std::string msg;
             for (gs_scene* m : s->members)
-                if (m->pending_err & (kErrOverflow | kErrBarrier | kErrBinning)) {
+                if (m->pending_err & (kErrOverflow | kErrBarrier | kErrBinning | kErrState)) {
                     const int r = guarded([&] { check_frame_errors(m); return GS_OK; });  // (sets m's device)
                     if (r != GS_OK && rc == GS_OK) {
                         rc = r;
@@ -2001,7 +2005,7 @@ int gs_render_device(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, cons
             return GS_OK;
         }
         HIPCHK(hipSetDevice(c->device));
-        if (s->pending_err & (kErrOverflow | kErrBarrier | kErrBinning)) check_frame_errors(s);
+        if (s->pending_err & (kErrOverflow | kErrBarrier | kErrBinning | kErrState)) check_frame_errors(s);
         hipStream_t st = stream ? (hipStream_t)stream : c->stream;
         render_frame(c, s, (const float*)uni, W, H, o, out_dev, st);
         return GS_OK;
@@ -2050,7 +2054,7 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
                     HIPCHK(hipDeviceSynchronize());
                     gs_scene* m = s->members[g];
                     collect_stats(m, true);
-                    if (m->pending_err & (kErrBarrier | kErrBinning)) check_frame_errors(m);
+                    if (m->pending_err & (kErrBarrier | kErrBinning | kErrState)) check_frame_errors(m);
                     if (m->pending_err & kErrOverflow) {
                         overflow = true;
                         m->pending_err = 0;
@@ -2071,7 +2075,7 @@ int gs_render(gs_ctx* c, gs_scene* s, const void* uni, int W, int H, const gs_op
             render_frame(c, s, (const float*)uni, W, H, o, c->d_out, c->stream);
             HIPCHK(hipStreamSynchronize(c->stream));
             collect_stats(s, true);
-            if (s->pending_err & (kErrBarrier | kErrBinning)) check_frame_errors(s);
+            if (s->pending_err & (kErrBarrier | kErrBinning | kErrState)) check_frame_errors(s);
             if (!(s->pending_err & kErrOverflow)) break;
             s->pending_err = 0;
             if (attempt >= 2) throw GsError(GS_ERR_DEVICE_FAULT, "tile-entry capacity exceeded");

@@ -53,6 +53,9 @@ constexpr uint32_t kErrOverflow = 1u;
 constexpr uint32_t kErrBarrier = 2u;   // a grid barrier of k_chunk1 timed out
 constexpr uint32_t kErrBinning = 4u;   // a binning workgroup emitted other entries than it counted
                                        // (k_bin_emit's check of BinParams::bchk): a tile list is wrong
+constexpr uint32_t kErrState = 8u;     // a frame-state count read from FrameCtl / StatShard exceeded the
+                                       // buffer it indexes (a unit list, the partition list, the wide
+                                       // list): the kernels skip the work instead of reading past it
 
 // Saturation-depth histogram: tile saturated at depth key k -> bucket (k >> 21) - base, clamped to
 // [0, kSatBuckets): quarter-octave buckets of depth from the last frame's nearest visible splat

@@ -447,6 +447,10 @@ struct Proj {
 // kSentinel) when invisible.  Deterministic: records_body recomputes the same record bit for bit.
 __device__ __forceinline__ bool project_core_g(const ProjParams& p, uint32_t i, const float4 g0, const float4 g1,
                                                const float4 g2, int row_lo, int row_hi, bool cull, Proj& o) {
+    // no contraction anywhere in it: k_project (chunk 0), c1_records_body (chunk 1) and the debug
+    // dump inline their own copies, and a splat's record and tile rect must not depend on which
+    // copy projected it (the image is invariant under the chunk split; see the binning's ellipse)
+#pragma clang fp contract(off)
     o.key = kSentinel;
     o.prect = kRectEmpty;
         const float x = g0.x, y = g0.y, z = g0.z;
@@ -778,7 +782,10 @@ __device__ __forceinline__ void wide_append(const ProjParams& p, int chunk, bool
     if (lane == 0) base = atomicAdd(&p.stats[sh].wl_n[chunk], (uint32_t)__popcll(b));
     base = __shfl(base, 0, 64);
     const uint32_t j = base + (uint32_t)__popcll(b & lanemask_lt()), cap = wide_shard_cap(proj_parts(p.n));
-    if (wide) p.wlist[(uint64_t)sh * cap + (chunk ? cap - 1u - j : j)] = slot;
+    if (wide) {
+        if (j < cap) p.wlist[(uint64_t)sh * cap + (chunk ? cap - 1u - j : j)] = slot;
+        else atomicOr(&p.ctl->err, kErrState);  // (never: a shard's partitions hold at most cap slots)
+    }
 }
 
 // Does the tile rectangle [tx0, tx1] x [ty0, ty1] (strip tile rows, absolute) hold a tile chunk 0
@@ -900,14 +907,25 @@ struct UnitList {
     uint32_t pre[kUnitShards + 1];
     uint32_t total;
 };
-__device__ __forceinline__ UnitList load_units(const uint32_t* units, const FrameCtl* ctl, uint32_t parts) {
+// A shard count past the shard's capacity (state the frame did not write) is an error, not a
+// read past the list: the frame's units are dropped and kErrState fails the frame.
+__device__ __forceinline__ UnitList load_units(const uint32_t* units, FrameCtl* ctl, uint32_t parts) {
     UnitList L;
     L.units = units;
     L.cap = unit_shard_cap(parts);
     L.pre[0] = 0;
+    bool bad = false;
 #pragma unroll
-    for (int k = 0; k < kUnitShards; ++k) L.pre[k + 1] = L.pre[k] + ctl->unit_n[k];
+    for (int k = 0; k < kUnitShards; ++k) {
+        const uint32_t c = ctl->unit_n[k];
+        bad = bad || c > L.cap;
+        L.pre[k + 1] = L.pre[k] + c;
+    }
     L.total = L.pre[kUnitShards];
+    if (bad) {
+        if (threadIdx.x == 0) atomicOr(&ctl->err, kErrState);
+        L.total = 0;
+    }
     return L;
 }
 // A listed unit: bits [0, 20) = partition * kProjRounds + round, bits [20, 28) = its candidate
@@ -1112,7 +1130,11 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = proj_parts(p.n), ucap = unit_shard_cap(parts);
     KT_MARK(0, 0, 0);
-    const uint32_t nl = p.ctl->c0_parts;  // the partitions k_part_list kept
+    uint32_t nl = p.ctl->c0_parts;  // the partitions k_part_list kept
+    if (nl > parts) {  // (never: k_part_list lists each partition at most once)
+        if (tid == 0) atomicOr(&p.ctl->err, kErrState);
+        nl = 0;
+    }
     const uint32_t T = frame_thresh(p);
     uint32_t kt_items = 0;
     // Software-pipelined over the workgroup's partitions: the next partition's cull planes are
@@ -1955,10 +1977,11 @@ __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, u
     if (!p.wlist) return;
     uint32_t pre[kWideShards + 1];  // the shards' lists, concatenated
     pre[0] = 0;
+    const uint32_t cap = wide_shard_cap(p.parts);
 #pragma unroll
-    for (uint32_t k = 0; k < kWideShards; ++k) pre[k + 1] = pre[k] + p.stats[k].wl_n[p.chunk];
-    const uint32_t wn = pre[kWideShards], cap = wide_shard_cap(p.parts);
+    for (uint32_t k = 0; k < kWideShards; ++k) pre[k + 1] = pre[k] + min(p.stats[k].wl_n[p.chunk], cap);
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t wn = pre[kWideShards];
     const uint32_t share = wn > part ? (wn - part + kBinParts - 1) / kBinParts : 0u;  // entries part + i kBinParts
     uint32_t k = 0;  // the workgroup's entries in turn: a splat of at most kWaveCells tile cells goes
                      // to one wave (round-robin), a larger one to every thread of the workgroup
@@ -4136,6 +4159,9 @@ void launch_project(const ProjParams& p, hipStream_t s) {
 #ifndef GS_CULL_GRID
 #define GS_CULL_GRID 2048
 #endif
+    // k_cull's unit shard = blockIdx.x % kUnitShards holds at most unit_shard_cap units only when the
+    // grid is a multiple of kUnitShards or has one partition per workgroup (grid = parts)
+    static_assert(GS_CULL_GRID % kUnitShards == 0, "GS_CULL_GRID must be a multiple of kUnitShards");
 #ifndef GS_PROJ_GRID
 #define GS_PROJ_GRID 1536
 #endif

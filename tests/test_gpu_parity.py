@@ -316,6 +316,49 @@ def test_lower_sh_degrees(gpu_ctx, nsh):
     assert r[2], r
 
 
+def test_scene_turnover_on_one_context(gpu_ctx):
+    """Round-5's unexplained fault: test_lower_sh_degrees[1] (n 5000, SH degree 0,
+    128x96) died in k_project with a memory aperture violation after 111 tests had run on the
+    session context.  This replays the suite's order on one context three times -- a large scene
+    rendered as frames in flight (chunked, seeded), a 64-Gaussian scene of full-screen splats,
+    then the three low-SH scenes -- each freed before the next is uploaded, and every small frame
+    against the oracle.  The frame-state guards (kErrState) turn a count that does not fit its
+    list into an error; none may fire."""
+    W, H = 128, 96
+    n = 5000
+    full = gs.synth_aos(n, 13, W, H).reshape(n, 80)
+    u = gs.bench_uniforms(W, H)
+    refs = {}
+    for rnd in range(3):
+        big_n = 400_000
+        big = gs.Scene(gpu_ctx, gs.synth_aos(big_n, 7 + rnd, 1280, 720), big_n, 16)
+        ub = gs.bench_uniforms(1280, 720)
+        bufs = [gs.DeviceBuffer(1280 * 720 * 8) for _ in range(4)]
+        o = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16)
+        for k in range(8):
+            big.render_device(ub if k % 3 else gs.cold_uniforms(1280, 720, k), 1280, 720, bufs[k % 4].ptr.value,
+                              1280 * 720 * 8, None, o)
+        gpu_ctx.sync()
+        for b in bufs:
+            b.free()
+        big.close()
+        hw, hh = 320, 240
+        huge = gs.synth_aos(64, 21, hw, hh).reshape(64, 80)
+        huge[:, 4:7] = 0.5
+        hs = gs.Scene(gpu_ctx, huge.reshape(-1), 64, 16)
+        hs.render(gs.bench_uniforms(hw, hh), hw, hh)
+        hs.close()
+        for nsh in (1, 4, 9):
+            rec = full[:, : 16 + 4 * nsh].copy().reshape(-1)
+            sc = gs.Scene(gpu_ctx, rec, n, nsh)
+            img = sc.render(u, W, H)
+            sc.close()
+            if nsh not in refs:
+                refs[nsh], _ = orc.render(rec.view(np.uint8), n, nsh, u, W, H)
+            r = image_close_fp32(img, refs[nsh])
+            assert r[2], (rnd, nsh, r)
+
+
 def test_bad_arguments(gpu_ctx):
     with pytest.raises(gs.GsError):
         gs.Scene(gpu_ctx, np.zeros(112, np.uint8), 1, 3)  # n_sh=3 is not a record size the reference makes
