@@ -59,7 +59,6 @@ def pmc_traffic(kernel):
     """HBM bytes per frame of `kernel` from the committed PMC profile of this bench command
     (profiles/<round>_pmc.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE, summed over the kernel's
     launches in a frame); None when no profile is committed."""
-    names = {"composite": "k_composite<false>", "project": "k_project"}
     prof = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc.json")) \
         if os.path.isdir(os.path.join(ROOT, "profiles")) else []
     if not prof:
@@ -67,20 +66,31 @@ def pmc_traffic(kernel):
     d = json.load(open(os.path.join(ROOT, "profiles", prof[-1])))
     tot = 0.0
     for lab, e in d.items():
-        if lab.startswith(names[kernel] + "#") and "traffic_bytes" in e:
+        if _is_kernel(lab, kernel) and "traffic_bytes" in e:
             tot += e["traffic_bytes"]
     return (tot if tot else None), prof[-1]
 
 
+def _is_kernel(label, kernel):
+    """A PMC profile label ("k_composite<false, 1, 2>#0": kernel name, template arguments, launch
+    position in the frame) of the chunk-0 composite (any of its template instances; not chunk 1's
+    k_composite_q) or of the projection."""
+    name = label.split("#")[0]
+    if kernel == "composite":
+        return name.startswith("k_composite<false")
+    if kernel == "project":
+        return name.startswith("k_project<")
+    raise KeyError(kernel)
+
+
 def pmc_valu(kernel):
     """VALU wave instructions per frame of `kernel` from the committed PMC profile (SQ_INSTS_VALU)."""
-    names = {"composite": "k_composite<false>", "project": "k_project"}
     prof = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc.json")) \
         if os.path.isdir(os.path.join(ROOT, "profiles")) else []
     if not prof:
         return None
     d = json.load(open(os.path.join(ROOT, "profiles", prof[-1])))
-    tot = sum(e.get("SQ_INSTS_VALU", 0.0) for lab, e in d.items() if lab.startswith(names[kernel] + "#"))
+    tot = sum(e.get("SQ_INSTS_VALU", 0.0) for lab, e in d.items() if _is_kernel(lab, kernel))
     return tot or None
 
 
@@ -458,7 +468,9 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4),
                          "traffic": int(traffic) if traffic else None,
-                         "traffic_source": traffic_src,
+                         # (PMC counters cannot run inside the timed loop: the traffic figure is
+                         # read from the committed profile of this same command, not this run)
+                         "traffic_source": ("committed profile profiles/%s" % traffic_src) if traffic_src else None,
                          "algorithmic_bytes_per_launch": int(a_bytes),
                          "per": "frame (the kernel's launches in one frame, HIP events on the render stream)"},
             # the dominant kernel's real bound: VALU issue (PMC instruction count of this command's
@@ -467,7 +479,8 @@ def main():
                                "achieved": round(valu / (stages[dom] * 1e-3) / 1e9, 1),
                                "peak": VALU_PEAK / 1e9, "unit": "G wave-instr/s",
                                "frac": round(valu / (stages[dom] * 1e-3) / VALU_PEAK, 4),
-                               "source": traffic_src} if valu else None),
+                               "source": "committed profile profiles/%s (instruction count); "
+                                         "duration live" % traffic_src} if valu else None),
             # SURVEY §8d's byte MODEL priced at the measured frame time.  Not bytes this design moves
             # (whole partitions past the chunk threshold cost 32 B, K is replaced by the chunk-0
             # entries; the measured bytes are frame_traffic), so its ratios can exceed 1 and are not
