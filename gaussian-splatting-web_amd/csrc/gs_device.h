@@ -218,7 +218,38 @@ struct ProjParams {
     uint32_t seed_base;       // depth bucket 0 = keys from (seed_base << kSatShift): the near plane
     int seed_cx, seed_cy;     // coarse cells (kSeedCell px) across the frame / strip
     float seed_tau;           // alpha mass per pixel taken as saturation
+    // per-tile chunk-0 cut (k_part_list snapshots it): tile_sat[abs tile] = depth key at which the
+    // tile saturated in the last frame that composited it (kSentinel: unknown / not saturated),
+    // written by the composites; cut[strip tile] = this frame's bound (tile_cut_bound), nullable
+    const uint32_t* tile_sat;
+    uint16_t* cut;
+    uint32_t* cutb;           // [cut_blocks] min | max << 16 of the block's bounds
+    float cut_margin;         // depth factor (>= 1) applied to the saturation key
 };
+// Per-tile chunk-0 cut (round 6).  A chunked frame's chunk 0 holds every visible splat nearer than
+// the global threshold T (the deepest tile's saturation depth), but most tiles saturate well before
+// it (bench view: 46 % of the chunk-0 entries are reached, tools/diag/sat_position.py).  With the
+// cut, chunk 0 bins entry (tile t, splat) only when the splat's key < cut[t] << 16, cut[t] = the
+// tile's saturation key in the last frame scaled by a margin, rounded up to 16 bits (0xFFFF: no
+// cut); the entries it leaves out are binned by chunk 1 into the tiles that are still unsaturated
+// after chunk 0 (a second walk over chunk 0's units, key >= cut[t], done[t] == 0), behind every
+// entry chunk 0 blended there, so each tile still blends its whole list in (key, index) order and
+// the image does not depend on the cut.
+constexpr int kCutMaxTiles = 16384;  // frames (strips) of at most this many tiles: the band's cut
+                                     // bounds fit beside the binning's LDS counters
+// keep iff key < c << 16 (a visible splat's key is below 0x80000000, so c = 0xFFFF keeps all)
+__host__ __device__ inline bool cut_keep(uint16_t c, uint32_t key) {
+    return (key >> 16) < (uint32_t)c;
+}
+// The bounds' minimum and maximum per block of kCutBlock x kCutBlock tiles (ProjParams::cutb),
+// so binning classifies a splat from its rect's few blocks: no entry kept, every entry kept, or
+// a test per entry.
+constexpr int kCutBlock = 4;
+constexpr int kCutMaxBlocks = 2048;  // blocks of a frame with the cut at most (k_chunk1's static LDS)
+__host__ __device__ inline uint32_t cut_blocks_x(int tiles_x) { return (uint32_t)(tiles_x + kCutBlock - 1) / kCutBlock; }
+__host__ __device__ inline uint32_t cut_blocks(int tiles_x, int rows) {
+    return cut_blocks_x(tiles_x) * (uint32_t)((rows + kCutBlock - 1) / kCutBlock);
+}
 
 // Coarse depth estimate of a seeded frame: sampled Gaussians' alpha mass op * 2 pi sigma^2 by
 // 64x64-pixel cell and quarter-octave depth bucket (sat_bucket's, from the near plane)
@@ -306,6 +337,12 @@ struct BinParams {
     // k_bin_count counted per tile (sum of counts, sum of count x bin_hash(tile)); k_bin_emit
     // compares the entries it emitted with them and sets kErrBinning on a difference
     uint2* bchk;
+    // per-tile chunk-0 cut (see kCutMaxTiles), nullable: chunk 0 keeps entry (t, g) iff
+    // cut_keep(cut[t], key(g)); chunk 1 also walks chunk 0's units (cut_units, counts in the unit
+    // entries) and bins the entries chunk 0 left out into the tiles it left unsaturated
+    const uint16_t* cut;
+    const uint32_t* cutb;         // [cut_blocks(tiles_x, rows)] (ProjParams::cutb)
+    const uint32_t* cut_units;
 };
 // Binning workgroups of a chunk at most (the launches' bands of up to kBandTilesMax tiles and
 // k_chunk1's of kBandTiles): the size of BinParams::bchk.
@@ -370,6 +407,8 @@ struct CompositeParams {
     // exactly zero).  4 for frames whose tiles mostly do not saturate (small faint splats, every
     // entry walked: the sparse scene's composite 482 -> 457 us), 2 otherwise (bench frame +2.5 %)
     int bands;
+    uint32_t* tile_sat;           // nullable: [abs tile] the tile's saturation key (kSentinel: none),
+                                  // for the next frame's per-tile cut (ProjParams::tile_sat)
 };
 // Wave pairs per tile for a chunk-0 composite of n_tiles tiles on `cus` CUs (gs_opts.list_split):
 // as many as keep every tile resident at once (a SEG-pair workgroup stages SEG x 14.5 KB in LDS:

@@ -769,6 +769,25 @@ __device__ __forceinline__ bool box_tiles(const ProjParams& p, float xl, float x
     return tx0 <= tx1 && ty0 <= ty1;
 }
 
+// The per-tile cut at projection: a chunk-0 candidate whose key is at or past every cut bound of
+// the blocks its conservative box reaches has no chunk-0 entry (binning's splat_mode would drop
+// it), so it is not projected in chunk 0; chunk 1 projects it (c1_records_body) if one of those
+// tiles is still unsaturated after chunk 0.  k_cull and chunk 1 evaluate this on the same inputs
+// (the cull plane, the frame's block map snapshot), so a Gaussian lands in exactly one chunk.
+// cutb: the block map (k_cull: its LDS copy).  Boxes of more than 16 blocks are never skipped.
+__device__ __forceinline__ bool cut_skip(const ProjParams& p, const uint32_t* cutb, uint32_t key, float cx0, float cy0,
+                                         float hb) {
+    uint32_t tx0, ty0, tx1, ty1;
+    if (!box_tiles(p, cx0 - hb, cx0 + hb, cy0 - hb, cy0 + hb, tx0, ty0, tx1, ty1)) return false;
+    const uint32_t rb = (uint32_t)p.tile_row_begin, bxn = cut_blocks_x(p.tiles_x);
+    const uint32_t bx0 = tx0 / kCutBlock, bx1 = tx1 / kCutBlock, by0 = (ty0 - rb) / kCutBlock, by1 = (ty1 - rb) / kCutBlock;
+    if ((bx1 - bx0 + 1) * (by1 - by0 + 1) > 16) return false;
+    uint32_t mx = 0;
+    for (uint32_t by = by0; by <= by1; ++by)
+        for (uint32_t bx = bx0; bx <= bx1; ++bx) mx = max(mx, cutb[by * bxn + bx] >> 16);
+    return (key >> 16) >= mx;
+}
+
 // A wide splat's slot into the chunk's list (ProjParams::wlist): the shard of its partition,
 // chunk 0 from the shard region's front, chunk 1 from its back (a partition's slots of both
 // chunks fit its block, so a shard's two lists fit its region); one counter add per wave.  Every
@@ -801,7 +820,7 @@ __device__ __forceinline__ bool sat_any(const ProjParams& p, uint32_t tx0, uint3
 // chunk 0 left unsaturated?
 __device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b, uint32_t T) {
     const PartTest t = part_test(p, b);
-    if (!t.vis || t.kmax < T) return false;
+    if (!t.vis || (t.kmax < T && !p.cut)) return false;  // (with the cut, nearer splats may be chunk 1's too)
     uint32_t tx0, ty0, tx1, ty1;
     if (!t.bounded) {
         tx0 = 0;
@@ -859,7 +878,8 @@ __device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t bl
             const uint32_t i = i0 + lane;
             bool want = false;
             float vz, cx0, cy0, hb;
-            if (i < p.n && cull_keep_box(p, p.cull[i], row_lo, row_hi, vz, cx0, cy0, hb) && sortable_key(vz) >= T) {
+            if (i < p.n && cull_keep_box(p, p.cull[i], row_lo, row_hi, vz, cx0, cy0, hb) &&
+                (sortable_key(vz) >= T || (p.cut && cut_skip(p, p.cutb, sortable_key(vz), cx0, cy0, hb)))) {
                 uint32_t tx0, ty0, tx1, ty1;
                 want = box_tiles(p, cx0 - hb, cx0 + hb, cy0 - hb, cy0 + hb, tx0, ty0, tx1, ty1) &&
                        sat_any(p, tx0, ty0, tx1, ty1);
@@ -961,11 +981,40 @@ __device__ __forceinline__ uint32_t unit_at(const UnitList& L, uint32_t j) {
 // partition's chunk counts are zeroed here (k_cull sets c0 of the listed ones, chunk 1 adds to c1).
 // A ruled-out partition costs one 32-B read and one lane, and k_cull's workgroups visit only the
 // listed ones (a strip lists about an eighth of them).
+// Per-tile cut bound (see kCutMaxTiles) from a tile's last saturation key: its depth scaled by
+// the margin, just past it (exclusive), rounded up to the 16-bit bound cut_keep compares with.
+__device__ __forceinline__ uint16_t tile_cut_bound(uint32_t sat, float margin) {
+    if (sat == kSentinel) return 0xFFFFu;
+    const float v = __uint_as_float((sat & 0x80000000u) ? (sat ^ 0x80000000u) : (sat ^ 0x80000001u)) * margin;
+    if (!isfinite(v)) return 0xFFFFu;
+    const uint32_t k = sortable_key(v);
+    if (k >= 0xFFFF0000u) return 0xFFFFu;
+    return (uint16_t)(((k + 1u) + 0xFFFFu) >> 16);
+}
+
 __global__ __launch_bounds__(256) void k_part_list(ProjParams p) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t parts = proj_parts(p.n), lane = lane_id();
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p.cut) {  // this frame's per-tile cut bounds, a snapshot (the composites keep updating
+                  // tile_sat), and their minimum and maximum per block: a thread per block
+        const uint32_t tx = (uint32_t)p.tiles_x, rows = (uint32_t)(p.tile_row_end - p.tile_row_begin);
+        const uint32_t base = (uint32_t)p.tile_row_begin * tx, bxn = cut_blocks_x(p.tiles_x);
+        const uint32_t nb = cut_blocks(p.tiles_x, (int)rows);
+        for (uint32_t b = q; b < nb; b += gridDim.x * blockDim.x) {
+            const uint32_t x0 = (b % bxn) * kCutBlock, y0 = (b / bxn) * kCutBlock;
+            uint32_t mn = 0xFFFFu, mx = 0u;
+            for (uint32_t y = y0; y < min(y0 + kCutBlock, rows); ++y)
+                for (uint32_t x = x0; x < min(x0 + kCutBlock, tx); ++x) {
+                    const uint32_t c = tile_cut_bound(p.tile_sat[base + y * tx + x], p.cut_margin);
+                    p.cut[y * tx + x] = (uint16_t)c;
+                    mn = min(mn, c);
+                    mx = max(mx, c);
+                }
+            p.cutb[b] = mn | (mx << 16);
+        }
+    }
     const uint32_t T = frame_thresh(p);
     if (q == 0) p.ctl->frame_T = T;
     const bool want = q < parts && part_maybe(p, p.bounds[q], row_lo, row_hi, T);
@@ -1148,6 +1197,12 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
 #pragma unroll
         for (int it = 0; it < kProjRounds; ++it) c[it] = p.cull[min(p0 + it * kProjThreads + tid, p.n - 1u)];
     };
+    // the per-tile cut's block map (cut_skip) into LDS
+    __shared__ uint32_t s_cutb[kCutMaxBlocks];
+    if (p.cut) {
+        const uint32_t nb = cut_blocks(p.tiles_x, p.tile_row_end - p.tile_row_begin);
+        for (uint32_t b = tid; b < nb; b += kProjThreads) s_cutb[b] = p.cutb[b];
+    }
     // the workgroup's partitions (list entries blockIdx.x + k gridDim.x) into LDS at once
     __shared__ uint32_t s_part[128];
     const uint32_t nmine = nl > blockIdx.x ? (nl - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u;
@@ -1191,10 +1246,10 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
         for (int it = 0; it < kProjRounds; ++it) {
             const uint32_t i = p0 + it * kProjThreads + tid;
             bool cd = false;
-            float vz;
-            if (i < p.n && cull_keep(p, c[it], row_lo, row_hi, vz)) {
+            float vz, cx0, cy0, hb;
+            if (i < p.n && cull_keep_box(p, c[it], row_lo, row_hi, vz, cx0, cy0, hb)) {
                 const uint32_t key = sortable_key(vz);
-                cd = key < T;
+                cd = key < T && !(p.cut && cut_skip(p, s_cutb, key, cx0, cy0, hb));
                 if (!cd) {  // past the threshold: counted, not projected
                     ++my_vis;
                     my_kmin_inv = max(my_kmin_inv, ~key);
@@ -1903,12 +1958,51 @@ __device__ __forceinline__ uint32_t bin_slot(const BinParams& p, const UnitList&
     return p.chunk ? slot_c1(part, q) : slot_c0(part, q);
 }
 
-// Entries of one splat (composite slot g) in tiles [t_lo, t_hi): f(tile) per entry.  (Starting
-// each lane's walk at a lane-dependent row and column, so that neighbouring splats' LDS counter
-// atomics stop colliding, measured binning 72 -> 78 us: the collisions are cheaper than the walk.)
+// The per-tile cut filter of a binning walk (see kCutMaxTiles): s = the band's cut bounds in LDS
+// (entry t - t_lo), mode 0 = every entry (chunk 1: of the unsaturated tiles), 1 = chunk 0 with the
+// cut (cut_keep), 2 = chunk 1's walk over chunk 0's splats (the entries the cut left out, in the
+// tiles chunk 0 left unsaturated).  Count and emission filter identically.
+struct CutWalk {
+    const uint16_t* s;
+    const uint32_t* sb;  // the frame's block minima / maxima in LDS (cut_blocks)
+    uint32_t t_lo, bxn, rb;
+    int mode;
+    // per entry, with a splat's class m (splat_mode): 0 keep, 1 cut_keep, 2 cut out and the tile
+    // unsaturated, 3 the tile unsaturated
+    __device__ __forceinline__ bool keep(const BinParams& p, uint32_t t, uint32_t key, int m) const {
+        if (m == 0) return true;
+        if (m == 3) return !p.done[t];
+        const bool k = cut_keep(s[t - t_lo], key);
+        return m == 1 ? k : (!k && !p.done[t]);
+    }
+    // A splat's class from the blocks of its tile rect: -1 none of its entries passes the walk's
+    // filter, 0 (mode 1) all do, 3 (mode 2) all are cut out (then the done test only), else `mode`
+    // (a test per entry); rects of more than 16 blocks are tested per entry.
+    __device__ __forceinline__ int splat_mode(const TileRect& tr, uint32_t key) const {
+        if (mode == 0) return 0;
+        const uint32_t bx0 = tr.x0 / kCutBlock, bx1 = tr.x1 / kCutBlock;
+        const uint32_t by0 = (tr.y0 - rb) / kCutBlock, by1 = (tr.y1 - rb) / kCutBlock;
+        if ((bx1 - bx0 + 1) * (by1 - by0 + 1) > 16) return mode;
+        uint32_t mn = 0xFFFFu, mx = 0u;
+        for (uint32_t by = by0; by <= by1; ++by)
+            for (uint32_t bx = bx0; bx <= bx1; ++bx) {
+                const uint32_t v = sb[by * bxn + bx];
+                mn = min(mn, v & 0xFFFFu);
+                mx = max(mx, v >> 16);
+            }
+        const uint32_t k16 = key >> 16;
+        if (mode == 1) return k16 >= mx ? -1 : (k16 < mn ? 0 : 1);
+        return k16 < mn ? -1 : (k16 >= mx ? 3 : 2);
+    }
+};
+
+// Entries of one splat (composite slot g, depth key `key`) in tiles [t_lo, t_hi): f(tile) per
+// entry.  (Starting each lane's walk at a lane-dependent row and column, so that neighbouring
+// splats' LDS counter atomics stop colliding, measured binning 72 -> 78 us: the collisions are
+// cheaper than the walk.)
 template <class F>
 __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect& tr, const Ellipse& e,
-                                              uint32_t t_lo, uint32_t t_hi, F&& f) {
+                                              uint32_t t_lo, uint32_t t_hi, uint32_t key, const CutWalk& cw, int m, F&& f) {
     const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
     const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
     for (uint32_t ty = ya; ty <= yb; ++ty) {
@@ -1924,6 +2018,19 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
             if (t_hi <= t0) continue;
             xb = min(xb, t_hi - 1u - t0);
             uint32_t x = xa;
+            if (m) {  // (four bound reads in flight together, then the kept entries)
+                for (; x + 3u <= xb; x += 4u) {
+                    const bool k0 = cw.keep(p, t0 + x, key, m), k1 = cw.keep(p, t0 + x + 1u, key, m);
+                    const bool k2 = cw.keep(p, t0 + x + 2u, key, m), k3 = cw.keep(p, t0 + x + 3u, key, m);
+                    if (k0) f(t0 + x);
+                    if (k1) f(t0 + x + 1u);
+                    if (k2) f(t0 + x + 2u);
+                    if (k3) f(t0 + x + 3u);
+                }
+                for (; x <= xb; ++x)
+                    if (cw.keep(p, t0 + x, key, m)) f(t0 + x);
+                continue;
+            }
             for (; x + 3u <= xb; x += 4u) {
                 f(t0 + x);
                 f(t0 + x + 1u);
@@ -1946,11 +2053,12 @@ __device__ __forceinline__ void splat_entries(const BinParams& p, const TileRect
 // cells l, l + 64, ... of the splat's tile box (in the band), each testing its cell against the
 // ellipse's column range in the cell's tile row.  f(tile) per entry.
 template <class F>
-__device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uint32_t t_lo, uint32_t t_hi, F&& f,
-                                             uint32_t first = lane_id(), uint32_t step = 64u) {
+__device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uint32_t t_lo, uint32_t t_hi,
+                                             const CutWalk& cw, F&& f, uint32_t first = lane_id(), uint32_t step = 64u) {
     const uint32_t tx = (uint32_t)p.tiles_x, rb = (uint32_t)p.tile_row_begin;
     TileRect tr;
     rect_unpack(p, p.srect[g], p.sidx[g], tr);
+    const uint32_t key = cw.mode ? p.skey[g].x : 0u;
     const float4* q = p.crec + 3 * (uint64_t)g;
     const Ellipse e = ellipse_of(q[0], q[1]);
     const uint32_t ya = max(tr.y0, rb + t_lo / tx), yb = min(tr.y1, rb + (t_hi - 1) / tx);
@@ -1961,7 +2069,7 @@ __device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uin
         uint32_t xa, xb;
         if (!ellipse_row(e, ty, xa, xb) || x < xa || x > xb) continue;
         const uint32_t t = (ty - rb) * tx + x;
-        if (t < t_lo || t >= t_hi || (p.chunk == 1 && p.done[t])) continue;
+        if (t < t_lo || t >= t_hi || (p.chunk == 1 && p.done[t]) || !cw.keep(p, t, key, cw.mode)) continue;
         f(t);
     }
 }
@@ -1973,7 +2081,8 @@ constexpr uint32_t kWaveCells = 1024;  // listed wide splats of at most this man
 // walked them all itself, one wave per splat: a near view's binning took 300 us).  Count and
 // emission walk the same assignment.  f(tile) or f(tile, slot) per entry.
 template <int NT, class F>
-__device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, uint32_t t_lo, uint32_t t_hi, F&& f) {
+__device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, uint32_t t_lo, uint32_t t_hi,
+                                            const CutWalk& cw, F&& f) {
     if (!p.wlist) return;
     uint32_t pre[kWideShards + 1];  // the shards' lists, concatenated
     pre[0] = 0;
@@ -2010,9 +2119,9 @@ __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, u
             if (!big && (k++ % (NT / 64)) != w) continue;  // (wave-uniform)
             const uint32_t first = big ? threadIdx.x : lane, step = big ? (uint32_t)NT : 64u;
             if constexpr (std::is_invocable_v<F, uint32_t, uint32_t>)
-                wide_entries(p, ge, t_lo, t_hi, [&](uint32_t t) { f(t, ge); }, first, step);
+                wide_entries(p, ge, t_lo, t_hi, cw, [&](uint32_t t) { f(t, ge); }, first, step);
             else
-                wide_entries(p, ge, t_lo, t_hi, f, first, step);
+                wide_entries(p, ge, t_lo, t_hi, cw, f, first, step);
         }
     }
 }
@@ -2024,15 +2133,16 @@ __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, u
 // Records are loaded for every slot (holes included: valid memory, unused).
 template <int NT, class F>
 __device__ __forceinline__ void bin_walk(const BinParams& p, const UnitList& L, uint32_t part, const uint32_t* s_pref,
-                                         uint32_t total, F&& f) {
+                                         uint32_t total, bool with_key, F&& f) {
     struct In {
-        uint32_t g, pr, sj;
+        uint32_t g, pr, sj, key;
         float4 q0, q1;
     };
     auto fetch = [&](uint32_t r, In& s) {
         s.g = bin_slot(p, L, part, s_pref, r);
         s.pr = p.srect[s.g];
         s.sj = p.sidx[s.g];
+        s.key = with_key ? p.skey[s.g].x : 0u;
         const float4* q = p.crec + 3 * (uint64_t)s.g;
         s.q0 = q[0];
         s.q1 = q[1];
@@ -2044,7 +2154,7 @@ __device__ __forceinline__ void bin_walk(const BinParams& p, const UnitList& L, 
     auto step = [&](In& cur, In& nxt) {
         const uint32_t rn = r + NT;
         fetch(min(rn, total - 1u), nxt);  // (past the end: the last slot again, unused)
-        f(cur.g, cur.pr, cur.sj, cur.q0, cur.q1);
+        f(cur.g, cur.pr, cur.sj, cur.key, cur.q0, cur.q1);
         r = rn;
     };
     for (;;) {
@@ -2073,6 +2183,60 @@ __device__ __forceinline__ void bin_chk_add(uint32_t* s_chk, uint32_t a, uint32_
 // Binning partition / band vb: counts of its splats' entries per tile of the band -> bmat row.
 // Wide splats (>= wide_tiles box tiles) are queued in LDS (up to wide_cap) and counted by whole
 // waves, as k_bin_emit emits them.
+// One walk of a unit list (the chunk's, or in chunk 1 also chunk 0's: cw.mode 2): the entries of
+// binning partition `part`'s splats in the band added to the LDS counters.  Contains barriers.
+template <int NT, bool LISTED>
+__device__ __forceinline__ void bin_count_walk(const BinParams& p, uint32_t part, uint32_t t_lo, uint32_t t_hi,
+                                               const CutWalk& cw, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp,
+                                               uint32_t* s_wide, uint32_t& s_nw) {
+    const UnitList L = bin_unit_list(p);
+    const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
+    bin_walk<NT>(p, L, part, s_pref, total, cw.mode != 0,
+                 [&](uint32_t g, uint32_t pr, uint32_t sj, uint32_t key, float4 q0, float4 q1) {
+        TileRect tr;
+        if (!rect_unpack(p, pr, sj, tr)) return;
+        if (rect_wide(p, tr)) {
+            if (p.wlist) return;  // listed: walked below
+            const uint32_t qi = atomicAdd(&s_nw, 1u);
+            if (qi < p.wide_cap) {
+                s_wide[qi] = g;
+                return;
+            }
+        }
+        const int m = cw.splat_mode(tr, key);
+        if (m < 0) return;
+        splat_entries(p, tr, ellipse_of(q0, q1), t_lo, t_hi, key, cw, m, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
+    });
+    __syncthreads();
+    const uint32_t nq = min(s_nw, p.wide_cap);
+    for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64)  // wave-uniform
+        wide_entries(p, s_wide[qi], t_lo, t_hi, cw, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
+    wide_listed<NT>(p, part, t_lo, t_hi, cw, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
+}
+
+// Chunk 1's second walk (per-tile cut): chunk 0's units and slots, the entries chunk 0 left out.
+__device__ __forceinline__ BinParams cut_pass_params(const BinParams& p) {
+    BinParams q = p;
+    q.units = p.cut_units;
+    q.chunk = 0;
+    q.uid_lds = 0;
+    return q;
+}
+
+// The band's cut bounds into LDS (before the walks' first barrier).
+// s_cut: the band's bounds (u16), then the frame's block map (bin_lds_words reserves both).
+template <int NT>
+__device__ __forceinline__ CutWalk cut_load(const BinParams& p, uint32_t t_lo, uint32_t t_hi, uint16_t* s_cut) {
+    uint32_t* s_cutb = (uint32_t*)s_cut + (p.band_tiles + 1) / 2;
+    CutWalk cw{s_cut, s_cutb, t_lo, cut_blocks_x(p.tiles_x), (uint32_t)p.tile_row_begin, 0};
+    if (!p.cut) return cw;
+    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) s_cut[t - t_lo] = p.cut[t];
+    const uint32_t nb = cut_blocks(p.tiles_x, p.rows);
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) s_cutb[b] = p.cutb[b];
+    cw.mode = p.chunk == 0 ? 1 : 0;
+    return cw;
+}
+
 template <int NT, bool LISTED>
 __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp,
                                                uint32_t* s_wide, uint32_t* s_nw_p) {
@@ -2086,26 +2250,14 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
         s_chk[0] = 0;
         s_chk[1] = 0;
     }
-    const UnitList L = bin_unit_list(p);
-    const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
-    bin_walk<NT>(p, L, part, s_pref, total, [&](uint32_t g, uint32_t pr, uint32_t sj, float4 q0, float4 q1) {
-        TileRect tr;
-        if (!rect_unpack(p, pr, sj, tr)) return;
-        if (rect_wide(p, tr)) {
-            if (p.wlist) return;  // listed: walked below
-            const uint32_t qi = atomicAdd(&s_nw, 1u);
-            if (qi < p.wide_cap) {
-                s_wide[qi] = g;
-                return;
-            }
-        }
-        splat_entries(p, tr, ellipse_of(q0, q1), t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
-    });
-    __syncthreads();
-    const uint32_t nq = min(s_nw, p.wide_cap);
-    for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64)  // wave-uniform
-        wide_entries(p, s_wide[qi], t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
-    wide_listed<NT>(p, part, t_lo, t_hi, [&](uint32_t t) { atomicAdd(&s_cnt[t - t_lo], 1u); });
+    CutWalk cw = cut_load<NT>(p, t_lo, t_hi, (uint16_t*)(s_nw_p + 3));
+    bin_count_walk<NT, LISTED>(p, part, t_lo, t_hi, cw, s_cnt, s_pref, s_tmp, s_wide, s_nw);
+    if (p.chunk == 1 && p.cut && p.cut_units) {
+        __syncthreads();  // (every thread has read s_nw and the unit prefix of the first walk)
+        if (threadIdx.x == 0) s_nw = 0;
+        cw.mode = 2;
+        bin_count_walk<NT, true>(cut_pass_params(p), part, t_lo, t_hi, cw, s_cnt, s_pref, s_tmp, s_wide, s_nw);
+    }
     __syncthreads();
     uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     uint32_t c1 = 0, c2 = 0;
@@ -2128,8 +2280,9 @@ __device__ __forceinline__ uint32_t* bin_lds() {
     extern __shared__ uint32_t dyn_lds[];
     return dyn_lds;
 }
-__host__ __device__ inline size_t bin_lds_words(uint32_t band_tiles, uint32_t pref_words, uint32_t wide_cap) {
-    return (size_t)band_tiles + pref_words + kBinThreads / 64 + wide_cap + 3;  // (s_nw, s_chk[2])
+__host__ __device__ inline size_t bin_lds_words(uint32_t band_tiles, uint32_t pref_words, uint32_t wide_cap, uint32_t cut_nb) {
+    // (s_nw, s_chk[2], then with the per-tile cut (cut_nb blocks) the band's 16-bit bounds and the block map)
+    return (size_t)band_tiles + pref_words + kBinThreads / 64 + wide_cap + 3 + (cut_nb ? (band_tiles + 1) / 2 + cut_nb : 0);
 }
 
 template <bool LISTED>  // LISTED: chunk 0 (k_cull's unit list); else chunk 1 (every unit, counts from c1)
@@ -2259,6 +2412,60 @@ __device__ __forceinline__ void tile_scan_body(const BinParams& p, uint32_t* s_w
 }
 
 
+// One emission walk of a unit list (see bin_count_walk): each entry takes its position from the
+// tile's LDS cursor.  stats: the walk adds to the chunk's wide-splat statistics (not chunk 1's
+// second walk).
+template <int NT, bool LISTED>
+__device__ __forceinline__ void bin_emit_walk(const BinParams& p, uint32_t part, uint32_t t_lo, uint32_t t_hi,
+                                              const CutWalk& cw, bool stats, uint32_t* s_cur, uint32_t* s_pref,
+                                              uint32_t* s_tmp, uint32_t* s_wide, uint32_t& s_nw) {
+    const uint32_t cap = p.capacity;
+    const UnitList L = bin_unit_list(p);
+    const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
+    // (not bin_walk: with the slot prefetch the emission ran slower, 1.60 -> 1.68 ms at the one-chunk
+    // 50 M / 4K frame: its scattered list stores, not its slot loads, bound it)
+    for (uint32_t r = threadIdx.x; r < total; r += NT) {
+        const uint32_t g = bin_slot(p, L, part, s_pref, r);
+        TileRect tr;
+        if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
+        if (rect_wide(p, tr)) {
+            if (p.wlist) continue;  // listed: walked below
+            const uint32_t qi = atomicAdd(&s_nw, 1u);
+            if (qi < p.wide_cap) {
+                s_wide[qi] = g;
+                continue;
+            }
+        }
+        const uint32_t key = cw.mode ? p.skey[g].x : 0u;
+        const int m = cw.splat_mode(tr, key);
+        if (m < 0) continue;
+        const float4* q = p.crec + 3 * (uint64_t)g;
+        splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, key, cw, m, [&](uint32_t t) {
+            const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
+            if (pos < cap) p.tvals[pos] = g;
+        });
+    }
+
+    __syncthreads();
+    const uint32_t nq = min(s_nw, p.wide_cap);
+    if (stats) {  // (the chunk's wide splats: the LDS queues of every workgroup, the listed ones once)
+        if (threadIdx.x == 0 && s_nw) atomicAdd(&p.ctl->wide_n[p.chunk], s_nw);
+        if (p.wlist && part == 0 && t_lo == 0 && threadIdx.x < kWideShards)
+            atomicAdd(&p.ctl->wide_n[p.chunk], p.stats[threadIdx.x].wl_n[p.chunk]);
+    }
+    for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64) {  // wave-uniform
+        const uint32_t g = s_wide[qi];
+        wide_entries(p, g, t_lo, t_hi, cw, [&](uint32_t t) {
+            const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
+            if (pos < cap) p.tvals[pos] = g;
+        });
+    }
+    wide_listed<NT>(p, part, t_lo, t_hi, cw, [&](uint32_t t, uint32_t g) {
+        const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
+        if (pos < cap) p.tvals[pos] = g;
+    });
+}
+
 // Wide splats (>= wide_tiles box tiles) are queued in LDS by the thread that meets them and
 // emitted row by row by whole waves (lanes over columns); the queue holds kWideQueue splats,
 // beyond that the thread emits its splat itself.
@@ -2342,45 +2549,14 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
         s_chk[0] = 0;
         s_chk[1] = 0;
     }
-    const UnitList L = bin_unit_list(p);
-    const uint32_t total = bin_slots<NT, LISTED>(p, L, part, s_pref, s_tmp);
-    // (not bin_walk: with the slot prefetch the emission ran slower, 1.60 -> 1.68 ms at the one-chunk
-    // 50 M / 4K frame: its scattered list stores, not its slot loads, bound it)
-    for (uint32_t r = threadIdx.x; r < total; r += NT) {
-        const uint32_t g = bin_slot(p, L, part, s_pref, r);
-        TileRect tr;
-        if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
-        if (rect_wide(p, tr)) {
-            if (p.wlist) continue;  // listed: walked below
-            const uint32_t qi = atomicAdd(&s_nw, 1u);
-            if (qi < p.wide_cap) {
-                s_wide[qi] = g;
-                continue;
-            }
-        }
-        const float4* q = p.crec + 3 * (uint64_t)g;
-        splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, [&](uint32_t t) {
-            const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
-            if (pos < cap) p.tvals[pos] = g;
-        });
+    CutWalk cw = cut_load<NT>(p, t_lo, t_hi, (uint16_t*)(s_nw_p + 3));
+    bin_emit_walk<NT, LISTED>(p, part, t_lo, t_hi, cw, true, s_cur, s_pref, s_tmp, s_wide, s_nw);
+    if (p.chunk == 1 && p.cut && p.cut_units) {
+        __syncthreads();  // (every thread has read s_nw and the unit prefix of the first walk)
+        if (threadIdx.x == 0) s_nw = 0;
+        cw.mode = 2;
+        bin_emit_walk<NT, true>(cut_pass_params(p), part, t_lo, t_hi, cw, false, s_cur, s_pref, s_tmp, s_wide, s_nw);
     }
-
-    __syncthreads();
-    const uint32_t nq = min(s_nw, p.wide_cap);
-    if (threadIdx.x == 0 && s_nw) atomicAdd(&p.ctl->wide_n[p.chunk], s_nw);  // statistics
-    if (p.wlist && part == 0 && band == 0 && threadIdx.x < kWideShards)
-        atomicAdd(&p.ctl->wide_n[p.chunk], p.stats[threadIdx.x].wl_n[p.chunk]);
-    for (uint32_t qi = threadIdx.x >> 6; qi < nq; qi += NT / 64) {  // wave-uniform
-        const uint32_t g = s_wide[qi];
-        wide_entries(p, g, t_lo, t_hi, [&](uint32_t t) {
-            const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
-            if (pos < cap) p.tvals[pos] = g;
-        });
-    }
-    wide_listed<NT>(p, part, t_lo, t_hi, [&](uint32_t t, uint32_t g) {
-        const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
-        if (pos < cap) p.tvals[pos] = g;
-    });
     __syncthreads();
     // the invariant: every cursor advanced by exactly the tile's count (end - start = n_t)
     for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) {
@@ -3482,6 +3658,15 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                 for (int bb = 1; bb < kBands; ++bb) cmax = max(cmax, sN[sg][cur][h][bb][seg]);
                 const int cnt = (int)cmax;
                 const uint16_t* list = &sL[sg][cur][h][qr][seg * 64];  // this lane's band
+                // the depth key bounding where this lane's band died (the wave died at or before
+                // step k): the band's entry at k, or past its list's end the band's last entry (the
+                // lockstep lists differ: the other band's entry at k may be nearer than this band's
+                // end).  The next frame's per-tile cut relies on it being an upper bound.
+                auto sat_key = [&](uint32_t off) -> uint32_t {
+                    if (off != kNullOff) return *(const uint32_t*)(sRb + off + 44);
+                    const uint32_t nq = sN[sg][cur][h][qr][seg];
+                    return nq ? *(const uint32_t*)(sRb + list[nq - 1] + 44) : 0u;
+                };
                 int k = 0;
                 for (; k + 3 < cnt; k += 4) {  // saturation checked every 4 steps
                     const uint32_t o3 = list[k + 3];
@@ -3491,7 +3676,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                     blend(o3);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (m == 0) atomicMax(&s_sat[sg], *(const uint32_t*)(sRb + o3 + 44));
+                        if (m == 0) atomicMax(&s_sat[sg], sat_key(o3));
                         break;
                     }
                 }
@@ -3500,7 +3685,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                     blend(ok);
                     if (!__any(live0 || live1)) {
                         wave_live = false;
-                        if (m == 0) atomicMax(&s_sat[sg], *(const uint32_t*)(sRb + ok + 44));
+                        if (m == 0) atomicMax(&s_sat[sg], sat_key(ok));
                     }
                 }
             }
@@ -3578,11 +3763,16 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
     }
     const bool tile_done = !block_any<NT>(sg == 0 && (live0 || live1), s_any[2]);
     if (SEG > 1 && sg != 0) return;
-    if (tile_done && tid == 0 && range0.y > range0.x) {  // saturation statistics for the chunk controller
+    if (tid == 0) {
+        const bool sat = tile_done && range0.y > range0.x;
         const uint32_t key = SEG > 1 && nseg > 1 ? s_sat[s_qsat] : s_sat[0];
-        StatShard* sh = p.stats + tile % kStatShards;
-        atomicAdd(&sh->sat_hist[sat_bucket(key, p.sat_base)], 1u);
-        atomicMax(&sh->sat_key, key);
+        if (sat) {  // saturation statistics for the chunk controller
+            StatShard* sh = p.stats + tile % kStatShards;
+            atomicAdd(&sh->sat_hist[sat_bucket(key, p.sat_base)], 1u);
+            atomicMax(&sh->sat_key, key);
+        }
+        // the next frame's per-tile cut: the depth at which this tile saturated (none: no cut)
+        if (p.tile_sat) p.tile_sat[(uint32_t)tile + (uint32_t)p.tile_row_begin * (uint32_t)p.tiles_x] = sat ? key : kSentinel;
     }
     if (p.mode == kCompFirst) {
         if (!tile_done) {  // park the pixels for chunk 1
@@ -3832,6 +4022,8 @@ __device__ __forceinline__ void composite_q_tile(const CompositeParams& p, const
         atomicAdd(&sh->sat_hist[sat_bucket(s_sat, p.sat_base)], 1u);
         atomicMax(&sh->sat_key, s_sat);
     }
+    if (tid == 0 && p.tile_sat)  // the next frame's per-tile cut (as composite_tile)
+        p.tile_sat[(uint32_t)tile + (uint32_t)p.tile_row_begin * (uint32_t)p.tiles_x] = tile_done && n > 0 ? s_sat : kSentinel;
     if (p.mode == kCompFirst) {
         if (!tile_done) {
             if (in) p.state[pix] = make_float4(cr, cg, cb, FP16_TARGET ? ca : T);
@@ -3908,7 +4100,7 @@ __device__ __forceinline__ void grid_sync(uint32_t* bar, FrameCtl* ctl, uint64_t
     __syncthreads();
 }
 
-constexpr size_t kBinLdsWords = kBandTiles + (kBinMaxUnits + 1) + 4 + kWideQueue + 3;  // (s_nw, s_chk[2])
+constexpr size_t kBinLdsWords = kBandTiles + (kBinMaxUnits + 1) + 4 + kWideQueue + 3 + kBandTiles / 2 + kCutMaxBlocks;  // (s_nw, s_chk[2], cut)
 constexpr size_t kChunk1Lds = std::max(std::max(kBinLdsWords * 4, sizeof(TsShared)), sizeof(CompQShared));
 
 #ifdef GS_C1_TIME
@@ -4222,11 +4414,16 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
     // wide-splat queue: larger frames hold more splats that cover many tiles (near splats at 4K);
     // a splat past the queue is walked by its own thread
     // the unit entries cached in LDS beside their prefix when that leaves the minimum wide queue
-    p.uid_lds = p.units && bin_lds_words(p.band_tiles, 2 * p.pref_words, kWideQueue) <= kBinLdsMaxWords ? 1u : 0u;
+    const uint32_t cut = p.cut ? cut_blocks(p.tiles_x, p.rows) : 0u;
+    if (p.cut && (p.n_tiles > (uint32_t)kCutMaxTiles || cut > (uint32_t)kCutMaxBlocks || !p.cutb)) {
+        std::fprintf(stderr, "gsplat: per-tile cut on a frame of %u tiles (%u blocks)\n", p.n_tiles, cut);  // (the host never asks)
+        std::abort();
+    }
+    p.uid_lds = p.units && bin_lds_words(p.band_tiles, 2 * p.pref_words, kWideQueue, cut) <= kBinLdsMaxWords ? 1u : 0u;
     const uint32_t pw = p.pref_words * (p.uid_lds ? 2u : 1u);
-    const uint32_t room = (uint32_t)(kBinLdsMaxWords - bin_lds_words(p.band_tiles, pw, 0));
+    const uint32_t room = (uint32_t)(kBinLdsMaxWords - bin_lds_words(p.band_tiles, pw, 0, cut));
     p.wide_cap = p.wlist ? 0u : std::min(room, std::max(kWideQueue, std::min(kWideQueueMax, p.n_tiles / 4)));
-    const size_t lds = bin_lds_words(p.band_tiles, pw, p.wide_cap) * 4;
+    const size_t lds = bin_lds_words(p.band_tiles, pw, p.wide_cap, cut) * 4;
     const unsigned grid = kBinParts * bin_bands(p.n_tiles, p.band_tiles);
     if (!p.bchk || grid > bin_chk_words(p.n_tiles)) {
         std::fprintf(stderr, "gsplat: launch_bin without room for its %u workgroups' checksums\n", grid);

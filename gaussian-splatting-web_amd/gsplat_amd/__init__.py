@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "gs_present_device", "gs_encode_png", "gs_look_at",
     "gs_perspective", "gs_camera_position", "gs_camera_from_json", "gs_pack_uniforms", "gs_synth_aos", "gs_ply_parse",
     "gs_debug_chunk1_grid", "gs_debug_sort_pairs", "gs_debug_last_order", "gs_debug_last_records", "gs_debug_last_slots",
-    "gs_debug_tile_lists", "gs_debug_tile_list_check",
+    "gs_debug_tile_lists", "gs_debug_tile_list_check", "gs_debug_cut_margin",
 )
 
 
@@ -146,6 +146,7 @@ def lib():
         L.gs_debug_last_slots.argtypes = [P, P, P, U64, ctypes.POINTER(U64)]
         L.gs_debug_tile_lists.argtypes = [P, P, P, U64, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]
         L.gs_debug_tile_list_check.argtypes = [P, P, P]
+        L.gs_debug_cut_margin.argtypes = [P, ctypes.c_float]
         _lib = L
     return _lib
 
@@ -394,6 +395,10 @@ class Context:
         st = GsStats()
         _check(lib().gs_timings(self.handle, ctypes.byref(st)))
         return st.as_dict()
+
+    def set_cut_margin(self, margin):
+        """gs_debug_cut_margin: 0 default, < 0 per-tile cut off, > 0 its depth margin."""
+        _check(lib().gs_debug_cut_margin(self.handle, float(margin)))
 
     def timings_reset(self):
         _check(lib().gs_timings_reset(self.handle))

@@ -308,6 +308,11 @@ int gs_ply_parse(const void* ply, uint64_t bytes, gs_ply_info* info, void* out_a
  * ctx != NULL: that context's grid and measured occupancy; ctx == NULL: the grid for the given
  * occupancy (workgroups per CU) and CU count (GS_ERR_UNSUPPORTED when nothing fits). */
 int gs_debug_chunk1_grid(const gs_ctx* ctx, int occupancy, int cus, int* out_grid, int* out_occupancy);
+/* The per-tile chunk-0 cut: margin 0 = default (a still camera's chunked frames bin
+ * each tile's splats only up to its last saturation depth x 1.01), < 0 = off, > 0 = that depth
+ * margin -- below 1 every tile is cut short of its saturation point, so chunk 1 must finish the
+ * tiles with the entries chunk 0 left out (a test of that path; the image never changes). */
+int gs_debug_cut_margin(gs_ctx* ctx, float margin);
 /* Stable ascending GPU radix sort of (key,value) on bits [begin_bit,end_bit): host in/out. */
 int gs_debug_sort_pairs(gs_ctx* ctx, uint32_t* keys, uint32_t* vals, uint64_t n, int begin_bit,
                         int end_bit);

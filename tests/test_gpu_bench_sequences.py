@@ -194,6 +194,44 @@ def test_bench_cold_sequence(gpu_ctx, bench_scene):
 
 
 @pytest.mark.timeout(600)
+def test_bench_per_tile_cut(gpu_ctx, bench_scene):
+    """The per-tile chunk-0 cut: a still camera's chunked frames bin each
+    tile's splats only up to the depth at which the tile saturated in the last frame.  Off
+    (gs_debug_cut_margin < 0), default, and with a margin of 0.6 (every tile cut short of its
+    saturation point: chunk 1 must finish every tile from the entries chunk 0 left out, its second
+    walk over chunk 0's units, and the Gaussians k_cull did not project): every frame bit-identical
+    to the one-chunk render; the default binds well under the uncut entry count."""
+    aos, sc = bench_scene
+    W, H = W3, H3
+    u = gs.bench_uniforms(W, H)
+    head = gs.make_opts(out_format=gs.GS_OUT_RGBA_F16, timing=2)
+    one = _one_chunk(sc, u, W, H)
+    bufs = [gs.DeviceBuffer(W * H * 8) for _ in range(10)]
+    k0 = {}
+    try:
+        for name, margin in (("off", -1.0), ("default", 0.0), ("short", 0.6)):
+            gpu_ctx.set_cut_margin(margin)
+            _frames(sc, gpu_ctx, [u] * 6, W, H, head, bufs[:1] * 6)  # the controller's steady state
+            gpu_ctx.timings_reset()
+            imgs = _frames(sc, gpu_ctx, [u] * 10, W, H, head, bufs)
+            st = gpu_ctx.timings()
+            k0[name] = st["k_chunk0"]
+            assert st["frames_chunked"] == 10, (name, st)
+            for k, im in enumerate(imgs):
+                assert np.array_equal(_bits(im), _bits(one)), "%s cut: frame %d differs from one chunk" % (name, k)
+            if name == "short":  # chunk 1 did the work the cut left
+                assert st["tiles_unsaturated"] > 1000 and st["k_chunk1"] > 0, st
+            else:
+                assert st["tiles_unsaturated"] == 0, (name, st)
+    finally:
+        gpu_ctx.set_cut_margin(0.0)
+        for b in bufs:
+            b.free()
+    assert k0["default"] < 0.7 * k0["off"], k0
+    assert k0["short"] < k0["default"], k0
+
+
+@pytest.mark.timeout(600)
 def test_bench_tile_lists_sound(gpu_ctx, bench_scene):
     """Round-5 bug regression: cold view 3 of the bench scene rendered as one chunk
     three times in a row -- tile (26, 47)'s list had one Gaussian counted but never emitted, so one
