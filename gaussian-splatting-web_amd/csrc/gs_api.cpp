@@ -414,6 +414,7 @@ static void ensure_tiles(FrameSet& F, int n_tiles) {
     dev_alloc(F.bmat, (size_t)kBinParts * n_tiles);
     dev_alloc(F.tbase, (size_t)n_tiles);
     F.tiles_cap = n_tiles;
+    F.meta_clean = false;  // (the new checksum array is zeroed with FrameCtl)
 }
 
 static void ensure_sat(FrameSet& F, size_t words) {
@@ -793,7 +794,11 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     // and a still camera: under a moving one each tile's content (and saturation depth) shifts
     // between frames, the last frame's per-tile bounds leave tiles unsaturated and chunk 1 then
     // re-walks chunk 0 (bench orbit 2372 -> 1433 fps with the cut on moving frames)
-    const bool cut_on = two_chunks && !seeded && !quirk && !moving && n_tiles > 0 && n_tiles <= kCutMaxTiles &&
+    // and whole frames (a row strip's chunk 0 is a few hundred entries per tile after a G-fold
+    // shorter chain: the cut's classification and bound reads cost more than they save there,
+    // 50 M / 4K G = 8 strip 0.140 -> 0.153 ms, 1080p G = 8 equal)
+    const bool cut_on = two_chunks && !seeded && !quirk && !moving && fr.tb == 0 && fr.te * kTile >= H &&
+                        n_tiles > 0 && n_tiles <= kCutMaxTiles &&
                         cut_blocks(TX, tr_end - tr_begin) <= (uint32_t)kCutMaxBlocks && tile_cut_enabled() &&
                         c->cut_margin >= 0.0f;
     c->n_rendered++;
@@ -825,7 +830,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
 
     // FrameCtl is zero at a frame's start: the end of the set's last frame cleared it, unless that
     // frame never ended (first frame, an error mid-frame)
-    if (!F.meta_clean) {
+    if (!F.meta_clean) {  // (and the binning checksums: k_bin_emit zeroes them only when it ran)
+        HIPCHK(hipMemsetAsync(F.bchk, 0, (size_t)bin_chk_words((uint32_t)F.tiles_cap) * sizeof(uint2), st));
         HIPCHK(hipMemsetAsync(F.ctl, 0, sizeof(FrameCtl), st));
         HIPCHK(hipMemsetAsync(F.stats, 0, kStatShards * sizeof(StatShard), st));
         HIPCHK(hipMemsetAsync(F.bar, 0, 16, st));

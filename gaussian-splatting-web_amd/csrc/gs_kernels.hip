@@ -450,7 +450,9 @@ __device__ __forceinline__ bool project_core_g(const ProjParams& p, uint32_t i, 
     // no contraction anywhere in it: k_project (chunk 0), c1_records_body (chunk 1) and the debug
     // dump inline their own copies, and a splat's record and tile rect must not depend on which
     // copy projected it (the image is invariant under the chunk split; see the binning's ellipse)
+#ifndef GS_PROJ_CONTRACT_FAST  // (diagnostics builds only: A/B of the contraction's cost)
 #pragma clang fp contract(off)
+#endif
     o.key = kSentinel;
     o.prect = kRectEmpty;
         const float x = g0.x, y = g0.y, z = g0.z;
@@ -1004,14 +1006,23 @@ __global__ __launch_bounds__(256) void k_part_list(ProjParams p) {
         const uint32_t nb = cut_blocks(p.tiles_x, (int)rows);
         for (uint32_t b = q; b < nb; b += gridDim.x * blockDim.x) {
             const uint32_t x0 = (b % bxn) * kCutBlock, y0 = (b / bxn) * kCutBlock;
+            uint32_t sat[kCutBlock][kCutBlock];  // (the block's 16 loads in flight together)
+#pragma unroll
+            for (int y = 0; y < kCutBlock; ++y)
+#pragma unroll
+                for (int x = 0; x < kCutBlock; ++x)
+                    sat[y][x] = y0 + y < rows && x0 + x < tx ? p.tile_sat[base + (y0 + y) * tx + x0 + x] : 0u;
             uint32_t mn = 0xFFFFu, mx = 0u;
-            for (uint32_t y = y0; y < min(y0 + kCutBlock, rows); ++y)
-                for (uint32_t x = x0; x < min(x0 + kCutBlock, tx); ++x) {
-                    const uint32_t c = tile_cut_bound(p.tile_sat[base + y * tx + x], p.cut_margin);
-                    p.cut[y * tx + x] = (uint16_t)c;
-                    mn = min(mn, c);
-                    mx = max(mx, c);
-                }
+#pragma unroll
+            for (int y = 0; y < kCutBlock; ++y)
+#pragma unroll
+                for (int x = 0; x < kCutBlock; ++x)
+                    if (y0 + y < rows && x0 + x < tx) {
+                        const uint32_t c = tile_cut_bound(sat[y][x], p.cut_margin);
+                        p.cut[(y0 + y) * tx + x0 + x] = (uint16_t)c;
+                        mn = min(mn, c);
+                        mx = max(mx, c);
+                    }
             p.cutb[b] = mn | (mx << 16);
         }
     }
@@ -1167,6 +1178,7 @@ __global__ __launch_bounds__(1024) void k_seed_pick(ProjParams p) {
     }
 }
 
+template <bool CUT>  // CUT: the frame has the per-tile cut (cut_skip; else none of its code or LDS)
 __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
     __shared__ uint32_t s_vis, s_kmin_inv, s_kmax;
     __shared__ unsigned long long s_mask[kProjRounds][kProjThreads / 64];
@@ -1198,8 +1210,8 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
         for (int it = 0; it < kProjRounds; ++it) c[it] = p.cull[min(p0 + it * kProjThreads + tid, p.n - 1u)];
     };
     // the per-tile cut's block map (cut_skip) into LDS
-    __shared__ uint32_t s_cutb[kCutMaxBlocks];
-    if (p.cut) {
+    __shared__ uint32_t s_cutb[CUT ? kCutMaxBlocks : 1];
+    if (CUT) {
         const uint32_t nb = cut_blocks(p.tiles_x, p.tile_row_end - p.tile_row_begin);
         for (uint32_t b = tid; b < nb; b += kProjThreads) s_cutb[b] = p.cutb[b];
     }
@@ -1249,7 +1261,7 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
             float vz, cx0, cy0, hb;
             if (i < p.n && cull_keep_box(p, c[it], row_lo, row_hi, vz, cx0, cy0, hb)) {
                 const uint32_t key = sortable_key(vz);
-                cd = key < T && !(p.cut && cut_skip(p, s_cutb, key, cx0, cy0, hb));
+                cd = key < T && !(CUT && cut_skip(p, s_cutb, key, cx0, cy0, hb));
                 if (!cd) {  // past the threshold: counted, not projected
                     ++my_vis;
                     my_kmin_inv = max(my_kmin_inv, ~key);
@@ -2169,7 +2181,10 @@ __device__ __forceinline__ void bin_walk(const BinParams& p, const UnitList& L, 
 // the entries it emitted, both as (sum over its tiles of n_t, sum of n_t * bin_hash(t)) mod 2^32.
 // Equal sums mean equal per-tile counts unless two or more tiles differ in a way that cancels in
 // both: a net change shows in the first, one entry moved between tiles a and b in the second
-// ((a - b) * odd != 0 mod 2^32).  s_chk: two LDS words, zeroed before the walk.
+// ((a - b) * odd != 0 mod 2^32).  k_bin_count's waves add their sums straight into
+// BinParams::bchk[vb] (agent-scope atomics: no barrier at the count's end); k_bin_emit reduces its
+// own in LDS (s_chk, zeroed before the walk), compares and zeroes bchk[vb] for the next chunk (the
+// host zeroes it with FrameCtl after a frame that did not end).
 __device__ __forceinline__ uint32_t bin_hash(uint32_t t) { return t * 0x9E3779B1u + 0x7F4A7C15u; }
 __device__ __forceinline__ void bin_chk_add(uint32_t* s_chk, uint32_t a, uint32_t b) {  // whole waves
     a = wave_incl_scan(a);
@@ -2177,6 +2192,14 @@ __device__ __forceinline__ void bin_chk_add(uint32_t* s_chk, uint32_t a, uint32_
     if (lane_id() == 63) {
         atomicAdd(&s_chk[0], a);
         atomicAdd(&s_chk[1], b);
+    }
+}
+__device__ __forceinline__ void bin_chk_add_global(uint2* chk, uint32_t a, uint32_t b) {  // whole waves
+    a = wave_incl_scan(a);
+    b = wave_incl_scan(b);
+    if (lane_id() == 63 && (a | b)) {
+        atomicAdd(&chk->x, a);
+        atomicAdd(&chk->y, b);
     }
 }
 
@@ -2237,7 +2260,7 @@ __device__ __forceinline__ CutWalk cut_load(const BinParams& p, uint32_t t_lo, u
     return cw;
 }
 
-template <int NT, bool LISTED>
+template <int NT, bool LISTED, bool CUT>  // CUT: the frame has the per-tile cut (else none of its code)
 __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, uint32_t* s_cnt, uint32_t* s_pref, uint32_t* s_tmp,
                                                uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
@@ -2250,9 +2273,9 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
         s_chk[0] = 0;
         s_chk[1] = 0;
     }
-    CutWalk cw = cut_load<NT>(p, t_lo, t_hi, (uint16_t*)(s_nw_p + 3));
+    CutWalk cw = CUT ? cut_load<NT>(p, t_lo, t_hi, (uint16_t*)(s_nw_p + 3)) : CutWalk{nullptr, nullptr, 0u, 0u, 0u, 0};
     bin_count_walk<NT, LISTED>(p, part, t_lo, t_hi, cw, s_cnt, s_pref, s_tmp, s_wide, s_nw);
-    if (p.chunk == 1 && p.cut && p.cut_units) {
+    if (CUT && p.chunk == 1 && p.cut_units) {
         __syncthreads();  // (every thread has read s_nw and the unit prefix of the first walk)
         if (threadIdx.x == 0) s_nw = 0;
         cw.mode = 2;
@@ -2261,15 +2284,17 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
     __syncthreads();
     uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     uint32_t c1 = 0, c2 = 0;
+#pragma unroll 1
     for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) {
         const uint32_t c = s_cnt[t - t_lo];
         row[t] = c;
         c1 += c;
         c2 += c * bin_hash(t);
     }
-    bin_chk_add(s_chk, c1, c2);
-    __syncthreads();
-    if (threadIdx.x == 0) p.bchk[vb] = make_uint2(s_chk[0], s_chk[1]);
+#ifndef GS_NO_BIN_CHECK  // (diagnostics builds only: A/B of the invariant's cost)
+    bin_chk_add_global(p.bchk + vb, c1, c2);
+    (void)s_chk;
+#endif
 }
 
 // The binning launches size their LDS to the frame: band_tiles counters (one band up to
@@ -2285,7 +2310,7 @@ __host__ __device__ inline size_t bin_lds_words(uint32_t band_tiles, uint32_t pr
     return (size_t)band_tiles + pref_words + kBinThreads / 64 + wide_cap + 3 + (cut_nb ? (band_tiles + 1) / 2 + cut_nb : 0);
 }
 
-template <bool LISTED>  // LISTED: chunk 0 (k_cull's unit list); else chunk 1 (every unit, counts from c1)
+template <bool LISTED, bool CUT>  // LISTED: chunk 0 (k_cull's unit list); else chunk 1 (every unit, counts from c1)
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     uint32_t* s_cnt = bin_lds();
     uint32_t* s_pref = s_cnt + p.band_tiles;
@@ -2293,7 +2318,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
     uint32_t* s_wide = s_tmp + kBinThreads / 64;
     uint32_t* s_nw = s_wide + p.wide_cap;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;  // chunk 0 saturated every tile
-    bin_count_body<kBinThreads, LISTED>(p, blockIdx.x, s_cnt, s_pref, s_tmp, s_wide, s_nw);
+    bin_count_body<kBinThreads, LISTED, CUT>(p, blockIdx.x, s_cnt, s_pref, s_tmp, s_wide, s_nw);
 }
 
 // Per tile: exclusive prefix of its column of bmat over the partitions (in place) and the tile's
@@ -2474,7 +2499,7 @@ __device__ __forceinline__ void bin_emit_walk(const BinParams& p, uint32_t part,
 // band's end (the tile scan, repeated per workgroup from L2 instead of one more launch on
 // the frame's critical path); the workgroups of partition 0 write the band's ranges, the one of
 // the last band the chunk's total.  Otherwise tbase holds the list begins (tile_scan_body).
-template <int NT, bool SCAN, bool LISTED>
+template <int NT, bool SCAN, bool LISTED, bool CUT>
 __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, uint32_t* s_cur, uint32_t* s_pref, uint32_t* s_tmp,
                               uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
@@ -2484,6 +2509,10 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
     const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     const uint32_t cap = p.capacity;
     uint32_t d1 = 0, d2 = 0;  // minus the thread's start cursors (the checksum of bin_chk_add)
+    if (threadIdx.x == 0) {  // (ordered before bin_chk_add's atomics by the barriers below)
+        s_chk[0] = 0;
+        s_chk[1] = 0;
+    }
     if (SCAN) {
         constexpr int nw = NT / 64, ipt = 8;
         const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -2543,36 +2572,41 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
             d1 -= c;
             d2 -= c * bin_hash(t);
         }
+        __syncthreads();  // (s_chk zeroed)
     }
-    if (threadIdx.x == 0) {
-        s_nw = 0;
-        s_chk[0] = 0;
-        s_chk[1] = 0;
-    }
-    CutWalk cw = cut_load<NT>(p, t_lo, t_hi, (uint16_t*)(s_nw_p + 3));
+#ifndef GS_NO_BIN_CHECK
+    bin_chk_add(s_chk, d1, d2);  // the start cursors, now (not held in registers through the walk)
+#endif
+    if (threadIdx.x == 0) s_nw = 0;
+    CutWalk cw = CUT ? cut_load<NT>(p, t_lo, t_hi, (uint16_t*)(s_nw_p + 3)) : CutWalk{nullptr, nullptr, 0u, 0u, 0u, 0};
     bin_emit_walk<NT, LISTED>(p, part, t_lo, t_hi, cw, true, s_cur, s_pref, s_tmp, s_wide, s_nw);
-    if (p.chunk == 1 && p.cut && p.cut_units) {
+    if (CUT && p.chunk == 1 && p.cut_units) {
         __syncthreads();  // (every thread has read s_nw and the unit prefix of the first walk)
         if (threadIdx.x == 0) s_nw = 0;
         cw.mode = 2;
         bin_emit_walk<NT, true>(cut_pass_params(p), part, t_lo, t_hi, cw, false, s_cur, s_pref, s_tmp, s_wide, s_nw);
     }
     __syncthreads();
+#ifndef GS_NO_BIN_CHECK
     // the invariant: every cursor advanced by exactly the tile's count (end - start = n_t)
+    uint32_t e1 = 0, e2 = 0;
+#pragma unroll 1
     for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += NT) {
         const uint32_t c = s_cur[t - t_lo];
-        d1 += c;
-        d2 += c * bin_hash(t);
+        e1 += c;
+        e2 += c * bin_hash(t);
     }
-    bin_chk_add(s_chk, d1, d2);
+    bin_chk_add(s_chk, e1, e2);
+    const uint2 want = p.bchk[vb];  // (uniform: a scalar load)
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint2 want = p.bchk[vb];
         if (want.x != s_chk[0] || want.y != s_chk[1]) atomicOr(&p.ctl->err, kErrBinning);
+        p.bchk[vb] = make_uint2(0u, 0u);  // (zero for the next chunk's count)
     }
+#endif
 }
 
-template <bool LISTED>
+template <bool LISTED, bool CUT>
 __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     uint32_t* s_cur = bin_lds();
     uint32_t* s_pref = s_cur + p.band_tiles;
@@ -2580,7 +2614,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(BinParams p) {
     uint32_t* s_wide = s_tmp + kBinThreads / 64;
     uint32_t* s_nw = s_wide + p.wide_cap;
     if (p.chunk == 1 && p.ctl->not_done == 0) return;
-    bin_emit_body<kBinThreads, true, LISTED>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, s_nw);
+    bin_emit_body<kBinThreads, true, LISTED, CUT>(p, blockIdx.x, s_cur, s_pref, s_tmp, s_wide, s_nw);
 }
 
 // End of a frame: the statistic shards summed into FrameCtl (and zeroed), the saturation
@@ -4133,7 +4167,10 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     uint32_t* s_wide = s_tmp + 4;
     uint32_t* s_nw = s_wide + kWideQueue;
     const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles, c.bp.band_tiles);
-    for (uint32_t vb = b; vb < nbin; vb += G) bin_count_body<256, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
+    for (uint32_t vb = b; vb < nbin; vb += G) {
+        if (c.bp.cut) bin_count_body<256, false, true>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
+        else bin_count_body<256, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
+    }
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(4);
     const uint32_t ncol = (c.bp.n_tiles + kColTiles - 1) / kColTiles;
@@ -4143,7 +4180,10 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     if (b == 0) tile_scan_body<256>(c.bp, s_a);
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(6);
-    for (uint32_t vb = b; vb < nbin; vb += G) bin_emit_body<256, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
+    for (uint32_t vb = b; vb < nbin; vb += G) {
+        if (c.bp.cut) bin_emit_body<256, false, false, true>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
+        else bin_emit_body<256, false, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
+    }
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(7);
     // (chunk 1's tiles: the compact list when the first pass kept one, else every tile)
@@ -4359,7 +4399,10 @@ void launch_project(const ProjParams& p, hipStream_t s) {
 #endif
     hipLaunchKernelGGL(k_part_list, dim3((parts + 255) / 256), dim3(256), 0, s, p);
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(GS_CULL_GRID, parts));
-    hipLaunchKernelGGL(k_cull, dim3(grid), dim3(kProjThreads), 0, s, p);
+    if (p.cut)
+        hipLaunchKernelGGL(k_cull<true>, dim3(grid), dim3(kProjThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_cull<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
     const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(GS_PROJ_GRID, (uint64_t)parts * kProjRounds));
     if (p.shq == 12)
         hipLaunchKernelGGL(k_project<true>, dim3(ugrid), dim3(kProjThreads), 0, s, p);
@@ -4400,8 +4443,10 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
     if (p0.n_tiles == 0) return;
     static const bool lds_ok = [] {  // dynamic LDS past the default 64 KB
         const int mx = (int)(kBinLdsMaxWords * 4);
-        for (const void* f : {(const void*)k_bin_count<true>, (const void*)k_bin_count<false>,
-                              (const void*)k_bin_emit<true>, (const void*)k_bin_emit<false>})
+        for (const void* f : {(const void*)k_bin_count<true, false>, (const void*)k_bin_count<false, false>,
+                              (const void*)k_bin_emit<true, false>, (const void*)k_bin_emit<false, false>,
+                              (const void*)k_bin_count<true, true>, (const void*)k_bin_count<false, true>,
+                              (const void*)k_bin_emit<true, true>, (const void*)k_bin_emit<false, true>})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess) return false;
         return true;
     }();
@@ -4429,15 +4474,13 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
         std::fprintf(stderr, "gsplat: launch_bin without room for its %u workgroups' checksums\n", grid);
         std::abort();
     }
-    if (p.units)
-        hipLaunchKernelGGL(k_bin_count<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
-    else
-        hipLaunchKernelGGL(k_bin_count<false>, dim3(grid), dim3(kBinThreads), lds, s, p);
+    auto count = p.units ? (cut ? k_bin_count<true, true> : k_bin_count<true, false>)
+                         : (cut ? k_bin_count<false, true> : k_bin_count<false, false>);
+    hipLaunchKernelGGL(count, dim3(grid), dim3(kBinThreads), lds, s, p);
     hipLaunchKernelGGL(k_bin_colscan, dim3((p.n_tiles + kColTiles - 1) / kColTiles), dim3(512), 0, s, p);
-    if (p.units)  // each workgroup scans the tile totals itself
-        hipLaunchKernelGGL(k_bin_emit<true>, dim3(grid), dim3(kBinThreads), lds, s, p);
-    else
-        hipLaunchKernelGGL(k_bin_emit<false>, dim3(grid), dim3(kBinThreads), lds, s, p);
+    auto emit = p.units ? (cut ? k_bin_emit<true, true> : k_bin_emit<true, false>)  // (each workgroup
+                        : (cut ? k_bin_emit<false, true> : k_bin_emit<false, false>);  // scans the tile totals)
+    hipLaunchKernelGGL(emit, dim3(grid), dim3(kBinThreads), lds, s, p);
 }
 void launch_tile_sort(const TileSortParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return;

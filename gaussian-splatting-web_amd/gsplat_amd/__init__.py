@@ -145,8 +145,9 @@ def lib():
         L.gs_debug_last_records.argtypes = [P, P, P, U64]
         L.gs_debug_last_slots.argtypes = [P, P, P, U64, ctypes.POINTER(U64)]
         L.gs_debug_tile_lists.argtypes = [P, P, P, U64, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64)]
-        L.gs_debug_tile_list_check.argtypes = [P, P, P]
-        L.gs_debug_cut_margin.argtypes = [P, ctypes.c_float]
+        if hasattr(L, "gs_debug_tile_list_check"):  # (absent from older builds loaded for A/B runs via GSPLAT_LIB)
+            L.gs_debug_tile_list_check.argtypes = [P, P, P]
+            L.gs_debug_cut_margin.argtypes = [P, ctypes.c_float]
         _lib = L
     return _lib
 
