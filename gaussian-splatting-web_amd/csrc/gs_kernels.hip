@@ -1790,7 +1790,7 @@ __device__ __forceinline__ bool rect_wide(const BinParams& p, const TileRect& r)
 #define GS_BIN_NO_CONTRACT
 #endif
 struct Ellipse {
-    float cx, cy, m00, m01, det, l, hy, dys, xm, rm00;  // xm: x margin; rm00 = 1 / m00
+    float cx, cy, m00, m01, det, l, hy, dys, xm, rm00, ml;  // xm: x margin; rm00 = 1 / m00; ml = m00 l
     uint32_t px0, px1;                             // pixel box columns
     bool ok;                                       // false: use the whole box row (degenerate)
 };
@@ -1809,12 +1809,14 @@ __device__ __forceinline__ Ellipse ellipse_of(const float4 q0, const float4 q1) 
     e.cy = q0.y;
     e.px0 = bbx & 0xffffu;
     e.px1 = bbx >> 16;
-    e.m00 = ax * ax + bx * bx;
-    e.m01 = ax * ay + bx * by;
-    const float m11 = ay * ay + by * by;
-    const float da = ax * by - ay * bx;
+    // (explicit FMAs: the speed of contraction, the same bits in every inlined copy)
+    e.m00 = __builtin_fmaf(ax, ax, bx * bx);
+    e.m01 = __builtin_fmaf(ax, ay, bx * by);
+    const float m11 = __builtin_fmaf(ay, ay, by * by);
+    const float da = __builtin_fmaf(ax, by, -(ay * bx));
     e.det = da * da;
     e.l = q1.z + 7.99435343f + 2e-3f;  // log2(op) + log2(255) + margin
+    e.ml = e.m00 * e.l;
     const float rdet = frcp(e.det);
     const float hx = fsqrt(e.l * m11 * rdet);
     e.hy = fsqrt(e.l * e.m00 * rdet) * 1.0001f + 0.02f;
@@ -1841,10 +1843,10 @@ __device__ __forceinline__ bool ellipse_cols_dy(const Ellipse& e, float dy0, flo
     const float hi = fminf(dy1, e.hy);
     if (!(lo <= hi)) return false;
     const float d1 = fminf(fmaxf(e.dys, lo), hi), d0 = fminf(fmaxf(-e.dys, lo), hi);
-    const float g1 = fsqrt(fmaxf(e.m00 * e.l - e.det * d1 * d1, 0.0f));
-    const float g0 = fsqrt(fmaxf(e.m00 * e.l - e.det * d0 * d0, 0.0f));
-    const float xmax = e.cx + (g1 - e.m01 * d1) * e.rm00 + e.xm;
-    const float xmin = e.cx - (g0 + e.m01 * d0) * e.rm00 - e.xm;
+    const float g1 = fsqrt(fmaxf(__builtin_fmaf(-(e.det * d1), d1, e.ml), 0.0f));
+    const float g0 = fsqrt(fmaxf(__builtin_fmaf(-(e.det * d0), d0, e.ml), 0.0f));
+    const float xmax = __builtin_fmaf(__builtin_fmaf(-e.m01, d1, g1), e.rm00, e.cx) + e.xm;
+    const float xmin = __builtin_fmaf(-__builtin_fmaf(e.m01, d0, g0), e.rm00, e.cx) - e.xm;
     // pixel columns px with px + 0.5 in [xmin, xmax], inside the box
     const float pl = fmaxf(ceilf(xmin - 0.5f), (float)e.px0), ph = fminf(floorf(xmax - 0.5f), (float)e.px1);
     if (!(pl <= ph)) {
