@@ -18,7 +18,7 @@ def demangle_short(name):
     """k_name<template args> (llvm-cxxfilt; the namespaces and the parameter list dropped)."""
     try:
         d = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
-        d = re.sub(r"\(gs::[A-Za-z]*Params\)$", "", d.replace("(anonymous namespace)::", "").replace("gs::", ""))
+        d = re.sub(r"\([^()]*\)$", "", d.replace("(anonymous namespace)::", "").replace("gs::", ""))
         d = re.sub(r"^void ", "", d)
         if d.startswith("k_"):
             return d.replace(" ", "")
