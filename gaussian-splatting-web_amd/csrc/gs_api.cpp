@@ -269,8 +269,8 @@ struct FrameSet {
     uint32_t* cutb = nullptr;           // [kCutMaxBlocks] their minimum / maximum per block
     uint8_t* done = nullptr;
     uint32_t* c1tiles = nullptr;  // chunk 1: the tiles chunk 0 left unsaturated, compact
-    uint32_t* sat = nullptr;            // (strip rows + 1) x (tiles_x + 1), then the bitmask
-    size_t sat_cap = 0;
+    uint32_t* umask = nullptr;          // chunk 1: the unsaturated tiles' bits, strip rows x umask_words
+    size_t umask_cap = 0;
     int tiles_cap = 0;
     float4* state = nullptr;
     uint64_t state_cap = 0;
@@ -417,11 +417,11 @@ static void ensure_tiles(FrameSet& F, int n_tiles) {
     F.meta_clean = false;  // (the new checksum array is zeroed with FrameCtl)
 }
 
-static void ensure_sat(FrameSet& F, size_t words) {
-    if (words <= F.sat_cap && F.sat) return;
-    dev_free(F.sat);
-    dev_alloc(F.sat, words);
-    F.sat_cap = words;
+static void ensure_umask(FrameSet& F, size_t words) {
+    if (words <= F.umask_cap && F.umask) return;
+    dev_free(F.umask);
+    dev_alloc(F.umask, words);
+    F.umask_cap = words;
 }
 
 static void ensure_seed(FrameSet& F, size_t words) {
@@ -809,7 +809,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     if (seeded) ensure_seed(F, (size_t)seed_cx * std::max(seed_cy, 1) * kSeedBuckets);
     if (two_chunks) {
         ensure_state(F, (uint64_t)W * H);
-        ensure_sat(F, (size_t)(tr_end - tr_begin + 1) * (TX + 1) + 2 + (size_t)(tr_end - tr_begin) * ((TX + 63) / 64) * 2);
+        ensure_umask(F, (size_t)(tr_end - tr_begin) * umask_words(TX));
     }
 
     // timing 1: events between every stage; 2: around the composite only (each event record costs
@@ -886,6 +886,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.cut = cut_on ? F.cut : nullptr;
     pp.cutb = F.cutb;
     pp.cut_margin = c->cut_margin > 0.0f ? c->cut_margin : kChunkMargin;
+    pp.umask = two_chunks ? F.umask : nullptr;  // (chunk 1's rectangle tests; zeroed by k_part_list)
+    pp.umask_w = umask_words(TX);
     if (seeded) {
         pp.thresh = kNoSplit;
         pp.thresh_dev = &F.ctl->seed_T;
@@ -995,6 +997,8 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     cp.out = out;
     cp.out_f16 = o.out_format == GS_OUT_RGBA_F16;
     cp.tile_sat = s->tile_sat;
+    cp.umask = pp.umask;
+    cp.umask_w = pp.umask_w;
     const bool split = o.list_split != 0 && o.accum != GS_ACCUM_FP16_TARGET;
     // chunk 0: as many wave pairs per tile as keep every tile resident (a function of the frame's
     // size only, so a view renders the same whatever came before it)
@@ -1025,7 +1029,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
        // slot, FrameCtl zeroed for the next frame; one launch
         Chunk1Params c1{};
         c1.pp = pp;
-        c1.pp.sat = F.sat;
         c1.pp.plist = F.plist;
         c1.pp.rec_all = 0;
         c1.bp = bp;
@@ -1042,7 +1045,6 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.cp.mode = kCompSecond;
         c1.cp.order = nullptr;
         c1.cp.seg = split ? 4 : 1;  // chunk 1: a few tiles with long lists (launch_chunk1_split)
-        c1.sat = F.sat;
         c1.bar = F.bar;
         c1.spin_ticks = c->spin_ticks;
         c1.cus = c->num_cus;
@@ -1964,7 +1966,7 @@ void gs_scene_free(gs_scene* s) {
         dev_free(F.order);
         dev_free(F.done);
         dev_free(F.c1tiles);
-        dev_free(F.sat);
+        dev_free(F.umask);
         dev_free(F.state);
         dev_free(F.seedh);
         if (F.ev_early) (void)hipEventDestroy(F.ev_early);

@@ -200,9 +200,11 @@ struct ProjParams {
     // chunk 1's from the back, sharded (kWideShards); binning spreads them over all its workgroups
     uint32_t* wlist;
     uint32_t wide_tiles;      // wide_tiles(n_tiles) of the frame (strip)
-    // chunk 1: per strip tile row, prefix counts of the tiles chunk 0 left unsaturated
-    // (unsat_rows_body); rec_all: k_records dumps every visible Gaussian's record (debug)
-    const uint32_t* sat;
+    // chunk 1: the tiles chunk 0 left unsaturated as bits, umask_w words per strip tile row (bit
+    // x & 31 of word x >> 5: tile x), set by the chunk-0 composite and zeroed by k_part_list (see
+    // CompositeParams::umask); rec_all: k_records dumps every visible Gaussian's record (debug)
+    uint32_t* umask;
+    uint32_t umask_w;
     uint32_t* plist;          // [parts] chunk 1: the partitions that may hold chunk-1 splats (k_chunk1)
     uint32_t* plist0;         // [parts] chunk 0: the partitions that may hold candidates (k_part_list)
     int rec_all;
@@ -409,6 +411,10 @@ struct CompositeParams {
     int bands;
     uint32_t* tile_sat;           // nullable: [abs tile] the tile's saturation key (kSentinel: none),
                                   // for the next frame's per-tile cut (ProjParams::tile_sat)
+    // kCompFirst (nullable): the tiles left unsaturated, one bit each (ProjParams::umask), for
+    // chunk 1's rectangle tests
+    uint32_t* umask;
+    uint32_t umask_w;
 };
 // Wave pairs per tile for a chunk-0 composite of n_tiles tiles on `cus` CUs (gs_opts.list_split):
 // as many as keep every tile resident at once (a SEG-pair workgroup stages SEG x 14.5 KB in LDS:
@@ -420,11 +426,10 @@ __host__ __device__ inline int composite_seg(int n_tiles, int cus) {
 }
 
 struct Chunk1Params {
-    ProjParams pp;                // chunk-1 slots (pp.sat = the unsaturated-tile row prefixes)
+    ProjParams pp;                // chunk-1 slots (pp.umask = the unsaturated tiles)
     BinParams bp;                 // chunk 1
     TileSortParams tp;
     CompositeParams cp;           // mode kCompSecond
-    uint32_t* sat;                // unsaturated-tile row prefix counts (written by the first phase)
     uint32_t* bar;                // grid-barrier arrival counter, zero at launch (the frame's end zeroes it)
     uint64_t spin_ticks;          // grid-barrier timeout in wall-clock ticks
     int two_chunks;               // chunk 1 may have work (else only the frame's end runs)
@@ -433,10 +438,11 @@ struct Chunk1Params {
     FrameCtl* host_ctl;
     uint32_t* host_seq;
     uint32_t seq;
-    uint32_t sat_lds_words;       // k_c1_rows: dynamic LDS of the summed-area table (0: global memory)
     int cus;                      // the device's CUs (grids that stride chunk 1's compact tile list)
 };
-constexpr uint32_t kSatLdsWords = 36864;  // summed-area table of the unsaturated tiles built in LDS up to this size
+// Words per strip tile row of the unsaturated-tile bits (ProjParams::umask).
+__host__ __device__ inline uint32_t umask_words(int tiles_x) { return (uint32_t)(tiles_x + 31) / 32u; }
+constexpr uint32_t kUmaskLdsWords = 4096;  // chunk 1's launches test rectangles against an LDS copy up to this size
 
 // launchers (gs_kernels.hip)
 void launch_bbox(const uint8_t* aos, uint64_t n, uint32_t rb, uint32_t* bbox, hipStream_t s);

@@ -810,17 +810,38 @@ __device__ __forceinline__ void wide_append(const ProjParams& p, int chunk, bool
 }
 
 // Does the tile rectangle [tx0, tx1] x [ty0, ty1] (strip tile rows, absolute) hold a tile chunk 0
-// left unsaturated?  Four reads of the summed-area table (unsat_sat_body).
-__device__ __forceinline__ bool sat_any(const ProjParams& p, uint32_t tx0, uint32_t ty0, uint32_t tx1, uint32_t ty1) {
-    const uint32_t sw = (uint32_t)p.tiles_x + 1, rb = (uint32_t)p.tile_row_begin;
-    const uint32_t* a = p.sat + (uint64_t)(ty0 - rb) * sw;
-    const uint32_t* b = p.sat + (uint64_t)(ty1 + 1 - rb) * sw;
-    return (b[tx1 + 1] - b[tx0]) - (a[tx1 + 1] - a[tx0]) != 0u;
+// left unsaturated?  m: the unsaturated-tile bits (ProjParams::umask, or chunk 1's LDS copy of
+// them), a word or two per row of the rectangle.
+__device__ __forceinline__ bool unsat_any(const ProjParams& p, const uint32_t* m, uint32_t tx0, uint32_t ty0,
+                                          uint32_t tx1, uint32_t ty1) {
+    const uint32_t mw = p.umask_w, rb = (uint32_t)p.tile_row_begin, w0 = tx0 >> 5, w1 = tx1 >> 5;
+    const uint32_t lo = ~0u << (tx0 & 31u), hi = ~0u >> (31u - (tx1 & 31u));
+    for (uint32_t ty = ty0; ty <= ty1; ++ty) {
+        const uint32_t* row = m + (ty - rb) * mw;
+        if (w0 == w1) {
+            if (row[w0] & lo & hi) return true;
+            continue;
+        }
+        if ((row[w0] & lo) | (row[w1] & hi)) return true;
+        for (uint32_t w = w0 + 1; w < w1; ++w)
+            if (row[w]) return true;
+    }
+    return false;
+}
+
+// The unsaturated-tile bits into LDS (`words` of room) when they fit, else the global array;
+// contains a barrier (every thread of the workgroup calls it).
+__device__ __forceinline__ const uint32_t* umask_lds(const ProjParams& p, uint32_t* lds, uint32_t words) {
+    const uint32_t n = (uint32_t)(p.tile_row_end - p.tile_row_begin) * p.umask_w;
+    if (n > words) return p.umask;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = p.umask[i];
+    __syncthreads();
+    return lds;
 }
 
 // Can partition b hold a chunk-1 splat: a Gaussian at or past thresh whose quad may touch a tile
 // chunk 0 left unsaturated?
-__device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b, uint32_t T) {
+__device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b, uint32_t T, const uint32_t* um) {
     const PartTest t = part_test(p, b);
     if (!t.vis || (t.kmax < T && !p.cut)) return false;  // (with the cut, nearer splats may be chunk 1's too)
     uint32_t tx0, ty0, tx1, ty1;
@@ -832,11 +853,11 @@ __device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b, uint32_t 
     } else if (!box_tiles(p, t.xl, t.xh, t.yl, t.yh, tx0, ty0, tx1, ty1)) {
         return false;
     }
-    return sat_any(p, tx0, ty0, tx1, ty1);
+    return unsat_any(p, um, tx0, ty0, tx1, ty1);
 }
 
-// Chunk 1, step 1: every thread of the grid tests partitions (part_maybe_c1 against the row
-// prefix counts of the unsaturated tiles); the ones that may hold a chunk-1 splat are appended to plist (one
+// Chunk 1, step 1: every thread of the grid tests partitions (part_maybe_c1 against the
+// unsaturated-tile bits um); the ones that may hold a chunk-1 splat are appended to plist (one
 // counter add per wave; list order does not matter: a partition's chunk-1 slots are its own).
 // With block bounds (p.bbounds) the list holds 64-slot blocks instead of partitions: a partition
 // that reaches an unsaturated tile mostly does so with a few of its 16 blocks (orbit frames list
@@ -844,12 +865,12 @@ __device__ bool part_maybe_c1(const ProjParams& p, const PartBound& b, uint32_t 
 __device__ __forceinline__ uint32_t c1_items(const ProjParams& p) {
     return p.bbounds ? (uint32_t)((p.n + kCullBlock - 1) / kCullBlock) : proj_parts(p.n);
 }
-__device__ __forceinline__ void c1_parts_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
+__device__ __forceinline__ void c1_parts_body(const ProjParams& p, uint32_t blk, uint32_t nblk, const uint32_t* um) {
     const uint32_t parts = c1_items(p), lane = lane_id(), T = frame_thresh(p);
     const PartBound* bnd = p.bbounds ? p.bbounds : p.bounds;
     for (uint32_t q0 = blk * blockDim.x + (threadIdx.x & ~63u); q0 < parts; q0 += nblk * blockDim.x) {
         const uint32_t q = q0 + lane;
-        const bool want = q < parts && part_maybe_c1(p, bnd[q], T);
+        const bool want = q < parts && part_maybe_c1(p, bnd[q], T, um);
         const uint64_t b = __ballot(want);
         if (!b) continue;
         uint32_t base = 0;
@@ -866,7 +887,7 @@ __device__ __forceinline__ void c1_parts_body(const ProjParams& p, uint32_t blk,
 // thresh whose conservative box touches an unsaturated tile is projected; the visible ones whose
 // rect touches one get a chunk-1 slot (slot_c1) with their record and colour.  The filter before
 // project_core only skips Gaussians the exact rect test after it would reject.
-__device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t blk, uint32_t nblk) {
+__device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t blk, uint32_t nblk, const uint32_t* um) {
     const int row_lo = p.tile_row_begin * kTile;
     const int row_hi = min(p.tile_row_end * kTile, p.H) - 1;
     const uint32_t lane = lane_id(), nl = p.ctl->c1_parts, T = frame_thresh(p);
@@ -884,7 +905,7 @@ __device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t bl
                 (sortable_key(vz) >= T || (p.cut && cut_skip(p, p.cutb, sortable_key(vz), cx0, cy0, hb)))) {
                 uint32_t tx0, ty0, tx1, ty1;
                 want = box_tiles(p, cx0 - hb, cx0 + hb, cy0 - hb, cy0 + hb, tx0, ty0, tx1, ty1) &&
-                       sat_any(p, tx0, ty0, tx1, ty1);
+                       unsat_any(p, um, tx0, ty0, tx1, ty1);
             }
             Proj o;
             want = want && project_core(p, i, row_lo, row_hi, false, o);
@@ -893,7 +914,7 @@ __device__ __forceinline__ void c1_records_body(const ProjParams& p, uint32_t bl
                 want = pr != kRectEmpty;
                 if (want && pr != kRectLarge) {
                     const uint32_t x0 = pr & 0xfffu, y0 = (pr >> 12) & 0xfffu;
-                    want = sat_any(p, x0, y0, x0 + ((pr >> 24) & 15u), y0 + (pr >> 28));
+                    want = unsat_any(p, um, x0, y0, x0 + ((pr >> 24) & 15u), y0 + (pr >> 28));
                 }
             }
             const uint64_t b = __ballot(want);
@@ -1025,6 +1046,10 @@ __global__ __launch_bounds__(256) void k_part_list(ProjParams p) {
                     }
             p.cutb[b] = mn | (mx << 16);
         }
+    }
+    if (p.umask) {  // the unsaturated-tile bits this frame's chunk-0 composite sets
+        const uint32_t nw = (uint32_t)(p.tile_row_end - p.tile_row_begin) * p.umask_w;
+        for (uint32_t i = q; i < nw; i += gridDim.x * blockDim.x) p.umask[i] = 0u;
     }
     const uint32_t T = frame_thresh(p);
     if (q == 0) p.ctl->frame_T = T;
@@ -2710,51 +2735,6 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
     FE_MARK(4);
 }
 
-// Row prefix counts of the tiles chunk 0 left unsaturated (done == 0): row r of the strip at
-// sat[r * (tiles_x + 1)], entry x = unsaturated tiles among the row's first x.  One wave per row,
-// the rows spread over every wave of the grid (no sequential pass).
-// Summed-area table of the tiles chunk 0 left unsaturated, by one workgroup: sat[r][x] (r <=
-// rows, x <= tiles_x, row and column 0 zero) = unsaturated tiles in strip rows < r and columns <
-// x, so any tile rectangle is tested with four reads (sat_any).  Row prefixes by ballots (one
-// wave per row), then the column prefix (one wave per column, a wave scan per 64 rows), in LDS
-// when the table fits `lds_words` (1080p: 8 K words, 4K: 33 K), else in global memory.  (A per-row prefix with a loop over the rectangle's rows made
-// the partition test of chunk 1 walk up to 68 rows per partition.)
-__device__ __forceinline__ void unsat_sat_body(const uint8_t* __restrict__ done, int tiles_x, int rows,
-                                               uint32_t* __restrict__ sat, uint32_t* lds, uint32_t lds_words) {
-    const uint32_t sw = (uint32_t)tiles_x + 1, lane = lane_id(), nt = blockDim.x;
-    const uint32_t words = ((uint32_t)rows + 1) * sw;
-    const bool in_lds = words <= lds_words;
-    uint32_t* t = in_lds ? lds : sat;
-    for (uint32_t x = threadIdx.x; x < sw; x += nt) t[x] = 0;  // row 0
-    for (uint32_t r = threadIdx.x >> 6; r < (uint32_t)rows; r += nt >> 6) {
-        uint32_t* row = t + (uint64_t)(r + 1) * sw;
-        uint32_t run = 0;
-        if (lane == 0) row[0] = 0;
-        for (int x0 = 0; x0 < tiles_x; x0 += 64) {
-            const int x = x0 + (int)lane;
-            const uint32_t v = (x < tiles_x && !done[(uint64_t)r * tiles_x + x]) ? 1u : 0u;
-            const uint64_t b = __ballot(v);
-            if (x < tiles_x) row[x + 1] = run + __popcll(b & ((lanemask_lt() << 1) | 1ull));
-            run += __popcll(b);
-        }
-    }
-    __syncthreads();
-    for (uint32_t x = threadIdx.x >> 6; x < sw; x += nt >> 6) {  // column prefix: a wave per column,
-        uint32_t carry = 0;                                       // lanes over 64 rows at a time
-        for (uint32_t r0 = 1; r0 <= (uint32_t)rows; r0 += 64) {
-            const uint32_t r = r0 + lane;
-            const uint32_t v = r <= (uint32_t)rows ? t[(uint64_t)r * sw + x] : 0u;
-            const uint32_t incl = wave_incl_scan(v) + carry;
-            if (r <= (uint32_t)rows) t[(uint64_t)r * sw + x] = incl;
-            carry = (uint32_t)__shfl((int)incl, 63, 64);
-        }
-    }
-    if (in_lds) {
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < words; i += nt) sat[i] = lds[i];
-    }
-}
-
 // ============================================================================ k_tile_sort
 // One workgroup per tile orders the tile's list by key (the slot itself, or (skey.x, skey.y)),
 // ascending; keys are unique.  Lists of up to kTsCap entries are sorted in one round: 1024
@@ -3356,6 +3336,12 @@ __global__ __launch_bounds__(TsBig::NT, 2) void k_tile_sort_list(TileSortParams 
 // per-pixel state of the others; kCompSecond resumes those from the state with chunk 1's list.
 constexpr int kCompBatch = 128;
 
+// A tile chunk 0 left unsaturated, as its bit for chunk 1's rectangle tests (ProjParams::umask).
+__device__ __forceinline__ void umask_set(const CompositeParams& p, int tile) {
+    const uint32_t x = (uint32_t)(tile % p.tiles_x), y = (uint32_t)(tile / p.tiles_x);
+    atomicOr(&p.umask[y * p.umask_w + (x >> 5)], 1u << (x & 31u));
+}
+
 #if defined(GS_COMP_PHASE) && !defined(GS_COMP_TIME)
 #define GS_COMP_TIME 1
 #endif
@@ -3818,6 +3804,7 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
                 p.done[tile] = 0;
                 const uint32_t at = atomicAdd(&p.ctl->not_done, 1u);
                 if (p.c1tiles) p.c1tiles[at] = (uint32_t)tile;  // chunk 1's tile list
+                if (p.umask) umask_set(p, tile);
             }
             return;
         }
@@ -4067,6 +4054,7 @@ __device__ __forceinline__ void composite_q_tile(const CompositeParams& p, const
                 p.done[tile] = 0;
                 const uint32_t at = atomicAdd(&p.ctl->not_done, 1u);
                 if (p.c1tiles) p.c1tiles[at] = (uint32_t)tile;  // chunk 1's tile list
+                if (p.umask) umask_set(p, tile);
             }
             return;
         }
@@ -4093,8 +4081,9 @@ __global__ __launch_bounds__(256) void k_composite_q(CompositeParams p) {
 // Chunk 1 as ONE launch.  It has work only in frames where chunk 0 left a tile unsaturated, so
 // its usual cost is this launch returning at once (eight gated launches cost ~35 us of floors).
 // When it runs, it is the chunk-0 pipeline's phases in order, separated by grid barriers, on a
-// grid of one 256-thread workgroup per CU (every workgroup co-resident): row prefix counts of the unsaturated
-// tiles -> the partitions that may hold chunk-1 splats (c1_parts_body) -> their chunk-1 slots
+// grid of one 256-thread workgroup per CU (every workgroup co-resident): the partitions that may
+// hold chunk-1 splats (c1_parts_body, against the unsaturated-tile bits the chunk-0 composite
+// set) -> their chunk-1 slots
 // (c1_records_body) -> bin count -> column scan -> tile scan -> emission ->
 // per-tile sort -> composite (kCompSecond) of the unsaturated tiles.
 
@@ -4154,14 +4143,13 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     FrameCtl* ctl = c.cp.ctl;
     const uint32_t G = gridDim.x, b = blockIdx.x;
     C1_MARK(0);
-    if (b == 0) unsat_sat_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat, (uint32_t*)lds, (uint32_t)(kChunk1Lds / 4));
-    grid_sync(c.bar, ctl, c.spin_ticks);
+    const uint32_t* um = umask_lds(c.pp, (uint32_t*)lds, (uint32_t)(kChunk1Lds / 4));
     C1_MARK(1);
-    c1_parts_body(c.pp, b, G);
+    c1_parts_body(c.pp, b, G, um);
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(2);
-    c1_records_body(c.pp, b, G);
-    grid_sync(c.bar, ctl, c.spin_ticks);
+    c1_records_body(c.pp, b, G, um);
+    grid_sync(c.bar, ctl, c.spin_ticks);  // (and every wave is done with the bits in LDS)
     C1_MARK(3);
     uint32_t* s_a = (uint32_t*)lds;
     uint32_t* s_pref = s_a + kBandTiles;
@@ -4214,19 +4202,18 @@ __global__ __launch_bounds__(256) void k_chunk1(Chunk1Params c) {
 // Chunk 1 as separate launches, for frames the host expects to leave tiles unsaturated (a recent
 // frame did): the phases of chunk1_phases at full occupancy with a kernel boundary (~1.5 us) in
 // place of each grid barrier; every launch returns at once when chunk 0 saturated every tile.
-// Binning, per-tile sort and composite are the chunk-0 kernels with chunk-1 parameters.
-__global__ __launch_bounds__(1024) void k_c1_rows(Chunk1Params c) {
-    extern __shared__ uint32_t sat_lds[];
-    if (c.cp.ctl->not_done == 0) return;
-    unsat_sat_body(c.cp.done, c.bp.tiles_x, c.bp.rows, c.sat, sat_lds, c.sat_lds_words);
-}
+// Binning, per-tile sort and composite are the chunk-0 kernels with chunk-1 parameters.  The two
+// projection-side launches test rectangles against an LDS copy of the unsaturated-tile bits.
+// (dynamic LDS: the bits' words when they fit kUmaskLdsWords, else none)
 __global__ __launch_bounds__(256) void k_c1_parts(ProjParams p) {
+    extern __shared__ uint32_t s_um[];
     if (p.ctl->not_done == 0) return;
-    c1_parts_body(p, blockIdx.x, gridDim.x);
+    c1_parts_body(p, blockIdx.x, gridDim.x, umask_lds(p, s_um, kUmaskLdsWords));
 }
 __global__ __launch_bounds__(256) void k_c1_records(ProjParams p) {
+    extern __shared__ uint32_t s_um[];
     if (p.ctl->not_done == 0) return;
-    c1_records_body(p, blockIdx.x, gridDim.x);
+    c1_records_body(p, blockIdx.x, gridDim.x, umask_lds(p, s_um, kUmaskLdsWords));
 }
 __global__ __launch_bounds__(64) void k_frame_end(Chunk1Params c) {
     __shared__ uint32_t lds[kStatShards * ((sizeof(StatShard) / 4) | 1u)];
@@ -4523,16 +4510,12 @@ int chunk1_occupancy() {
 }
 void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
     if (c.two_chunks && c.cp.n_tiles > 0) {
-        static const bool lds_ok = hipFuncSetAttribute((const void*)k_c1_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)(kSatLdsWords * 4)) == hipSuccess;
-        Chunk1Params cr = c;
-        const uint32_t words = (uint32_t)(c.bp.rows + 1) * (uint32_t)(c.bp.tiles_x + 1);
-        cr.sat_lds_words = lds_ok && words <= kSatLdsWords ? words : 0u;  // else the column pass in global memory
-        hipLaunchKernelGGL(k_c1_rows, dim3(1), dim3(1024), (size_t)cr.sat_lds_words * 4, s, cr);
         const unsigned parts = proj_parts(c.pp.n);
         const unsigned items = c.pp.bbounds ? (unsigned)((c.pp.n + kCullBlock - 1) / kCullBlock) : parts;
-        hipLaunchKernelGGL(k_c1_parts, dim3(std::max(1u, (items + 255) / 256)), dim3(256), 0, s, c.pp);
-        hipLaunchKernelGGL(k_c1_records, dim3(kMaxGrid), dim3(256), 0, s, c.pp);
+        const uint32_t uw = (uint32_t)c.bp.rows * c.pp.umask_w;
+        const size_t ulds = uw <= kUmaskLdsWords ? (size_t)uw * 4 : 0;
+        hipLaunchKernelGGL(k_c1_parts, dim3(std::max(1u, (items + 255) / 256)), dim3(256), ulds, s, c.pp);
+        hipLaunchKernelGGL(k_c1_records, dim3(kMaxGrid), dim3(256), ulds, s, c.pp);
         launch_bin(c.bp, s);
         launch_tile_sort(c.tp, s);
         // the unsaturated tiles only, each with a long list: 4 waves per tile at any frame size;
