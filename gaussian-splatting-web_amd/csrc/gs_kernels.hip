@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 
 #include "gs_device.h"
 
@@ -3866,6 +3867,10 @@ struct CompQShared {
 
 template <bool FP16_TARGET>
 __device__ __forceinline__ void composite_q_tile(const CompositeParams& p, const int tile, CompQShared& S);
+#ifdef GS_CQ_TIME
+__device__ unsigned long long g_cq_time[16384][3];
+__device__ unsigned long long g_cq_phase[16384][4][4];  // per tile, wave: start clock, walk, park, barrier cycles
+#endif
 
 // Workgroup item vb -> tile: XCD-banded (through the tile order when set), or chunk 1's compact
 // list of the tiles chunk 0 left unsaturated (kCompSecond with c1tiles).
@@ -3882,7 +3887,17 @@ __device__ __forceinline__ void composite_q_body(const CompositeParams& p, uint3
         tile = p.order ? (int)p.order[j] : j;
         if (p.mode == kCompSecond && p.done[tile]) return;
     }
+#ifdef GS_CQ_TIME  // diagnostics builds only: chunk 1's composite per listed tile (tile | n << 32, start, end)
+    const unsigned long long t0 = wall_clock64();
+#endif
     composite_q_tile<FP16_TARGET>(p, tile, S);  // one inlined copy
+#ifdef GS_CQ_TIME
+    if (threadIdx.x == 0 && p.mode == kCompSecond && vb < 16384) {
+        g_cq_time[vb][0] = (unsigned long long)tile | ((unsigned long long)(p.ranges[tile].y - p.ranges[tile].x) << 32);
+        g_cq_time[vb][1] = t0;
+        g_cq_time[vb][2] = wall_clock64();
+    }
+#endif
 }
 
 template <bool FP16_TARGET>
@@ -3999,6 +4014,10 @@ __device__ __forceinline__ void composite_q_tile(const CompositeParams& p, const
             live = T >= t_min;  // (pixels off the image: T = -1)
         }
     };
+#ifdef GS_CQ_TIME
+    unsigned long long q_walk = 0, q_park = 0, q_bar = 0;
+    const unsigned long long q_start = clock64();
+#endif
     if (tid == 0) s_sat = 0;
     if (nb > 0) {
         load_slots(0);
@@ -4008,6 +4027,9 @@ __device__ __forceinline__ void composite_q_tile(const CompositeParams& p, const
     __syncthreads();
     for (uint32_t b = 0; b < nb; ++b) {
         const int cur = b & 1;
+#ifdef GS_CQ_TIME
+        const unsigned long long q_t0 = clock64();
+#endif
         if (b + 1 < nb) gather(b + 1);
         if (wave_live) {
             for (int seg = 0; seg < 4 && wave_live; ++seg) {
@@ -4036,9 +4058,29 @@ __device__ __forceinline__ void composite_q_tile(const CompositeParams& p, const
                 }
             }
         }
+#ifdef GS_CQ_TIME
+        const unsigned long long q_t1 = clock64();
+#endif
         if (b + 1 < nb) park(cur ^ 1);
-        if (!block_any<256>(wave_live, S.any[b & 1])) break;
+#ifdef GS_CQ_TIME
+        const unsigned long long q_t2 = clock64();
+#endif
+        const bool q_go = block_any<256>(wave_live, S.any[b & 1]);
+#ifdef GS_CQ_TIME
+        q_walk += q_t1 - q_t0;
+        q_park += q_t2 - q_t1;
+        q_bar += clock64() - q_t2;
+#endif
+        if (!q_go) break;
     }
+#ifdef GS_CQ_TIME
+    if (p.mode == kCompSecond && lane == 0) {  // per wave: start clock, walks, parks, barriers (shader cycles)
+        g_cq_phase[tile & 16383][qw][0] = q_start;
+        g_cq_phase[tile & 16383][qw][1] = q_walk;
+        g_cq_phase[tile & 16383][qw][2] = q_park;
+        g_cq_phase[tile & 16383][qw][3] = q_bar;
+    }
+#endif
     const bool tile_done = !block_any<256>(live, S.any[2]);
     if (tile_done && tid == 0 && n > 0) {
         StatShard* sh = p.stats + tile % kStatShards;
@@ -4177,11 +4219,15 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(7);
     // (chunk 1's tiles: the compact list when the first pass kept one, else every tile)
-    const uint32_t ntb = c.cp.c1tiles ? ctl->not_done : 8u * (((uint32_t)c.tp.n_tiles + 7u) / 8u);
-    for (uint32_t vb = b; vb < ntb; vb += G) tile_sort_body<TsBig>(c.tp, vb, *(TsShared*)lds);
-    grid_sync(c.bar, ctl, c.spin_ticks);
-    C1_MARK(8);
-    for (uint32_t vb = b; vb < ntb; vb += G) composite_q_body<FP16_TARGET>(c.cp, vb, *(CompQShared*)lds);
+    // each listed tile sorted and composited by one workgroup (c1tiles: both map item vb to the
+    // same tile; the sorted list is the workgroup's own writes)
+    const uint32_t ntb = ctl->not_done;
+    for (uint32_t vb = b; vb < ntb; vb += G) {
+        tile_sort_body<TsBig>(c.tp, vb, *(TsShared*)lds);
+        __syncthreads();
+        composite_q_body<FP16_TARGET>(c.cp, vb, *(CompQShared*)lds);
+        __syncthreads();
+    }
     grid_sync(c.bar, ctl, c.spin_ticks);
     C1_MARK(9);  // every phase done before the frame's end reads FrameCtl
 }
@@ -4214,6 +4260,21 @@ __global__ __launch_bounds__(256) void k_c1_records(ProjParams p) {
     extern __shared__ uint32_t s_um[];
     if (p.ctl->not_done == 0) return;
     c1_records_body(p, blockIdx.x, gridDim.x, umask_lds(p, s_um, kUmaskLdsWords));
+}
+// Chunk 1's per-tile sort and composite as one launch: workgroup j sorts entry j of the compact
+// list of unsaturated tiles and composites it from the list it just wrote (the tile's chain is its
+// own sort then its blend walk, not the slowest sort then the slowest walk; one launch fewer).
+union C1TileShared {
+    TsShared ts;
+    CompQShared cq;
+};
+template <bool FP16_TARGET>
+__global__ __launch_bounds__(256, 2) void k_c1_tiles(TileSortParams tp, CompositeParams cp) {
+    __shared__ C1TileShared S;
+    if (blockIdx.x >= cp.ctl->not_done) return;
+    tile_sort_body<TsBig>(tp, blockIdx.x, S.ts);
+    __syncthreads();  // (the sorted list: this workgroup's stores, through its CU's L1)
+    composite_q_body<FP16_TARGET>(cp, blockIdx.x, S.cq);
 }
 __global__ __launch_bounds__(64) void k_frame_end(Chunk1Params c) {
     __shared__ uint32_t lds[kStatShards * ((sizeof(StatShard) / 4) | 1u)];
@@ -4517,17 +4578,18 @@ void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
         hipLaunchKernelGGL(k_c1_parts, dim3(std::max(1u, (items + 255) / 256)), dim3(256), ulds, s, c.pp);
         hipLaunchKernelGGL(k_c1_records, dim3(kMaxGrid), dim3(256), ulds, s, c.pp);
         launch_bin(c.bp, s);
-        launch_tile_sort(c.tp, s);
         // the unsaturated tiles only, each with a long list: 4 waves per tile at any frame size;
         // workgroup j takes entry j of the compact tile list (c1tiles), the rest return at once
         // (list split: the 4-pair half-tile kernel, the long lists cut into segments)
         const unsigned cgrid = 8u * (unsigned)((c.cp.n_tiles + 7) / 8);
-        if (accum_fp16)
-            hipLaunchKernelGGL(k_composite_q<true>, dim3(cgrid), dim3(256), 0, s, c.cp);
-        else if (c.cp.seg > 1)
+        if (c.cp.seg > 1 && !accum_fp16) {
+            launch_tile_sort(c.tp, s);
             hipLaunchKernelGGL((k_composite_c1<false, 4>), dim3(cgrid), dim3(512), 0, s, c.cp);
-        else
-            hipLaunchKernelGGL(k_composite_q<false>, dim3(cgrid), dim3(256), 0, s, c.cp);
+        } else if (accum_fp16) {
+            hipLaunchKernelGGL(k_c1_tiles<true>, dim3(cgrid), dim3(256), 0, s, c.tp, c.cp);
+        } else {
+            hipLaunchKernelGGL(k_c1_tiles<false>, dim3(cgrid), dim3(256), 0, s, c.tp, c.cp);
+        }
     }
     hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, c);
 }
@@ -4554,6 +4616,16 @@ void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
 
 }  // namespace gs
 
+#ifdef GS_CQ_TIME
+extern "C" int gs_diag_cq_phase(unsigned long long* out) {  // out: 16384 x 4 x 4
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_cq_phase), sizeof(gs::g_cq_phase)) == hipSuccess ? 0 : -1;
+}
+extern "C" int gs_diag_cq_times(unsigned long long* out, int n) {  // out: n x 3 (read and zeroed)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_cq_time), (size_t)n * 24) != hipSuccess) return -1;
+    std::vector<unsigned long long> z((size_t)n * 3, 0ull);
+    return hipMemcpyToSymbol(HIP_SYMBOL(gs::g_cq_time), z.data(), (size_t)n * 24) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef GS_C1_TIME
 extern "C" int gs_diag_c1_times(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(gs::g_c1_time), 16 * 8) == hipSuccess ? 0 : -1;

@@ -285,7 +285,7 @@ def test_kernel_resources_no_scratch():
     # every instantiation of each per-frame kernel (names carry their template arguments)
     frame = ["k_cull<", "k_project<", "k_bin_count<", "k_bin_colscan", "k_bin_emit<", "k_tile_sort",
              "k_tile_sort_big", "k_tile_sort_huge", "k_composite<", "k_composite_q<", "k_chunk1<",
-             "k_c1_parts", "k_c1_records", "k_part_list", "k_frame_end"]
+             "k_c1_parts", "k_c1_records", "k_c1_tiles<", "k_part_list", "k_frame_end"]
     for k in frame:
         found = [n for n in res if n == k or (k.endswith("<") and n.startswith(k))]
         assert found, (k, sorted(res))
