@@ -411,7 +411,7 @@ static void ensure_tiles(FrameSet& F, int n_tiles) {
     dev_alloc(F.order, (size_t)n_tiles);
     dev_alloc(F.done, (size_t)n_tiles);
     dev_alloc(F.c1tiles, (size_t)n_tiles);
-    dev_alloc(F.bmat, (size_t)kBinParts * n_tiles);
+    dev_alloc(F.bmat, (size_t)kBmatRows * n_tiles);
     dev_alloc(F.tbase, (size_t)n_tiles);
     F.tiles_cap = n_tiles;
     F.meta_clean = false;  // (the new checksum array is zeroed with FrameCtl)
@@ -656,6 +656,16 @@ static double seed_tau() {
         return x > 0.0 ? x : 9.21;
     }();
     return v;
+}
+// Binning partitions (A/B runs: GS_NPARTS_MOVE, GS_NPARTS_C1 = 128 or 256)
+static uint32_t env_nparts(const char* name, uint32_t dflt) {
+    const char* e = std::getenv(name);
+    const uint32_t v = e ? (uint32_t)std::atoi(e) : dflt;
+    return v == kBinPartsSmall || v == (uint32_t)kBinParts ? v : dflt;
+}
+// ... each partition holding at most kBinMaxUnits of the frame's units (else kBinParts)
+static uint32_t fit_nparts(uint32_t parts, uint32_t want) {
+    return (uint64_t)parts * kProjRounds <= (uint64_t)kBinMaxUnits * want ? want : (uint32_t)kBinParts;
 }
 // Per-tile chunk-0 cut (kCutMaxTiles; GS_TILE_CUT=0 turns it off, for A/B runs)
 static bool tile_cut_enabled() {
@@ -939,6 +949,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     bp.bmat = F.bmat;
     bp.tbase = F.tbase;
     bp.bchk = F.bchk;
+    // binning partitions: fewer under a moving camera and in chunk 1.  A moving frame is bound by
+    // the caller's stream (chunk 0's composite, then chunk 1's chain); its chunk-0 binning runs
+    // beside the previous frame's, and 128 workgroups of it leave that more of the device, while
+    // chunk 1's few entries cost the per-partition work over every tile, not the walk.  Orbit
+    // (tools/ab_env.sh, two runs each): 256 / 256 2431-2434 fps, 128 / 256 2460-2463, 256 / 128
+    // 2414-2420, 128 / 128 2528-2533.  A still frame's chunk-0 binning is slower with 128 (85 ->
+    // 111 us, bench 3507 -> 3434-3456 fps), so it keeps 256.
+    bp.nparts = fit_nparts(bp.parts, moving ? env_nparts("GS_NPARTS_MOVE", kBinPartsSmall) : (uint32_t)kBinParts);
     bp.cut = cut_on ? F.cut : nullptr;
     bp.cutb = F.cutb;
     bp.tvals = F.tvA;
@@ -956,7 +974,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     tsp.out = F.tvB;
     tsp.skey = F.skey;
     tsp.done = nullptr;
-    tsp.scratch = F.bmat;  // kBinParts (256) words per tile, dead once the emission has read them
+    tsp.scratch = F.bmat;  // kBmatRows (>= 256) words per tile, dead once the emission has read them
     tsp.n_tiles = n_tiles;
     {  // lists of more than kTsBigMean entries on average (last frame; the 128-thread shape sorts rounds of 1024): most
        // tiles would take the multi-round path (each round re-reads the whole list), so the
@@ -1036,6 +1054,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         c1.bp.units = nullptr;  // chunk 1: every unit
         c1.bp.cut_units = cut_on ? F.units : nullptr;  // ... and chunk 0's again for the entries the cut left out
         c1.bp.chunk = 1;
+        c1.bp.nparts = fit_nparts(c1.bp.parts, env_nparts("GS_NPARTS_C1", kBinPartsSmall));
         c1.bp.order = nullptr;
         c1.tp = tsp;
         c1.tp.done = F.done;

@@ -23,7 +23,14 @@ constexpr float kCullFaint = -1.0f;   // cull plane w of a Gaussian whose opacit
 constexpr int kUnitShards = 8;        // the frame's work-unit list, sharded (FrameCtl::unit_n)
 constexpr int kSortTile = kSortThreads * kSortIPT;  // 4096 elements per radix partition
 constexpr int kBinThreads = 1024;     // binning workgroup (one partition of the chunk's ranks)
-constexpr int kBinParts = 256;        // binning partitions per chunk (rows of BinParams::bmat)
+#ifndef GS_BIN_PARTS
+#define GS_BIN_PARTS 256
+#endif
+constexpr int kBinParts = GS_BIN_PARTS;  // binning partitions per chunk (rows of BinParams::bmat)
+constexpr uint32_t kBinPartsSmall = 128;  // moving frames' and chunk 1's binning partitions (BinParams::nparts)
+constexpr uint32_t kBinMaxUnits = 4096;   // units per binning partition (scenes up to 2^28 Gaussians at kBinParts)
+constexpr int kBmatRows = kBinParts > 256 ? kBinParts : 256;  // bmat rows: binning partitions, and the
+                                                              // per-tile sort's long-list scratch (256 per tile)
 constexpr int kBandTiles = 8192;      // tiles per binning band inside k_chunk1 (static LDS)
 constexpr int kBandTilesMax = 36000;  // largest band of the binning launches (dynamic LDS)
 constexpr int kHistShards = 8;        // global histograms sharded by blockIdx % 8 (XCD group)
@@ -345,6 +352,9 @@ struct BinParams {
     const uint16_t* cut;
     const uint32_t* cutb;         // [cut_blocks(tiles_x, rows)] (ProjParams::cutb)
     const uint32_t* cut_units;
+    // binning partitions of this chunk: kBinParts, or kBinPartsSmall for chunk 1 and for chunk 0
+    // under a moving camera (render_frame; each holds at most kBinMaxUnits units)
+    uint32_t nparts;
 };
 // Binning workgroups of a chunk at most (the launches' bands of up to kBandTilesMax tiles and
 // k_chunk1's of kBandTiles): the size of BinParams::bchk.

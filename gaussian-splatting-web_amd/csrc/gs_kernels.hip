@@ -1907,7 +1907,7 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
 
 // ---- binning into per-tile lists, a two-level counting sort without global atomics.  The
 // chunk's slots come in units of (projection partition, round of kProjThreads slots); binning
-// partition b (of kBinParts) takes units b, b + kBinParts, ... (interleaved: balanced whatever
+// partition b (of BinParams::nparts) takes units b, b + nparts, ... (interleaved: balanced whatever
 // the scene order, also when a few partitions hold all the splats); the tiles are cut into bands
 // of <= kBandTiles.
 //   k_bin_count    workgroup (partition b, band): LDS counters of its splats' entries per tile
@@ -1918,7 +1918,6 @@ __device__ __forceinline__ bool ellipse_row(const Ellipse& e, uint32_t ty, uint3
 //   k_bin_emit     workgroup (b, band): LDS cursors tbase[t] + bmat[b][t]; each entry takes a
 //                  position with an LDS atomic (lists are unordered inside a tile: k_tile_sort)
 // Count and emission walk the same ellipse rows, so a tile's count and its entries agree.
-constexpr uint32_t kBinMaxUnits = 4096;  // units per binning partition (scenes up to 2^28 Gaussians)
 constexpr uint32_t kWideQueue = 512;     // wide splats queued per binning workgroup (k_chunk1)
 constexpr uint32_t kWideQueueMax = 8192; // ... and at most, in the binning launches
 constexpr size_t kBinLdsMaxWords = 40448; // 158 KiB: the binning launches' dynamic LDS bound
@@ -1932,17 +1931,17 @@ __device__ __forceinline__ UnitList bin_unit_list(const BinParams& p) {
     return L;
 }
 
-__device__ __forceinline__ uint32_t bin_units(const UnitList& L, uint32_t b) {
-    return L.total > b ? (L.total - b + kBinParts - 1) / kBinParts : 0u;
+__device__ __forceinline__ uint32_t bin_units(const UnitList& L, uint32_t b, uint32_t np) {
+    return L.total > b ? (L.total - b + np - 1) / np : 0u;
 }
 
-// The slots of binning partition b (units b, b + kBinParts, ... of the chunk's list):
+// The slots of binning partition b (units b, b + nparts, ... of the chunk's list):
 // s_pref[k] = slots of its first k units; returns the total.  Contains barriers.
 // LISTED: the chunk's units come from k_cull's list, counts packed in the entries (chunk 0);
 // otherwise every unit of every partition, counts from p.cnt (chunk 1)
 template <int NT, bool LISTED>
 __device__ uint32_t bin_slots(const BinParams& p, const UnitList& L, uint32_t b, uint32_t* s_pref, uint32_t* s_tmp) {
-    const uint32_t m = min(bin_units(L, b), kBinMaxUnits);
+    const uint32_t m = min(bin_units(L, b, p.nparts), kBinMaxUnits);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     constexpr int per = kBinMaxUnits / NT;
     uint32_t* s_uid = LISTED && p.uid_lds ? s_pref + p.pref_words : nullptr;  // (bin_slot reads them)
@@ -1952,7 +1951,7 @@ __device__ uint32_t bin_slots(const BinParams& p, const UnitList& L, uint32_t b,
         const uint32_t j = (uint32_t)tid * per + k;
         c[k] = 0;
         if (j < m) {
-            const uint32_t u = unit_at(L, b + j * kBinParts);
+            const uint32_t u = unit_at(L, b + j * p.nparts);
             if (LISTED) {
                 c[k] = unit_count(u);
                 if (s_uid) s_uid[j] = u;
@@ -1985,14 +1984,14 @@ __device__ uint32_t bin_slots(const BinParams& p, const UnitList& L, uint32_t b,
 // The r-th slot of binning partition b (r < total of bin_slots).
 __device__ __forceinline__ uint32_t bin_slot(const BinParams& p, const UnitList& L, uint32_t b,
                                              const uint32_t* s_pref, uint32_t r) {
-    const uint32_t m = min(bin_units(L, b), kBinMaxUnits);
+    const uint32_t m = min(bin_units(L, b, p.nparts), kBinMaxUnits);
     uint32_t lo = 0, hi = m;  // largest k < m with s_pref[k] <= r
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (s_pref[mid] <= r) lo = mid; else hi = mid;
     }
     // (the unit entry from LDS when bin_slots cached it: no global round trip per slot)
-    const uint32_t u = unit_id(p.uid_lds && L.units ? s_pref[p.pref_words + lo] : unit_at(L, b + lo * kBinParts)),
+    const uint32_t u = unit_id(p.uid_lds && L.units ? s_pref[p.pref_words + lo] : unit_at(L, b + lo * p.nparts)),
                    part = u / kProjRounds;
     const uint32_t q = (u % kProjRounds) * kProjThreads + (r - s_pref[lo]);
     return p.chunk ? slot_c1(part, q) : slot_c0(part, q);
@@ -2116,7 +2115,7 @@ __device__ __forceinline__ void wide_entries(const BinParams& p, uint32_t g, uin
 
 constexpr uint32_t kWaveCells = 1024;  // listed wide splats of at most this many box tiles: one wave
 // The chunk's listed wide splats (BinParams::wlist) that binning partition `part` walks: list
-// entries part, part + kBinParts, ..., each by the whole workgroup (threads over the splat's tile
+// entries part, part + nparts, ..., each by the whole workgroup (threads over the splat's tile
 // cells), so the wide splats spread over every workgroup (a partition that held many of them
 // walked them all itself, one wave per splat: a near view's binning took 300 us).  Count and
 // emission walk the same assignment.  f(tile) or f(tile, slot) per entry.
@@ -2131,14 +2130,15 @@ __device__ __forceinline__ void wide_listed(const BinParams& p, uint32_t part, u
     for (uint32_t k = 0; k < kWideShards; ++k) pre[k + 1] = pre[k] + min(p.stats[k].wl_n[p.chunk], cap);
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     const uint32_t wn = pre[kWideShards];
-    const uint32_t share = wn > part ? (wn - part + kBinParts - 1) / kBinParts : 0u;  // entries part + i kBinParts
+    const uint32_t np = p.nparts;
+    const uint32_t share = wn > part ? (wn - part + np - 1) / np : 0u;  // entries part + i nparts
     uint32_t k = 0;  // the workgroup's entries in turn: a splat of at most kWaveCells tile cells goes
                      // to one wave (round-robin), a larger one to every thread of the workgroup
     for (uint32_t i0 = 0; i0 < share; i0 += 64) {
         // 64 entries' slots and tile counts loaded at once (one lane each), then broadcast
         uint32_t g = 0, cells = 0;
         if (i0 + lane < share) {
-            const uint32_t j = part + (i0 + lane) * kBinParts;
+            const uint32_t j = part + (i0 + lane) * np;
             uint32_t sh = 0, base = 0;  // (selects, not an indexed array: no scratch)
 #pragma unroll
             for (uint32_t k = 1; k < kWideShards; ++k)
@@ -2293,7 +2293,7 @@ __device__ __forceinline__ void bin_count_body(const BinParams& p, uint32_t vb, 
                                                uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
     uint32_t* s_chk = s_nw_p + 1;
-    const uint32_t part = vb % kBinParts, band = vb / kBinParts;
+    const uint32_t part = vb % p.nparts, band = vb / p.nparts;
     const uint32_t t_lo = band * p.band_tiles, t_hi = min(p.n_tiles, t_lo + p.band_tiles);
     for (uint32_t t = threadIdx.x; t < t_hi - t_lo; t += NT) s_cnt[t] = 0;
     if (threadIdx.x == 0) {
@@ -2351,26 +2351,27 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(BinParams p) {
 
 // Per tile: exclusive prefix of its column of bmat over the partitions (in place) and the tile's
 // total into tbase.  The prefix runs XCD-major: partition p is emitted by workgroup p (and
-// p + kBinParts ...) on XCD p % 8, so ordering the partitions (p % 8, p / 8) gives every XCD one
+// p + nparts ...) on XCD p % 8, so ordering the partitions (p % 8, p / 8) gives every XCD one
 // contiguous sub-range of each tile's list and its L2 merges the scattered 4-B stores into whole
 // lines.  Workgroup = 64 tiles x NW waves; wave w sums ordered partitions [w R, w R + R),
-// R = kBinParts / NW (k_bin_colscan: 8 waves of 32 rows; k_chunk1's 256-thread phase: 4 of 64).
+// R = nparts / NW (k_bin_colscan: 8 waves of 32 or 16 rows; k_chunk1's 256-thread phase: 4 of 64 or 32).
 constexpr int kColTiles = 64;
-static_assert(kBinParts % 8 == 0, "binning partitions must split evenly over the 8 XCDs");
-__device__ __forceinline__ uint32_t colscan_part(uint32_t q) {  // q-th partition in XCD-major order
-    return (q % (kBinParts / 8)) * 8 + q / (kBinParts / 8);
+static_assert(kBinParts % 64 == 0 && kBinPartsSmall % 64 == 0, "binning partitions split evenly over the 8 XCDs and the column waves");
+template <uint32_t NP>
+__device__ __forceinline__ uint32_t colscan_part(uint32_t q) {  // q-th of NP partitions in XCD-major order
+    return (q % (NP / 8)) * 8 + q / (NP / 8);
 }
 
-template <int NW>
-__device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, uint32_t (*s_sum)[kColTiles]) {
-    constexpr int kColRows = kBinParts / NW;
+template <int NW, uint32_t NP>
+__device__ __forceinline__ void colscan_rows(const BinParams& p, uint32_t vb, uint32_t (*s_sum)[kColTiles]) {
+    constexpr int kColRows = (int)NP / NW;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t = vb * kColTiles + lane;
     const bool ok = t < p.n_tiles;
     uint32_t v[kColRows], sum = 0;
 #pragma unroll
     for (int k = 0; k < kColRows; ++k) {
-        v[k] = ok ? p.bmat[(uint64_t)colscan_part(w * kColRows + k) * p.n_tiles + t] : 0u;
+        v[k] = ok ? p.bmat[(uint64_t)colscan_part<NP>(w * kColRows + k) * p.n_tiles + t] : 0u;
         sum += v[k];
     }
     s_sum[w][lane] = sum;
@@ -2380,7 +2381,7 @@ __device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, ui
     if (ok) {
 #pragma unroll
         for (int k = 0; k < kColRows; ++k) {
-            p.bmat[(uint64_t)colscan_part(w * kColRows + k) * p.n_tiles + t] = run;
+            p.bmat[(uint64_t)colscan_part<NP>(w * kColRows + k) * p.n_tiles + t] = run;
             run += v[k];
         }
         if (w == NW - 1) p.tbase[t] = run;
@@ -2411,6 +2412,12 @@ __device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, ui
         }
     }
     __syncthreads();
+}
+
+template <int NW>
+__device__ __forceinline__ void colscan_body(const BinParams& p, uint32_t vb, uint32_t (*s_sum)[kColTiles]) {
+    if (p.nparts == kBinPartsSmall) colscan_rows<NW, kBinPartsSmall>(p, vb, s_sum);
+    else colscan_rows<NW, kBinParts>(p, vb, s_sum);
 }
 
 __global__ __launch_bounds__(512) void k_bin_colscan(BinParams p) {
@@ -2532,7 +2539,7 @@ __device__ __forceinline__ void bin_emit_body(const BinParams& p, uint32_t vb, u
                               uint32_t* s_wide, uint32_t* s_nw_p) {
     uint32_t& s_nw = *s_nw_p;
     uint32_t* s_chk = s_nw_p + 1;
-    const uint32_t part = vb % kBinParts, band = vb / kBinParts;
+    const uint32_t part = vb % p.nparts, band = vb / p.nparts;
     const uint32_t t_lo = band * p.band_tiles, t_hi = min(p.n_tiles, t_lo + p.band_tiles);
     const uint32_t* row = p.bmat + (uint64_t)part * p.n_tiles;
     const uint32_t cap = p.capacity;
@@ -3084,6 +3091,7 @@ __device__ void ts_rounds(const TileSortParams& p, TsSharedT<C>& S, const uint32
 // Four reads of the list and its keys per entry, one write of the scatter and one of the sort.
 constexpr int kTsLongBB = 8;
 constexpr uint32_t kTsLongBuckets = 1u << kTsLongBB;
+static_assert(kTsLongBuckets <= (uint32_t)kBmatRows, "the long-list scratch is the binning matrix (kBmatRows per tile)");
 __device__ __forceinline__ unsigned long long uniform64(unsigned long long x) {
     return ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
@@ -4198,7 +4206,7 @@ __device__ __forceinline__ void chunk1_phases(const Chunk1Params& c, uint8_t* ld
     uint32_t* s_tmp = s_pref + kBinMaxUnits + 1;
     uint32_t* s_wide = s_tmp + 4;
     uint32_t* s_nw = s_wide + kWideQueue;
-    const uint32_t nbin = kBinParts * bin_bands(c.bp.n_tiles, c.bp.band_tiles);
+    const uint32_t nbin = c.bp.nparts * bin_bands(c.bp.n_tiles, c.bp.band_tiles);
     for (uint32_t vb = b; vb < nbin; vb += G) {
         if (c.bp.cut) bin_count_body<256, false, true>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
         else bin_count_body<256, false, false>(c.bp, vb, s_a, s_pref, s_tmp, s_wide, s_nw);
@@ -4502,10 +4510,15 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
     }();
     (void)lds_ok;
     BinParams p = p0;
+    if ((p.nparts != (uint32_t)kBinParts && p.nparts != kBinPartsSmall) ||
+        (uint64_t)p.parts * kProjRounds > (uint64_t)kBinMaxUnits * p.nparts) {
+        std::fprintf(stderr, "gsplat: launch_bin with %u binning partitions for %u units\n", p.nparts, p.parts * (uint32_t)kProjRounds);
+        std::abort();  // (the host never asks)
+    }
     const uint32_t bands = (p.n_tiles + kBandTilesMax - 1) / kBandTilesMax;
     p.band_tiles = (p.n_tiles + bands - 1) / bands;  // equal bands
-    // units of one binning partition: at most ceil(all units / kBinParts)
-    p.pref_words = std::min<uint32_t>(kBinMaxUnits, (p.parts * (uint32_t)kProjRounds + kBinParts - 1) / kBinParts) + 1;
+    // units of one binning partition: at most ceil(all units / nparts)
+    p.pref_words = std::min<uint32_t>(kBinMaxUnits, (p.parts * (uint32_t)kProjRounds + p.nparts - 1) / p.nparts) + 1;
     // wide-splat queue: larger frames hold more splats that cover many tiles (near splats at 4K);
     // a splat past the queue is walked by its own thread
     // the unit entries cached in LDS beside their prefix when that leaves the minimum wide queue
@@ -4519,7 +4532,7 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
     const uint32_t room = (uint32_t)(kBinLdsMaxWords - bin_lds_words(p.band_tiles, pw, 0, cut));
     p.wide_cap = p.wlist ? 0u : std::min(room, std::max(kWideQueue, std::min(kWideQueueMax, p.n_tiles / 4)));
     const size_t lds = bin_lds_words(p.band_tiles, pw, p.wide_cap, cut) * 4;
-    const unsigned grid = kBinParts * bin_bands(p.n_tiles, p.band_tiles);
+    const unsigned grid = p.nparts * bin_bands(p.n_tiles, p.band_tiles);
     if (!p.bchk || grid > bin_chk_words(p.n_tiles)) {
         std::fprintf(stderr, "gsplat: launch_bin without room for its %u workgroups' checksums\n", grid);
         std::abort();
