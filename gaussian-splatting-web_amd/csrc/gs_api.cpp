@@ -898,6 +898,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.cut_margin = c->cut_margin > 0.0f ? c->cut_margin : kChunkMargin;
     pp.umask = two_chunks ? F.umask : nullptr;  // (chunk 1's rectangle tests; zeroed by k_part_list)
     pp.umask_w = umask_words(TX);
+    // k_cull on 512 workgroups when the camera moves (the default 2048 otherwise): cold frames (a
+    // camera cut every frame) 2690-2696 -> 2767-2779 fps, 1024: 2755; orbit unchanged (2538-2545);
+    // k_project's grid at 768 made the orbit slower (2526-2530).  GS_CULL_GRID_MOVE overrides (A/B).
+    static const uint32_t cull_grid_move = [] {
+        const char* e = std::getenv("GS_CULL_GRID_MOVE");
+        return e ? (uint32_t)std::atoi(e) : 512u;
+    }();
+    pp.cull_grid = moving ? cull_grid_move : 0u;
     if (seeded) {
         pp.thresh = kNoSplit;
         pp.thresh_dev = &F.ctl->seed_T;

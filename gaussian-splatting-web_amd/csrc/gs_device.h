@@ -234,6 +234,7 @@ struct ProjParams {
     uint16_t* cut;
     uint32_t* cutb;           // [cut_blocks] min | max << 16 of the block's bounds
     float cut_margin;         // depth factor (>= 1) applied to the saturation key
+    uint32_t cull_grid, proj_grid;  // k_cull / k_project grids (0: the defaults)
 };
 // Per-tile chunk-0 cut (round 6).  A chunked frame's chunk 0 holds every visible splat nearer than
 // the global threshold T (the deepest tile's saturation depth), but most tiles saturate well before

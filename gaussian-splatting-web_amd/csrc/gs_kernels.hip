@@ -4456,12 +4456,14 @@ void launch_project(const ProjParams& p, hipStream_t s) {
 #define GS_PROJ_GRID 1536
 #endif
     hipLaunchKernelGGL(k_part_list, dim3((parts + 255) / 256), dim3(256), 0, s, p);
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(GS_CULL_GRID, parts));
+    const uint64_t cg = p.cull_grid && p.cull_grid % kUnitShards == 0 ? p.cull_grid : GS_CULL_GRID;  // (a multiple of kUnitShards)
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(cg, parts));
     if (p.cut)
         hipLaunchKernelGGL(k_cull<true>, dim3(grid), dim3(kProjThreads), 0, s, p);
     else
         hipLaunchKernelGGL(k_cull<false>, dim3(grid), dim3(kProjThreads), 0, s, p);
-    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(GS_PROJ_GRID, (uint64_t)parts * kProjRounds));
+    const uint64_t pg = p.proj_grid ? p.proj_grid : GS_PROJ_GRID;
+    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(pg, (uint64_t)parts * kProjRounds));
     if (p.shq == 12)
         hipLaunchKernelGGL(k_project<true>, dim3(ugrid), dim3(kProjThreads), 0, s, p);
     else
