@@ -657,6 +657,10 @@ static double seed_tau() {
     }();
     return v;
 }
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* e = std::getenv(name);
+    return e ? (uint32_t)std::atoi(e) : dflt;
+}
 // Binning partitions (A/B runs: GS_NPARTS_MOVE, GS_NPARTS_C1 = 128 or 256)
 static uint32_t env_nparts(const char* name, uint32_t dflt) {
     const char* e = std::getenv(name);
@@ -898,14 +902,18 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     pp.cut_margin = c->cut_margin > 0.0f ? c->cut_margin : kChunkMargin;
     pp.umask = two_chunks ? F.umask : nullptr;  // (chunk 1's rectangle tests; zeroed by k_part_list)
     pp.umask_w = umask_words(TX);
-    // k_cull on 512 workgroups when the camera moves (the default 2048 otherwise): cold frames (a
-    // camera cut every frame) 2690-2696 -> 2767-2779 fps, 1024: 2755; orbit unchanged (2538-2545);
-    // k_project's grid at 768 made the orbit slower (2526-2530).  GS_CULL_GRID_MOVE overrides (A/B).
-    static const uint32_t cull_grid_move = [] {
-        const char* e = std::getenv("GS_CULL_GRID_MOVE");
-        return e ? (uint32_t)std::atoi(e) : 512u;
-    }();
-    pp.cull_grid = moving ? cull_grid_move : 0u;
+    // Grids of the frame's culling and projection, which run beside the previous frame's composite
+    // (tools/ab_env.sh, two runs each): k_cull on 1024 workgroups for a still camera, 512 when it
+    // moves (2048 before: bench 3485-3506 -> 3625-3628 fps, 1536: 3502, 768: 3614-3625, the
+    // composite beside it 175.5 -> 171 us; cold frames 2690-2696 -> 2767-2779 with 512, 1024:
+    // 2755; orbit unchanged); k_project on 1280 for a still camera (1536 before: bench 3625 -> 3640;
+    // 1024: 3464; 768 under a moving camera made the orbit slower, 2526-2530 against 2538-2545).
+    // GS_CULL_GRID_STILL, GS_CULL_GRID_MOVE, GS_PROJ_GRID_STILL override (A/B runs).
+    static const uint32_t cull_grid_move = env_u32("GS_CULL_GRID_MOVE", 512u);
+    static const uint32_t cull_grid_still = env_u32("GS_CULL_GRID_STILL", 1024u);
+    static const uint32_t proj_grid_still = env_u32("GS_PROJ_GRID_STILL", 1280u);
+    pp.cull_grid = moving ? cull_grid_move : cull_grid_still;
+    pp.proj_grid = moving ? 0u : proj_grid_still;
     if (seeded) {
         pp.thresh = kNoSplit;
         pp.thresh_dev = &F.ctl->seed_T;
