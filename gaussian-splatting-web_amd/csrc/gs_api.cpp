@@ -972,7 +972,10 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     // (tools/ab_env.sh, two runs each): 256 / 256 2431-2434 fps, 128 / 256 2460-2463, 256 / 128
     // 2414-2420, 128 / 128 2528-2533.  A still frame's chunk-0 binning is slower with 128 (85 ->
     // 111 us, bench 3507 -> 3434-3456 fps), so it keeps 256.
-    bp.nparts = fit_nparts(bp.parts, moving ? env_nparts("GS_NPARTS_MOVE", kBinPartsSmall) : (uint32_t)kBinParts);
+    // (frames of up to 16384 tiles: at 3840 x 2160 the moving frame's chunk 0 is bound by its own
+    // binning, orbit 741 fps with 128 against 765 with 256)
+    bp.nparts = fit_nparts(bp.parts, moving && n_tiles <= 16384 ? env_nparts("GS_NPARTS_MOVE", kBinPartsSmall)
+                                                                 : (uint32_t)kBinParts);
     bp.cut = cut_on ? F.cut : nullptr;
     bp.cutb = F.cutb;
     bp.tvals = F.tvA;

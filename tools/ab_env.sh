@@ -9,7 +9,7 @@ for rep in $(seq $REPS); do
   for v in "$@"; do
     i=$((i+1))
     env=""; [ "$v" != "-" ] && env=$(echo $v | tr ',' ' ')
-    env $env timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 200 > $OUT/v${i}_$rep.log 2>&1 || { tail -5 $OUT/v${i}_$rep.log; exit 1; }
+    env $env timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps ${STEPS:-200} ${BENCH_ARGS:-} > $OUT/v${i}_$rep.log 2>&1 || { tail -5 $OUT/v${i}_$rep.log; exit 1; }
     python3 -c "
 import json
 d=json.loads(open('$OUT/v${i}_$rep.log').read().strip().splitlines()[-1]); s=d['stages_ms']
