@@ -1048,7 +1048,14 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
     mark(EV_DSORT_0);
     launch_bin(bp, st);
     mark(EV_BIN_0);
-    launch_tile_sort(tsp, st);
+    // A still camera's chunk-0 per-tile sort in the composite's launch (composite_sorts): the set
+    // stream's chain then ends with the emission, and a still frame waits for the end of that chain
+    // (bench 3626-3640 -> 3683-3695 fps).  Not under a moving camera, whose frames are bound by the
+    // caller's stream (chunk 0's composite, then chunk 1): orbit 2528 -> 2416 with it.
+    // GS_FUSE_SORT=0 keeps the separate sort (A/B runs).
+    static const uint32_t fuse_sort = env_u32("GS_FUSE_SORT", 1u);
+    const bool sort_in_composite = fuse_sort && !moving && composite_sorts(tsp, cp);
+    if (!sort_in_composite) launch_tile_sort(tsp, st);
     mark(EV_TSORT_0);
     HIPCHK(hipEventRecord(F.ev_early, st));
     HIPCHK(hipStreamWaitEvent(cst, F.ev_early, 0));
@@ -1060,7 +1067,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
         HIPCHK(hipMemsetAsync((char*)out + (size_t)(fr.rows - fr.pad) * (size_t)W * px, 0,
                               (size_t)fr.pad * (size_t)W * px, st));
     }
-    launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st);
+    launch_composite(cp, o.accum == GS_ACCUM_FP16_TARGET, st, sort_in_composite ? &tsp : nullptr);
     mark(EV_COMP_0);
     {  // chunk 1 (when chunk 0 left tiles unsaturated), then the frame's end: statistics into the
        // slot, FrameCtl zeroed for the next frame; one launch

@@ -495,7 +495,14 @@ __host__ __device__ inline int chunk1_grid(int occupancy, int cus) {
 // the same as separate launches (for frames expected to leave tiles unsaturated), then the frame's end
 void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s);
 void launch_tile_sort(const TileSortParams& p, hipStream_t s);
-void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s);
+// ts (nullable): chunk 0's per-tile sort in the composite's launch (composite_sorts)
+void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s, const TileSortParams* ts = nullptr);
+// Does launch_composite sort the tiles itself: chunk 0 lists of the 128-thread sort's shape, one
+// wave pair per tile, frames past the quarter-kernel size
+int composite_quarter_tiles();
+inline bool composite_sorts(const TileSortParams& tp, const CompositeParams& cp) {
+    return tp.big == 0 && cp.seg <= 1 && cp.n_tiles > composite_quarter_tiles() && (cp.bands == 2 || cp.bands == 4);
+}
 void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void* out, hipStream_t s);
 
 __host__ __device__ inline uint32_t sort_parts(uint64_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }

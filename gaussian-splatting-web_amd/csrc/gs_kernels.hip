@@ -3431,23 +3431,34 @@ __device__ __forceinline__ void band_lane(int l, int& band, int& idx) {
 // merge: SEG is 1 there.
 constexpr uint32_t kSegMin = 96;  // shortest segment worth a pair of waves
 
+// composite_tile's LDS (the kernel declares it, so a kernel can share it with another phase)
+template <int SEG, int BANDS>
+struct CompShared {
+    // staged record per batch entry: [0] c0u, c0v, a, b  [1] c, d, log2(op), slot (bits)
+    // [2] r, g, b, -   with u = a lx + b ly + c0u, v = c lx + d ly + c0v in tile-local pixels;
+    // entry kCompBatch of buffer 1 is the null record (log2 op = -inf: alpha 0, nothing blended)
+    float4 sR[SEG][2][kCompBatch + 1][3];
+    uint16_t sL[SEG][2][2][BANDS][kCompBatch];  // per half, per row band: LDS byte offsets of the
+                                                // staged records in sR (segment = producing wave,
+                                                // tail: the null record)
+    uint32_t sN[SEG][2][2][BANDS][2];           // per half, band, producing wave: list length
+    uint32_t s_sat[SEG];                        // depth key of the splat that saturated the pair's last wave
+    uint32_t s_any[3][2 * SEG];                 // block_any flags: batches by parity, the tile's end
+    uint32_t s_qsat;                            // SEG > 1: the segment in which the merged tile saturated
+};
+
 template <bool FP16_TARGET, int SEG, int BANDS>
-__device__ __forceinline__ void composite_tile(const CompositeParams& p, const int tile) {
+__device__ __forceinline__ void composite_tile(const CompositeParams& p, const int tile, CompShared<SEG, BANDS>& S) {
     static_assert(SEG == 1 || (!FP16_TARGET && (SEG == 2 || SEG == 4)), "list split: fp32 accumulation, 2 or 4 pairs");
     static_assert(BANDS == 2 || BANDS == 4, "row bands per wave");
     constexpr int kBands = BANDS, kBandRows = 16 / BANDS;
     constexpr int NT = 128 * SEG;
-    // staged record per batch entry: [0] c0u, c0v, a, b  [1] c, d, log2(op), slot (bits)
-    // [2] r, g, b, -   with u = a lx + b ly + c0u, v = c lx + d ly + c0v in tile-local pixels;
-    // entry kCompBatch of buffer 1 is the null record (log2 op = -inf: alpha 0, nothing blended)
-    __shared__ float4 sR[SEG][2][kCompBatch + 1][3];
-    __shared__ uint16_t sL[SEG][2][2][kBands][kCompBatch];  // per half, per row band: LDS byte offsets
-                                                            // of the staged records in sR (segment =
-                                                            // producing wave, tail: the null record)
-    __shared__ uint32_t sN[SEG][2][2][kBands][2];           // per half, band, producing wave: list length
-    __shared__ uint32_t s_sat[SEG];               // depth key of the splat that saturated the pair's last wave
-    __shared__ uint32_t s_any[3][2 * SEG];        // block_any flags: batches by parity, the tile's end
-    __shared__ uint32_t s_qsat;                   // SEG > 1: the segment in which the merged tile saturated
+    auto& sR = S.sR;
+    auto& sL = S.sL;
+    auto& sN = S.sN;
+    auto& s_sat = S.s_sat;
+    auto& s_any = S.s_any;
+    uint32_t& s_qsat = S.s_qsat;
     const int tid = threadIdx.x;
     if (p.mode == kCompSecond && p.done[tile]) return;
 #ifdef GS_COMP_DIAG
@@ -3842,9 +3853,32 @@ __device__ __forceinline__ void composite_tile(const CompositeParams& p, const i
 // (285 us) and one ticket counter for all bands (352 us) were all slower than this (230 us).
 template <bool FP16_TARGET, int SEG, int BANDS = kBands>
 __global__ __launch_bounds__(128 * SEG, SEG == 1 ? GS_COMP_WAVES : (SEG == 2 ? 5 : 2)) void k_composite(CompositeParams p) {
+    __shared__ CompShared<SEG, BANDS> S;
     const int per = (p.n_tiles + 7) >> 3;
     const int j = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // XCD band, position
-    if (j < p.n_tiles) composite_tile<FP16_TARGET, SEG, BANDS>(p, p.order ? (int)p.order[j] : j);
+    if (j < p.n_tiles) composite_tile<FP16_TARGET, SEG, BANDS>(p, p.order ? (int)p.order[j] : j, S);
+}
+
+// Chunk 0's per-tile sort and composite as one launch (the sort's 128-thread shape is the
+// composite's): the workgroup sorts its tile's list, then composites it from the list it just
+// wrote, in the same LDS.  The frame's chain then ends with the emission, one launch earlier.
+template <bool FP16_TARGET, int BANDS = kBands>
+__global__ __launch_bounds__(128, GS_COMP_WAVES) void k_composite_ts(CompositeParams p, TileSortParams tp) {
+    static_assert(TsSmall::NT == 128, "the sort's shape is the composite's");
+    constexpr size_t kLds = sizeof(CompShared<1, BANDS>) > sizeof(TsSharedT<TsSmall>) ? sizeof(CompShared<1, BANDS>)
+                                                                                      : sizeof(TsSharedT<TsSmall>);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
+    const int per = (p.n_tiles + 7) >> 3;
+    const int j = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // XCD band, position
+    if (j >= p.n_tiles) return;
+    const int tile = p.order ? (int)p.order[j] : j;
+    tile_sort_tile<TsSmall>(tp, tile, *reinterpret_cast<TsSharedT<TsSmall>*>(lds));
+    __syncthreads();  // (the sorted list: this workgroup's stores, through its CU's L1; the LDS reused)
+    // an opaque copy of the tile: nothing of the composite is computed before the sort and held
+    // across it (one such address was spilled to scratch)
+    int tc;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(tc) : "s"(tile));
+    composite_tile<FP16_TARGET, 1, BANDS>(p, tc, *reinterpret_cast<CompShared<1, BANDS>*>(lds));
 }
 
 // Chunk 1 (kCompSecond): workgroup j takes entry j of the compact list of the tiles chunk 0 left
@@ -3854,8 +3888,9 @@ __global__ __launch_bounds__(128 * SEG, SEG == 1 ? GS_COMP_WAVES : (SEG == 2 ? 5
 // them one after another.)
 template <bool FP16_TARGET, int SEG>
 __global__ __launch_bounds__(128 * SEG, 2) void k_composite_c1(CompositeParams p) {
+    __shared__ CompShared<SEG, kBands> S;
     if (blockIdx.x >= p.ctl->not_done) return;
-    composite_tile<FP16_TARGET, SEG, kBands>(p, __builtin_amdgcn_readfirstlane((int)p.c1tiles[blockIdx.x]));
+    composite_tile<FP16_TARGET, SEG, kBands>(p, __builtin_amdgcn_readfirstlane((int)p.c1tiles[blockIdx.x]), S);
 }
 
 // Quarter variant for frames with few tiles (row strips): 4 waves per tile, wave q owns the 8x8
@@ -4608,9 +4643,19 @@ void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s) {
     }
     hipLaunchKernelGGL(k_frame_end, dim3(1), dim3(64), 0, s, c);
 }
-void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s) {
+int composite_quarter_tiles() { return kQuarterTiles; }
+void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s, const TileSortParams* ts) {
     if (p.n_tiles <= 0) return;
     const unsigned grid = 8u * (unsigned)((p.n_tiles + 7) / 8);  // see k_composite's tile order
+    if (ts) {  // the per-tile sort in the same launch (the host checked composite_sorts)
+        if (accum_fp16)
+            hipLaunchKernelGGL((k_composite_ts<true, 2>), dim3(grid), dim3(128), 0, s, p, *ts);
+        else if (p.bands == 4)
+            hipLaunchKernelGGL((k_composite_ts<false, 4>), dim3(grid), dim3(128), 0, s, p, *ts);
+        else
+            hipLaunchKernelGGL((k_composite_ts<false, 2>), dim3(grid), dim3(128), 0, s, p, *ts);
+        return;
+    }
     if (p.n_tiles <= kQuarterTiles) {  // (see kQuarterTiles)
         if (accum_fp16)
             hipLaunchKernelGGL(k_composite_q<true>, dim3(grid), dim3(256), 0, s, p);
