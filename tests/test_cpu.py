@@ -292,6 +292,10 @@ def test_kernel_resources_no_scratch():
         for n in found:
             assert res[n]["scratch"] == 0, (n, res[n])
     assert res["k_composite<false,1,2>"]["vgpr"] <= 96, res["k_composite<false,1,2>"]
+    # the still camera's fused sort + composite: one 8-B value of the sort held in scratch across
+    # a barrier (present at any VGPR budget), nothing more
+    for n in [n for n in res if n.startswith("k_composite_ts<")]:
+        assert res[n]["scratch"] <= 16 and res[n]["vgpr"] <= 96, (n, res[n])
 
 
 def test_chunk1_grid_residency_rule():
