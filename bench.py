@@ -42,8 +42,10 @@ CONFIGS = {  # BASELINE.json configs the bench can run (index: N, W, H, seed)
 }
 
 
-def algorithmic_bytes(stage, n, n_vis, k, W, H, n_chunk0=None):
-    """Bytes a kernel group must move per launch."""
+def algorithmic_bytes(stage, n, n_vis, k, W, H, n_chunk0=None, sorts=False):
+    """Bytes a kernel group must move per launch.  sorts: the composite sorts its
+    tile's list in the same launch (a still camera's frames, k_composite_ts): 16 B more per entry
+    (the unordered slot read, its 8-B sort key gathered, the ordered slot written)."""
     if stage == "project":
         # k_cull reads the 16-B cull plane of every Gaussian of a surviving partition (<= N);
         # each chunk-0 splat: its 48-B geometry record and 192-B SH read, 80 B of slot records
@@ -51,7 +53,7 @@ def algorithmic_bytes(stage, n, n_vis, k, W, H, n_chunk0=None):
         return 16 * n + 320 * (n_vis if n_chunk0 is None else n_chunk0)
     if stage == "composite":
         # per (tile, splat) entry: the 4-B slot and the 48-B composite record; RGBA f16 out
-        return 52 * k + 8 * W * H
+        return (68 if sorts else 52) * k + 8 * W * H
     raise KeyError(stage)
 
 
@@ -76,8 +78,8 @@ def _is_kernel(label, kernel):
     position in the frame) of the chunk-0 composite (any of its template instances; not chunk 1's
     k_composite_q) or of the projection."""
     name = label.split("#")[0]
-    if kernel == "composite":
-        return name.startswith("k_composite<false")
+    if kernel == "composite":  # (k_composite_ts: with its tile's sort, a still camera's frames)
+        return name.startswith("k_composite<false") or name.startswith("k_composite_ts<false")
     if kernel == "project":
         return name.startswith("k_project<")
     raise KeyError(kernel)
@@ -417,8 +419,11 @@ def main():
     stages = {"project": st["ms_project"], "composite": st["ms_composite"]}
     dom = max(stages, key=stages.get)
     rows_here = max(0, min(t1 * 16, H) - row0)
+    # (the per-tile sort ran inside the composite when its own stage is only the events' gap: a
+    # separate sort takes >= 19 us at this size)
+    sorts_in_composite = st["ms_tile_sort"] < 0.010
     a_bytes = algorithmic_bytes(dom, N, ex["n_vis"], st["k_entries"], W, rows_here,
-                                n_chunk0=int(round(st["chunk_fraction"] * st["n_vis"])))
+                                n_chunk0=int(round(st["chunk_fraction"] * st["n_vis"])), sorts=sorts_in_composite)
     achieved = a_bytes / (stages[dom] * 1e-3) / 1e9
     # the committed PMC profile is of the default command (configs[3] on one GPU): its counters
     # only describe that workload
@@ -453,7 +458,8 @@ def main():
             # per-stage HIP-event times from the separate timing=1 loop (events between stages add
             # ~20 us to its frame), except ms_composite, timed live in the headline loop:
             # project = partition cull + cull + projection/colour, bin = count + scans + emission,
-            # tile_sort = per-tile sort, chunk1 = the chunk-1 launch (returns at once when chunk 0
+            # tile_sort = per-tile sort (a still camera: inside the composite's launch, this stage
+            # then only the events' gap), chunk1 = the chunk-1 launch (returns at once when chunk 0
             # saturated every tile)
             "stages_ms": {"ms_total": round(st["ms_total"], 4), "ms_project": round(st["ms_project"], 4),
                           "ms_bin": round(st["ms_bin"], 4), "ms_tile_sort": round(st["ms_tile_sort"], 4),
@@ -472,6 +478,7 @@ def main():
                          # read from the committed profile of this same command, not this run)
                          "traffic_source": ("committed profile profiles/%s" % traffic_src) if traffic_src else None,
                          "algorithmic_bytes_per_launch": int(a_bytes),
+                         "includes_tile_sort": bool(sorts_in_composite and dom == "composite"),
                          "per": "frame (the kernel's launches in one frame, HIP events on the render stream)"},
             # the dominant kernel's real bound: VALU issue (PMC instruction count of this command's
             # committed profile / the live event-timed duration)
