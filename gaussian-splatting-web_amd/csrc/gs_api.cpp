@@ -1,9 +1,11 @@
 // gs_api.cpp — C ABI (include/gsplat.h): contexts, scenes and the per-frame pipeline.
 //
-// A frame (render_frame) is a fixed sequence of 8 launches with no host round trip; data-
+// A frame (render_frame) is a fixed sequence of launches with no host round trip; data-
 // dependent sizes live in FrameCtl on the device:
-//   k_cull -> k_project -> k_bin_count -> k_bin_colscan -> k_bin_emit -> k_tile_sort ->
-//   k_composite -> k_chunk1 (chunk 1 when chunk 0 left tiles unsaturated, then the frame's end)
+//   k_part_list -> k_cull -> k_project -> k_bin_count -> k_bin_colscan -> k_bin_emit ->
+//   k_tile_sort -> k_composite (a still camera: k_composite_ts, the sort inside it) ->
+//   k_chunk1 (chunk 1 when chunk 0 left tiles unsaturated, then the frame's end; or chunk 1's
+//   separate launches and k_frame_end)
 // Chunk 0 = the visible splats nearer than a depth key T; chunk 1 = the rest, binned only into
 // tiles chunk 0 left unsaturated.  T adapts from earlier frames' statistics (read back
 // asynchronously); the image does not depend on T.  Frames rotate over kFrameSets sets of

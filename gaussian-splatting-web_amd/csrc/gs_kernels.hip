@@ -15,10 +15,13 @@
 //                 depth sort (src/renderer.ts:175-183) restricted to the tile
 //   k_composite   16x16 tile: front-to-back "under" blending of fs_main's alpha
 //                 (src/simple_render.ts:169-200, blend state :455-471), batches staged in LDS
+//                 (k_composite_ts: a still camera's frames sort each tile in the composite's launch)
 //   k_chunk1      chunk 1 (tiles chunk 0 left unsaturated) as one launch of 64 co-resident
 //                 workgroups with grid barriers (a plain launch: one 256-thread workgroup per CU
 //                 at most, so the grid always fits beside the other kernels), then the frame's
-//                 end (statistics shards -> FrameCtl -> pinned host slot)
+//                 end (statistics shards -> FrameCtl -> pinned host slot); or, after frames that
+//                 left tiles unsaturated and under a moving camera, as separate launches
+//                 (k_c1_parts, k_c1_records, binning, k_c1_tiles, k_frame_end)
 //
 // Inter-workgroup hand-offs (the grid barrier) follow cdna_hip_programming.md Guideline 16:
 // agent-scope release / acquire, bounded spins, counters zeroed by the frame's end.
