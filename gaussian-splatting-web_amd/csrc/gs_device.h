@@ -497,11 +497,13 @@ void launch_chunk1_split(const Chunk1Params& c, int accum_fp16, hipStream_t s);
 void launch_tile_sort(const TileSortParams& p, hipStream_t s);
 // ts (nullable): chunk 0's per-tile sort in the composite's launch (composite_sorts)
 void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s, const TileSortParams* ts = nullptr);
-// Does launch_composite sort the tiles itself: chunk 0 lists of the 128-thread sort's shape, one
-// wave pair per tile, frames past the quarter-kernel size
+// Does launch_composite sort the tiles itself: one wave pair per tile, frames past the
+// quarter-kernel size, chunk-0 lists of the 128-thread sort's shape or of the 256-thread one (the
+// composite sorts those with 128 threads too: the sparse scene's lists of ~900 entries, 1036 ->
+// 1059-1061 fps), not the 1024-thread shape's thousands
 int composite_quarter_tiles();
 inline bool composite_sorts(const TileSortParams& tp, const CompositeParams& cp) {
-    return tp.big == 0 && cp.seg <= 1 && cp.n_tiles > composite_quarter_tiles() && (cp.bands == 2 || cp.bands == 4);
+    return tp.big <= 1 && cp.seg <= 1 && cp.n_tiles > composite_quarter_tiles() && (cp.bands == 2 || cp.bands == 4);
 }
 void launch_present(const void* in, int in_f16, int W, int H, int out_kind, void* out, hipStream_t s);
 
