@@ -1007,7 +1007,7 @@ static void render_frame(gs_ctx* c, gs_scene* s, const float* uni, int W, int H,
                                                                    : 0;
     }
     tsp.stats = F.stats;
-    if (tsp.big == 2) {  // lists past one 8192-entry LDS round: the linear long-list path (256 threads);
+    if (tsp.big == 2) {  // lists past one 7168-entry LDS round: the linear long-list path (256 threads);
                          // c1tiles is free until the composite appends chunk 1's tiles to it
         tsp.long_tiles = F.c1tiles;
         tsp.long_n = &F.ctl->long_n;

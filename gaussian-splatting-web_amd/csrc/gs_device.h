@@ -93,7 +93,7 @@ struct FrameCtl {                 // zeroed at the start of every frame
     uint32_t sat_hist[kSatBuckets];  // tiles saturated by the end of the frame, by saturation depth
                                      // (sat_bucket; summed from the shards at the frame's end)
     uint32_t list_max;            // longest tile list of the frame (either chunk) when > kListMaxMin, else 0
-    uint32_t long_n;              // tiles the 1024-thread sort shape left to the long-list pass (TileSortParams::long_tiles)
+    uint32_t long_n;              // tiles the huge sort shape left to the long-list pass (TileSortParams::long_tiles)
 };
 
 // Per-frame counters that many workgroups add to, sharded so that no address takes more than a
@@ -374,15 +374,15 @@ struct TileSortParams {
     uint32_t* scratch;            // [n_tiles][256] long lists' bucket ends (the binning's bmat, dead by then)
     int n_tiles;
     int big;                      // chunk 0 with long lists: 1 = the 256-thread shape (k_tile_sort_big),
-                                  // 2 = the 1024-thread shape (k_tile_sort_huge: lists of <= 8192 in LDS)
+                                  // 2 = the huge shape (k_tile_sort_huge: lists of <= 7168 in LDS)
     // chunk 1: the tiles chunk 0 left unsaturated, a compact list (CompositeParams::c1tiles) of
     // *c1_n entries; the launch walks it instead of every tile (nullable)
     const uint32_t* c1tiles;
     const uint32_t* c1_n;
-    // the 1024-thread shape (big == 2) sorts lists of <= 8192 entries in one LDS round; a longer
-    // list's tile is appended here (count FrameCtl::long_n) and sorted afterwards by the 256-thread
-    // shape's linear long-list path (launch_tile_sort's second launch) instead of in rounds that
-    // each re-read the list (O(L^2 / 8192))
+    // the huge shape (big == 2: two 1024-thread workgroups per CU) sorts lists of <= 7168 entries in
+    // one LDS round; a longer list's tile, or one with more than kTsHeavy keys in one bucket, is
+    // appended here (count FrameCtl::long_n) and sorted afterwards by the 256-thread shape's
+    // linear long-list path (launch_tile_sort's second launch; required with big == 2)
     uint32_t* long_tiles;
     uint32_t* long_n;             // &FrameCtl::long_n
     StatShard* stats;             // nullable: list_max
@@ -500,7 +500,7 @@ void launch_composite(const CompositeParams& p, int accum_fp16, hipStream_t s, c
 // Does launch_composite sort the tiles itself: one wave pair per tile, frames past the
 // quarter-kernel size, chunk-0 lists of the 128-thread sort's shape or of the 256-thread one (the
 // composite sorts those with 128 threads too: the sparse scene's lists of ~900 entries, 1036 ->
-// 1059-1061 fps), not the 1024-thread shape's thousands
+// 1059-1061 fps), not the huge shape's thousands
 int composite_quarter_tiles();
 inline bool composite_sorts(const TileSortParams& tp, const CompositeParams& cp) {
     return tp.big <= 1 && cp.seg <= 1 && cp.n_tiles > composite_quarter_tiles() && (cp.bands == 2 || cp.bands == 4);

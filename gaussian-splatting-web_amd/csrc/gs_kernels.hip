@@ -2759,28 +2759,34 @@ __device__ __forceinline__ void frame_end_body(FrameCtl* ctl, StatShard* stats, 
 // SIMD pair instead of one 256-thread workgroup per SIMD; 50 -> 40 us at the bench frame);
 // chunk 1's lists (thousands of entries in the few tiles that never saturate) by TsBig, as in
 // k_chunk1's 256-thread workgroups.
-template <int NT_, int IPT_, int BB_>
+template <int NT_, int IPT_, int BB_, bool VS_ = true>
 struct TsCfg {
     static constexpr int NT = NT_;                            // threads
     static constexpr int IPT = IPT_;                          // entries per thread and round
     static constexpr uint32_t Cap = (uint32_t)(NT_ * IPT_);   // entries per round
     static constexpr int BB = BB_;                            // bucket bits
     static constexpr uint32_t Buckets = 1u << BB_;
+    static constexpr bool VS = VS_;                           // slots staged in LDS (the bitonic path)
     static_assert(NT_ % 64 == 0 && (1 << BB_) % NT_ == 0, "tile sort shape");
 };
 using TsBig = TsCfg<256, 8, 10>;
 using TsSmall = TsCfg<128, 8, 9>;
-// Lists of a few thousand entries (a one-chunk frame at 4K: ~6300 per tile): the whole list in
-// LDS (128 KB, one workgroup per CU), one gather of the keys instead of ts_long's four passes;
-// 8192 buckets (a thread's eight counters, two 16-B words): a bucket holds ~3 of a tile's keys at
-// 4096, and the count ranking loops over the bucket (sort 1.62 -> 1.56 ms at 50 M / 4K).
-using TsHuge = TsCfg<1024, 8, 13>;
+// Lists of a few thousand entries (a one-chunk frame at 4K: ~6300 per tile): the whole list's keys
+// in LDS, one gather of the keys instead of ts_long's four passes.  Two workgroups per CU, each
+// 72 KB of LDS (7168 8-B keys and 4096 bucket counters; no slot staging: the count ranking writes
+// the slots from registers, and a list the ranking cannot take -- a bucket of more than kTsHeavy
+// keys -- or longer than one round goes to the long-list launch), so one workgroup's phases hide
+// the other's latency: with one 128-KB workgroup per CU (1024 threads, 8192 keys and slots) 67 %
+// of its wave cycles waited.  One-chunk 50 M / 4K: sort 1.56 -> 1.28 ms at 2 x 512 threads (14
+// entries each, 102 VGPRs), frame 7.35 -> 7.11 ms at 2 x 1024 (7 entries each, 56 VGPRs of the 64
+// that 8 waves per SIMD allow).
+using TsHuge = TsCfg<1024, 7, 12, false>;
 constexpr uint32_t kTsHeavy = 64;  // largest bucket ranked by counting
 
 template <class C>
 struct TsSharedT {
     unsigned long long k[C::Cap];
-    uint32_t v[C::Cap];
+    uint32_t v[C::VS ? C::Cap : 1];
     alignas(16) uint32_t cnt[C::Buckets];  // a thread's per = Buckets / NT = 4 (8) counters are one (two) 16-B
                                            // word (ds_read/write_b128, no stride-4 conflicts); after
                                            // the scatter cnt[b] is bucket b's end = bucket b+1's start
@@ -2839,7 +2845,7 @@ __device__ __forceinline__ int ts_shift(unsigned long long span) {
 }
 
 #ifdef GS_TS_TIME  // diagnostics builds only (make diag DIAGFLAGS=-DGS_TS_TIME): the long-list phases
-// cycles summed over tiles.  ts_long: minmax, hist, scan, scatter, rounds, heavy; the 1024-thread
+// cycles summed over tiles.  ts_long: minmax, hist, scan, scatter, rounds, heavy; the huge
 // shape's one-round lists: load + gather, minmax, count, scan + scatter, rank + write; then tiles, entries
 __device__ unsigned long long g_ts_time[8];
 #define TS_T(i)                                                                        \
@@ -2857,15 +2863,16 @@ __device__ unsigned long long g_ts_time[8];
 #endif
 
 // Sort n <= C::Cap elements held in registers (element j * NT + tid of k/v) with keys in
-// [kmin, kmax]; out[rank] = value.
+// [kmin, kmax]; out[rank] = value.  False (nothing written, block-uniform) when a shape without
+// slot staging (!C::VS) meets a bucket of more than kTsHeavy keys.
 template <class C>
-__device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT], const uint32_t (&v)[C::IPT],
+__device__ bool ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT], const uint32_t (&v)[C::IPT],
                            uint32_t n, unsigned long long kmin, unsigned long long kmax, uint32_t* __restrict__ out) {
     constexpr int kTsThreads = C::NT, kTsIpt = C::IPT;
     constexpr uint32_t kTsBuckets = C::Buckets;
     const int tid = threadIdx.x;
 #ifdef GS_TS_TIME
-    constexpr bool kT = C::NT > 256;  // the 1024-thread shape's phases
+    constexpr bool kT = C::NT > 256;  // the huge shape's phases
     unsigned long long ts_t0 = clock64();
 #endif
     const int s = ts_shift<C>(kmax - kmin);  // S.cnt was zeroed by the caller before block_minmax64's barrier
@@ -2902,12 +2909,15 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
         b += c4[q].x + c4[q].y + c4[q].z + c4[q].w;
     }
     const bool heavy = block_any<kTsThreads>(big > kTsHeavy, S.any);
+    if constexpr (!C::VS)
+        if (heavy) return false;
 #pragma unroll
     for (int j = 0; j < kTsIpt; ++j) {
         if (j * kTsThreads + tid < (int)n) {
             const uint32_t pos = atomicAdd(&S.cnt[bk[j]], 1u);
             S.k[pos] = k[j];
-            if (heavy) S.v[pos] = v[j];  // the count ranking writes v from registers
+            if constexpr (C::VS)
+                if (heavy) S.v[pos] = v[j];  // the count ranking writes v from registers
         }
     }
     __syncthreads();
@@ -2924,7 +2934,7 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
                 out[r] = v[j];
             }
         }
-    } else {  // bitonic sort of the (bucket-ordered) elements, padded to a power of two
+    } else if constexpr (C::VS) {  // bitonic sort of the (bucket-ordered) elements, padded to a power of two
         uint32_t P = 1;
         while (P < n) P <<= 1;
         for (uint32_t i = n + tid; i < P; i += kTsThreads) {
@@ -2955,6 +2965,7 @@ __device__ void ts_segment(TsSharedT<C>& S, const unsigned long long (&k)[C::IPT
 #ifdef GS_TS_TIME
     if (kT) TS_T(5);
 #endif
+    return true;
 }
 
 // Sort the n <= C::Cap (key, slot) pairs staged in S.k / S.v (after a barrier) into out[0, n).
@@ -3243,8 +3254,8 @@ __device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const in
     if (L == 0) return;
     const int tid = threadIdx.x;
     if (L > kListMaxMin && tid == 0 && p.stats) atomicMax(&p.stats[tile % kStatShards].list_max, L);
-    if constexpr (C::NT > TsBig::NT) {
-        if (L > kTsCap && p.long_tiles) {  // left to the long-list launch (ts_long at 256 threads)
+    if constexpr (!C::VS) {  // (the host always gives this shape a long-list launch)
+        if (L > kTsCap) {  // left to the long-list launch (ts_long at 256 threads)
             if (tid == 0) p.long_tiles[atomicAdd(p.long_n, 1u)] = (uint32_t)tile;
             return;
         }
@@ -3292,22 +3303,18 @@ __device__ __forceinline__ void tile_sort_tile(const TileSortParams& p, const in
 #ifdef GS_TS_TIME
         if (kT) TS_T(2);
 #endif
-        ts_segment<C>(S, k, v, L, mn, mx, out);
+        if (!ts_segment<C>(S, k, v, L, mn, mx, out) && tid == 0)  // a heavy bucket: the long-list launch
+            p.long_tiles[atomicAdd(p.long_n, 1u)] = (uint32_t)tile;
         return;
     }
-    // k_tile_sort_huge without a long-list launch: a list past 8192 in rounds of 8192 (ts_long at
-    // 1024 threads would spill)
-    if constexpr (C::NT > TsBig::NT)
-        ts_rounds<C>(p, S, in, out, L);
-    else
-        ts_long<C>(p, S, p.in + range.x, out, L, p.scratch + (size_t)tile * kTsLongBuckets);
+    if constexpr (C::VS) ts_long<C>(p, S, p.in + range.x, out, L, p.scratch + (size_t)tile * kTsLongBuckets);
 }
 
 __global__ __launch_bounds__(TsSmall::NT, 5) void k_tile_sort(TileSortParams p) {
     __shared__ TsSharedT<TsSmall> S;
     tile_sort_body<TsSmall>(p, blockIdx.x, S);
 }
-__global__ __launch_bounds__(TsHuge::NT, 1) void k_tile_sort_huge(TileSortParams p) {
+__global__ __launch_bounds__(TsHuge::NT, 2 * TsHuge::NT / 256) void k_tile_sort_huge(TileSortParams p) {
     __shared__ TsSharedT<TsHuge> S;
     tile_sort_body<TsHuge>(p, blockIdx.x, S);
 }
