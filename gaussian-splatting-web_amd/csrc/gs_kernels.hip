@@ -1357,6 +1357,11 @@ __global__ __launch_bounds__(kProjThreads) void k_cull(ProjParams p) {
 // frame's unit list; a visible one gets its records and (from its shading block, one thread per
 // splat in the reference's expression order: sh_colour) its colour in its slot, an invisible one
 // leaves the slot a hole (rect kRectHole).  Publishes the visible count, their tile total, the depth range.
+#ifdef GS_PROJ_NT  // (A/B builds: the model read with the streaming policy)
+#define GS_PROJ_LOAD_POLICY " nt"
+#else
+#define GS_PROJ_LOAD_POLICY ""
+#endif
 template <bool SH12>  // SH12: degree-3 scenes (12 coefficient quads), staged through LDS
 __global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
     __shared__ unsigned long long s_k;
@@ -1425,7 +1430,7 @@ __global__ __launch_bounds__(kProjThreads, 3) void k_project(ProjParams p) {
                 asm volatile(
                     "s_mov_b32 %[msave], m0\n"
                     "s_mov_b32 m0, %[lds]\n s_nop 0\n"
-                    "global_load_lds_dwordx4 %[sp], off\n"
+                    "global_load_lds_dwordx4 %[sp], off" GS_PROJ_LOAD_POLICY "\n"
                     "s_mov_b32 m0, %[msave]\n"
                     : [msave] "=&s"(m0save)
                     : [sp] "v"(src), [lds] "s"(dst)
@@ -2475,6 +2480,15 @@ __device__ __forceinline__ void tile_scan_body(const BinParams& p, uint32_t* s_w
 }
 
 
+// A list entry's store (GS_EMIT_NT: a non-temporal store, A/B builds).
+__device__ __forceinline__ void emit_entry(uint32_t* __restrict__ tv, uint32_t pos, uint32_t g) {
+#ifdef GS_EMIT_NT
+    __builtin_nontemporal_store(g, tv + pos);
+#else
+    tv[pos] = g;
+#endif
+}
+
 // One emission walk of a unit list (see bin_count_walk): each entry takes its position from the
 // tile's LDS cursor.  stats: the walk adds to the chunk's wide-splat statistics (not chunk 1's
 // second walk).
@@ -2505,7 +2519,7 @@ __device__ __forceinline__ void bin_emit_walk(const BinParams& p, uint32_t part,
         const float4* q = p.crec + 3 * (uint64_t)g;
         splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, key, cw, m, [&](uint32_t t) {
             const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
-            if (pos < cap) p.tvals[pos] = g;
+            if (pos < cap) emit_entry(p.tvals, pos, g);
         });
     }
 
@@ -2520,12 +2534,12 @@ __device__ __forceinline__ void bin_emit_walk(const BinParams& p, uint32_t part,
         const uint32_t g = s_wide[qi];
         wide_entries(p, g, t_lo, t_hi, cw, [&](uint32_t t) {
             const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
-            if (pos < cap) p.tvals[pos] = g;
+            if (pos < cap) emit_entry(p.tvals, pos, g);
         });
     }
     wide_listed<NT>(p, part, t_lo, t_hi, cw, [&](uint32_t t, uint32_t g) {
         const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
-        if (pos < cap) p.tvals[pos] = g;
+        if (pos < cap) emit_entry(p.tvals, pos, g);
     });
 }
 
