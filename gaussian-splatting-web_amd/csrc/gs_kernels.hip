@@ -4576,7 +4576,11 @@ void launch_bin(const BinParams& p0, hipStream_t s) {
         std::fprintf(stderr, "gsplat: launch_bin with %u binning partitions for %u units\n", p.nparts, p.parts * (uint32_t)kProjRounds);
         std::abort();  // (the host never asks)
     }
-    const uint32_t bands = (p.n_tiles + kBandTilesMax - 1) / kBandTilesMax;
+    static const uint32_t min_bands = [] {  // (A/B runs: GS_BIN_BANDS, a smaller band per workgroup)
+        const char* e = std::getenv("GS_BIN_BANDS");
+        return e ? (uint32_t)std::max(1, std::min(4, std::atoi(e))) : 1u;
+    }();
+    const uint32_t bands = std::max(min_bands, (p.n_tiles + kBandTilesMax - 1) / kBandTilesMax);
     p.band_tiles = (p.n_tiles + bands - 1) / bands;  // equal bands
     // units of one binning partition: at most ceil(all units / nparts)
     p.pref_words = std::min<uint32_t>(kBinMaxUnits, (p.parts * (uint32_t)kProjRounds + p.nparts - 1) / p.nparts) + 1;
