@@ -2489,6 +2489,25 @@ __device__ __forceinline__ void emit_entry(uint32_t* __restrict__ tv, uint32_t p
 #endif
 }
 
+// The emission's slot loads (GS_EMIT_SLOT_NT: the streaming policy, A/B builds -- the slots are
+// read once, the list lines they would evict from L2 are still being filled).
+__device__ __forceinline__ uint32_t emit_ld(const uint32_t* a) {
+#ifdef GS_EMIT_SLOT_NT
+    return __builtin_nontemporal_load(a);
+#else
+    return *a;
+#endif
+}
+__device__ __forceinline__ float4 emit_ld(const float4* a) {
+#ifdef GS_EMIT_SLOT_NT
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(a));
+    return make_float4(v[0], v[1], v[2], v[3]);
+#else
+    return *a;
+#endif
+}
+
 // One emission walk of a unit list (see bin_count_walk): each entry takes its position from the
 // tile's LDS cursor.  stats: the walk adds to the chunk's wide-splat statistics (not chunk 1's
 // second walk).
@@ -2504,7 +2523,7 @@ __device__ __forceinline__ void bin_emit_walk(const BinParams& p, uint32_t part,
     for (uint32_t r = threadIdx.x; r < total; r += NT) {
         const uint32_t g = bin_slot(p, L, part, s_pref, r);
         TileRect tr;
-        if (!rect_unpack(p, p.srect[g], p.sidx[g], tr)) continue;
+        if (!rect_unpack(p, emit_ld(p.srect + g), emit_ld(p.sidx + g), tr)) continue;
         if (rect_wide(p, tr)) {
             if (p.wlist) continue;  // listed: walked below
             const uint32_t qi = atomicAdd(&s_nw, 1u);
@@ -2517,7 +2536,7 @@ __device__ __forceinline__ void bin_emit_walk(const BinParams& p, uint32_t part,
         const int m = cw.splat_mode(tr, key);
         if (m < 0) continue;
         const float4* q = p.crec + 3 * (uint64_t)g;
-        splat_entries(p, tr, ellipse_of(q[0], q[1]), t_lo, t_hi, key, cw, m, [&](uint32_t t) {
+        splat_entries(p, tr, ellipse_of(emit_ld(q), emit_ld(q + 1)), t_lo, t_hi, key, cw, m, [&](uint32_t t) {
             const uint32_t pos = atomicAdd(&s_cur[t - t_lo], 1u);
             if (pos < cap) emit_entry(p.tvals, pos, g);
         });
